@@ -1,0 +1,190 @@
+"""Benchmark: skeleton-frames/sec (fwd+bwd) of the 10-layer ST-GCN (fcn_in + 9 StgcnLayers, as_is BN,
+Kt=9) at N=64 T=300 V=25 (BASELINE.json config 2), bf16 MFMA path, synthetic data.
+
+One step = forward of the whole model on one (64, 3, 300, 25) batch + the reference loss
+(weighted CE + clamped temporal MSE, utils/loss.py:25-41, windows as the time axis like
+WindowSegment.mask_segment) + backward + Adam step.  Inputs are resident in HBM before timing.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+N > 1: launched by torch.distributed.run, one process per GPU, RCCL (backend "nccl") DDP gradient
+all-reduce; each rank processes its own 64-window batch (weak scaling).
+Rank 0 prints ONE JSON line (metric/value/..., roofline, cpu_baseline).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+ARCH = {
+    "strategy": "spatial", "in_feat": 3, "normalization": "BatchNorm", "num_classes": 52, "output_type": "logits",
+    "st-gcn": {"in_feat": 3, "layers": 9, "kernel": 9, "importance": True,
+               "in_ch": [64, 64, 64, 64, 128, 128, 128, 256, 256],
+               "out_ch": [64, 64, 64, 128, 128, 128, 256, 256, 256],
+               "stride": [1, 1, 1, 2, 1, 1, 2, 1, 1], "residual": [1] * 9, "dropout": [0] * 9},
+}
+N_BATCH, T_LEN, V_J, CLASSES = 64, 300, 25, 52
+BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 MFMA
+HBM_PEAK_GBS = 8000.0
+
+
+def loss_fn(logits, labels, weight):
+    """utils/loss.py:25-41 with WindowSegment.mask_segment (N',C',1) -> (1,C',N') (segment_generator.py:151)."""
+    pred = logits.permute(2, 1, 0)                      # (1, classes, windows)
+    ce = torch.nn.functional.cross_entropy(pred, labels, weight=weight)
+    ls = torch.log_softmax(pred, dim=1)
+    mse = 0.15 * torch.clamp((ls[:, :, 1:] - ls.detach()[:, :, :-1]) ** 2, 0, 16).mean()
+    return ce + mse
+
+
+def tcn_flops_c64():
+    # temporal conv of a C=64, stride-1 layer: 2*N*T*V*C*C*Kt
+    return 2.0 * N_BATCH * T_LEN * V_J * 64 * 64 * 9
+
+
+def cpu_baseline(pkg, model_cpu_sd):
+    """Oracle (CPU restatement, oracle/stgcn_oracle.py) fwd+bwd on a bounded sample of the workload."""
+    from oracle import stgcn_oracle as O
+
+    threads = torch.get_num_threads()
+    n_sample = int(os.environ.get("STGCN_CPU_SAMPLE_N", "8"))
+    arch = dict(ARCH, graph=pkg.PKU_MMD)
+    sd = {k: v.detach().float().clone().requires_grad_(v.dtype.is_floating_point) for k, v in model_cpu_sd.items()}
+    gen = torch.Generator().manual_seed(0)
+    weight = 1 - torch.rand(CLASSES, generator=gen) / CLASSES
+
+    def step(n):
+        x = torch.randn(n, 3, T_LEN, V_J, generator=gen)
+        labels = torch.randint(0, CLASSES, (1, n), generator=gen)
+        y = O.stgcn_model(x, sd, arch)
+        loss_fn(y, labels, weight).backward()
+
+    step(2)  # warm-up (allocator, oneDNN primitives)
+    t0 = time.perf_counter()
+    reps = 2
+    for _ in range(reps):
+        step(n_sample)
+    dt = time.perf_counter() - t0
+    return {"value": reps * n_sample * T_LEN / dt, "unit": "skeleton-frames/s", "cores": threads, "kind": "port",
+            "sample": f"oracle fwd+bwd (torch CPU fp32) of the same 9-layer model at N={n_sample} T={T_LEN} V=25, "
+                      f"{reps} steps, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    import __graft_entry__ as ge
+    pkg = ge.load_package()
+    K = pkg.native
+
+    torch.manual_seed(1538574472)  # config seed (stgcn_local.json optimizer.seed)
+    model = pkg.MODELS["st-gcn"](rank=None, **dict(ARCH, graph=pkg.PKU_MMD))
+    cpu_sd = {k: v.clone() for k, v in model.state_dict().items()}
+    model = model.to(dev).set_compute_dtype(args.dtype)
+    train_model = model
+    if world > 1:
+        from torch.nn.parallel import DistributedDataParallel as DDP
+        train_model = DDP(model, device_ids=[local], bucket_cap_mb=16, gradient_as_bucket_view=True)
+    opt = torch.optim.Adam(model.parameters(), lr=5e-4, foreach=True)
+
+    gen = torch.Generator(device=dev).manual_seed(rank)
+    x = torch.randn(N_BATCH, 3, T_LEN, V_J, device=dev, generator=gen)
+    labels = torch.randint(0, CLASSES, (1, N_BATCH), device=dev, generator=gen)
+    weight = (1 - torch.rand(CLASSES, device=dev, generator=gen) / CLASSES)
+
+    def step():
+        y = train_model(x)
+        loss = loss_fn(y, labels, weight)
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+
+    for _ in range(args.warmup):
+        step()
+
+    # live timing of the dominant kernel (temporal-conv forward of the C=64 layers) on its stream
+    events = []
+
+    def hook(tag, phase):
+        if tag != "tcn_fwd_c64":
+            return
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream())
+        events.append(ev)
+
+    K.EVENT_HOOK = hook
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    K.EVENT_HOOK = None
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = t.item()
+
+    kt = [events[i].elapsed_time(events[i + 1]) for i in range(0, len(events) - 1, 2)]
+    k_ms = sum(kt) / len(kt) if kt else float("nan")
+    achieved = tcn_flops_c64() / (k_ms * 1e-3) / 1e12 if kt else None
+
+    frames = world * args.steps * N_BATCH * T_LEN
+    value = frames / elapsed
+    if rank == 0:
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_tcn_fwd_c64.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(pkg, cpu_sd)
+        out = {
+            "metric": "skeleton-frames/sec/GPU (fwd+bwd), 10-layer ST-GCN N=64 T=300 V=25",
+            "value": round(value, 1), "unit": "skeleton-frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic (randn skeletons, random labels/class weights), random-init weights",
+            "config": {"workload": "config 2: as_is st-gcn (fcn_in + 9 StgcnLayer, BatchNorm, Kt=9), fwd + loss + "
+                                   "bwd + Adam", "global_batch": N_BATCH * world, "seq_len": T_LEN, "joints": V_J,
+                       "parallelism": f"dp{world}" if world > 1 else "single"},
+            "roofline": {"kernel": "conv_rows_kernel (temporal conv fwd, C=64, Kt=9, stride 1)", "bound": "mfma",
+                         "achieved": round(achieved, 2) if achieved else None, "peak": BF16_DENSE_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4) if achieved else None,
+                         "traffic": traffic, "avg_launch_ms": round(k_ms, 4), "launches_timed": len(kt)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,143 @@
+/*
+ * stgcn_amd.h — C-ABI of the MI355X-native ST-GCN hot path (libstgcn_amd.so).
+ *
+ * The reference (maximyudayev/Realtime-ST-GCN) has no native code and no FFI: its hot path is
+ * a stack of PyTorch aten ops inside nn.Modules.  Each entry point below replaces one or more of
+ * those aten calls; the reference call site it replaces is cited (file:line, relative to the
+ * reference root).  The Python package realtime-st-gcn_amd/ binds these with ctypes underneath
+ * modules that keep the reference's nn.Module API and state_dict names.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; device pointers unless noted; no framework types.
+ *   - Activations are the reference's logical (N, C, T, V) tensors stored channels-last:
+ *     element (n, c, t, v) at ((n*T + t)*V + v)*ld + c  ("rows" of ld >= C elements).
+ *   - dtype: 0 = fp32 (parity path), 1 = bf16 (perf path).  Accumulation is fp32.
+ *   - stream: a hipStream_t (NULL = default stream).  Every call is asynchronous.
+ *   - Return: 0 ok, 1 bad shape/arguments, 2 unsupported dtype, 3 HIP launch error.
+ *   - Thread-safety: no global mutable state; calls on different streams/devices are independent
+ *     (the reference runs replicas from nn.DataParallel threads, processor.py:32-33).
+ */
+#ifndef STGCN_AMD_H
+#define STGCN_AMD_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define STGCN_ABI_VERSION 1
+
+/* Implicit-GEMM (Kt x 1) row convolution; see conv_rows.hip for the exact contract.
+ * Replaces: nn.Conv2d tcn.2 (models/stgcn/stgcn.py:154-159), residual.0 (stgcn.py:165-170),
+ * gcn.conv (models/utils/tgcn.py:48-55,71), fcn_in/fcn_out (stgcn.py:49,74,85,95), OfflineLayer
+ * conv/residual (models/rtstgcn/rtstgcn.py:316,330) and their input-gradients (trans = 1). */
+typedef struct {
+  const void* in;
+  void* out;
+  const void* w;          /* packed [Kt][Cout_pad][Cin_pad], element type = dtype */
+  const float* bias;      /* [Cout] (bias_mode 1) | [V][Cout] (2) | [N][V][Cout] (3) | NULL */
+  const float* pro_a;     /* prologue scale [Cin] (pro 1) | LN gamma [Cin][V] (pro 2) */
+  const float* pro_b;     /* prologue shift [Cin] | LN beta [Cin][V] */
+  const float* pro_stats; /* pro 2: float2 (mean, rstd) per input frame [N*T_in] */
+  float* stats;           /* optional BN partials: float4 (count, mean, M2, 0) [row_blocks][Cout_pad] */
+  int N, T_in, T_out, V, Cin, Cout, Cin_pad, Cout_pad;
+  int Kt, stride, pad, trans, pro, bias_mode, accumulate;
+  int in_ld, out_ld;
+} stgcn_conv_desc;
+
+int stgcn_conv_rows(const stgcn_conv_desc* d, int dtype, void* stream);
+/* column tile the packed weights must be padded to (Cout_pad % tile == 0) */
+int stgcn_conv_rows_col_tile(int cout);
+/* number of row blocks (first dim of the BN partial-stat buffer) for M output rows */
+long stgcn_conv_rows_row_blocks(long M, int cout);
+
+/* Weight gradient of stgcn_conv_rows (trans = 0): dw[Kt][Cout][Cin] += ... (fp32, zeroed by caller).
+ * Replaces: convolution_backward weight path of the convs above (autograd of stgcn.py:154-170). */
+typedef struct {
+  const void* in;
+  const void* dy;
+  float* dw;
+  const float* pro_a;
+  const float* pro_b;
+  const float* pro_stats;
+  int N, T_in, T_out, V, Cin, Cout, Kt, stride, pad, pro;
+  int in_ld, dy_ld;
+  long rows_per_block; /* filled by the library */
+} stgcn_wgrad_desc;
+
+int stgcn_conv_wgrad(const stgcn_wgrad_desc* d, int dtype, void* stream);
+
+/* Graph (joint-axis) mixing of ConvTemporalGraphical (models/utils/tgcn.py:58-79), A applied first.
+ *   fwd  : XA[(n,t,w)][p*Cin+ci] = sum_v A[(n),p,v,w] x[(n,t,v)][ci]             (tgcn.py:76)
+ *   trans: dx[(n,t,v)][ci] (+)= sum_{p,w} A[(n),p,v,w] DW[(n,t,w)][p*Cin+ci]       (autograd of :76)
+ *   dA   : dA[(n),p,v,w] += sum_{t,ci} x[(n,t,v)][ci] DW[(n,t,w)][p*Cin+ci]          (grad of A)
+ *   bias : bias2d[(n),w,c] = sum_p b[p*C+c] sum_v A[(n),p,v,w]   (the conv bias pushed through A)
+ * A is fp32 [P][V][V] (shared) or [N][P][V][V] (per_sample, AAGCN models/aagcn/aagcn.py:148). */
+typedef struct {
+  const void* x;
+  void* out;
+  const float* A;
+  int N, T, V, P, Cin, per_sample, accumulate;
+  int x_ld, out_ld;
+} stgcn_amix_desc;
+
+int stgcn_amix_fwd(const stgcn_amix_desc* d, int dtype, void* stream);
+int stgcn_amix_trans(const stgcn_amix_desc* d, int dtype, void* stream);
+int stgcn_amix_dA(const stgcn_amix_desc* d, const void* dw, float* dA, int dtype, void* stream);
+int stgcn_gcn_bias(const float* A, const float* b, float* out, int N, int P, int V, int C, int per_sample,
+                   void* stream);
+
+/* BatchNorm with batch statistics (nn.BatchNorm2d(track_running_stats=False), stgcn.py:152,160,171;
+ * BatchNorm1d input norm, models/utils/batchnorm.py:13-23 viewed as [N*T][V*C]).
+ * Partials are float4 (count, mean, M2, 0) per (row block, channel); finalize merges them (fp64). */
+long stgcn_bn_stat_blocks(long M);
+int stgcn_bn_stats_partial(const void* x, int ld, long M, int C, void* part_f4, int dtype, void* stream);
+int stgcn_bn_finalize(const void* part_f4, int nblocks, int ld_part, int C, const float* gamma, const float* beta,
+                      float eps, void* mean_rstd_f2, float* scale, float* shift, void* stream);
+/* y = act(u*sc + sh + res), res_mode 0 none | 1 r | 2 r*rsc + rsh  (stgcn.py:191-193, rtstgcn.py:386-389) */
+int stgcn_bn_apply(const void* u, int ldu, const float* sc, const float* sh, int res_mode, const void* r, int ldr,
+                   const float* rsc, const float* rsh, int relu, void* y, int ldy, long M, int C, int dtype,
+                   void* stream);
+/* sums_f2[c] = (sum dz, sum dz*xhat) with dz = dy * mask (mask 0 none | 1 mref>0 | 2 mref*msc+msh>0);
+ * x may be NULL (then only sum dz).  part_f2 scratch: [stgcn_bn_stat_blocks(M)][C] float2. */
+int stgcn_bn_bwd_reduce(const void* dy, int lddy, int mask, const void* mref, int ldm, const float* msc,
+                        const float* msh, const void* x, int ldx, const void* mean_rstd_f2, long M, int C,
+                        void* part_f2, void* sums_f2, int dtype, void* stream);
+/* dx (+)= gamma*rstd*(dz - S1/M - xhat*S2/M); x == NULL: dx (+)= dz */
+int stgcn_bn_bwd_apply(const void* dy, int lddy, int mask, const void* mref, int ldm, const float* msc,
+                       const float* msh, const void* x, int ldx, const void* mean_rstd_f2, const float* gamma,
+                       const void* sums_f2, long M, int C, void* dx, int lddx, int accumulate, int dtype,
+                       void* stream);
+/* S[g][c] += sum_{m % G == g} x[m][c]  (per-joint column sums: GCN bias gradient);
+ * period > 0: per-sample S[n][g][c] over rows [n*period, (n+1)*period) (per-sample A, AAGCN). */
+int stgcn_rowgroup_sum(const void* x, int ld, long M, int C, int G, long period, float* S, int dtype, void* stream);
+
+/* Custom LayerNorm([C,1,V]) (models/utils/layernorm.py:4-28): per (n,t) frame over (C,V),
+ * unbiased variance, per-(c,v) affine. */
+int stgcn_ln_stats(const void* x, int ld, long frames, int V, int C, float eps, void* stats_f2, int dtype,
+                   void* stream);
+int stgcn_ln_apply(const void* u, int ldu, const void* st_f2, const float* g, const float* b, int res_mode,
+                   const void* r, int ldr, const void* rst_f2, const float* rg, const float* rb, int relu, void* y,
+                   int ldy, long M, int V, int C, int dtype, void* stream);
+int stgcn_ln_bwd(const void* dy, int lddy, int mask, const void* mref, int ldm, const void* x, int ldx,
+                 const void* st_f2, const float* g, const float* b, long frames, int V, int C, void* dx, int lddx,
+                 int accumulate, float* dgb, int dtype, void* stream);
+
+/* Head: F.avg_pool2d over (T,V) (stgcn.py:92) and its gradient. */
+int stgcn_pool_rows(const void* x, int ld, int N, int R, int C, void* out, int ldo, int dtype, void* stream);
+int stgcn_unpool_rows(const void* dp, int ldp, int R, int C, long M, void* dx, int ldx, int dtype, void* stream);
+
+/* RT-ST-GCN temporal aggregation (models/rtstgcn/rtstgcn.py):
+ *   box_sum : y[...,t] = sum_{i < K/S} x[..., t - i*S]  on rows (Toeplitz matmul rtstgcn.py:366-379),
+ *             trans = 1 gives its adjoint (gradient).
+ *   online  : one frame of AggregateStgcn.forward (rtstgcn.py:591-627) with device-resident FIFO. */
+int stgcn_box_sum(const void* x, int ldx, void* y, int ldy, int N, int T, int V, int C, int K, int S, int trans,
+                  int accumulate, int dtype, void* stream);
+int stgcn_rt_online_step(const void* z_f32, float* fifo, float* acc, int* idx, int C, int V, int fifo_size, int S,
+                         float* out, void* stream);
+
+int stgcn_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STGCN_AMD_H */

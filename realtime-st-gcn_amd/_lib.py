@@ -1,0 +1,129 @@
+"""ctypes binding of libstgcn_amd.so (the C-ABI declared in include/stgcn_amd.h).
+
+The library is the ONLY compute path of this package: there is no CPU or eager-PyTorch
+fallback.  If the shared object is missing, or no HIP device is visible, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libstgcn_amd.so")
+
+_ERR = {1: "bad shape/arguments", 2: "unsupported dtype", 3: "HIP launch error"}
+
+c_void_p = ctypes.c_void_p
+c_int = ctypes.c_int
+c_long = ctypes.c_long
+c_float = ctypes.c_float
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [("in_", c_void_p), ("out", c_void_p), ("w", c_void_p), ("bias", c_void_p), ("pro_a", c_void_p),
+                ("pro_b", c_void_p), ("pro_stats", c_void_p), ("stats", c_void_p)] + \
+               [(n, c_int) for n in ("N", "T_in", "T_out", "V", "Cin", "Cout", "Cin_pad", "Cout_pad", "Kt", "stride",
+                                     "pad", "trans", "pro", "bias_mode", "accumulate", "in_ld", "out_ld")]
+
+
+class WgradDesc(ctypes.Structure):
+    _fields_ = [("in_", c_void_p), ("dy", c_void_p), ("dw", c_void_p), ("pro_a", c_void_p), ("pro_b", c_void_p),
+                ("pro_stats", c_void_p)] + \
+               [(n, c_int) for n in ("N", "T_in", "T_out", "V", "Cin", "Cout", "Kt", "stride", "pad", "pro",
+                                     "in_ld", "dy_ld")] + [("rows_per_block", c_long)]
+
+
+class AmixDesc(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("out", c_void_p), ("A", c_void_p)] + \
+               [(n, c_int) for n in ("N", "T", "V", "P", "Cin", "per_sample", "accumulate", "x_ld", "out_ld")]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "stgcn_abi_version": (c_int, []),
+    "stgcn_conv_rows": (c_int, [ctypes.POINTER(ConvDesc), c_int, c_void_p]),
+    "stgcn_conv_rows_col_tile": (c_int, [c_int]),
+    "stgcn_conv_rows_row_blocks": (c_long, [c_long, c_int]),
+    "stgcn_conv_wgrad": (c_int, [ctypes.POINTER(WgradDesc), c_int, c_void_p]),
+    "stgcn_amix_fwd": (c_int, [ctypes.POINTER(AmixDesc), c_int, c_void_p]),
+    "stgcn_amix_trans": (c_int, [ctypes.POINTER(AmixDesc), c_int, c_void_p]),
+    "stgcn_amix_dA": (c_int, [ctypes.POINTER(AmixDesc), c_void_p, c_void_p, c_int, c_void_p]),
+    "stgcn_gcn_bias": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
+    "stgcn_bn_stat_blocks": (c_long, [c_long]),
+    "stgcn_bn_stats_partial": (c_int, [c_void_p, c_int, c_long, c_int, c_void_p, c_int, c_void_p]),
+    "stgcn_bn_finalize": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p,
+                                  c_void_p, c_void_p]),
+    "stgcn_bn_apply": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                               c_int, c_void_p, c_int, c_long, c_int, c_int, c_void_p]),
+    "stgcn_bn_bwd_reduce": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                                    c_void_p, c_long, c_int, c_void_p, c_void_p, c_int, c_void_p]),
+    "stgcn_bn_bwd_apply": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                                   c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p, c_int, c_int, c_int,
+                                   c_void_p]),
+    "stgcn_rowgroup_sum": (c_int, [c_void_p, c_int, c_long, c_int, c_int, c_long, c_void_p, c_int, c_void_p]),
+    "stgcn_ln_stats": (c_int, [c_void_p, c_int, c_long, c_int, c_int, c_float, c_void_p, c_int, c_void_p]),
+    "stgcn_ln_apply": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p,
+                               c_void_p, c_void_p, c_int, c_void_p, c_int, c_long, c_int, c_int, c_int, c_void_p]),
+    "stgcn_ln_bwd": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                             c_long, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "stgcn_pool_rows": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p]),
+    "stgcn_unpool_rows": (c_int, [c_void_p, c_int, c_int, c_int, c_long, c_void_p, c_int, c_int, c_void_p]),
+    "stgcn_box_sum": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                              c_int, c_int, c_void_p]),
+    "stgcn_rt_online_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                                     c_void_p]),
+}
+
+EXPORTS = tuple(_SIGS)
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load the shared object and bind every exported symbol (raises if anything is missing)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"stgcn_amd: native library not built: {path} (run __graft_entry__.build())")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)  # AttributeError if the symbol is missing
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def lib():
+    if _lib is None:
+        load_library()
+    return _lib
+
+
+def check(rc: int, name: str):
+    if rc != 0:
+        raise RuntimeError(f"stgcn_amd.{name} failed with code {rc} ({_ERR.get(rc, 'unknown')})")
+
+
+def require_device(t: torch.Tensor):
+    if not t.is_cuda:
+        raise RuntimeError("stgcn_amd ops run on the HIP device only (no CPU fallback); got a CPU tensor")
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.float32:
+        return 0
+    if dt == torch.bfloat16:
+        return 1
+    raise RuntimeError(f"stgcn_amd: unsupported dtype {dt} (fp32 or bf16)")
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()

@@ -1,0 +1,180 @@
+// extern "C" entry points of libstgcn_amd.so (declared and documented in include/stgcn_amd.h).
+// Thin validation + dispatch to the kernel launchers; no global mutable state.
+#include <hip/hip_runtime.h>
+
+#include "../../include/stgcn_amd.h"
+
+typedef stgcn_conv_desc ConvArgs;
+typedef stgcn_wgrad_desc WgradArgs;
+typedef stgcn_amix_desc AmixArgs;
+
+#define STGCN_OK 0
+#define STGCN_EBADSHAPE 1
+#define STGCN_EDTYPE 2
+
+// launchers (defined in the .hip translation units)
+int conv_rows_launch(const ConvArgs& a, int dtype, hipStream_t s);
+int conv_rows_bn_tile(int cout);
+long conv_rows_num_row_blocks(long M, int cout);
+int conv_wgrad_launch(WgradArgs a, int dtype, hipStream_t s);
+int amix_fwd_launch(const AmixArgs& a, int dtype, hipStream_t s);
+int amix_trans_launch(const AmixArgs& a, int dtype, hipStream_t s);
+int amix_dA_launch(const AmixArgs& a, const void* dw, float* dA, int dtype, hipStream_t s);
+int gcn_bias_launch(const float* A, const float* b, float* out, int N, int P, int V, int C, int per_sample,
+                    hipStream_t s);
+long norm_stats_num_blocks(long M);
+int bn_stats_partial_launch(const void* x, int ld, long M, int C, float4* part, int dtype, hipStream_t s);
+int bn_finalize_launch(const float4* part, int nb, int ldp, int C, const float* gamma, const float* beta, float eps,
+                       float2* mean_rstd, float* scale, float* shift, hipStream_t s);
+int bn_apply_launch(const void* u, int ldu, const float* sc, const float* sh, int res_mode, const void* r, int ldr,
+                    const float* rsc, const float* rsh, int relu, void* y, int ldy, long M, int C, int dtype,
+                    hipStream_t s);
+int bn_bwd_reduce_launch(const void* dy, int lddy, int mask, const void* mref, int ldm, const float* msc,
+                         const float* msh, const void* x, int ldx, const float2* mean_rstd, long M, int C,
+                         float2* part, float2* out, int dtype, hipStream_t s);
+int bn_bwd_apply_launch(const void* dy, int lddy, int mask, const void* mref, int ldm, const float* msc,
+                        const float* msh, const void* x, int ldx, const float2* mean_rstd, const float* gamma,
+                        const float2* sums, long M, int C, void* dx, int lddx, int accumulate, int dtype,
+                        hipStream_t s);
+int rowgroup_sum_launch(const void* x, int ld, long M, int C, int G, long period, float* S, int dtype,
+                        hipStream_t s);
+int ln_stats_launch(const void* x, int ld, long F, int V, int C, float eps, float2* stats, int dtype, hipStream_t s);
+int ln_apply_launch(const void* u, int ldu, const float2* st, const float* g, const float* b, int res_mode,
+                    const void* r, int ldr, const float2* rst, const float* rg, const float* rb, int relu, void* y,
+                    int ldy, long M, int V, int C, int dtype, hipStream_t s);
+int ln_bwd_launch(const void* dy, int lddy, int mask, const void* mref, int ldm, const void* x, int ldx,
+                  const float2* st, const float* g, const float* b, long F, int V, int C, void* dx, int lddx,
+                  int accumulate, float* dgb, int dtype, hipStream_t s);
+int pool_rows_launch(const void* x, int ld, int N, int R, int C, void* out, int ldo, int dtype, hipStream_t s);
+int unpool_rows_launch(const void* dp, int ldp, int R, int C, long M, void* dx, int ldx, int dtype, hipStream_t s);
+int box_sum_launch(const void* x, int ldx, void* y, int ldy, int N, int T_, int V, int C, int K, int S, int trans,
+                   int accumulate, int dtype, hipStream_t s);
+int rt_online_launch(const float* z, float* fifo, float* acc, int* idx, int C, int V, int fifo_size, int S,
+                     float* out, hipStream_t s);
+
+#define CHECK_DTYPE(dt) \
+  if ((dt) != 0 && (dt) != 1) return STGCN_EDTYPE
+#define STREAM(s) reinterpret_cast<hipStream_t>(s)
+
+extern "C" {
+
+int stgcn_abi_version(void) { return STGCN_ABI_VERSION; }
+
+int stgcn_conv_rows(const stgcn_conv_desc* d, int dtype, void* stream) {
+  CHECK_DTYPE(dtype);
+  if (!d || !d->in || !d->out || !d->w || d->N <= 0 || d->V <= 0 || d->T_in <= 0 || d->T_out <= 0 || d->Kt <= 0 ||
+      d->stride <= 0 || d->Cin <= 0 || d->Cout <= 0 || d->in_ld < d->Cin || d->out_ld < d->Cout ||
+      d->Cin_pad < d->Cin || d->Cout_pad < d->Cout)
+    return STGCN_EBADSHAPE;
+  if ((d->pro == 1 && (!d->pro_a || !d->pro_b)) || (d->pro == 2 && (!d->pro_a || !d->pro_b || !d->pro_stats)))
+    return STGCN_EBADSHAPE;
+  if (d->bias_mode && !d->bias) return STGCN_EBADSHAPE;
+  return conv_rows_launch(*d, dtype, STREAM(stream));
+}
+
+int stgcn_conv_rows_col_tile(int cout) { return conv_rows_bn_tile(cout); }
+long stgcn_conv_rows_row_blocks(long M, int cout) { return conv_rows_num_row_blocks(M, cout); }
+
+int stgcn_conv_wgrad(const stgcn_wgrad_desc* d, int dtype, void* stream) {
+  CHECK_DTYPE(dtype);
+  if (!d || !d->in || !d->dy || !d->dw || d->N <= 0 || d->Kt <= 0 || d->stride <= 0) return STGCN_EBADSHAPE;
+  if (d->pro && (!d->pro_a || !d->pro_b || (d->pro == 2 && !d->pro_stats))) return STGCN_EBADSHAPE;
+  return conv_wgrad_launch(*d, dtype, STREAM(stream));
+}
+
+int stgcn_amix_fwd(const stgcn_amix_desc* d, int dtype, void* stream) {
+  CHECK_DTYPE(dtype);
+  if (!d || !d->x || !d->out || !d->A) return STGCN_EBADSHAPE;
+  return amix_fwd_launch(*d, dtype, STREAM(stream));
+}
+int stgcn_amix_trans(const stgcn_amix_desc* d, int dtype, void* stream) {
+  CHECK_DTYPE(dtype);
+  if (!d || !d->x || !d->out || !d->A) return STGCN_EBADSHAPE;
+  return amix_trans_launch(*d, dtype, STREAM(stream));
+}
+int stgcn_amix_dA(const stgcn_amix_desc* d, const void* dw, float* dA, int dtype, void* stream) {
+  CHECK_DTYPE(dtype);
+  if (!d || !d->x || !dw || !dA) return STGCN_EBADSHAPE;
+  return amix_dA_launch(*d, dw, dA, dtype, STREAM(stream));
+}
+int stgcn_gcn_bias(const float* A, const float* b, float* out, int N, int P, int V, int C, int per_sample,
+                   void* stream) {
+  if (!A || !b || !out) return STGCN_EBADSHAPE;
+  return gcn_bias_launch(A, b, out, N, P, V, C, per_sample, STREAM(stream));
+}
+
+long stgcn_bn_stat_blocks(long M) { return norm_stats_num_blocks(M); }
+int stgcn_bn_stats_partial(const void* x, int ld, long M, int C, void* part, int dtype, void* stream) {
+  CHECK_DTYPE(dtype);
+  return bn_stats_partial_launch(x, ld, M, C, (float4*)part, dtype, STREAM(stream));
+}
+int stgcn_bn_finalize(const void* part, int nb, int ldp, int C, const float* gamma, const float* beta, float eps,
+                      void* mean_rstd, float* scale, float* shift, void* stream) {
+  return bn_finalize_launch((const float4*)part, nb, ldp, C, gamma, beta, eps, (float2*)mean_rstd, scale, shift,
+                            STREAM(stream));
+}
+int stgcn_bn_apply(const void* u, int ldu, const float* sc, const float* sh, int res_mode, const void* r, int ldr,
+                   const float* rsc, const float* rsh, int relu, void* y, int ldy, long M, int C, int dtype,
+                   void* stream) {
+  CHECK_DTYPE(dtype);
+  if (res_mode && !r) return STGCN_EBADSHAPE;
+  return bn_apply_launch(u, ldu, sc, sh, res_mode, r, ldr, rsc, rsh, relu, y, ldy, M, C, dtype, STREAM(stream));
+}
+int stgcn_bn_bwd_reduce(const void* dy, int lddy, int mask, const void* mref, int ldm, const float* msc,
+                        const float* msh, const void* x, int ldx, const void* mean_rstd, long M, int C, void* part,
+                        void* sums, int dtype, void* stream) {
+  CHECK_DTYPE(dtype);
+  return bn_bwd_reduce_launch(dy, lddy, mask, mref, ldm, msc, msh, x, ldx, (const float2*)mean_rstd, M, C,
+                              (float2*)part, (float2*)sums, dtype, STREAM(stream));
+}
+int stgcn_bn_bwd_apply(const void* dy, int lddy, int mask, const void* mref, int ldm, const float* msc,
+                       const float* msh, const void* x, int ldx, const void* mean_rstd, const float* gamma,
+                       const void* sums, long M, int C, void* dx, int lddx, int accumulate, int dtype,
+                       void* stream) {
+  CHECK_DTYPE(dtype);
+  return bn_bwd_apply_launch(dy, lddy, mask, mref, ldm, msc, msh, x, ldx, (const float2*)mean_rstd, gamma,
+                             (const float2*)sums, M, C, dx, lddx, accumulate, dtype, STREAM(stream));
+}
+int stgcn_rowgroup_sum(const void* x, int ld, long M, int C, int G, long period, float* S, int dtype,
+                       void* stream) {
+  CHECK_DTYPE(dtype);
+  return rowgroup_sum_launch(x, ld, M, C, G, period, S, dtype, STREAM(stream));
+}
+int stgcn_ln_stats(const void* x, int ld, long frames, int V, int C, float eps, void* st, int dtype, void* stream) {
+  CHECK_DTYPE(dtype);
+  return ln_stats_launch(x, ld, frames, V, C, eps, (float2*)st, dtype, STREAM(stream));
+}
+int stgcn_ln_apply(const void* u, int ldu, const void* st, const float* g, const float* b, int res_mode,
+                   const void* r, int ldr, const void* rst, const float* rg, const float* rb, int relu, void* y,
+                   int ldy, long M, int V, int C, int dtype, void* stream) {
+  CHECK_DTYPE(dtype);
+  return ln_apply_launch(u, ldu, (const float2*)st, g, b, res_mode, r, ldr, (const float2*)rst, rg, rb, relu, y, ldy,
+                         M, V, C, dtype, STREAM(stream));
+}
+int stgcn_ln_bwd(const void* dy, int lddy, int mask, const void* mref, int ldm, const void* x, int ldx,
+                 const void* st, const float* g, const float* b, long frames, int V, int C, void* dx, int lddx,
+                 int accumulate, float* dgb, int dtype, void* stream) {
+  CHECK_DTYPE(dtype);
+  return ln_bwd_launch(dy, lddy, mask, mref, ldm, x, ldx, (const float2*)st, g, b, frames, V, C, dx, lddx,
+                       accumulate, dgb, dtype, STREAM(stream));
+}
+int stgcn_pool_rows(const void* x, int ld, int N, int R, int C, void* out, int ldo, int dtype, void* stream) {
+  CHECK_DTYPE(dtype);
+  return pool_rows_launch(x, ld, N, R, C, out, ldo, dtype, STREAM(stream));
+}
+int stgcn_unpool_rows(const void* dp, int ldp, int R, int C, long M, void* dx, int ldx, int dtype, void* stream) {
+  CHECK_DTYPE(dtype);
+  return unpool_rows_launch(dp, ldp, R, C, M, dx, ldx, dtype, STREAM(stream));
+}
+int stgcn_box_sum(const void* x, int ldx, void* y, int ldy, int N, int T, int V, int C, int K, int S, int trans,
+                  int accumulate, int dtype, void* stream) {
+  CHECK_DTYPE(dtype);
+  return box_sum_launch(x, ldx, y, ldy, N, T, V, C, K, S, trans, accumulate, dtype, STREAM(stream));
+}
+int stgcn_rt_online_step(const void* z, float* fifo, float* acc, int* idx, int C, int V, int fifo_size, int S,
+                         float* out, void* stream) {
+  if (!z || !fifo || !acc || !idx || !out) return STGCN_EBADSHAPE;
+  return rt_online_launch((const float*)z, fifo, acc, idx, C, V, fifo_size, S, out, STREAM(stream));
+}
+
+}  // extern "C"

@@ -1,0 +1,600 @@
+// Normalisation, activation and reduction kernels of the ST-GCN layer (channels-last rows).
+//
+//  BatchNorm2d(C, track_running_stats=False)  (stgcn.py:152,160,171): batch statistics over
+//    all N*T*V rows even in eval(), biased variance, eps 1e-5.  Forward statistics come as
+//    (count, mean, M2) partials from the producing GEMM's epilogue (conv_rows.hip) or from
+//    bn_stats_partial; bn_finalize merges them (Chan, fp64) and emits mean/rstd and the folded
+//    affine (scale, shift) that the consumer's prologue applies.
+//  BatchNorm1d(V*C) input norm (batchnorm.py:13-23): the same kernels viewing the NTVC input as
+//    [N*T rows][V*C channels].
+//  Custom LayerNorm([C,1,V]) (layernorm.py:22-28): per-frame statistics over the V*C contiguous
+//    elements of an (n,t) frame, UNBIASED variance, per-(c,v) affine.
+//  Backward: dz = dy * relu-mask; BN: dx = g*rstd*(dz - E[dz] - xhat*E[dz*xhat]);
+//    LN: dx = rstd*(gz - mean(gz) - xhat*sum(gz*xhat)/(F-1)), gz = dz*gamma.
+#include "common.h"
+
+namespace {
+
+template <typename T, int VEC>
+DEV void ldv(const T* p, float* f) {
+  if constexpr (VEC == 1) {
+    f[0] = Tr<T>::to_f(*p);
+  } else {
+    unpack16(*reinterpret_cast<const uint4*>(p), f, (T*)nullptr);
+  }
+}
+template <typename T, int VEC>
+DEV void stv(T* p, const float* f) {
+  if constexpr (VEC == 1) {
+    *p = Tr<T>::from_f(f[0]);
+  } else {
+    *reinterpret_cast<uint4*>(p) = pack16(f, (T*)nullptr);
+  }
+}
+
+// rows per block for the channel-wise row kernels
+DEV void row_layout(int C, int VEC, int& cu_n, int& rpi) {
+  cu_n = C / VEC;
+  rpi = 256 / cu_n;
+  if (rpi < 1) rpi = 1;
+}
+
+// ------------------------------------------------------------------ BN forward statistics
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void bn_stats_partial_kernel(const T* __restrict__ x, int ld, long M, int C,
+                                                                long rpb, float4* part) {
+  __shared__ float4 red[256 * 8];
+  int CU, RPI;
+  row_layout(C, VEC, CU, RPI);
+  const int tid = threadIdx.x;
+  const int cu = tid % CU, rs = tid / CU;
+  const long mb = blockIdx.x * rpb, me = min(M, mb + rpb);
+  float k[VEC], s1[VEC], s2[VEC];
+  float n = 0.f;
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) k[j] = s1[j] = s2[j] = 0.f;
+  if (rs < RPI && cu < CU) {
+    for (long m = mb + rs; m < me; m += RPI) {
+      float f[VEC];
+      ldv<T, VEC>(x + m * ld + cu * VEC, f);
+      if (n == 0.f) {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) k[j] = f[j];
+      }
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const float d = f[j] - k[j];
+        s1[j] += d;
+        s2[j] += d * d;
+      }
+      n += 1.f;
+    }
+  }
+  // per-thread (n, mean, M2)
+  if (rs < RPI && cu < CU) {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const float mean = n > 0.f ? k[j] + s1[j] / n : 0.f;
+      const float m2 = n > 0.f ? fmaxf(s2[j] - s1[j] * s1[j] / n, 0.f) : 0.f;
+      red[rs * C + cu * VEC + j] = make_float4(n, mean, m2, 0.f);
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    Welford w = {0.f, 0.f, 0.f};
+    for (int r = 0; r < RPI; ++r) {
+      const float4 g = red[r * C + c];
+      w = welford_merge(w, Welford{g.x, g.y, g.z});
+    }
+    part[(long)blockIdx.x * C + c] = make_float4(w.n, w.mean, w.m2, 0.f);
+  }
+}
+
+// one block per channel: merge nb (count, mean, M2) partials in fp64
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float4* part, int nb, int ldp, int C,
+                                                          const float* gamma, const float* beta, float eps,
+                                                          float2* mean_rstd, float* scale, float* shift) {
+  __shared__ double sn[256], sm[256], sq[256];
+  const int c = blockIdx.x;
+  double n = 0, mean = 0, m2 = 0;
+  for (int b = threadIdx.x; b < nb; b += 256) {
+    const float4 g = part[(long)b * ldp + c];
+    const double nb_ = g.x;
+    if (nb_ == 0) continue;
+    const double tot = n + nb_;
+    const double d = g.y - mean;
+    mean += d * nb_ / tot;
+    m2 += g.z + d * d * n * nb_ / tot;
+    n = tot;
+  }
+  sn[threadIdx.x] = n;
+  sm[threadIdx.x] = mean;
+  sq[threadIdx.x] = m2;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      const double na = sn[threadIdx.x], nb2 = sn[threadIdx.x + s];
+      const double tot = na + nb2;
+      if (tot > 0) {
+        const double d = sm[threadIdx.x + s] - sm[threadIdx.x];
+        sm[threadIdx.x] += d * nb2 / tot;
+        sq[threadIdx.x] += sq[threadIdx.x + s] + d * d * na * nb2 / tot;
+        sn[threadIdx.x] = tot;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double var = sn[0] > 0 ? sq[0] / sn[0] : 0.0;  // biased (BatchNorm)
+    const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float mu = (float)sm[0];
+    mean_rstd[c] = make_float2(mu, rstd);
+    if (scale) {
+      const float g = gamma ? gamma[c] : 1.f;
+      const float b = beta ? beta[c] : 0.f;
+      scale[c] = g * rstd;
+      shift[c] = b - mu * g * rstd;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ BN apply (+res) (+ReLU)
+// y = act(u*sc + sh + res), res: 0 none | 1 r | 2 r*rsc + rsh
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ u, int ldu, const float* sc,
+                                                       const float* sh, int res_mode, const T* __restrict__ r,
+                                                       int ldr, const float* rsc, const float* rsh, int relu,
+                                                       T* __restrict__ y, int ldy, long M, int C) {
+  const int CU = C / VEC;
+  const long total = M * CU;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long m = i / CU;
+    const int c0 = (int)(i % CU) * VEC;
+    float f[VEC];
+    ldv<T, VEC>(u + m * ldu + c0, f);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) f[j] = f[j] * sc[c0 + j] + sh[c0 + j];
+    if (res_mode) {
+      float g[VEC];
+      ldv<T, VEC>(r + m * ldr + c0, g);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) f[j] += res_mode == 2 ? g[j] * rsc[c0 + j] + rsh[c0 + j] : g[j];
+    }
+    if (relu) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) f[j] = fmaxf(f[j], 0.f);
+    }
+    stv<T, VEC>(y + m * ldy + c0, f);
+  }
+}
+
+// ------------------------------------------------------------------ BN backward
+// partial sums per channel of dz and dz*xhat, dz = dy * mask.
+// mask: 0 none | 1 (mref > 0) | 2 (mref*msc + msh > 0)
+template <typename T, int VEC>
+DEV void dz_load(const T* dy, int lddy, int mask, const T* mref, int ldm, const float* msc, const float* msh,
+                 long m, int c0, float* dz) {
+  ldv<T, VEC>(dy + m * lddy + c0, dz);
+  if (mask) {
+    float g[VEC];
+    ldv<T, VEC>(mref + m * ldm + c0, g);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const float pre = mask == 1 ? g[j] : g[j] * msc[c0 + j] + msh[c0 + j];
+      if (!(pre > 0.f)) dz[j] = 0.f;
+    }
+  }
+}
+
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict__ dy, int lddy, int mask,
+                                                            const T* __restrict__ mref, int ldm, const float* msc,
+                                                            const float* msh, const T* __restrict__ x, int ldx,
+                                                            const float2* mean_rstd, long M, int C, long rpb,
+                                                            float2* part) {
+  __shared__ float2 red[256 * 8];
+  int CU, RPI;
+  row_layout(C, VEC, CU, RPI);
+  const int tid = threadIdx.x;
+  const int cu = tid % CU, rs = tid / CU;
+  const long mb = blockIdx.x * rpb, me = min(M, mb + rpb);
+  float s1[VEC], s2[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) s1[j] = s2[j] = 0.f;
+  if (rs < RPI) {
+    const int c0 = cu * VEC;
+    float mu[VEC], rsd[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const float2 st = x ? mean_rstd[c0 + j] : make_float2(0.f, 0.f);
+      mu[j] = st.x;
+      rsd[j] = st.y;
+    }
+    for (long m = mb + rs; m < me; m += RPI) {
+      float dz[VEC];
+      dz_load<T, VEC>(dy, lddy, mask, mref, ldm, msc, msh, m, c0, dz);
+      float xv[VEC];
+      if (x) ldv<T, VEC>(x + m * ldx + c0, xv);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        s1[j] += dz[j];
+        if (x) s2[j] += dz[j] * (xv[j] - mu[j]) * rsd[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) red[rs * C + c0 + j] = make_float2(s1[j], s2[j]);
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < RPI; ++r) {
+      a += red[r * C + c].x;
+      b += red[r * C + c].y;
+    }
+    part[(long)blockIdx.x * C + c] = make_float2(a, b);
+  }
+}
+
+// column sums of float2 partials -> out[c] (double accumulation), one block per channel
+__global__ __launch_bounds__(256) void sum_partials_kernel(const float2* part, int nb, int C, float2* out) {
+  __shared__ double sa[256], sb[256];
+  const int c = blockIdx.x;
+  double a = 0, b = 0;
+  for (int i = threadIdx.x; i < nb; i += 256) {
+    const float2 g = part[(long)i * C + c];
+    a += g.x;
+    b += g.y;
+  }
+  sa[threadIdx.x] = a;
+  sb[threadIdx.x] = b;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      sa[threadIdx.x] += sa[threadIdx.x + s];
+      sb[threadIdx.x] += sb[threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[c] = make_float2((float)sa[0], (float)sb[0]);
+}
+
+// dx (+)= gamma*rstd*(dz - S1/M - xhat*S2/M); with x == nullptr: dx (+)= dz (identity branch)
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ dy, int lddy, int mask,
+                                                           const T* __restrict__ mref, int ldm, const float* msc,
+                                                           const float* msh, const T* __restrict__ x, int ldx,
+                                                           const float2* mean_rstd, const float* gamma,
+                                                           const float2* sums, long M, int C, T* __restrict__ dx,
+                                                           int lddx, int accumulate) {
+  const int CU = C / VEC;
+  const long total = M * CU;
+  const float invM = 1.f / (float)M;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long m = i / CU;
+    const int c0 = (int)(i % CU) * VEC;
+    float dz[VEC];
+    dz_load<T, VEC>(dy, lddy, mask, mref, ldm, msc, msh, m, c0, dz);
+    float o[VEC];
+    if (x) {
+      float xv[VEC];
+      ldv<T, VEC>(x + m * ldx + c0, xv);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const float2 st = mean_rstd[c0 + j];
+        const float2 sm = sums[c0 + j];
+        const float g = gamma ? gamma[c0 + j] : 1.f;
+        const float xh = (xv[j] - st.x) * st.y;
+        o[j] = g * st.y * (dz[j] - sm.x * invM - xh * sm.y * invM);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) o[j] = dz[j];
+    }
+    if (accumulate) {
+      float p[VEC];
+      ldv<T, VEC>(dx + m * lddx + c0, p);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) o[j] += p[j];
+    }
+    stv<T, VEC>(dx + m * lddx + c0, o);
+  }
+}
+
+// S[g][c] += sum_{m : m % G == g} x[m][c]   (G = V: per-joint column sums for the GCN bias grad)
+// period > 0: per-sample sums S[n][g][c] over the rows [n*period, (n+1)*period) (grid.y = n).
+template <typename T>
+__global__ __launch_bounds__(256) void rowgroup_sum_kernel(const T* __restrict__ x, int ld, long M, int C, int G,
+                                                           long rpb, long period, float* S) {
+  extern __shared__ float sS[];
+  for (int i = threadIdx.x; i < G * C; i += 256) sS[i] = 0.f;
+  __syncthreads();
+  const long base = period > 0 ? (long)blockIdx.y * period : 0;
+  const long lim = period > 0 ? base + period : M;
+  const long mb = base + blockIdx.x * rpb, me = min(lim, mb + rpb);
+  const long total = me > mb ? (me - mb) * C : 0;
+  for (long i = threadIdx.x; i < total; i += 256) {
+    const long m = mb + i / C;
+    const int c = (int)(i % C);
+    atomicAdd(&sS[(int)(m % G) * C + c], Tr<T>::to_f(x[m * ld + c]));
+  }
+  __syncthreads();
+  float* dst = S + (period > 0 ? (long)blockIdx.y * G * C : 0);
+  for (int i = threadIdx.x; i < G * C; i += 256) atomicAdd(dst + i, sS[i]);
+}
+
+// ------------------------------------------------------------------ LayerNorm([C,1,V])
+// one wave per frame: frame = V rows x C channels (row stride ld)
+template <typename T>
+__global__ __launch_bounds__(256) void ln_stats_kernel(const T* __restrict__ x, int ld, long F, int V, int C,
+                                                       float eps, float2* stats) {
+  const int lane = threadIdx.x & 63;
+  const long f = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (f >= F) return;
+  const int E = V * C;
+  const T* base = x + f * V * (long)ld;
+  float s = 0.f;
+  for (int e = lane; e < E; e += 64) s += Tr<T>::to_f(base[(e / C) * (long)ld + e % C]);
+  s = wave_sum(s);
+  const float mean = s / (float)E;
+  float q = 0.f;
+  for (int e = lane; e < E; e += 64) {
+    const float d = Tr<T>::to_f(base[(e / C) * (long)ld + e % C]) - mean;
+    q += d * d;
+  }
+  q = wave_sum(q);
+  const float var = q / (float)(E - 1);  // unbiased (torch.var default, layernorm.py:24)
+  if (lane == 0) stats[f] = make_float2(mean, 1.f / sqrtf(var + eps));
+}
+
+// y = act((u-mu)*rs*g[c*V+v] + b[c*V+v] + res); res: 0 none | 1 r | 2 LN(r) with its own stats/affine
+template <typename T>
+__global__ __launch_bounds__(256) void ln_apply_kernel(const T* __restrict__ u, int ldu, const float2* st,
+                                                       const float* g, const float* b, int res_mode,
+                                                       const T* __restrict__ r, int ldr, const float2* rst,
+                                                       const float* rg, const float* rb, int relu,
+                                                       T* __restrict__ y, int ldy, long M, int V, int C) {
+  const long total = M * C;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long m = i / C;
+    const int c = (int)(i % C);
+    const int v = (int)(m % V);
+    const long f = m / V;
+    const int gi = c * V + v;
+    const float2 s = st[f];
+    float o = (Tr<T>::to_f(u[m * ldu + c]) - s.x) * s.y * g[gi] + b[gi];
+    if (res_mode == 1) o += Tr<T>::to_f(r[m * ldr + c]);
+    if (res_mode == 2) {
+      const float2 q = rst[f];
+      o += (Tr<T>::to_f(r[m * ldr + c]) - q.x) * q.y * rg[gi] + rb[gi];
+    }
+    if (relu) o = fmaxf(o, 0.f);
+    y[m * ldy + c] = Tr<T>::from_f(o);
+  }
+}
+
+// LN backward, one wave per frame.  mask: 0 none | 1 (mref > 0) | 2 (LN-output of x > 0, i.e. relu(LN(x)))
+// dgb: optional [2][C*V] accumulators for dgamma (sum dz*xhat) and dbeta (sum dz)
+template <typename T>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, int lddy, int mask,
+                                                     const T* __restrict__ mref, int ldm, const T* __restrict__ x,
+                                                     int ldx, const float2* st, const float* g, const float* b,
+                                                     long F, int V, int C, T* __restrict__ dx, int lddx,
+                                                     int accumulate, float* dgb) {
+  extern __shared__ float sg[];  // [2][C*V] per block
+  const int E = V * C;
+  for (int i = threadIdx.x; i < 2 * E; i += 256) sg[i] = 0.f;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const long f = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (f < F) {
+    const float2 s = st[f];
+    float a1 = 0.f, a2 = 0.f;
+    for (int e = lane; e < E; e += 64) {
+      const int v = e / C, c = e % C;
+      const long m = f * V + v;
+      float dz = Tr<T>::to_f(dy[m * lddy + c]);
+      const float xh = (Tr<T>::to_f(x[m * ldx + c]) - s.x) * s.y;
+      const int gi = c * V + v;
+      if (mask == 1 && !(Tr<T>::to_f(mref[m * ldm + c]) > 0.f)) dz = 0.f;
+      if (mask == 2 && !(xh * g[gi] + b[gi] > 0.f)) dz = 0.f;
+      const float gz = dz * g[gi];
+      a1 += gz;
+      a2 += gz * xh;
+      if (dgb) {
+        atomicAdd(&sg[gi], dz * xh);
+        atomicAdd(&sg[E + gi], dz);
+      }
+    }
+    a1 = wave_sum(a1);
+    a2 = wave_sum(a2);
+    const float k1 = a1 / (float)E, k2 = a2 / (float)(E - 1);
+    for (int e = lane; e < E; e += 64) {
+      const int v = e / C, c = e % C;
+      const long m = f * V + v;
+      float dz = Tr<T>::to_f(dy[m * lddy + c]);
+      const float xh = (Tr<T>::to_f(x[m * ldx + c]) - s.x) * s.y;
+      const int gi = c * V + v;
+      if (mask == 1 && !(Tr<T>::to_f(mref[m * ldm + c]) > 0.f)) dz = 0.f;
+      if (mask == 2 && !(xh * g[gi] + b[gi] > 0.f)) dz = 0.f;
+      float o = s.y * (dz * g[gi] - k1 - xh * k2);
+      T* p = dx + m * lddx + c;
+      if (accumulate) o += Tr<T>::to_f(*p);
+      *p = Tr<T>::from_f(o);
+    }
+  }
+  if (dgb) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * E; i += 256) atomicAdd(dgb + i, sg[i]);
+  }
+}
+
+// ------------------------------------------------------------------ head: global average pool
+// out[n][c] = mean_{r < R} x[(n*R + r)][c]
+template <typename T>
+__global__ __launch_bounds__(256) void pool_rows_kernel(const T* __restrict__ x, int ld, int R, int C,
+                                                        T* __restrict__ out, int ldo) {
+  __shared__ float red[256];
+  const int n = blockIdx.y;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rs = threadIdx.x >> 6;
+  float s = 0.f;
+  if (c < C)
+    for (int r = rs; r < R; r += 4) s += Tr<T>::to_f(x[((long)n * R + r) * ld + c]);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (rs == 0 && c < C) {
+    const float t = red[threadIdx.x] + red[threadIdx.x + 64] + red[threadIdx.x + 128] + red[threadIdx.x + 192];
+    out[(long)n * ldo + c] = Tr<T>::from_f(t / (float)R);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void unpool_rows_kernel(const T* __restrict__ dp, int ldp, int R, int C, long M,
+                                                          T* __restrict__ dx, int ldx) {
+  const long total = M * C;
+  const float inv = 1.f / (float)R;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long m = i / C;
+    const int c = (int)(i % C);
+    dx[m * ldx + c] = Tr<T>::from_f(Tr<T>::to_f(dp[(m / R) * ldp + c]) * inv);
+  }
+}
+
+int grid_for(long work) {
+  long g = (work + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+long rows_per_block(long M) {
+  long rpb = (M + 1023) / 1024;
+  return rpb < 64 ? 64 : rpb;
+}
+
+}  // namespace
+
+#define DISPATCH_VEC(dtype, C, ...)                                   \
+  if (dtype == 1) {                                                   \
+    typedef bf16 T;                                                   \
+    if (C % 8 == 0) { constexpr int VEC = 8; __VA_ARGS__; }           \
+    else { constexpr int VEC = 1; __VA_ARGS__; }                      \
+  } else {                                                            \
+    typedef float T;                                                  \
+    if (C % 4 == 0) { constexpr int VEC = 4; __VA_ARGS__; }           \
+    else { constexpr int VEC = 1; __VA_ARGS__; }                      \
+  }
+
+#define DISPATCH_T(dtype, ...)                  \
+  if (dtype == 1) { typedef bf16 T; __VA_ARGS__; } \
+  else { typedef float T; __VA_ARGS__; }
+
+#define RET_HIP return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP
+
+long norm_stats_num_blocks(long M) { return (M + rows_per_block(M) - 1) / rows_per_block(M); }
+
+static bool rows_fit(int C, int dtype) {  // one row of C channels must fit the 256 threads
+  const int vec = dtype == 1 ? (C % 8 == 0 ? 8 : 1) : (C % 4 == 0 ? 4 : 1);
+  return C / vec <= 256;
+}
+
+int bn_stats_partial_launch(const void* x, int ld, long M, int C, float4* part, int dtype, hipStream_t s) {
+  if (!rows_fit(C, dtype)) return STGCN_EBADSHAPE;
+  const long rpb = rows_per_block(M);
+  const int nb = (int)((M + rpb - 1) / rpb);
+  DISPATCH_VEC(dtype, C, hipLaunchKernelGGL((bn_stats_partial_kernel<T, VEC>), dim3(nb), dim3(256), 0, s,
+                                            (const T*)x, ld, M, C, rpb, part));
+  RET_HIP;
+}
+
+int bn_finalize_launch(const float4* part, int nb, int ldp, int C, const float* gamma, const float* beta, float eps,
+                       float2* mean_rstd, float* scale, float* shift, hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, s, part, nb, ldp, C, gamma, beta, eps, mean_rstd,
+                     scale, shift);
+  RET_HIP;
+}
+
+int bn_apply_launch(const void* u, int ldu, const float* sc, const float* sh, int res_mode, const void* r, int ldr,
+                    const float* rsc, const float* rsh, int relu, void* y, int ldy, long M, int C, int dtype,
+                    hipStream_t s) {
+  DISPATCH_VEC(dtype, C, hipLaunchKernelGGL((bn_apply_kernel<T, VEC>), dim3(grid_for(M * C / VEC)), dim3(256), 0, s,
+                                            (const T*)u, ldu, sc, sh, res_mode, (const T*)r, ldr, rsc, rsh, relu,
+                                            (T*)y, ldy, M, C));
+  RET_HIP;
+}
+
+int bn_bwd_reduce_launch(const void* dy, int lddy, int mask, const void* mref, int ldm, const float* msc,
+                         const float* msh, const void* x, int ldx, const float2* mean_rstd, long M, int C,
+                         float2* part, float2* out, int dtype, hipStream_t s) {
+  if (!rows_fit(C, dtype)) return STGCN_EBADSHAPE;
+  const long rpb = rows_per_block(M);
+  const int nb = (int)((M + rpb - 1) / rpb);
+  DISPATCH_VEC(dtype, C, hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, VEC>), dim3(nb), dim3(256), 0, s,
+                                            (const T*)dy, lddy, mask, (const T*)mref, ldm, msc, msh, (const T*)x,
+                                            ldx, mean_rstd, M, C, rpb, part));
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(C), dim3(256), 0, s, part, nb, C, out);
+  RET_HIP;
+}
+
+int bn_bwd_apply_launch(const void* dy, int lddy, int mask, const void* mref, int ldm, const float* msc,
+                        const float* msh, const void* x, int ldx, const float2* mean_rstd, const float* gamma,
+                        const float2* sums, long M, int C, void* dx, int lddx, int accumulate, int dtype,
+                        hipStream_t s) {
+  DISPATCH_VEC(dtype, C, hipLaunchKernelGGL((bn_bwd_apply_kernel<T, VEC>), dim3(grid_for(M * C / VEC)), dim3(256), 0,
+                                            s, (const T*)dy, lddy, mask, (const T*)mref, ldm, msc, msh, (const T*)x,
+                                            ldx, mean_rstd, gamma, sums, M, C, (T*)dx, lddx, accumulate));
+  RET_HIP;
+}
+
+int rowgroup_sum_launch(const void* x, int ld, long M, int C, int G, long period, float* S, int dtype,
+                        hipStream_t s) {
+  if ((size_t)G * C * 4 > 64 * 1024) return STGCN_EBADSHAPE;
+  if (period > 0 && (period % G || M % period)) return STGCN_EBADSHAPE;
+  const long span = period > 0 ? period : M;
+  const long nsamp = period > 0 ? M / period : 1;
+  long rpb = (span * nsamp + 511) / 512;
+  if (rpb < 256) rpb = 256;
+  const int nb = (int)((span + rpb - 1) / rpb);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(rowgroup_sum_kernel<T>, dim3(nb, (unsigned)nsamp), dim3(256), G * C * 4, s,
+                                       (const T*)x, ld, M, C, G, rpb, period, S));
+  RET_HIP;
+}
+
+int ln_stats_launch(const void* x, int ld, long F, int V, int C, float eps, float2* stats, int dtype, hipStream_t s) {
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ln_stats_kernel<T>, dim3((unsigned)((F + 3) / 4)), dim3(256), 0, s,
+                                       (const T*)x, ld, F, V, C, eps, stats));
+  RET_HIP;
+}
+
+int ln_apply_launch(const void* u, int ldu, const float2* st, const float* g, const float* b, int res_mode,
+                    const void* r, int ldr, const float2* rst, const float* rg, const float* rb, int relu, void* y,
+                    int ldy, long M, int V, int C, int dtype, hipStream_t s) {
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ln_apply_kernel<T>, dim3(grid_for(M * C)), dim3(256), 0, s, (const T*)u, ldu,
+                                       st, g, b, res_mode, (const T*)r, ldr, rst, rg, rb, relu, (T*)y, ldy, M, V, C));
+  RET_HIP;
+}
+
+int ln_bwd_launch(const void* dy, int lddy, int mask, const void* mref, int ldm, const void* x, int ldx,
+                  const float2* st, const float* g, const float* b, long F, int V, int C, void* dx, int lddx,
+                  int accumulate, float* dgb, int dtype, hipStream_t s) {
+  const size_t lds = dgb ? (size_t)2 * V * C * 4 : 0;
+  if (lds > 150 * 1024) return STGCN_EBADSHAPE;
+  DISPATCH_T(dtype, {
+    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)ln_bwd_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(ln_bwd_kernel<T>, dim3((unsigned)((F + 3) / 4)), dim3(256), lds, s, (const T*)dy, lddy, mask,
+                       (const T*)mref, ldm, (const T*)x, ldx, st, g, b, F, V, C, (T*)dx, lddx, accumulate, dgb);
+  });
+  RET_HIP;
+}
+
+int pool_rows_launch(const void* x, int ld, int N, int R, int C, void* out, int ldo, int dtype, hipStream_t s) {
+  DISPATCH_T(dtype, hipLaunchKernelGGL(pool_rows_kernel<T>, dim3((C + 63) / 64, N), dim3(256), 0, s, (const T*)x, ld,
+                                       R, C, (T*)out, ldo));
+  RET_HIP;
+}
+
+int unpool_rows_launch(const void* dp, int ldp, int R, int C, long M, void* dx, int ldx, int dtype, hipStream_t s) {
+  DISPATCH_T(dtype, hipLaunchKernelGGL(unpool_rows_kernel<T>, dim3(grid_for(M * C)), dim3(256), 0, s, (const T*)dp,
+                                       ldp, R, C, M, (T*)dx, ldx));
+  RET_HIP;
+}

@@ -1,0 +1,407 @@
+"""Forward/backward of one ST-GCN layer as a sequence of HIP kernel launches.
+
+StgcnLayer.forward (models/stgcn/stgcn.py:181-193) is
+
+    res = identity(x) | norm_r(conv1x1_s(x)) | 0
+    g   = ConvTemporalGraphical(x, A)                 tgcn.py:58-79   (1x1 conv -> @A -> sum_P)
+    u   = conv_Kt_s(relu(norm1(g)))                    stgcn.py:151-159
+    y   = relu(norm2(u) + res)                         stgcn.py:160,193
+
+with norm = BatchNorm2d(track_running_stats=False) or the custom LayerNorm([C,1,V]).
+
+Kernel schedule (forward, BatchNorm):
+  amix_fwd(x, A)                -> XA                     (A applied first, exact)
+  gcn_bias(A, b)                -> bias2d[V][C]
+  conv_rows(XA, Wg, bias2d)     -> g   + BN1 partial stats (epilogue)
+  bn_finalize                   -> scale1/shift1
+  conv_rows(g, Wt, pro=BN1+ReLU)-> u   + BN2 partial stats (prologue applies norm1+ReLU on load)
+  [conv_rows(x, Wr, s) -> r + stats ; finalize]
+  bn_finalize, bn_apply(u, +res, ReLU) -> y
+Backward mirrors it with the transposed convs (conv_rows trans=1), the m-reduction weight-grad
+kernel (conv_wgrad), the BN reduce/apply pair, amix_trans / amix_dA for the graph part.
+Everything is a HIP kernel of libstgcn_amd.so; the only torch work here is allocation, weight
+re-packing (tiny tensors) and the (P x V)-sized reshuffles of the A/bias gradients.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import native as K
+
+BN, LN = "BatchNorm", "LayerNorm"
+
+
+def _flat_ln(p):
+    """LayerNorm([C,1,V]) parameter (C,1,V) -> flat fp32 [C*V] indexed c*V+v (kernel convention)."""
+    return p.detach().reshape(-1).float().contiguous()
+
+
+class StgcnLayerFunction(torch.autograd.Function):
+    """Autograd node for the whole StgcnLayer (BN or LN variant)."""
+
+    @staticmethod
+    def forward(ctx, x, A, wg, bg, n1w, n1b, wt, bt, n2w, n2b, wr, br, nrw, nrb, cfg):
+        kt, stride, residual, norm, dtype = cfg
+        dev = x.device
+        x = K.to_rows(x, dtype)
+        N, Cin, T, V = x.shape
+        P = A.shape[-3]
+        Cout = wt.shape[0]
+        pad = (kt - 1) // 2
+        T_out = (T + 2 * pad - kt) // stride + 1
+        M1, M2 = N * T * V, N * T_out * V
+        A32 = A.detach().float().contiguous()
+        res_conv = residual and not (Cin == Cout and stride == 1)
+
+        # ---- graph convolution: g = sum_p (A_p-mix x) W_p + bias2d
+        XA = K.amix_fwd(x, A32)
+        wg3 = wg.detach().float().view(P, Cout, Cin).permute(1, 0, 2).reshape(1, Cout, P * Cin)
+        wgp, cpg, kpg = K.pack_weight(wg3, dtype)
+        bias2d = K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
+        bmode = 3 if A32.dim() == 4 else 2
+        if norm == BN:
+            st1 = torch.empty((K.row_blocks(M1, Cout), cpg, 4), dtype=torch.float32, device=dev)
+        g = K.conv_rows(XA, wgp, P * Cin, Cout, cpg, kpg, T, T, bias=bias2d, bias_mode=bmode,
+                        stats=st1 if norm == BN else None)
+        if norm == BN:
+            mr1, sc1, sh1 = K.bn_finalize(st1, st1.shape[0], cpg, Cout, n1w.detach().float(), n1b.detach().float())
+            pro1 = dict(pro=1, pro_a=sc1, pro_b=sh1)
+        else:
+            ls1 = K.ln_stats(g, N * T, V, Cout)
+            g1, b1 = _flat_ln(n1w), _flat_ln(n1b)
+            pro1 = dict(pro=2, pro_a=g1, pro_b=b1, pro_stats=ls1)
+
+        # ---- temporal conv on relu(norm1(g)) (norm applied in the prologue)
+        wt3 = wt.detach().float().squeeze(-1).permute(2, 0, 1)  # [Kt][Cout][Cin]
+        wtp, cpt, kpt = K.pack_weight(wt3, dtype)
+        if norm == BN:
+            st2 = torch.empty((K.row_blocks(M2, Cout), cpt, 4), dtype=torch.float32, device=dev)
+        u = K.conv_rows(g, wtp, Cout, Cout, cpt, kpt, T, T_out, Kt=kt, stride=stride, pad=pad,
+                        bias=bt.detach().float().contiguous(), stats=st2 if norm == BN else None,
+                        tag=f"tcn_fwd_c{Cout}" if stride == 1 else None, **pro1)
+
+        # ---- residual branch
+        r = None
+        if res_conv:
+            wr3 = wr.detach().float().view(1, Cout, Cin)
+            wrp, cpr, kpr = K.pack_weight(wr3, dtype)
+            if norm == BN:
+                str_ = torch.empty((K.row_blocks(M2, Cout), cpr, 4), dtype=torch.float32, device=dev)
+            r = K.conv_rows(x, wrp, Cin, Cout, cpr, kpr, T, T_out, Kt=1, stride=stride, pad=0,
+                            bias=br.detach().float().contiguous(), stats=str_ if norm == BN else None)
+
+        # ---- y = relu(norm2(u) + res)
+        if norm == BN:
+            mr2, sc2, sh2 = K.bn_finalize(st2, st2.shape[0], cpt, Cout, n2w.detach().float(), n2b.detach().float())
+            if res_conv:
+                mrr, scr, shr = K.bn_finalize(str_, str_.shape[0], cpr, Cout, nrw.detach().float(),
+                                              nrb.detach().float())
+                y = K.bn_apply(u, sc2, sh2, M2, Cout, res_mode=2, r=r, rsc=scr, rsh=shr)
+            else:
+                y = K.bn_apply(u, sc2, sh2, M2, Cout, res_mode=1 if residual else 0, r=x if residual else None)
+        else:
+            ls2 = K.ln_stats(u, N * T_out, V, Cout)
+            g2, b2 = _flat_ln(n2w), _flat_ln(n2b)
+            if res_conv:
+                lsr = K.ln_stats(r, N * T_out, V, Cout)
+                y = K.ln_apply(u, ls2, g2, b2, M2, V, Cout, res_mode=2, r=r, rst=lsr, rg=_flat_ln(nrw),
+                               rb=_flat_ln(nrb))
+            else:
+                y = K.ln_apply(u, ls2, g2, b2, M2, V, Cout, res_mode=1 if residual else 0,
+                               r=x if residual else None)
+
+        ctx.cfg = cfg
+        ctx.dims = (N, Cin, Cout, T, T_out, V, P, pad, res_conv)
+        ctx.packs = (cpg, kpg, cpt, kpt)
+        saved = [x, A32, XA, g, u, y, wg, bg, wt, n1w, n1b, n2w, n2b]
+        if norm == BN:
+            saved += [mr1, sc1, sh1, mr2]
+        else:
+            saved += [ls1, ls2]
+        if res_conv:
+            saved += [r, wr, nrw, nrb] + ([mrr] if norm == BN else [lsr])
+        ctx.save_for_backward(*saved)
+        ctx.in_dtype = A.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        kt, stride, residual, norm, dtype = ctx.cfg
+        N, Cin, Cout, T, T_out, V, P, pad, res_conv = ctx.dims
+        sv = list(ctx.saved_tensors)
+        x, A32, XA, g, u, y, wg, bg, wt, n1w, n1b, n2w, n2b = sv[:13]
+        rest = sv[13:]
+        if norm == BN:
+            mr1, sc1, sh1, mr2 = rest[:4]
+            rest = rest[4:]
+        else:
+            ls1, ls2 = rest[:2]
+            rest = rest[2:]
+        if res_conv:
+            r, wr, nrw, nrb, strr = rest
+        dev = x.device
+        dy = K.to_rows(dy, dtype)
+        M1, M2 = N * T * V, N * T_out * V
+        grads = {}
+
+        # ---- through relu(norm2(u) + res): dz = dy * [y > 0]
+        du = K.cl_empty(N, Cout, T_out, V, dtype, dev)
+        dx = K.cl_empty(N, Cin, T, V, dtype, dev)
+        dx_written = False
+        if norm == BN:
+            s2 = K.bn_bwd_reduce(dy, M2, Cout, mask=1, mref=y, x=u, mean_rstd=mr2)
+            K.bn_bwd_apply(dy, M2, Cout, du, mask=1, mref=y, x=u, mean_rstd=mr2, gamma=n2w.detach().float(), sums=s2)
+            grads["n2w"], grads["n2b"] = s2[:, 1].clone(), s2[:, 0].clone()
+        else:
+            dgb2 = torch.zeros((2, Cout * V), dtype=torch.float32, device=dev)
+            K.ln_bwd(dy, u, ls2, _flat_ln(n2w), _flat_ln(n2b), N * T_out, V, Cout, du, mask=1, mref=y, dgb=dgb2)
+            grads["n2w"], grads["n2b"] = dgb2[0].view(n2w.shape), dgb2[1].view(n2b.shape)
+
+        if res_conv:
+            dr = K.cl_empty(N, Cout, T_out, V, dtype, dev)
+            if norm == BN:
+                sr = K.bn_bwd_reduce(dy, M2, Cout, mask=1, mref=y, x=r, mean_rstd=strr)
+                K.bn_bwd_apply(dy, M2, Cout, dr, mask=1, mref=y, x=r, mean_rstd=strr, gamma=nrw.detach().float(),
+                               sums=sr)
+                grads["nrw"], grads["nrb"] = sr[:, 1].clone(), sr[:, 0].clone()
+            else:
+                dgbr = torch.zeros((2, Cout * V), dtype=torch.float32, device=dev)
+                K.ln_bwd(dy, r, strr, _flat_ln(nrw), _flat_ln(nrb), N * T_out, V, Cout, dr, mask=1, mref=y,
+                         dgb=dgbr)
+                grads["nrw"], grads["nrb"] = dgbr[0].view(nrw.shape), dgbr[1].view(nrb.shape)
+            # residual conv (1x1, stride s, bias): data grad (transposed), weight grad, bias grad
+            wrT = wr.detach().float().view(Cout, Cin).t().reshape(1, Cin, Cout)
+            wrTp, cq, kq = K.pack_weight(wrT, dtype)
+            K.conv_rows(dr, wrTp, Cout, Cin, cq, kq, T_out, T, Kt=1, stride=stride, pad=0, trans=True, out=dx)
+            dx_written = True
+            grads["wr"] = K.conv_wgrad(x, dr, Cin, Cout, T, T_out, Kt=1, stride=stride, pad=0).view(Cout, Cin, 1, 1)
+            grads["br"] = K.bn_bwd_reduce(dr, M2, Cout)[:, 0].clone()
+        elif residual:
+            K.bn_bwd_apply(dy, M2, Cin, dx, mask=1, mref=y)  # dx = dz
+            dx_written = True
+
+        # ---- temporal conv: dh = conv^T(du), dWt, dbt
+        wtT = wt.detach().float().squeeze(-1).permute(2, 1, 0)  # [Kt][Cin=Cout][Cout]: W[co][ci][dt] -> [dt][ci][co]
+        wtTp, cq, kq = K.pack_weight(wtT, dtype)
+        dh = K.conv_rows(du, wtTp, Cout, Cout, cq, kq, T_out, T, Kt=kt, stride=stride, pad=pad, trans=True)
+        if norm == BN:
+            pro1 = dict(pro=1, pro_a=sc1, pro_b=sh1)
+        else:
+            pro1 = dict(pro=2, pro_a=_flat_ln(n1w), pro_b=_flat_ln(n1b), pro_stats=ls1)
+        dwt = K.conv_wgrad(g, du, Cout, Cout, T, T_out, Kt=kt, stride=stride, pad=pad, **pro1)
+        grads["wt"] = dwt.permute(1, 2, 0).unsqueeze(-1)  # [Kt][co][ci] -> (co, ci, Kt, 1)
+        grads["bt"] = K.bn_bwd_reduce(du, M2, Cout)[:, 0].clone()
+
+        # ---- through relu(norm1(g))
+        dg = K.cl_empty(N, Cout, T, V, dtype, dev)
+        if norm == BN:
+            s1 = K.bn_bwd_reduce(dh, M1, Cout, mask=2, mref=g, msc=sc1, msh=sh1, x=g, mean_rstd=mr1)
+            K.bn_bwd_apply(dh, M1, Cout, dg, mask=2, mref=g, msc=sc1, msh=sh1, x=g, mean_rstd=mr1,
+                           gamma=n1w.detach().float(), sums=s1)
+            grads["n1w"], grads["n1b"] = s1[:, 1].clone(), s1[:, 0].clone()
+        else:
+            dgb1 = torch.zeros((2, Cout * V), dtype=torch.float32, device=dev)
+            K.ln_bwd(dh, g, ls1, _flat_ln(n1w), _flat_ln(n1b), N * T, V, Cout, dg, mask=2, dgb=dgb1)
+            grads["n1w"], grads["n1b"] = dgb1[0].view(n1w.shape), dgb1[1].view(n1b.shape)
+
+        # ---- graph convolution backward
+        # DW[(n,t,w)][p*Cin+ci] = sum_c dg[(n,t,w)][c] Wg[p*Cout+c][ci]
+        wgT = wg.detach().float().view(P, Cout, Cin).permute(0, 2, 1).reshape(1, P * Cin, Cout)
+        wgTp, cq, kq = K.pack_weight(wgT, dtype)
+        DW = K.conv_rows(dg, wgTp, Cout, P * Cin, cq, kq, T, T)
+        K.amix_trans(DW, A32, Cin, dx, accumulate=dx_written)
+        dA = K.amix_dA(x, DW, A32)
+        bgp = bg.detach().float().view(P, Cout)
+        # bias pushed through A: dA[p][v][w] += sum_c b_p[c] S[w][c]  (independent of v)
+        if A32.dim() == 4:
+            Sn = K.rowgroup_sum(dg, M1, Cout, V, per_sample=True)            # [N][V(w)][Cout]
+            dA += torch.einsum("pc,nwc->npw", bgp, Sn).unsqueeze(2)
+            colsum = A32.sum(dim=2)                                         # [N][P][W]
+            grads["bg"] = torch.einsum("npw,nwc->pc", colsum, Sn).reshape(-1)
+        else:
+            S = K.rowgroup_sum(dg, M1, Cout, V)                               # [V(w)][Cout]
+            dA += (bgp @ S.t()).unsqueeze(1)
+            colsum = A32.sum(dim=1)                                         # [P][W]
+            grads["bg"] = (colsum @ S).reshape(-1)
+        dwg = K.conv_wgrad(XA, dg, P * Cin, Cout, T, T, Kt=1)              # [1][Cout][P*Cin]
+        grads["wg"] = dwg.view(Cout, P, Cin).permute(1, 0, 2).reshape(P * Cout, Cin, 1, 1)
+
+        def gr(name, like):
+            v = grads.get(name)
+            if v is None or like is None or not like.requires_grad:
+                return None
+            return v.to(like.dtype).view(like.shape)
+
+        wr_, br_, nrw_, nrb_ = (wr, None, nrw, nrb) if res_conv else (None, None, None, None)
+        return (dx, dA.to(ctx.in_dtype), gr("wg", wg), gr("bg", bg), gr("n1w", n1w), gr("n1b", n1b), gr("wt", wt),
+                grads["bt"], gr("n2w", n2w), gr("n2b", n2b), gr("wr", wr_),
+                grads.get("br"), gr("nrw", nrw_), gr("nrb", nrb_), None)
+
+
+class GcnFunction(torch.autograd.Function):
+    """ConvTemporalGraphical.forward alone (models/utils/tgcn.py:58-79): conv1x1(+bias) -> @A -> sum_P."""
+
+    @staticmethod
+    def forward(ctx, x, A, wg, bg, dtype):
+        x = K.to_rows(x, dtype)
+        N, Cin, T, V = x.shape
+        P = A.shape[-3]
+        Cout = wg.shape[0] // P
+        A32 = A.detach().float().contiguous()
+        XA = K.amix_fwd(x, A32)
+        wg3 = wg.detach().float().view(P, Cout, Cin).permute(1, 0, 2).reshape(1, Cout, P * Cin)
+        wgp, cp, kp = K.pack_weight(wg3, dtype)
+        bias2d = K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
+        g = K.conv_rows(XA, wgp, P * Cin, Cout, cp, kp, T, T, bias=bias2d, bias_mode=3 if A32.dim() == 4 else 2)
+        ctx.save_for_backward(x, A32, XA, wg, bg)
+        ctx.meta = (dtype, A.dtype)
+        return g
+
+    @staticmethod
+    def backward(ctx, dg):
+        x, A32, XA, wg, bg = ctx.saved_tensors
+        dtype, adt = ctx.meta
+        N, Cin, T, V = x.shape
+        P = A32.shape[-3]
+        Cout = wg.shape[0] // P
+        dg = K.to_rows(dg, dtype)
+        M = N * T * V
+        wgT = wg.detach().float().view(P, Cout, Cin).permute(0, 2, 1).reshape(1, P * Cin, Cout)
+        wgTp, cq, kq = K.pack_weight(wgT, dtype)
+        DW = K.conv_rows(dg, wgTp, Cout, P * Cin, cq, kq, T, T)
+        dx = K.cl_empty(N, Cin, T, V, dtype, x.device)
+        K.amix_trans(DW, A32, Cin, dx, accumulate=False)
+        dA = K.amix_dA(x, DW, A32)
+        bgp = bg.detach().float().view(P, Cout)
+        if A32.dim() == 4:
+            Sn = K.rowgroup_sum(dg, M, Cout, V, per_sample=True)
+            dA += torch.einsum("pc,nwc->npw", bgp, Sn).unsqueeze(2)
+            dbg = torch.einsum("npw,nwc->pc", A32.sum(dim=2), Sn).reshape(-1)
+        else:
+            S = K.rowgroup_sum(dg, M, Cout, V)
+            dA += (bgp @ S.t()).unsqueeze(1)
+            dbg = (A32.sum(dim=1) @ S).reshape(-1)
+        dwg = K.conv_wgrad(XA, dg, P * Cin, Cout, T, T, Kt=1)
+        dwg = dwg.view(Cout, P, Cin).permute(1, 0, 2).reshape(P * Cout, Cin, 1, 1)
+        return dx, dA.to(adt), dwg.to(wg.dtype), dbg.to(bg.dtype), None
+
+
+class Conv1x1Function(torch.autograd.Function):
+    """Pointwise conv on channels-last rows (fcn_in / fcn_out, stgcn.py:49,74): y = W x + b."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, dtype):
+        x = K.to_rows(x, dtype)
+        N, Cin, T, V = x.shape
+        Cout = w.shape[0]
+        wp, cp, kp = K.pack_weight(w.detach().float().view(1, Cout, Cin), dtype)
+        y = K.conv_rows(x, wp, Cin, Cout, cp, kp, T, T, bias=b.detach().float().contiguous())
+        ctx.save_for_backward(x, w)
+        ctx.dtype = dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dtype = ctx.dtype
+        N, Cin, T, V = x.shape
+        Cout = w.shape[0]
+        dy = K.to_rows(dy, dtype)
+        wT, cq, kq = K.pack_weight(w.detach().float().view(Cout, Cin).t().reshape(1, Cin, Cout), dtype)
+        dx = K.conv_rows(dy, wT, Cout, Cin, cq, kq, T, T, trans=True)
+        dw = K.conv_wgrad(x, dy, Cin, Cout, T, T).view(Cout, Cin, 1, 1)
+        db = K.bn_bwd_reduce(dy, N * T * V, Cout)[:, 0]
+        return dx, dw.to(w.dtype), db.to(w.dtype), None
+
+
+class InputBatchNormFunction(torch.autograd.Function):
+    """BatchNorm1d(V*C) on (N, V*C, T) (models/utils/batchnorm.py:13-23): per-(v,c) batch stats over
+    (N,T).  Channels-last NTVC rows are exactly [N*T][V*C], so it is a row BatchNorm with V*C channels."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, dtype):
+        x = K.to_rows(x, dtype)
+        N, C, T, V = x.shape
+        if K.rows_ld(x) != C:
+            x = x.contiguous(memory_format=torch.channels_last)
+        F_, CV = N * T, V * C
+        part, nb, _ = K.bn_stats_partial(x, F_, CV, ld=CV)
+        # reference weight index = v*C + c == channels-last (v, c) order
+        mr, sc, sh = K.bn_finalize(part, nb, CV, CV, w.detach().float(), b.detach().float())
+        y = K.cl_empty(N, C, T, V, dtype, x.device)
+        K.bn_apply(x, sc, sh, F_, CV, relu=False, out=y, ldu=CV, ldy=CV)
+        ctx.save_for_backward(x, w, mr)
+        ctx.dtype = dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, mr = ctx.saved_tensors
+        N, C, T, V = x.shape
+        F_, CV = N * T, V * C
+        dy = K.to_rows(dy, ctx.dtype)
+        if K.rows_ld(dy) != C:
+            dy = dy.contiguous(memory_format=torch.channels_last)
+        sums = _bn_reduce_flat(dy, x, mr, F_, CV)
+        dx = K.cl_empty(N, C, T, V, ctx.dtype, x.device)
+        _bn_apply_flat(dy, x, mr, w.detach().float(), sums, F_, CV, dx)
+        return dx, sums[:, 1].to(w.dtype), sums[:, 0].to(w.dtype), None
+
+
+def _as_rows(t, F_, CV):
+    # a (F_, 1, 1, CV) contiguous buffer viewed as logical (F_, CV, 1, 1) channels-last
+    return t.permute(0, 2, 3, 1).contiguous().view(F_, 1, 1, CV).permute(0, 3, 1, 2)
+
+
+def _bn_reduce_flat(dy, x, mr, F_, CV):
+    return K.bn_bwd_reduce(_as_rows(dy, F_, CV), F_, CV, x=_as_rows(x, F_, CV), mean_rstd=mr)
+
+
+def _bn_apply_flat(dy, x, mr, gamma, sums, F_, CV, dx):
+    out = _as_rows(dx, F_, CV)
+    K.bn_bwd_apply(_as_rows(dy, F_, CV), F_, CV, out, x=_as_rows(x, F_, CV), mean_rstd=mr, gamma=gamma, sums=sums)
+    return out
+
+
+class LayerNormFunction(torch.autograd.Function):
+    """Custom LayerNorm([C,1,V]) (models/utils/layernorm.py:22-28) on channels-last rows."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, dtype):
+        x = K.to_rows(x, dtype)
+        N, C, T, V = x.shape
+        st = K.ln_stats(x, N * T, V, C)
+        y = K.ln_apply(x, st, _flat_ln(w), _flat_ln(b), N * T * V, V, C, relu=False)
+        ctx.save_for_backward(x, w, b, st)
+        ctx.dtype = dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, b, st = ctx.saved_tensors
+        N, C, T, V = x.shape
+        dy = K.to_rows(dy, ctx.dtype)
+        dx = K.cl_empty(N, C, T, V, ctx.dtype, x.device)
+        dgb = torch.zeros((2, C * V), dtype=torch.float32, device=x.device)
+        K.ln_bwd(dy, x, st, _flat_ln(w), _flat_ln(b), N * T, V, C, dx, dgb=dgb)
+        return dx, dgb[0].view(w.shape).to(w.dtype), dgb[1].view(b.shape).to(b.dtype), None
+
+
+class PoolFunction(torch.autograd.Function):
+    """F.avg_pool2d(x, x.size()[2:]) (stgcn.py:92) -> (N, C, 1, 1)."""
+
+    @staticmethod
+    def forward(ctx, x, dtype):
+        x = K.to_rows(x, dtype)
+        N, C, T, V = x.shape
+        ctx.shape = (N, C, T, V)
+        ctx.dtype = dtype
+        return K.pool_rows(x, N, T * V, C)
+
+    @staticmethod
+    def backward(ctx, dp):
+        N, C, T, V = ctx.shape
+        dp = K.to_rows(dp, ctx.dtype)
+        dx = K.cl_empty(N, C, T, V, ctx.dtype, dp.device)
+        K.unpool_rows(dp, T * V, C, N * T * V, dx)
+        return dx, None

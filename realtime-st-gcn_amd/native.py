@@ -1,0 +1,280 @@
+"""Tensor-level wrappers over the C-ABI (one function per entry point of include/stgcn_amd.h).
+
+Activations are torch tensors whose memory is channels-last rows: either logical (N, C, T, V)
+tensors in ``torch.channels_last`` format or plain contiguous (N, T, V, C) buffers.  Every
+wrapper only validates, extracts raw pointers/strides and calls the library on the current
+HIP stream; all arithmetic happens in the HIP kernels.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib as L
+
+# Optional instrumentation: callable(tag, phase) invoked right before ("start") and after ("end")
+# a tagged launch, on the launching stream (bench.py records HIP events with it).  None = off.
+EVENT_HOOK = None
+
+
+def rows_ld(t: torch.Tensor) -> int:
+    """Row stride (elements) of a logical (N,C,T,V) activation stored channels-last."""
+    if t.dim() != 4 or (t.stride(1) != 1 and t.shape[1] > 1):
+        raise RuntimeError(f"stgcn_amd: expected a channels-last (N,C,T,V) activation, strides {t.stride()}")
+    N, C, T, V = t.shape
+    if V > 1:
+        ld = t.stride(3)
+        if T > 1 and t.stride(2) != V * ld:
+            raise RuntimeError("stgcn_amd: activation rows are not evenly strided")
+        if N > 1 and t.stride(0) != T * V * ld:
+            raise RuntimeError("stgcn_amd: activation rows are not evenly strided")
+        return ld
+    if T > 1:
+        return t.stride(2)
+    return t.stride(0) if N > 1 else C
+
+
+def cl_empty(N, C, T, V, dtype, device):
+    """Logical (N,C,T,V) tensor with channels-last (rows) memory."""
+    return torch.empty((N, T, V, C), dtype=dtype, device=device).permute(0, 3, 1, 2)
+
+
+def to_rows(x: torch.Tensor, dtype) -> torch.Tensor:
+    """Make ``x`` (N,C,T,V) a channels-last tensor of ``dtype`` (no copy if already)."""
+    L.require_device(x)
+    if x.dtype != dtype:
+        x = x.to(dtype)
+    if not (x.stride(1) == 1 and x.is_contiguous(memory_format=torch.channels_last)):
+        x = x.contiguous(memory_format=torch.channels_last)
+    return x
+
+
+def col_tile(cout: int) -> int:
+    return L.lib().stgcn_conv_rows_col_tile(cout)
+
+
+def row_blocks(M: int, cout: int) -> int:
+    return L.lib().stgcn_conv_rows_row_blocks(M, cout)
+
+
+def pack_weight(w3: torch.Tensor, dtype) -> tuple:
+    """[Kt][Cout][Cin] float weight -> padded contiguous [Kt][Cout_pad][Cin_pad] of ``dtype``."""
+    Kt, Co, Ci = w3.shape
+    cp = -(-Co // col_tile(Co)) * col_tile(Co)
+    kp = -(-Ci // 32) * 32
+    out = torch.zeros((Kt, cp, kp), dtype=dtype, device=w3.device)
+    out[:, :Co, :Ci] = w3
+    return out, cp, kp
+
+
+def conv_rows(x, w3p, Cin, Cout, cp, kp, T_in, T_out, Kt=1, stride=1, pad=0, trans=False, bias=None, bias_mode=None,
+              pro=0, pro_a=None, pro_b=None, pro_stats=None, stats=None, out=None, accumulate=False, tag=None):
+    """Implicit-GEMM row conv (stgcn_conv_rows).  x rows: [N, T_in, V, Cin] (any channels-last view).
+
+    Returns ``out`` as a logical (N, Cout, T_out, V) channels-last tensor.
+    """
+    N, V = x.shape[0], x.shape[3]
+    if out is None:
+        out = cl_empty(N, Cout, T_out, V, x.dtype, x.device)
+    d = L.ConvDesc()
+    d.in_, d.out, d.w = x.data_ptr(), out.data_ptr(), w3p.data_ptr()
+    d.bias = L.ptr(bias)
+    d.pro_a, d.pro_b, d.pro_stats = L.ptr(pro_a), L.ptr(pro_b), L.ptr(pro_stats)
+    d.stats = L.ptr(stats)
+    d.N, d.T_in, d.T_out, d.V, d.Cin, d.Cout, d.Cin_pad, d.Cout_pad = N, T_in, T_out, V, Cin, Cout, kp, cp
+    d.Kt, d.stride, d.pad, d.trans, d.pro = Kt, stride, pad, int(trans), pro
+    d.bias_mode = (0 if bias is None else 1) if bias_mode is None else bias_mode
+    d.accumulate = int(accumulate)
+    d.in_ld, d.out_ld = rows_ld(x), rows_ld(out)
+    hook = EVENT_HOOK if tag is not None else None
+    if hook:
+        hook(tag, "start")
+    L.check(L.lib().stgcn_conv_rows(d, L.dtype_code(x.dtype), L.stream()), "conv_rows")
+    if hook:
+        hook(tag, "end")
+    return out
+
+
+def conv_wgrad(x, dy, Cin, Cout, T_in, T_out, Kt=1, stride=1, pad=0, pro=0, pro_a=None, pro_b=None, pro_stats=None,
+               dw=None):
+    """dw[Kt][Cout][Cin] (fp32) += weight gradient (stgcn_conv_wgrad)."""
+    N, V = x.shape[0], x.shape[3]
+    if dw is None:
+        dw = torch.zeros((Kt, Cout, Cin), dtype=torch.float32, device=x.device)
+    d = L.WgradDesc()
+    d.in_, d.dy, d.dw = x.data_ptr(), dy.data_ptr(), dw.data_ptr()
+    d.pro_a, d.pro_b, d.pro_stats = L.ptr(pro_a), L.ptr(pro_b), L.ptr(pro_stats)
+    d.N, d.T_in, d.T_out, d.V, d.Cin, d.Cout, d.Kt, d.stride, d.pad, d.pro = \
+        N, T_in, T_out, V, Cin, Cout, Kt, stride, pad, pro
+    d.in_ld, d.dy_ld = rows_ld(x), rows_ld(dy)
+    L.check(L.lib().stgcn_conv_wgrad(d, L.dtype_code(x.dtype), L.stream()), "conv_wgrad")
+    return dw
+
+
+def _amix_desc(x, out, A, N, T, V, P, Cin, accumulate=False, x_ld=None, out_ld=None):
+    d = L.AmixDesc()
+    d.x, d.out, d.A = x.data_ptr(), L.ptr(out), A.data_ptr()
+    d.N, d.T, d.V, d.P, d.Cin = N, T, V, P, Cin
+    d.per_sample = int(A.dim() == 4)
+    d.accumulate = int(accumulate)
+    d.x_ld = x_ld if x_ld is not None else rows_ld(x)
+    d.out_ld = out_ld if out_ld is not None else (rows_ld(out) if out is not None else 0)
+    return d
+
+
+def amix_fwd(x, A):
+    """XA (N, P*Cin, T, V) channels-last = A-mix of x (stgcn_amix_fwd)."""
+    N, Cin, T, V = x.shape
+    P = A.shape[-3]
+    out = cl_empty(N, P * Cin, T, V, x.dtype, x.device)
+    d = _amix_desc(x, out, A, N, T, V, P, Cin)
+    L.check(L.lib().stgcn_amix_fwd(d, L.dtype_code(x.dtype), L.stream()), "amix_fwd")
+    return out
+
+
+def amix_trans(dw, A, Cin, out, accumulate):
+    """out (N,Cin,T,V) (+)= A^T-mix of DW (N, P*Cin, T, V) (stgcn_amix_trans)."""
+    N, _, T, V = dw.shape
+    P = A.shape[-3]
+    d = _amix_desc(dw, out, A, N, T, V, P, Cin, accumulate)
+    L.check(L.lib().stgcn_amix_trans(d, L.dtype_code(dw.dtype), L.stream()), "amix_trans")
+    return out
+
+
+def amix_dA(x, dw, A):
+    """dA (fp32, shape of A) = sum x (x) DW (stgcn_amix_dA)."""
+    N, Cin, T, V = x.shape
+    P = A.shape[-3]
+    dA = torch.zeros(A.shape, dtype=torch.float32, device=x.device)
+    d = _amix_desc(x, None, A, N, T, V, P, Cin)
+    L.check(L.lib().stgcn_amix_dA(d, dw.data_ptr(), dA.data_ptr(), L.dtype_code(x.dtype), L.stream()), "amix_dA")
+    return dA
+
+
+def gcn_bias(A, b, N, C):
+    """bias2d [V, C] (shared A) or [N, V, C] (per-sample A) = sum_p b_p * colsum(A_p)."""
+    P, V = A.shape[-3], A.shape[-1]
+    per = A.dim() == 4
+    out = torch.empty(((N,) if per else ()) + (V, C), dtype=torch.float32, device=A.device)
+    L.check(L.lib().stgcn_gcn_bias(A.data_ptr(), b.data_ptr(), out.data_ptr(), N, P, V, C, int(per), L.stream()),
+            "gcn_bias")
+    return out
+
+
+# ------------------------------------------------------------------------------------ BatchNorm
+def bn_stat_blocks(M: int) -> int:
+    return L.lib().stgcn_bn_stat_blocks(M)
+
+
+def bn_stats_partial(x, M, C, ld=None):
+    nb = bn_stat_blocks(M)
+    part = torch.empty((nb, C, 4), dtype=torch.float32, device=x.device)
+    L.check(L.lib().stgcn_bn_stats_partial(x.data_ptr(), ld or rows_ld(x), M, C, part.data_ptr(),
+                                           L.dtype_code(x.dtype), L.stream()), "bn_stats_partial")
+    return part, nb, C
+
+
+def bn_finalize(part, nb, ld_part, C, gamma, beta, eps=1e-5):
+    dev = part.device
+    mr = torch.empty((C, 2), dtype=torch.float32, device=dev)
+    sc = torch.empty(C, dtype=torch.float32, device=dev)
+    sh = torch.empty(C, dtype=torch.float32, device=dev)
+    L.check(L.lib().stgcn_bn_finalize(part.data_ptr(), nb, ld_part, C, L.ptr(gamma), L.ptr(beta), eps, mr.data_ptr(),
+                                      sc.data_ptr(), sh.data_ptr(), L.stream()), "bn_finalize")
+    return mr, sc, sh
+
+
+def bn_apply(u, sc, sh, M, C, res_mode=0, r=None, rsc=None, rsh=None, relu=True, out=None, ldu=None, ldy=None):
+    if out is None:
+        out = torch.empty_like(u)
+    L.check(L.lib().stgcn_bn_apply(u.data_ptr(), ldu or rows_ld(u), sc.data_ptr(), sh.data_ptr(), res_mode, L.ptr(r),
+                                   rows_ld(r) if r is not None else 0, L.ptr(rsc), L.ptr(rsh), int(relu),
+                                   out.data_ptr(), ldy or rows_ld(out), M, C, L.dtype_code(u.dtype), L.stream()),
+            "bn_apply")
+    return out
+
+
+def bn_bwd_reduce(dy, M, C, mask=0, mref=None, msc=None, msh=None, x=None, mean_rstd=None, lddy=None):
+    nb = bn_stat_blocks(M)
+    part = torch.empty((nb, C, 2), dtype=torch.float32, device=dy.device)
+    sums = torch.empty((C, 2), dtype=torch.float32, device=dy.device)
+    L.check(L.lib().stgcn_bn_bwd_reduce(dy.data_ptr(), lddy or rows_ld(dy), mask, L.ptr(mref),
+                                        rows_ld(mref) if mref is not None else 0, L.ptr(msc), L.ptr(msh), L.ptr(x),
+                                        rows_ld(x) if x is not None else 0, L.ptr(mean_rstd), M, C, part.data_ptr(),
+                                        sums.data_ptr(), L.dtype_code(dy.dtype), L.stream()), "bn_bwd_reduce")
+    return sums
+
+
+def bn_bwd_apply(dy, M, C, out, mask=0, mref=None, msc=None, msh=None, x=None, mean_rstd=None, gamma=None,
+                 sums=None, accumulate=False, lddy=None):
+    L.check(L.lib().stgcn_bn_bwd_apply(dy.data_ptr(), lddy or rows_ld(dy), mask, L.ptr(mref),
+                                       rows_ld(mref) if mref is not None else 0, L.ptr(msc), L.ptr(msh), L.ptr(x),
+                                       rows_ld(x) if x is not None else 0, L.ptr(mean_rstd), L.ptr(gamma),
+                                       L.ptr(sums), M, C, out.data_ptr(), rows_ld(out), int(accumulate),
+                                       L.dtype_code(dy.dtype), L.stream()), "bn_bwd_apply")
+    return out
+
+
+def rowgroup_sum(x, M, C, G, per_sample=False):
+    """[G][C] (or [N][G][C] per sample) sums of rows grouped by m % G."""
+    N = x.shape[0]
+    S = torch.zeros(((N,) if per_sample else ()) + (G, C), dtype=torch.float32, device=x.device)
+    period = M // N if per_sample else 0
+    L.check(L.lib().stgcn_rowgroup_sum(x.data_ptr(), rows_ld(x), M, C, G, period, S.data_ptr(),
+                                       L.dtype_code(x.dtype), L.stream()), "rowgroup_sum")
+    return S
+
+
+# ------------------------------------------------------------------------------------ LayerNorm
+def ln_stats(x, frames, V, C, eps=1e-5):
+    st = torch.empty((frames, 2), dtype=torch.float32, device=x.device)
+    L.check(L.lib().stgcn_ln_stats(x.data_ptr(), rows_ld(x), frames, V, C, eps, st.data_ptr(),
+                                   L.dtype_code(x.dtype), L.stream()), "ln_stats")
+    return st
+
+
+def ln_apply(u, st, g, b, M, V, C, res_mode=0, r=None, rst=None, rg=None, rb=None, relu=True, out=None):
+    if out is None:
+        out = torch.empty_like(u)
+    L.check(L.lib().stgcn_ln_apply(u.data_ptr(), rows_ld(u), st.data_ptr(), g.data_ptr(), b.data_ptr(), res_mode,
+                                   L.ptr(r), rows_ld(r) if r is not None else 0, L.ptr(rst), L.ptr(rg), L.ptr(rb),
+                                   int(relu), out.data_ptr(), rows_ld(out), M, V, C, L.dtype_code(u.dtype),
+                                   L.stream()), "ln_apply")
+    return out
+
+
+def ln_bwd(dy, x, st, g, b, frames, V, C, out, mask=0, mref=None, accumulate=False, dgb=None):
+    L.check(L.lib().stgcn_ln_bwd(dy.data_ptr(), rows_ld(dy), mask, L.ptr(mref),
+                                 rows_ld(mref) if mref is not None else 0, x.data_ptr(), rows_ld(x), st.data_ptr(),
+                                 g.data_ptr(), b.data_ptr(), frames, V, C, out.data_ptr(), rows_ld(out),
+                                 int(accumulate), L.ptr(dgb), L.dtype_code(dy.dtype), L.stream()), "ln_bwd")
+    return out
+
+
+# ------------------------------------------------------------------------------------ head / RT
+def pool_rows(x, N, R, C):
+    """(N, C, 1, 1) channels-last mean over the R = T*V rows of each sample."""
+    out = cl_empty(N, C, 1, 1, x.dtype, x.device)
+    L.check(L.lib().stgcn_pool_rows(x.data_ptr(), rows_ld(x), N, R, C, out.data_ptr(), C, L.dtype_code(x.dtype),
+                                    L.stream()), "pool_rows")
+    return out
+
+
+def unpool_rows(dp, R, C, M, out):
+    L.check(L.lib().stgcn_unpool_rows(dp.data_ptr(), rows_ld(dp), R, C, M, out.data_ptr(), rows_ld(out),
+                                      L.dtype_code(dp.dtype), L.stream()), "unpool_rows")
+    return out
+
+
+def box_sum(x, K, S, trans=False, out=None, accumulate=False):
+    N, C, T, V = x.shape
+    if out is None:
+        out = cl_empty(N, C, T, V, x.dtype, x.device)
+    L.check(L.lib().stgcn_box_sum(x.data_ptr(), rows_ld(x), out.data_ptr(), rows_ld(out), N, T, V, C, K, S, int(trans),
+                                  int(accumulate), L.dtype_code(x.dtype), L.stream()), "box_sum")
+    return out
+
+
+def rt_online_step(z, fifo, acc, idx, C, V, fifo_size, S, out):
+    L.check(L.lib().stgcn_rt_online_step(z.data_ptr(), fifo.data_ptr(), acc.data_ptr(), idx.data_ptr(), C, V,
+                                         fifo_size, S, out.data_ptr(), L.stream()), "rt_online_step")
+    return out

@@ -1,0 +1,73 @@
+"""ST-GCN classifier (models/stgcn/stgcn.py:8-101) on the HIP kernels.
+
+``Model(**arch)`` takes the reference's ``arch`` config dict (+ injected ``graph`` and
+``num_classes``, processor.py:164-166); ``rank`` is accepted and ignored like in the reference.
+state_dict keys are identical (``A``, ``norm_in.*``, ``fcn_in.*``, ``gcn_networks.i.*``,
+``edge_importance.i``, ``fcn_out.*``).  forward(x (N, C, T, V)) -> (N, num_classes, 1).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import layer_fn as LF
+from .graph import Graph
+from .modules import BatchNorm1d, LayerNorm, StgcnLayer, resolve_dtype
+
+IN_PAD = 8  # fcn_in input channels are zero-padded to one 16-byte unit (kernel vector width)
+
+
+class Model(nn.Module):
+    def __init__(self, rank=None, **kwargs):
+        super().__init__()
+        conf = kwargs["st-gcn"]
+        self.graph = Graph(strategy=kwargs["strategy"], **kwargs["graph"])
+        A = torch.tensor(self.graph.A, dtype=torch.float32, requires_grad=False)
+        self.register_buffer("A", A)
+        kernel_size = (conf["kernel"], kwargs["graph"]["num_node"])
+        self.normalization = kwargs["normalization"]
+        self.norm_in = (LayerNorm([kwargs["in_feat"], 1, A.size(1)]) if kwargs["normalization"] == "LayerNorm"
+                        else BatchNorm1d(kwargs["in_feat"] * A.size(1), track_running_stats=False))
+        self.fcn_in = nn.Conv2d(in_channels=conf["in_feat"], out_channels=conf["in_ch"][0], kernel_size=1)
+        self.gcn_networks = nn.ModuleList([
+            StgcnLayer(in_channels=conf["in_ch"][i], out_channels=conf["out_ch"][i], kernel_size=kernel_size,
+                       partitions=A.size(0), num_joints=A.size(1), stride=conf["stride"][i],
+                       residual=not not conf["residual"][i], dropout=conf["dropout"][i],
+                       normalization=kwargs["normalization"])
+            for i in range(conf["layers"])])
+        if conf["importance"]:
+            self.edge_importance = nn.ParameterList([nn.Parameter(torch.ones(self.A.size()))
+                                                     for _ in self.gcn_networks])
+        else:
+            self.edge_importance = [1] * len(self.gcn_networks)
+        self.fcn_out = nn.Conv2d(conf["out_ch"][-1], out_channels=kwargs["num_classes"], kernel_size=1)
+        self.compute_dtype = torch.float32
+
+    def set_compute_dtype(self, dtype):
+        """fp32 (parity) or bf16 (perf) arithmetic for every layer; the input norm stays fp32."""
+        dt = resolve_dtype(dtype)
+        self.compute_dtype = dt
+        for layer in self.gcn_networks:
+            for m in layer.modules():
+                if hasattr(m, "compute_dtype"):
+                    m.compute_dtype = dt
+        return self
+
+    def forward(self, x):
+        x = self.norm_in(x)                                          # stgcn.py:82 (fp32)
+        C = x.shape[1]
+        if C % IN_PAD:
+            x = F.pad(x.permute(0, 2, 3, 1), (0, IN_PAD - C % IN_PAD)).permute(0, 3, 1, 2)
+            w = F.pad(self.fcn_in.weight, (0, 0, 0, 0, 0, IN_PAD - C % IN_PAD))
+        else:
+            w = self.fcn_in.weight
+        x = LF.Conv1x1Function.apply(x, w, self.fcn_in.bias, self.compute_dtype)   # stgcn.py:85
+        for gcn, importance in zip(self.gcn_networks, self.edge_importance):       # stgcn.py:88-89
+            x = gcn(x, self.A * importance)
+        x = LF.PoolFunction.apply(x, self.compute_dtype)                            # stgcn.py:92
+        x = LF.Conv1x1Function.apply(x, self.fcn_out.weight, self.fcn_out.bias, self.compute_dtype)  # :95
+        return x.squeeze(-1).float()                                                # :97
+
+    def prepare_benchmark(self, arch_conf):
+        return arch_conf

@@ -1,0 +1,76 @@
+"""CPU-side checks (no GPU): the C-ABI library loads and exports every symbol include/stgcn_amd.h
+declares, the host-side Graph matches the reference's, modules keep the reference's API and
+state_dict layout, and the product refuses to run without the HIP device (no CPU fallback)."""
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT, load_golden
+
+
+def test_header_symbols_exported(pkg):
+    hdr = open(f"{ROOT}/include/stgcn_amd.h").read()
+    declared = set(re.findall(r"^\s*(?:int|long)\s+(stgcn_\w+)\s*\(", hdr, flags=re.M))
+    assert declared, "no declarations parsed"
+    lib = pkg._lib.load_library()
+    for name in declared:
+        assert hasattr(lib, name), f"{name} declared but not exported"
+    assert declared == set(pkg._lib.EXPORTS), "ctypes binding and header disagree"
+    assert lib.stgcn_abi_version() == 1
+
+
+def test_abi_rejects_bad_args_without_gpu(pkg):
+    L = pkg._lib
+    lib = L.load_library()
+    d = L.ConvDesc()  # all-null descriptor: validated on the host, no launch
+    assert lib.stgcn_conv_rows(d, 0, None) == 1
+    assert lib.stgcn_conv_rows(d, 7, None) == 2
+    assert lib.stgcn_conv_rows_col_tile(64) == 64 and lib.stgcn_conv_rows_col_tile(256) == 128
+
+
+@pytest.mark.parametrize("key,name", [("pku_mmd", "pku-mmd"), ("ntu_rgbpd", "ntu"), ("openpose", "op"),
+                                      ("coco", "coco"), ("imu_fogit_ABCD", "imu"), ("hugadb", "hugadb")])
+def test_graph_golden(pkg, key, name):
+    g = np.load(f"{ROOT}/tests/golden/graphs.npz")
+    V, center = g["meta/" + key]
+    edge = g["edge/" + key].tolist()
+    G = pkg.Graph(int(V), edge, int(center))
+    np.testing.assert_allclose(G.A, g["A/" + key], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(G.get_adjacency_raw(), g["Araw/" + key], rtol=0, atol=0)
+    for strat in ("distance", "uniform"):
+        np.testing.assert_allclose(pkg.Graph(int(V), edge, int(center), strategy=strat).A,
+                                   g["A_%s/%s" % (strat, key)], rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("case", ["stgcn_bn_1layer", "stgcn_bn_9layer_narrow", "stgcn_ln_9layer_narrow_k69"])
+def test_model_state_dict_layout(pkg, case):
+    d = load_golden("model_" + case)
+    m = pkg.MODELS["st-gcn"](rank=None, **d["arch"])
+    ref_keys = {k[3:]: v.shape for k, v in d.items() if k.startswith("sd/")}
+    ours = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    assert set(ours) == set(ref_keys)
+    for k, s in ref_keys.items():
+        assert ours[k] == tuple(s), k
+    m.load_state_dict({k[3:]: v for k, v in d.items() if k.startswith("sd/")}, strict=True)
+
+
+def test_config2_model_size(pkg):
+    arch = {"strategy": "spatial", "graph": pkg.PKU_MMD, "in_feat": 3, "normalization": "BatchNorm",
+            "num_classes": 52, "st-gcn": {"in_feat": 3, "layers": 9, "kernel": 9, "importance": True,
+                                           "in_ch": [64, 64, 64, 64, 128, 128, 128, 256, 256],
+                                           "out_ch": [64, 64, 64, 128, 128, 128, 256, 256, 256],
+                                           "stride": [1, 1, 1, 2, 1, 1, 2, 1, 1], "residual": [1] * 9,
+                                           "dropout": [0] * 9}}
+    m = pkg.MODELS["st-gcn"](rank=None, **arch)
+    # as_is ST-GCN = 3 057 205 fp32 params, 96 state_dict keys
+    assert sum(p.numel() for p in m.parameters()) == 3057205
+    assert len(m.state_dict()) == 96
+
+
+def test_no_cpu_fallback(pkg):
+    layer = pkg.StgcnLayer(8, 8, (9, 25), 3, 25, normalization="BatchNorm")
+    A = torch.tensor(pkg.Graph(**pkg.PKU_MMD).A, dtype=torch.float32)
+    with pytest.raises(RuntimeError, match="HIP device only"):
+        layer(torch.randn(1, 8, 4, 25), A)

@@ -1,0 +1,171 @@
+"""Kernel-level numerics on the MI355X: each HIP entry point vs a plain PyTorch fp32 reference of
+the same op (fp32 path: 1e-4 relative; bf16 path: 2e-2 relative).  Calls go through the C-ABI."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import assert_close
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def K(pkg):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return pkg.native
+
+
+def cl(x, dtype=torch.float32):
+    return x.to(DEV, dtype).contiguous(memory_format=torch.channels_last)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 2e-2)])
+@pytest.mark.parametrize("cin,cout,kt,stride,T", [(64, 64, 9, 1, 37), (32, 128, 9, 2, 30), (16, 24, 1, 1, 11),
+                                                  (128, 256, 9, 1, 12), (8, 64, 1, 1, 5), (64, 52, 1, 1, 1),
+                                                  (24, 48, 9, 2, 11), (768, 256, 1, 1, 9), (256, 768, 1, 1, 9),
+                                                  (256, 256, 9, 1, 10), (4, 8, 9, 2, 9)])
+def test_conv_rows_fwd_and_trans(K, dtype, tol, cin, cout, kt, stride, T):
+    torch.manual_seed(0)
+    N, V = 3, 25
+    pad = (kt - 1) // 2
+    x = torch.randn(N, cin, T, V)
+    w = torch.randn(cout, cin, kt, 1) / (cin * kt) ** 0.5
+    b = torch.randn(cout)
+    ref = F.conv2d(x, w, b, stride=(stride, 1), padding=(pad, 0))
+    T_out = ref.shape[2]
+    wp, cp, kp = K.pack_weight(w.squeeze(-1).permute(2, 0, 1).to(DEV), dtype)
+    y = K.conv_rows(cl(x, dtype), wp, cin, cout, cp, kp, T, T_out, Kt=kt, stride=stride, pad=pad,
+                    bias=b.to(DEV))
+    assert_close(y.float(), ref, tol, "conv fwd")
+    # transposed (data gradient)
+    dy = torch.randn(ref.shape)
+    xr = x.clone().requires_grad_(True)
+    F.conv2d(xr, w, b, stride=(stride, 1), padding=(pad, 0)).backward(dy)
+    wtp, cq, kq = K.pack_weight(w.squeeze(-1).permute(2, 1, 0).to(DEV), dtype)
+    dx = K.conv_rows(cl(dy, dtype), wtp, cout, cin, cq, kq, T_out, T, Kt=kt, stride=stride, pad=pad, trans=True)
+    assert_close(dx.float(), xr.grad, tol, "conv trans")
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 2e-2)])
+@pytest.mark.parametrize("cin,cout,kt,stride,T", [(64, 64, 9, 1, 37), (32, 128, 9, 2, 30), (16, 24, 1, 1, 11),
+                                                  (128, 64, 9, 1, 12), (24, 48, 9, 2, 11)])
+def test_conv_wgrad(K, dtype, tol, cin, cout, kt, stride, T):
+    torch.manual_seed(1)
+    N, V = 3, 25
+    pad = (kt - 1) // 2
+    x = torch.randn(N, cin, T, V)
+    w = (torch.randn(cout, cin, kt, 1) / (cin * kt) ** 0.5).requires_grad_(True)
+    y = F.conv2d(x, w, None, stride=(stride, 1), padding=(pad, 0))
+    dy = torch.randn(y.shape)
+    y.backward(dy)
+    dw = K.conv_wgrad(cl(x, dtype), cl(dy, dtype), cin, cout, T, y.shape[2], Kt=kt, stride=stride, pad=pad)
+    assert_close(dw.cpu().permute(1, 2, 0).unsqueeze(-1), w.grad, tol, "wgrad")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_conv_prologue_bn_relu_and_stats(K, dtype):
+    torch.manual_seed(2)
+    N, C, T, V = 2, 64, 20, 25
+    x = torch.randn(N, C, T, V) * 2 + 1
+    sc, sh = torch.rand(C) + 0.5, torch.randn(C)
+    w = torch.randn(C, C, 9, 1) / 24
+    b = torch.randn(C)
+    h = torch.relu(x * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1))
+    ref = F.conv2d(h, w, b, padding=(4, 0))
+    wp, cp, kp = K.pack_weight(w.squeeze(-1).permute(2, 0, 1).to(DEV), dtype)
+    st = torch.empty((K.row_blocks(N * T * V, C), cp, 4), device=DEV)
+    y = K.conv_rows(cl(x, dtype), wp, C, C, cp, kp, T, T, Kt=9, pad=4, bias=b.to(DEV), pro=1, pro_a=sc.to(DEV),
+                    pro_b=sh.to(DEV), stats=st)
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    assert_close(y.float(), ref, tol, "conv+prologue")
+    mr, _, _ = K.bn_finalize(st, st.shape[0], cp, C, None, None)
+    yr = y.float().cpu()
+    mean = yr.mean(dim=(0, 2, 3))
+    var = yr.var(dim=(0, 2, 3), unbiased=False)
+    # stats come from the fp32 accumulators (before the bf16 rounding of the stored output)
+    stol = 1e-4 if dtype == torch.float32 else 2e-3
+    assert_close(mr[:, 0].cpu(), mean, stol, "bn mean")
+    assert_close(mr[:, 1].cpu(), 1 / torch.sqrt(var + 1e-5), stol, "bn rstd")
+
+
+@pytest.mark.parametrize("C", [16, 64, 256, 4])
+@pytest.mark.parametrize("per_sample", [False, True])
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 2e-2)])
+def test_amix(K, per_sample, dtype, tol, C):
+    torch.manual_seed(3)
+    N, T, V, P = 2, 7, 25, 3
+    x = torch.randn(N, C, T, V)
+    A = torch.randn((N, P, V, V) if per_sample else (P, V, V))
+    xa = torch.einsum("nctv,npvw->npctw", x, A) if per_sample else torch.einsum("nctv,pvw->npctw", x, A)
+    got = K.amix_fwd(cl(x, dtype), A.to(DEV).contiguous())
+    assert_close(got.float().cpu().reshape(N, P, C, T, V), xa, tol, "amix fwd")
+    dw = torch.randn(N, P, C, T, V)
+    dw_cl = cl(dw.reshape(N, P * C, T, V), dtype)
+    dx = K.cl_empty(N, C, T, V, dtype, DEV)
+    K.amix_trans(dw_cl, A.to(DEV).contiguous(), C, dx, accumulate=False)
+    ref_dx = torch.einsum("npctw,npvw->nctv", dw, A) if per_sample else torch.einsum("npctw,pvw->nctv", dw, A)
+    assert_close(dx.float().cpu(), ref_dx, tol, "amix trans")
+    dA = K.amix_dA(cl(x, dtype), dw_cl, A.to(DEV).contiguous())
+    ref_dA = torch.einsum("nctv,npctw->npvw", x, dw)
+    if not per_sample:
+        ref_dA = ref_dA.sum(0)
+    assert_close(dA.cpu(), ref_dA, tol, "amix dA")
+
+
+def test_bn_kernels(K):
+    torch.manual_seed(4)
+    M, C = 5000, 64
+    u = torch.randn(1, C, M, 1) * 3 + 2
+    part, nb, _ = K.bn_stats_partial(cl(u), M, C)
+    g, b = torch.rand(C) + 0.5, torch.randn(C)
+    mr, sc, sh = K.bn_finalize(part, nb, C, C, g.to(DEV), b.to(DEV))
+    ur = u.clone().requires_grad_(True)
+    y = torch.relu(F.batch_norm(ur, None, None, g, b, training=True))
+    dy = torch.randn(y.shape)
+    y.backward(dy)
+    yg = K.bn_apply(cl(u), sc, sh, M, C, relu=True)
+    assert_close(yg.cpu(), y, 1e-5, "bn apply")
+    sums = K.bn_bwd_reduce(cl(dy), M, C, mask=1, mref=yg, x=cl(u), mean_rstd=mr)
+    dx = K.cl_empty(1, C, M, 1, torch.float32, DEV)
+    K.bn_bwd_apply(cl(dy), M, C, dx, mask=1, mref=yg, x=cl(u), mean_rstd=mr, gamma=g.to(DEV), sums=sums)
+    assert_close(dx.cpu(), ur.grad, 1e-4, "bn bwd")
+
+
+def test_ln_kernels(K):
+    torch.manual_seed(5)
+    N, C, T, V = 3, 16, 9, 25
+    x = torch.randn(N, C, T, V) * 2 - 1
+    w, b = torch.rand(C, 1, V) + 0.5, torch.randn(C, 1, V) * 0.1
+    xr = x.clone().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    mean = xr.mean(dim=(1, 3), keepdim=True)
+    var = xr.var(dim=(1, 3), keepdim=True)
+    y = torch.relu(wr * (xr - mean) / torch.sqrt(var + 1e-5) + br)
+    dy = torch.randn(y.shape)
+    y.backward(dy)
+    st = K.ln_stats(cl(x), N * T, V, C)
+    yg = K.ln_apply(cl(x), st, w.reshape(-1).to(DEV), b.reshape(-1).to(DEV), N * T * V, V, C, relu=True)
+    assert_close(yg.cpu(), y, 1e-5, "ln fwd")
+    dx = K.cl_empty(N, C, T, V, torch.float32, DEV)
+    dgb = torch.zeros(2, C * V, device=DEV)
+    K.ln_bwd(cl(dy), cl(x), st, w.reshape(-1).to(DEV), b.reshape(-1).to(DEV), N * T, V, C, dx, mask=2, dgb=dgb)
+    assert_close(dx.cpu(), xr.grad, 1e-4, "ln dx")
+    assert_close(dgb[0].cpu().view(C, 1, V), wr.grad, 1e-4, "ln dgamma")
+    assert_close(dgb[1].cpu().view(C, 1, V), br.grad, 1e-4, "ln dbeta")
+
+
+def test_box_sum(K):
+    torch.manual_seed(6)
+    N, C, T, V = 2, 8, 30, 25
+    x = torch.randn(N, C, T, V)
+    for Kt, S in ((9, 1), (9, 2)):
+        ref = torch.zeros_like(x)
+        for i in range(Kt // S):
+            ref[:, :, i * S:] += x[:, :, :T - i * S]
+        assert_close(K.box_sum(cl(x), Kt, S).cpu(), ref, 1e-6, "box sum")
+        adj = torch.zeros_like(x)
+        for i in range(Kt // S):
+            adj[:, :, :T - i * S] += x[:, :, i * S:]
+        assert_close(K.box_sum(cl(x), Kt, S, trans=True).cpu(), adj, 1e-6, "box sum adjoint")
