@@ -54,7 +54,7 @@ def cpu_baseline(pkg, model_cpu_sd):
     from oracle import stgcn_oracle as O
 
     threads = torch.get_num_threads()
-    n_sample = int(os.environ.get("STGCN_CPU_SAMPLE_N", "8"))
+    n_sample = int(os.environ.get("STGCN_CPU_SAMPLE_N", "32"))
     arch = dict(ARCH, graph=pkg.PKU_MMD)
     sd = {k: v.detach().float().clone().requires_grad_(v.dtype.is_floating_point) for k, v in model_cpu_sd.items()}
     gen = torch.Generator().manual_seed(0)

@@ -47,7 +47,7 @@ typedef struct {
 int stgcn_conv_rows(const stgcn_conv_desc* d, int dtype, void* stream);
 /* column tile the packed weights must be padded to (Cout_pad % tile == 0) */
 int stgcn_conv_rows_col_tile(int cout);
-/* number of row blocks (first dim of the BN partial-stat buffer) for M output rows */
+/* upper bound on row blocks (first dim of the BN partial-stat buffer, which the caller zero-fills) */
 long stgcn_conv_rows_row_blocks(long M, int cout);
 
 /* Weight gradient of stgcn_conv_rows (trans = 0): dw[Kt][Cout][Cin] += ... (fp32, zeroed by caller).

@@ -22,6 +22,7 @@
 // tap dt) pairs; A (gathered rows) and B (packed weights) tiles are double-buffered in LDS with
 // register prefetch of the next pair, XOR-swizzled so fragment reads are bank-conflict free.
 #include "common.h"
+#include <stdlib.h>
 
 #include "../../include/stgcn_amd.h"
 typedef stgcn_conv_desc ConvArgs;
@@ -318,9 +319,16 @@ int launch_conv(const ConvArgs& a, hipStream_t s) {
 
 // Column tile = 64 for Cout <= 64, 128 otherwise; weights are packed to a multiple of it.
 int conv_rows_bn_tile(int cout) { return cout <= 64 ? 64 : 128; }
-long conv_rows_num_row_blocks(long M, int cout) { const int bm = cout <= 64 ? 256 : 128; return (M + bm - 1) / bm; }
+// upper bound over both kernels (smallest row tile = 128); unused partial slots must be zeroed
+long conv_rows_num_row_blocks(long M, int cout) { (void)cout; return (M + 127) / 128; }
+
+int conv_halo_launch(const ConvArgs& a, int dtype, hipStream_t s);
 
 int conv_rows_launch(const ConvArgs& a, int dtype, hipStream_t s) {
+  if (getenv("STGCN_HALO")) {  // experimental stride-1 halo kernel (opt-in until it beats this one)
+    const int r = conv_halo_launch(a, dtype, s);
+    if (r >= 0) return r;
+  }
   const int bn = conv_rows_bn_tile(a.Cout);
   if (a.Cout_pad % bn || a.Cin_pad % KC) return STGCN_EBADSHAPE;
   if (dtype == 1) {

@@ -20,73 +20,142 @@ typedef stgcn_amix_desc AmixArgs;
 namespace {
 constexpr int VMAX = 32;
 
-template <typename T>
-__global__ __launch_bounds__(256) void amix_fwd_kernel(const AmixArgs a, int tpf, int fpb) {
-  __shared__ float sA[4 * VMAX * VMAX];
-  const int n = blockIdx.y;
-  const float* A = a.A + (a.per_sample ? (long)n * a.P * a.V * a.V : 0);
-  for (int i = threadIdx.x; i < a.P * a.V * a.V; i += 256) sA[i] = A[i];
+// Neighbour lists of A built in LDS by every block (A's zero pattern is exploited exactly: a zero
+// coefficient contributes nothing).  The ST-GCN spatial graph has 73 non-zeros of 3*25*25, so the
+// mixing is ~1 FMA per output element and both kernels are HBM-bound gathers; a dense A (AAGCN's
+// A+B+C) simply yields full lists.
+struct MixLists {
+  float A[4 * VMAX * VMAX];
+  float fco[4 * VMAX * VMAX];     // fwd: per (p,w) coefficients, stride V
+  unsigned char fv[4 * VMAX * VMAX];
+  int fcnt[4 * VMAX];
+  float tco[4 * VMAX * VMAX];     // trans: per v, entries (p,w), stride P*V
+  short tpw[4 * VMAX * VMAX];
+  int tcnt[VMAX];
+};
+
+DEV void build_lists(MixLists& L, const float* A, int P, int V, bool fwd) {
+  for (int i = threadIdx.x; i < P * V * V; i += blockDim.x) L.A[i] = A[i];
   __syncthreads();
-  const int f = threadIdx.x / tpf, ct = threadIdx.x % tpf;
-  const int t = blockIdx.x * fpb + f;
-  if (f >= fpb || t >= a.T) return;
+  if (fwd) {
+    for (int pw = threadIdx.x; pw < P * V; pw += blockDim.x) {
+      const int p = pw / V, w = pw % V;
+      int c = 0;
+      for (int v = 0; v < V; ++v) {
+        const float a = L.A[(p * V + v) * V + w];
+        if (a != 0.f) {
+          L.fco[pw * V + c] = a;
+          L.fv[pw * V + c] = (unsigned char)v;
+          ++c;
+        }
+      }
+      L.fcnt[pw] = c;
+    }
+  } else {
+    for (int v = threadIdx.x; v < V; v += blockDim.x) {
+      int c = 0;
+      for (int p = 0; p < P; ++p)
+        for (int w = 0; w < V; ++w) {
+          const float a = L.A[(p * V + v) * V + w];
+          if (a != 0.f) {
+            L.tco[v * P * V + c] = a;
+            L.tpw[v * P * V + c] = (short)(p * V + w);
+            ++c;
+          }
+        }
+      L.tcnt[v] = c;
+    }
+  }
+  __syncthreads();
+}
+
+template <typename T, int VEC>
+DEV void ld_unit(const T* p, float* f) {
+  if constexpr (VEC == 1) f[0] = Tr<T>::to_f(*p);
+  else unpack16(*reinterpret_cast<const uint4*>(p), f, (T*)nullptr);
+}
+template <typename T, int VEC>
+DEV void st_unit(T* p, const float* f) {
+  if constexpr (VEC == 1) *p = Tr<T>::from_f(f[0]);
+  else *reinterpret_cast<uint4*>(p) = pack16(f, (T*)nullptr);
+}
+
+// XA[(n,t,w)][p*Cin + ci] = sum_{v in nbr(p,w)} A[p][v][w] x[(n,t,v)][ci]; work item = (frame, w, p, unit)
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void amix_fwd_kernel(const AmixArgs a, int fpb) {
+  __shared__ MixLists L;
+  const int n = blockIdx.y;
+  build_lists(L, a.A + (a.per_sample ? (long)n * a.P * a.V * a.V : 0), a.P, a.V, true);
+  const int CU = a.Cin / VEC;
+  const int per_frame = a.V * a.P * CU;
+  const int t0 = blockIdx.x * fpb;
+  const int nf = min(fpb, a.T - t0);
   const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
   T* __restrict__ out = reinterpret_cast<T*>(a.out);
-  const long row0 = ((long)n * a.T + t) * a.V;
-  const int ld_out = a.P * a.Cin;
-  for (int ci = ct; ci < a.Cin; ci += tpf) {
-    float xv[VMAX];
+  const int ldo = a.P * a.Cin;
+  for (int it = threadIdx.x; it < nf * per_frame; it += 256) {
+    const int f = it / per_frame;
+    int r = it - f * per_frame;
+    const int w = r / (a.P * CU);
+    r -= w * a.P * CU;
+    const int p = r / CU, u = r - p * CU;
+    const long row0 = ((long)n * a.T + t0 + f) * a.V;
+    float acc[VEC];
 #pragma unroll
-    for (int v = 0; v < VMAX; ++v) xv[v] = v < a.V ? Tr<T>::to_f(x[(row0 + v) * a.x_ld + ci]) : 0.f;
-    for (int p = 0; p < a.P; ++p) {
-      const float* Ap = sA + p * a.V * a.V;
-      for (int w = 0; w < a.V; ++w) {
-        float s = 0.f;
+    for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
+    const int pw = p * a.V + w;
+    const int cnt = L.fcnt[pw];
+    for (int k = 0; k < cnt; ++k) {
+      const float c = L.fco[pw * a.V + k];
+      float f8[VEC];
+      ld_unit<T, VEC>(x + (row0 + L.fv[pw * a.V + k]) * a.x_ld + u * VEC, f8);
 #pragma unroll
-        for (int v = 0; v < VMAX; ++v)
-          if (v < a.V) s += Ap[v * a.V + w] * xv[v];
-        out[(row0 + w) * ld_out + p * a.Cin + ci] = Tr<T>::from_f(s);
-      }
+      for (int j = 0; j < VEC; ++j) acc[j] += c * f8[j];
     }
+    st_unit<T, VEC>(out + (row0 + w) * ldo + p * a.Cin + u * VEC, acc);
   }
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void amix_trans_kernel(const AmixArgs a, int tpf, int fpb) {
-  __shared__ float sA[4 * VMAX * VMAX];
+// dx[(n,t,v)][ci] (+)= sum_{(p,w) in nbr^T(v)} A[p][v][w] DW[(n,t,w)][p*Cin+ci]; item = (frame, v, unit)
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void amix_trans_kernel(const AmixArgs a, int fpb) {
+  __shared__ MixLists L;
   const int n = blockIdx.y;
-  const float* A = a.A + (a.per_sample ? (long)n * a.P * a.V * a.V : 0);
-  for (int i = threadIdx.x; i < a.P * a.V * a.V; i += 256) sA[i] = A[i];
-  __syncthreads();
-  const int f = threadIdx.x / tpf, ct = threadIdx.x % tpf;
-  const int t = blockIdx.x * fpb + f;
-  if (f >= fpb || t >= a.T) return;
+  build_lists(L, a.A + (a.per_sample ? (long)n * a.P * a.V * a.V : 0), a.P, a.V, false);
+  const int CU = a.Cin / VEC;
+  const int per_frame = a.V * CU;
+  const int t0 = blockIdx.x * fpb;
+  const int nf = min(fpb, a.T - t0);
   const T* __restrict__ dw = reinterpret_cast<const T*>(a.x);
   T* __restrict__ out = reinterpret_cast<T*>(a.out);
-  const long row0 = ((long)n * a.T + t) * a.V;
-  const int ld_in = a.P * a.Cin;
-  for (int ci = ct; ci < a.Cin; ci += tpf) {
-    float acc[VMAX];
+  const int ldi = a.P * a.Cin;
+  for (int it = threadIdx.x; it < nf * per_frame; it += 256) {
+    const int f = it / per_frame;
+    int r = it - f * per_frame;
+    const int v = r / CU, u = r - v * CU;
+    const long row0 = ((long)n * a.T + t0 + f) * a.V;
+    float acc[VEC];
 #pragma unroll
-    for (int v = 0; v < VMAX; ++v) acc[v] = 0.f;
-    for (int p = 0; p < a.P; ++p) {
-      const float* Ap = sA + p * a.V * a.V;
-      for (int w = 0; w < a.V; ++w) {
-        const float d = Tr<T>::to_f(dw[(row0 + w) * ld_in + p * a.Cin + ci]);
+    for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
+    const int cnt = L.tcnt[v];
+    const int PV = a.P * a.V;
+    for (int k = 0; k < cnt; ++k) {
+      const float c = L.tco[v * PV + k];
+      const int pw = L.tpw[v * PV + k];
+      const int p = pw / a.V, w = pw - p * a.V;
+      float f8[VEC];
+      ld_unit<T, VEC>(dw + (row0 + w) * ldi + p * a.Cin + u * VEC, f8);
 #pragma unroll
-        for (int v = 0; v < VMAX; ++v)
-          if (v < a.V) acc[v] += Ap[v * a.V + w] * d;
-      }
+      for (int j = 0; j < VEC; ++j) acc[j] += c * f8[j];
     }
+    T* po = out + (row0 + v) * a.out_ld + u * VEC;
+    if (a.accumulate) {
+      float prev[VEC];
+      ld_unit<T, VEC>(po, prev);
 #pragma unroll
-    for (int v = 0; v < VMAX; ++v) {
-      if (v < a.V) {
-        T* p = out + (row0 + v) * a.out_ld + ci;
-        float r = acc[v];
-        if (a.accumulate) r += Tr<T>::to_f(*p);
-        *p = Tr<T>::from_f(r);
-      }
+      for (int j = 0; j < VEC; ++j) acc[j] += prev[j];
     }
+    st_unit<T, VEC>(po, acc);
   }
 }
 
@@ -174,33 +243,44 @@ __global__ void gcn_bias_kernel(const float* A, const float* b, float* out, int 
   }
 }
 
-void tpf_fpb(int cin, int& tpf, int& fpb) {
-  tpf = cin < 256 ? cin : 256;
-  fpb = 256 / tpf;
+// frames per block so that a block has ~16 work items per thread
+int frames_per_block(int items_per_frame) {
+  int f = (4096 + items_per_frame - 1) / items_per_frame;
+  return f < 1 ? 1 : f;
 }
 }  // namespace
 
-int amix_fwd_launch(const AmixArgs& a, int dtype, hipStream_t s) {
-  if (a.V > VMAX || a.P > 4) return STGCN_EBADSHAPE;
-  int tpf, fpb;
-  tpf_fpb(a.Cin, tpf, fpb);
-  dim3 grid((a.T + fpb - 1) / fpb, a.N);
-  if (dtype)
-    hipLaunchKernelGGL(amix_fwd_kernel<bf16>, grid, dim3(256), 0, s, a, tpf, fpb);
-  else
-    hipLaunchKernelGGL(amix_fwd_kernel<float>, grid, dim3(256), 0, s, a, tpf, fpb);
+#define AMIX_DISPATCH(KERNEL, a, per_frame_units, dtype, s)                                          \
+  do {                                                                                              \
+    const bool v8 = (a.Cin % 8 == 0) && (a.x_ld % 8 == 0) && (a.out_ld % 8 == 0);                   \
+    const bool v4 = (a.Cin % 4 == 0) && (a.x_ld % 4 == 0) && (a.out_ld % 4 == 0);                   \
+    const int vec = dtype ? (v8 ? 8 : 1) : (v4 ? 4 : 1);                                           \
+    const int fpb = frames_per_block((per_frame_units) * (a.Cin / vec));                           \
+    dim3 grid((a.T + fpb - 1) / fpb, a.N);                                                          \
+    if (dtype) {                                                                                    \
+      if (vec == 8) hipLaunchKernelGGL((KERNEL<bf16, 8>), grid, dim3(256), 0, s, a, fpb);           \
+      else hipLaunchKernelGGL((KERNEL<bf16, 1>), grid, dim3(256), 0, s, a, fpb);                    \
+    } else {                                                                                        \
+      if (vec == 4) hipLaunchKernelGGL((KERNEL<float, 4>), grid, dim3(256), 0, s, a, fpb);          \
+      else hipLaunchKernelGGL((KERNEL<float, 1>), grid, dim3(256), 0, s, a, fpb);                   \
+    }                                                                                               \
+  } while (0)
+
+int amix_fwd_launch(const AmixArgs& a0, int dtype, hipStream_t s) {
+  if (a0.V > VMAX || a0.P > 4) return STGCN_EBADSHAPE;
+  AmixArgs a = a0;
+  a.out_ld = a.P * a.Cin;
+  AMIX_DISPATCH(amix_fwd_kernel, a, a.V * a.P, dtype, s);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
 
-int amix_trans_launch(const AmixArgs& a, int dtype, hipStream_t s) {
-  if (a.V > VMAX || a.P > 4) return STGCN_EBADSHAPE;
-  int tpf, fpb;
-  tpf_fpb(a.Cin, tpf, fpb);
-  dim3 grid((a.T + fpb - 1) / fpb, a.N);
-  if (dtype)
-    hipLaunchKernelGGL(amix_trans_kernel<bf16>, grid, dim3(256), 0, s, a, tpf, fpb);
-  else
-    hipLaunchKernelGGL(amix_trans_kernel<float>, grid, dim3(256), 0, s, a, tpf, fpb);
+int amix_trans_launch(const AmixArgs& a0, int dtype, hipStream_t s) {
+  if (a0.V > VMAX || a0.P > 4) return STGCN_EBADSHAPE;
+  AmixArgs a = a0;
+  const int xld = a.x_ld;
+  a.x_ld = a.P * a.Cin;  // DW rows
+  (void)xld;
+  AMIX_DISPATCH(amix_trans_kernel, a, a.V, dtype, s);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
 

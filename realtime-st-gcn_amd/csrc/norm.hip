@@ -144,21 +144,31 @@ template <typename T, int VEC>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ u, int ldu, const float* sc,
                                                        const float* sh, int res_mode, const T* __restrict__ r,
                                                        int ldr, const float* rsc, const float* rsh, int relu,
-                                                       T* __restrict__ y, int ldy, long M, int C) {
-  const int CU = C / VEC;
-  const long total = M * CU;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const long m = i / CU;
-    const int c0 = (int)(i % CU) * VEC;
+                                                       T* __restrict__ y, int ldy, long M, int C, long rpb) {
+  int CU, RPI;
+  row_layout(C, VEC, CU, RPI);
+  const int cu = threadIdx.x % CU, rs = threadIdx.x / CU;
+  if (rs >= RPI) return;
+  const int c0 = cu * VEC;
+  float a[VEC], b[VEC], ra[VEC], rb[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) {
+    a[j] = sc[c0 + j];
+    b[j] = sh[c0 + j];
+    ra[j] = res_mode == 2 ? rsc[c0 + j] : 1.f;
+    rb[j] = res_mode == 2 ? rsh[c0 + j] : 0.f;
+  }
+  const long mb = blockIdx.x * rpb, me = min(M, mb + rpb);
+  for (long m = mb + rs; m < me; m += RPI) {
     float f[VEC];
     ldv<T, VEC>(u + m * ldu + c0, f);
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) f[j] = f[j] * sc[c0 + j] + sh[c0 + j];
+    for (int j = 0; j < VEC; ++j) f[j] = f[j] * a[j] + b[j];
     if (res_mode) {
       float g[VEC];
       ldv<T, VEC>(r + m * ldr + c0, g);
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) f[j] += res_mode == 2 ? g[j] * rsc[c0 + j] + rsh[c0 + j] : g[j];
+      for (int j = 0; j < VEC; ++j) f[j] += g[j] * ra[j] + rb[j];
     }
     if (relu) {
 #pragma unroll
@@ -265,13 +275,31 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
                                                            const float* msh, const T* __restrict__ x, int ldx,
                                                            const float2* mean_rstd, const float* gamma,
                                                            const float2* sums, long M, int C, T* __restrict__ dx,
-                                                           int lddx, int accumulate) {
-  const int CU = C / VEC;
-  const long total = M * CU;
+                                                           int lddx, int accumulate, long rpb) {
+  int CU, RPI;
+  row_layout(C, VEC, CU, RPI);
+  const int cu = threadIdx.x % CU, rs = threadIdx.x / CU;
+  if (rs >= RPI) return;
+  const int c0 = cu * VEC;
   const float invM = 1.f / (float)M;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const long m = i / CU;
-    const int c0 = (int)(i % CU) * VEC;
+  // dx = k1*dz + k2*x + k3  with k1 = g*rstd, k2 = -g*rstd^2*S2/M, k3 = -g*rstd*S1/M + g*rstd^2*S2/M*mean
+  float k1[VEC], k2[VEC], k3[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) {
+    if (x) {
+      const float2 st = mean_rstd[c0 + j];
+      const float2 sm = sums[c0 + j];
+      const float g = gamma ? gamma[c0 + j] : 1.f;
+      k1[j] = g * st.y;
+      k2[j] = -g * st.y * st.y * sm.y * invM;
+      k3[j] = -g * st.y * sm.x * invM - k2[j] * st.x;
+    } else {
+      k1[j] = 1.f;
+      k2[j] = k3[j] = 0.f;
+    }
+  }
+  const long mb = blockIdx.x * rpb, me = min(M, mb + rpb);
+  for (long m = mb + rs; m < me; m += RPI) {
     float dz[VEC];
     dz_load<T, VEC>(dy, lddy, mask, mref, ldm, msc, msh, m, c0, dz);
     float o[VEC];
@@ -279,13 +307,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
       float xv[VEC];
       ldv<T, VEC>(x + m * ldx + c0, xv);
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) {
-        const float2 st = mean_rstd[c0 + j];
-        const float2 sm = sums[c0 + j];
-        const float g = gamma ? gamma[c0 + j] : 1.f;
-        const float xh = (xv[j] - st.x) * st.y;
-        o[j] = g * st.y * (dz[j] - sm.x * invM - xh * sm.y * invM);
-      }
+      for (int j = 0; j < VEC; ++j) o[j] = k1[j] * dz[j] + k2[j] * xv[j] + k3[j];
     } else {
 #pragma unroll
       for (int j = 0; j < VEC; ++j) o[j] = dz[j];
@@ -300,26 +322,43 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
   }
 }
 
-// S[g][c] += sum_{m : m % G == g} x[m][c]   (G = V: per-joint column sums for the GCN bias grad)
-// period > 0: per-sample sums S[n][g][c] over the rows [n*period, (n+1)*period) (grid.y = n).
-template <typename T>
-__global__ __launch_bounds__(256) void rowgroup_sum_kernel(const T* __restrict__ x, int ld, long M, int C, int G,
-                                                           long rpb, long period, float* S) {
-  extern __shared__ float sS[];
-  for (int i = threadIdx.x; i < G * C; i += 256) sS[i] = 0.f;
-  __syncthreads();
-  const long base = period > 0 ? (long)blockIdx.y * period : 0;
-  const long lim = period > 0 ? base + period : M;
-  const long mb = base + blockIdx.x * rpb, me = min(lim, mb + rpb);
-  const long total = me > mb ? (me - mb) * C : 0;
-  for (long i = threadIdx.x; i < total; i += 256) {
-    const long m = mb + i / C;
-    const int c = (int)(i % C);
-    atomicAdd(&sS[(int)(m % G) * C + c], Tr<T>::to_f(x[m * ld + c]));
+// S[w][c] += sum_f x[(f*V + w)][c] over the block's frames; thread item = (w, channel unit), registers
+// accumulate over frames, one atomicAdd per item per block.  period > 0: per-sample S[n][w][c].
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void rowgroup_sum_kernel(const T* __restrict__ x, int ld, long F, int C, int G,
+                                                           long fpb, long frames_per_sample, float* S) {
+  const int CU = C / VEC;
+  const long fb0 = frames_per_sample > 0 ? (long)blockIdx.y * frames_per_sample : 0;
+  const long flim = frames_per_sample > 0 ? fb0 + frames_per_sample : F;
+  const long fb = fb0 + blockIdx.x * fpb, fe = min(flim, fb + fpb);
+  float* dst = S + (frames_per_sample > 0 ? (long)blockIdx.y * G * C : 0);
+  for (int item = threadIdx.x; item < G * CU; item += 256) {
+    const int w = item / CU, cu = item - w * CU;
+    float acc[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
+    const T* base = x + w * (long)ld + cu * VEC;
+    long f = fb;
+    for (; f + 4 <= fe; f += 4) {  // 4 independent loads in flight
+      float v0[VEC], v1[VEC], v2[VEC], v3[VEC];
+      ldv<T, VEC>(base + (f + 0) * G * (long)ld, v0);
+      ldv<T, VEC>(base + (f + 1) * G * (long)ld, v1);
+      ldv<T, VEC>(base + (f + 2) * G * (long)ld, v2);
+      ldv<T, VEC>(base + (f + 3) * G * (long)ld, v3);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] += (v0[j] + v1[j]) + (v2[j] + v3[j]);
+    }
+    for (; f < fe; ++f) {
+      float v[VEC];
+      ldv<T, VEC>(base + f * G * (long)ld, v);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] += v[j];
+    }
+    if (fe > fb) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) atomicAdd(dst + w * C + cu * VEC + j, acc[j]);
+    }
   }
-  __syncthreads();
-  float* dst = S + (period > 0 ? (long)blockIdx.y * G * C : 0);
-  for (int i = threadIdx.x; i < G * C; i += 256) atomicAdd(dst + i, sS[i]);
 }
 
 // ------------------------------------------------------------------ LayerNorm([C,1,V])
@@ -467,6 +506,11 @@ int grid_for(long work) {
   return (int)g;
 }
 
+long elt_rows_per_block(long M) {  // elementwise kernels: ~4096 blocks
+  long rpb = (M + 4095) / 4096;
+  return rpb < 32 ? 32 : rpb;
+}
+
 long rows_per_block(long M) {
   long rpb = (M + 1023) / 1024;
   return rpb < 64 ? 64 : rpb;
@@ -517,9 +561,12 @@ int bn_finalize_launch(const float4* part, int nb, int ldp, int C, const float* 
 int bn_apply_launch(const void* u, int ldu, const float* sc, const float* sh, int res_mode, const void* r, int ldr,
                     const float* rsc, const float* rsh, int relu, void* y, int ldy, long M, int C, int dtype,
                     hipStream_t s) {
-  DISPATCH_VEC(dtype, C, hipLaunchKernelGGL((bn_apply_kernel<T, VEC>), dim3(grid_for(M * C / VEC)), dim3(256), 0, s,
+  if (!rows_fit(C, dtype)) return STGCN_EBADSHAPE;
+  const long rpb = elt_rows_per_block(M);
+  const int nb = (int)((M + rpb - 1) / rpb);
+  DISPATCH_VEC(dtype, C, hipLaunchKernelGGL((bn_apply_kernel<T, VEC>), dim3(nb), dim3(256), 0, s,
                                             (const T*)u, ldu, sc, sh, res_mode, (const T*)r, ldr, rsc, rsh, relu,
-                                            (T*)y, ldy, M, C));
+                                            (T*)y, ldy, M, C, rpb));
   RET_HIP;
 }
 
@@ -540,23 +587,27 @@ int bn_bwd_apply_launch(const void* dy, int lddy, int mask, const void* mref, in
                         const float* msh, const void* x, int ldx, const float2* mean_rstd, const float* gamma,
                         const float2* sums, long M, int C, void* dx, int lddx, int accumulate, int dtype,
                         hipStream_t s) {
-  DISPATCH_VEC(dtype, C, hipLaunchKernelGGL((bn_bwd_apply_kernel<T, VEC>), dim3(grid_for(M * C / VEC)), dim3(256), 0,
-                                            s, (const T*)dy, lddy, mask, (const T*)mref, ldm, msc, msh, (const T*)x,
-                                            ldx, mean_rstd, gamma, sums, M, C, (T*)dx, lddx, accumulate));
+  if (!rows_fit(C, dtype)) return STGCN_EBADSHAPE;
+  const long rpb = elt_rows_per_block(M);
+  const int nb = (int)((M + rpb - 1) / rpb);
+  DISPATCH_VEC(dtype, C, hipLaunchKernelGGL((bn_bwd_apply_kernel<T, VEC>), dim3(nb), dim3(256), 0, s,
+                                            (const T*)dy, lddy, mask, (const T*)mref, ldm, msc, msh, (const T*)x,
+                                            ldx, mean_rstd, gamma, sums, M, C, (T*)dx, lddx, accumulate, rpb));
   RET_HIP;
 }
 
 int rowgroup_sum_launch(const void* x, int ld, long M, int C, int G, long period, float* S, int dtype,
                         hipStream_t s) {
-  if ((size_t)G * C * 4 > 64 * 1024) return STGCN_EBADSHAPE;
-  if (period > 0 && (period % G || M % period)) return STGCN_EBADSHAPE;
-  const long span = period > 0 ? period : M;
+  if (M % G || (period > 0 && (period % G || M % period))) return STGCN_EBADSHAPE;
+  const long F = M / G;
+  const long fps = period > 0 ? period / G : 0;
   const long nsamp = period > 0 ? M / period : 1;
-  long rpb = (span * nsamp + 511) / 512;
-  if (rpb < 256) rpb = 256;
-  const int nb = (int)((span + rpb - 1) / rpb);
-  DISPATCH_T(dtype, hipLaunchKernelGGL(rowgroup_sum_kernel<T>, dim3(nb, (unsigned)nsamp), dim3(256), G * C * 4, s,
-                                       (const T*)x, ld, M, C, G, rpb, period, S));
+  const long span = period > 0 ? fps : F;
+  long fpb = (F + 2047) / 2048;  // ~2048 blocks overall
+  if (fpb < 8) fpb = 8;
+  const int nb = (int)((span + fpb - 1) / fpb);
+  DISPATCH_VEC(dtype, C, hipLaunchKernelGGL((rowgroup_sum_kernel<T, VEC>), dim3(nb, (unsigned)nsamp), dim3(256), 0, s,
+                                            (const T*)x, ld, F, C, G, fpb, fps, S));
   RET_HIP;
 }
 

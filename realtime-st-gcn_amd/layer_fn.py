@@ -60,7 +60,7 @@ class StgcnLayerFunction(torch.autograd.Function):
         bias2d = K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
         bmode = 3 if A32.dim() == 4 else 2
         if norm == BN:
-            st1 = torch.empty((K.row_blocks(M1, Cout), cpg, 4), dtype=torch.float32, device=dev)
+            st1 = torch.zeros((K.row_blocks(M1, Cout), cpg, 4), dtype=torch.float32, device=dev)
         g = K.conv_rows(XA, wgp, P * Cin, Cout, cpg, kpg, T, T, bias=bias2d, bias_mode=bmode,
                         stats=st1 if norm == BN else None)
         if norm == BN:
@@ -75,7 +75,7 @@ class StgcnLayerFunction(torch.autograd.Function):
         wt3 = wt.detach().float().squeeze(-1).permute(2, 0, 1)  # [Kt][Cout][Cin]
         wtp, cpt, kpt = K.pack_weight(wt3, dtype)
         if norm == BN:
-            st2 = torch.empty((K.row_blocks(M2, Cout), cpt, 4), dtype=torch.float32, device=dev)
+            st2 = torch.zeros((K.row_blocks(M2, Cout), cpt, 4), dtype=torch.float32, device=dev)
         u = K.conv_rows(g, wtp, Cout, Cout, cpt, kpt, T, T_out, Kt=kt, stride=stride, pad=pad,
                         bias=bt.detach().float().contiguous(), stats=st2 if norm == BN else None,
                         tag=f"tcn_fwd_c{Cout}" if stride == 1 else None, **pro1)
@@ -86,7 +86,7 @@ class StgcnLayerFunction(torch.autograd.Function):
             wr3 = wr.detach().float().view(1, Cout, Cin)
             wrp, cpr, kpr = K.pack_weight(wr3, dtype)
             if norm == BN:
-                str_ = torch.empty((K.row_blocks(M2, Cout), cpr, 4), dtype=torch.float32, device=dev)
+                str_ = torch.zeros((K.row_blocks(M2, Cout), cpr, 4), dtype=torch.float32, device=dev)
             r = K.conv_rows(x, wrp, Cin, Cout, cpr, kpr, T, T_out, Kt=1, stride=stride, pad=0,
                             bias=br.detach().float().contiguous(), stats=str_ if norm == BN else None)
 

@@ -68,11 +68,13 @@ def grad_floor(grads, key):
     return 0.0
 
 
-def assert_grad_close(got, ref, rel=1e-3, name="", scale_floor=0.0):
+def assert_grad_close(got, ref, rel=1e-3, name="", scale_floor=0.0, reduction=False):
     """Gradient parity.  Max-norm ``rel`` as in assert_close, except that gradients downstream of a
     ReLU whose input is within rounding of 0 can legitimately flip (the reference's own CPU and GPU
     runs differ in the last bits; a flipped mask moves dy=O(1) into/out of the sum).  So: pass on the
-    max-norm criterion, or on L2-relative <= 3*rel with at most 0.5% of elements beyond rel*max."""
+    max-norm criterion, or on L2-relative <= 3*rel with at most 0.5% of elements beyond rel*max
+    (``reduction=True``: weight / adjacency gradients sum over all rows, so a flip touches every
+    element: L2 only)."""
     g = got.detach().double().cpu()
     r = ref.detach().double().cpu()
     assert g.shape == r.shape, f"{name}: shape {tuple(g.shape)} != {tuple(r.shape)}"
@@ -82,5 +84,5 @@ def assert_grad_close(got, ref, rel=1e-3, name="", scale_floor=0.0):
         return
     l2 = ((g - r).norm() / max(r.norm().item(), 1e-30)).item()
     frac = (err > rel * scale + 1e-6).double().mean().item()
-    assert l2 <= 3 * rel and frac <= 5e-3, \
+    assert l2 <= 3 * rel and (frac <= 5e-3 or reduction), \
         f"{name}: max err {err.max().item():.3e} > {rel:g}*{scale:.3e}; L2 rel {l2:.2e}, frac beyond {frac:.2e}"

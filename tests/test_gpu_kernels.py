@@ -75,7 +75,7 @@ def test_conv_prologue_bn_relu_and_stats(K, dtype):
     h = torch.relu(x * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1))
     ref = F.conv2d(h, w, b, padding=(4, 0))
     wp, cp, kp = K.pack_weight(w.squeeze(-1).permute(2, 0, 1).to(DEV), dtype)
-    st = torch.empty((K.row_blocks(N * T * V, C), cp, 4), device=DEV)
+    st = torch.zeros((K.row_blocks(N * T * V, C), cp, 4), device=DEV)
     y = K.conv_rows(cl(x, dtype), wp, C, C, cp, kp, T, T, Kt=9, pad=4, bias=b.to(DEV), pro=1, pro_a=sc.to(DEV),
                     pro_b=sh.to(DEV), stats=st)
     tol = 1e-4 if dtype == torch.float32 else 2e-2

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Official numbers: tests, bench (with cpu baseline), rocprofv3 kernel stats.  Output in gpurun_out/.
+export TMPDIR=/tmp
+TAG=${1:-r01}
+timeout -k 10 600 python -m pytest tests -m gpu -q --timeout=300 -p no:cacheprovider > gpurun_out/gpu_tests_$TAG.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/gpu_tests_$TAG.log
+{ [ $rc -eq 0 ] || [ $rc -eq 1 ]; } || exit $rc
+timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
+rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench_$TAG.json
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o bench --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/prof_$TAG.log 2>&1
+echo "prof rc=$?"
