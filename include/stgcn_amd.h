@@ -93,7 +93,8 @@ long stgcn_bn_stat_blocks(long M);
 int stgcn_bn_stats_partial(const void* x, int ld, long M, int C, void* part_f4, int dtype, void* stream);
 int stgcn_bn_finalize(const void* part_f4, int nblocks, int ld_part, int C, const float* gamma, const float* beta,
                       float eps, void* mean_rstd_f2, float* scale, float* shift, void* stream);
-/* y = act(u*sc + sh + res), res_mode 0 none | 1 r | 2 r*rsc + rsh  (stgcn.py:191-193, rtstgcn.py:386-389) */
+/* y = act(u*sc + sh + res), res_mode 0 none | 1 r | 2 r*rsc + rsh  (stgcn.py:191-193, rtstgcn.py:386-389);
+ * relu bit 0: ReLU after the residual add; bit 1: ReLU on the normalised branch before the add. */
 int stgcn_bn_apply(const void* u, int ldu, const float* sc, const float* sh, int res_mode, const void* r, int ldr,
                    const float* rsc, const float* rsh, int relu, void* y, int ldy, long M, int C, int dtype,
                    void* stream);
@@ -109,7 +110,10 @@ int stgcn_bn_bwd_apply(const void* dy, int lddy, int mask, const void* mref, int
                        void* stream);
 /* S[g][c] += sum_{m % G == g} x[m][c]  (per-joint column sums: GCN bias gradient);
  * period > 0: per-sample S[n][g][c] over rows [n*period, (n+1)*period) (per-sample A, AAGCN). */
-int stgcn_rowgroup_sum(const void* x, int ld, long M, int C, int G, long period, float* S, int dtype, void* stream);
+int stgcn_rowgroup_sum(const void* x, int ld, long M, int C, int G, long period, float* S, float* work, int dtype,
+                       void* stream);
+/* floats of scratch `work` stgcn_rowgroup_sum needs (per-block partial slabs, reduced deterministically) */
+long stgcn_rowgroup_sum_workspace(long M, int C, int G, long period);
 
 /* Custom LayerNorm([C,1,V]) (models/utils/layernorm.py:4-28): per (n,t) frame over (C,V),
  * unbiased variance, per-(c,v) affine. */
@@ -134,6 +138,14 @@ int stgcn_box_sum(const void* x, int ldx, void* y, int ldy, int N, int T, int V,
                   int accumulate, int dtype, void* stream);
 int stgcn_rt_online_step(const void* z_f32, float* fifo, float* acc, int* idx, int C, int V, int fifo_size, int S,
                          float* out, void* stream);
+
+/* AAGCN attention adjacency (models/aagcn/aagcn.py:142-145): C[n,p] = softmax_w(theta_p^T phi_p) over
+ * K = T*ce, theta/phi rows [N][T][V][ld] (channel p*ce+c).  C: fp32 [N][P][V][V].  Backward writes
+ * dS (scratch, fp32 like C) and dtheta/dphi (rows like theta/phi). */
+int stgcn_attn_scores(const void* theta, const void* phi, int ld, int N, int T, int V, int P, int ce, float* C,
+                      int dtype, void* stream);
+int stgcn_attn_bwd(const void* theta, const void* phi, int ld, int N, int T, int V, int P, int ce, const float* C,
+                   const float* dC, float* dS, void* dtheta, void* dphi, int dtype, void* stream);
 
 int stgcn_abi_version(void);
 

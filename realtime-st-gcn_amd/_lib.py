@@ -62,7 +62,9 @@ _SIGS = {
     "stgcn_bn_bwd_apply": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
                                    c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p, c_int, c_int, c_int,
                                    c_void_p]),
-    "stgcn_rowgroup_sum": (c_int, [c_void_p, c_int, c_long, c_int, c_int, c_long, c_void_p, c_int, c_void_p]),
+    "stgcn_rowgroup_sum": (c_int, [c_void_p, c_int, c_long, c_int, c_int, c_long, c_void_p, c_void_p, c_int,
+                                   c_void_p]),
+    "stgcn_rowgroup_sum_workspace": (c_long, [c_long, c_int, c_int, c_long]),
     "stgcn_ln_stats": (c_int, [c_void_p, c_int, c_long, c_int, c_int, c_float, c_void_p, c_int, c_void_p]),
     "stgcn_ln_apply": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p,
                                c_void_p, c_void_p, c_int, c_void_p, c_int, c_long, c_int, c_int, c_int, c_void_p]),
@@ -74,6 +76,10 @@ _SIGS = {
                               c_int, c_int, c_void_p]),
     "stgcn_rt_online_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                                      c_void_p]),
+    "stgcn_attn_scores": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                                  c_void_p]),
+    "stgcn_attn_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                               c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
 }
 
 EXPORTS = tuple(_SIGS)

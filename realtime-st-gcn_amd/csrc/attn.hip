@@ -1,0 +1,172 @@
+// AAGCN self-attention adjacency (models/aagcn/aagcn.py:139-145):
+//
+//   theta, phi = conv1x1(x) -> (N, P*ce, T, V)  (rows, channels-last)
+//   S[n,p,v,w] = sum_{t,c<ce} theta[(n,t,v)][p*ce+c] * phi[(n,t,w)][p*ce+c]      (matmul, :145)
+//   C[n,p,v,:] = softmax_w(S[n,p,v,:])                                            (softmax dim=3)
+// Backward: dS = C * (dC - sum_w dC*C);  dtheta[(n,t,v)][p*ce+c] = sum_w dS[v][w] phi[(n,t,w)][.]
+//                                        dphi[(n,t,w)][p*ce+c]   = sum_v dS[v][w] theta[(n,t,v)][.]
+// The score GEMM (K = T*ce, up to 4800) runs on MFMA with both operands loaded straight from the rows
+// (8 consecutive channels per lane = 16 B); blocks split T and add fp32 partials.
+#include "common.h"
+
+namespace {
+constexpr int VMAX = 32;
+
+template <typename T>
+__global__ __launch_bounds__(256) void attn_scores_kernel(const T* __restrict__ th, const T* __restrict__ ph,
+                                                          int ld, int T_, int V, int P, int ce, int tpb, float* S) {
+  constexpr int VEC = 16 / sizeof(T);
+  __shared__ float red[4][VMAX * VMAX];
+  const int n = blockIdx.z, p = blockIdx.y;
+  const int t0 = blockIdx.x * tpb, t1 = min(T_, t0 + tpb);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const bool vec = (ce % 8 == 0) && (ld % VEC == 0);
+  f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  const long K = (long)(t1 - t0) * ce;
+  // k = (t - t0)*ce + c ; each wave takes k-steps of 16 round-robin
+  for (long k0 = (long)wave * 16; k0 < K; k0 += 64) {
+    typename Tr<T>::frag fa, fb;
+    float fx[8], fy[8];
+    if (vec && r < V) {
+      const long k = k0 + 8 * h;
+      const int t = t0 + (int)(k / ce), c = (int)(k % ce);
+      if (k < K) {
+        const long base = ((long)n * T_ + t) * V;
+        const T* pa = th + (base + r) * ld + p * ce + c;
+        const T* pb = ph + (base + r) * ld + p * ce + c;
+#pragma unroll
+        for (int u = 0; u < 8; u += VEC) {
+          unpack16(*reinterpret_cast<const uint4*>(pa + u), fx + u, (T*)nullptr);
+          unpack16(*reinterpret_cast<const uint4*>(pb + u), fy + u, (T*)nullptr);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) fx[j] = fy[j] = 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const long k = k0 + 8 * h + j;
+        fx[j] = fy[j] = 0.f;
+        if (r < V && k < K) {
+          const int t = t0 + (int)(k / ce), c = (int)(k % ce);
+          const long row = ((long)n * T_ + t) * V + r;
+          fx[j] = Tr<T>::to_f(th[row * ld + p * ce + c]);
+          fy[j] = Tr<T>::to_f(ph[row * ld + p * ce + c]);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      fa[j] = Tr<T>::from_f(fx[j]);
+      fb[j] = Tr<T>::from_f(fy[j]);
+    }
+    Tr<T>::mma(acc, fa, fb);  // rows v (theta), cols w (phi)
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) red[wave][acc_row(i, lane) * VMAX + r] = acc[i];
+  __syncthreads();
+  float* dst = S + ((long)n * P + p) * V * V;
+  for (int i = threadIdx.x; i < V * V; i += 256) {
+    const int v = i / V, w = i % V;
+    atomicAdd(dst + i, red[0][v * VMAX + w] + red[1][v * VMAX + w] + red[2][v * VMAX + w] + red[3][v * VMAX + w]);
+  }
+}
+
+// in-place row softmax over w of S (N*P*V rows of V)
+__global__ void attn_softmax_kernel(float* S, long rows, int V) {
+  const long r = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  float* s = S + r * V;
+  float m = -INFINITY;
+  for (int w = 0; w < V; ++w) m = fmaxf(m, s[w]);
+  float z = 0.f;
+  for (int w = 0; w < V; ++w) z += __expf(s[w] - m);
+  const float iz = 1.f / z;
+  for (int w = 0; w < V; ++w) s[w] = __expf(s[w] - m) * iz;
+}
+
+// dS = C * (dC - sum_w dC*C), per row
+__global__ void attn_softmax_bwd_kernel(const float* C, const float* dC, float* dS, long rows, int V) {
+  const long r = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  const float* c = C + r * V;
+  const float* g = dC + r * V;
+  float s = 0.f;
+  for (int w = 0; w < V; ++w) s += g[w] * c[w];
+  for (int w = 0; w < V; ++w) dS[r * V + w] = c[w] * (g[w] - s);
+}
+
+// out[(n,t,a)][p*ce+c] = sum_b Mt[n][p][a][b] in[(n,t,b)][p*ce+c], Mt = dS (trans=0) or dS^T (trans=1)
+template <typename T>
+__global__ __launch_bounds__(256) void attn_mix_kernel(const T* __restrict__ in, int ld, const float* M, int T_,
+                                                       int V, int P, int ce, int trans, int fpb,
+                                                       T* __restrict__ out) {
+  __shared__ float sM[4 * VMAX * VMAX];
+  const int n = blockIdx.y;
+  for (int i = threadIdx.x; i < P * V * V; i += 256) {
+    const int p = i / (V * V), rem = i % (V * V), a = rem / V, b = rem % V;
+    const float v = M[((long)n * P + p) * V * V + rem];
+    if (trans) sM[(p * V + b) * V + a] = v; else sM[(p * V + a) * V + b] = v;
+  }
+  __syncthreads();
+  const int CH = P * ce;
+  const int per_frame = V * CH;
+  const int t0 = blockIdx.x * fpb;
+  const int nf = min(fpb, T_ - t0);
+  for (int it = threadIdx.x; it < nf * per_frame; it += 256) {
+    const int f = it / per_frame, rem = it % per_frame;
+    const int a = rem / CH, ch = rem % CH;
+    const int p = ch / ce;
+    const long row0 = ((long)n * T_ + t0 + f) * V;
+    const float* m = sM + (p * V + a) * V;
+    float s = 0.f;
+    for (int b = 0; b < V; ++b) s += m[b] * Tr<T>::to_f(in[(row0 + b) * ld + ch]);
+    out[(row0 + a) * ld + ch] = Tr<T>::from_f(s);
+  }
+}
+}  // namespace
+
+int attn_scores_launch(const void* th, const void* ph, int ld, int N, int T_, int V, int P, int ce, float* S,
+                       int dtype, hipStream_t s) {
+  if (V > VMAX || P > 4) return STGCN_EBADSHAPE;
+  (void)hipMemsetAsync(S, 0, sizeof(float) * N * P * V * V, s);
+  int tpb = (int)(((long)T_ * N * P + 1023) / 1024);  // ~1024 blocks
+  if (tpb < 8) tpb = 8;
+  dim3 grid((T_ + tpb - 1) / tpb, P, N);
+  if (dtype)
+    hipLaunchKernelGGL(attn_scores_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)th, (const bf16*)ph, ld, T_, V,
+                       P, ce, tpb, S);
+  else
+    hipLaunchKernelGGL(attn_scores_kernel<float>, grid, dim3(256), 0, s, (const float*)th, (const float*)ph, ld, T_,
+                       V, P, ce, tpb, S);
+  const long rows = (long)N * P * V;
+  hipLaunchKernelGGL(attn_softmax_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, S, rows, V);
+  return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
+}
+
+int attn_bwd_launch(const void* th, const void* ph, int ld, int N, int T_, int V, int P, int ce, const float* C,
+                    const float* dC, float* dS, void* dth, void* dph, int dtype, hipStream_t s) {
+  if (V > VMAX || P > 4) return STGCN_EBADSHAPE;
+  const long rows = (long)N * P * V;
+  hipLaunchKernelGGL(attn_softmax_bwd_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, C, dC, dS, rows,
+                     V);
+  int fpb = (4096 + V * P * ce - 1) / (V * P * ce);
+  if (fpb < 1) fpb = 1;
+  dim3 grid((T_ + fpb - 1) / fpb, N);
+  if (dtype) {
+    hipLaunchKernelGGL(attn_mix_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)ph, ld, dS, T_, V, P, ce, 0, fpb,
+                       (bf16*)dth);
+    hipLaunchKernelGGL(attn_mix_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)th, ld, dS, T_, V, P, ce, 1, fpb,
+                       (bf16*)dph);
+  } else {
+    hipLaunchKernelGGL(attn_mix_kernel<float>, grid, dim3(256), 0, s, (const float*)ph, ld, dS, T_, V, P, ce, 0, fpb,
+                       (float*)dth);
+    hipLaunchKernelGGL(attn_mix_kernel<float>, grid, dim3(256), 0, s, (const float*)th, ld, dS, T_, V, P, ce, 1, fpb,
+                       (float*)dph);
+  }
+  return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
+}

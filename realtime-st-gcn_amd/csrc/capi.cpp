@@ -36,8 +36,9 @@ int bn_bwd_apply_launch(const void* dy, int lddy, int mask, const void* mref, in
                         const float* msh, const void* x, int ldx, const float2* mean_rstd, const float* gamma,
                         const float2* sums, long M, int C, void* dx, int lddx, int accumulate, int dtype,
                         hipStream_t s);
-int rowgroup_sum_launch(const void* x, int ld, long M, int C, int G, long period, float* S, int dtype,
+int rowgroup_sum_launch(const void* x, int ld, long M, int C, int G, long period, float* S, float* work, int dtype,
                         hipStream_t s);
+long rowgroup_sum_workspace(long M, int C, int G, long period);
 int ln_stats_launch(const void* x, int ld, long F, int V, int C, float eps, float2* stats, int dtype, hipStream_t s);
 int ln_apply_launch(const void* u, int ldu, const float2* st, const float* g, const float* b, int res_mode,
                     const void* r, int ldr, const float2* rst, const float* rg, const float* rb, int relu, void* y,
@@ -51,6 +52,11 @@ int box_sum_launch(const void* x, int ldx, void* y, int ldy, int N, int T_, int 
                    int accumulate, int dtype, hipStream_t s);
 int rt_online_launch(const float* z, float* fifo, float* acc, int* idx, int C, int V, int fifo_size, int S,
                      float* out, hipStream_t s);
+
+int attn_scores_launch(const void* th, const void* ph, int ld, int N, int T_, int V, int P, int ce, float* S,
+                       int dtype, hipStream_t s);
+int attn_bwd_launch(const void* th, const void* ph, int ld, int N, int T_, int V, int P, int ce, const float* C,
+                    const float* dC, float* dS, void* dth, void* dph, int dtype, hipStream_t s);
 
 #define CHECK_DTYPE(dt) \
   if ((dt) != 0 && (dt) != 1) return STGCN_EDTYPE
@@ -135,10 +141,14 @@ int stgcn_bn_bwd_apply(const void* dy, int lddy, int mask, const void* mref, int
   return bn_bwd_apply_launch(dy, lddy, mask, mref, ldm, msc, msh, x, ldx, (const float2*)mean_rstd, gamma,
                              (const float2*)sums, M, C, dx, lddx, accumulate, dtype, STREAM(stream));
 }
-int stgcn_rowgroup_sum(const void* x, int ld, long M, int C, int G, long period, float* S, int dtype,
+long stgcn_rowgroup_sum_workspace(long M, int C, int G, long period) {
+  return rowgroup_sum_workspace(M, C, G, period);
+}
+int stgcn_rowgroup_sum(const void* x, int ld, long M, int C, int G, long period, float* S, float* work, int dtype,
                        void* stream) {
   CHECK_DTYPE(dtype);
-  return rowgroup_sum_launch(x, ld, M, C, G, period, S, dtype, STREAM(stream));
+  if (!x || !S || !work || G <= 0) return STGCN_EBADSHAPE;
+  return rowgroup_sum_launch(x, ld, M, C, G, period, S, work, dtype, STREAM(stream));
 }
 int stgcn_ln_stats(const void* x, int ld, long frames, int V, int C, float eps, void* st, int dtype, void* stream) {
   CHECK_DTYPE(dtype);
@@ -175,6 +185,19 @@ int stgcn_rt_online_step(const void* z, float* fifo, float* acc, int* idx, int C
                          float* out, void* stream) {
   if (!z || !fifo || !acc || !idx || !out) return STGCN_EBADSHAPE;
   return rt_online_launch((const float*)z, fifo, acc, idx, C, V, fifo_size, S, out, STREAM(stream));
+}
+
+int stgcn_attn_scores(const void* th, const void* ph, int ld, int N, int T, int V, int P, int ce, float* C, int dtype,
+                      void* stream) {
+  CHECK_DTYPE(dtype);
+  if (!th || !ph || !C || ld < P * ce) return STGCN_EBADSHAPE;
+  return attn_scores_launch(th, ph, ld, N, T, V, P, ce, C, dtype, STREAM(stream));
+}
+int stgcn_attn_bwd(const void* th, const void* ph, int ld, int N, int T, int V, int P, int ce, const float* C,
+                   const float* dC, float* dS, void* dth, void* dph, int dtype, void* stream) {
+  CHECK_DTYPE(dtype);
+  if (!th || !ph || !C || !dC || !dS || !dth || !dph || ld < P * ce) return STGCN_EBADSHAPE;
+  return attn_bwd_launch(th, ph, ld, N, T, V, P, ce, C, dC, dS, dth, dph, dtype, STREAM(stream));
 }
 
 }  // extern "C"

@@ -164,13 +164,17 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ u, 
     ldv<T, VEC>(u + m * ldu + c0, f);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) f[j] = f[j] * a[j] + b[j];
+    if (relu & 2) {  // inner ReLU on the normalised branch (RT-ST-GCN bn_relu, rtstgcn.py:319-321)
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) f[j] = fmaxf(f[j], 0.f);
+    }
     if (res_mode) {
       float g[VEC];
       ldv<T, VEC>(r + m * ldr + c0, g);
 #pragma unroll
       for (int j = 0; j < VEC; ++j) f[j] += g[j] * ra[j] + rb[j];
     }
-    if (relu) {
+    if (relu & 1) {
 #pragma unroll
       for (int j = 0; j < VEC; ++j) f[j] = fmaxf(f[j], 0.f);
     }
@@ -326,12 +330,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
 // accumulate over frames, one atomicAdd per item per block.  period > 0: per-sample S[n][w][c].
 template <typename T, int VEC>
 __global__ __launch_bounds__(256) void rowgroup_sum_kernel(const T* __restrict__ x, int ld, long F, int C, int G,
-                                                           long fpb, long frames_per_sample, float* S) {
+                                                           long fpb, long frames_per_sample, float* part) {
   const int CU = C / VEC;
   const long fb0 = frames_per_sample > 0 ? (long)blockIdx.y * frames_per_sample : 0;
   const long flim = frames_per_sample > 0 ? fb0 + frames_per_sample : F;
   const long fb = fb0 + blockIdx.x * fpb, fe = min(flim, fb + fpb);
-  float* dst = S + (frames_per_sample > 0 ? (long)blockIdx.y * G * C : 0);
   for (int item = threadIdx.x; item < G * CU; item += 256) {
     const int w = item / CU, cu = item - w * CU;
     float acc[VEC];
@@ -354,10 +357,20 @@ __global__ __launch_bounds__(256) void rowgroup_sum_kernel(const T* __restrict__
 #pragma unroll
       for (int j = 0; j < VEC; ++j) acc[j] += v[j];
     }
-    if (fe > fb) {
+    float* slab = part + ((long)blockIdx.y * gridDim.x + blockIdx.x) * G * C;  // per-block partial
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) atomicAdd(dst + w * C + cu * VEC + j, acc[j]);
-    }
+    for (int j = 0; j < VEC; ++j) slab[w * C + cu * VEC + j] = acc[j];
+  }
+}
+
+// S[s][e] += sum_b part[s][b][e]  (deterministic reduction of the per-block partial slabs)
+__global__ __launch_bounds__(256) void sum_slabs_kernel(const float* part, int nb, int E, float* S) {
+  const int s = blockIdx.y;
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < E; e += gridDim.x * 256) {
+    float acc = 0.f;
+    const float* p = part + (long)s * nb * E + e;
+    for (int b = 0; b < nb; ++b) acc += p[(long)b * E];
+    S[(long)s * E + e] += acc;
   }
 }
 
@@ -401,12 +414,13 @@ __global__ __launch_bounds__(256) void ln_apply_kernel(const T* __restrict__ u, 
     const int gi = c * V + v;
     const float2 s = st[f];
     float o = (Tr<T>::to_f(u[m * ldu + c]) - s.x) * s.y * g[gi] + b[gi];
+    if (relu & 2) o = fmaxf(o, 0.f);
     if (res_mode == 1) o += Tr<T>::to_f(r[m * ldr + c]);
     if (res_mode == 2) {
       const float2 q = rst[f];
       o += (Tr<T>::to_f(r[m * ldr + c]) - q.x) * q.y * rg[gi] + rb[gi];
     }
-    if (relu) o = fmaxf(o, 0.f);
+    if (relu & 1) o = fmaxf(o, 0.f);
     y[m * ldy + c] = Tr<T>::from_f(o);
   }
 }
@@ -596,18 +610,33 @@ int bn_bwd_apply_launch(const void* dy, int lddy, int mask, const void* mref, in
   RET_HIP;
 }
 
-int rowgroup_sum_launch(const void* x, int ld, long M, int C, int G, long period, float* S, int dtype,
+static void rowgroup_geometry(long M, int G, long period, long& F, long& fps, long& nsamp, long& fpb, int& nb) {
+  F = M / G;
+  fps = period > 0 ? period / G : 0;
+  nsamp = period > 0 ? M / period : 1;
+  const long span = period > 0 ? fps : F;
+  fpb = (span + 63) / 64;  // <= 64 partial slabs per sample
+  if (fpb < 16) fpb = 16;
+  nb = (int)((span + fpb - 1) / fpb);
+}
+
+long rowgroup_sum_workspace(long M, int C, int G, long period) {
+  long F, fps, nsamp, fpb;
+  int nb;
+  rowgroup_geometry(M, G, period, F, fps, nsamp, fpb, nb);
+  return (long)nb * nsamp * G * C;
+}
+
+int rowgroup_sum_launch(const void* x, int ld, long M, int C, int G, long period, float* S, float* work, int dtype,
                         hipStream_t s) {
   if (M % G || (period > 0 && (period % G || M % period))) return STGCN_EBADSHAPE;
-  const long F = M / G;
-  const long fps = period > 0 ? period / G : 0;
-  const long nsamp = period > 0 ? M / period : 1;
-  const long span = period > 0 ? fps : F;
-  long fpb = (F + 2047) / 2048;  // ~2048 blocks overall
-  if (fpb < 8) fpb = 8;
-  const int nb = (int)((span + fpb - 1) / fpb);
+  long F, fps, nsamp, fpb;
+  int nb;
+  rowgroup_geometry(M, G, period, F, fps, nsamp, fpb, nb);
   DISPATCH_VEC(dtype, C, hipLaunchKernelGGL((rowgroup_sum_kernel<T, VEC>), dim3(nb, (unsigned)nsamp), dim3(256), 0, s,
-                                            (const T*)x, ld, F, C, G, fpb, fps, S));
+                                            (const T*)x, ld, F, C, G, fpb, fps, work));
+  const int E = G * C;
+  hipLaunchKernelGGL(sum_slabs_kernel, dim3((E + 255) / 256, (unsigned)nsamp), dim3(256), 0, s, work, nb, E, S);
   RET_HIP;
 }
 

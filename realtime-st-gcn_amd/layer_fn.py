@@ -36,6 +36,51 @@ def _flat_ln(p):
     return p.detach().reshape(-1).float().contiguous()
 
 
+def gcn_forward(x, A32, wg, bg, dtype, stats=None):
+    """ConvTemporalGraphical forward on rows: XA = A-mix(x); g = XA @ Wg' + bias2d.  Returns (XA, g, cp)."""
+    N, Cin, T, V = x.shape
+    P = A32.shape[-3]
+    Cout = wg.shape[0] // P
+    XA = K.amix_fwd(x, A32)
+    wg3 = wg.detach().float().view(P, Cout, Cin).permute(1, 0, 2).reshape(1, Cout, P * Cin)
+    wgp, cp, kp = K.pack_weight(wg3, dtype)
+    bias2d = K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
+    g = K.conv_rows(XA, wgp, P * Cin, Cout, cp, kp, T, T, bias=bias2d, bias_mode=3 if A32.dim() == 4 else 2,
+                    stats=stats)
+    return XA, g, cp
+
+
+def gcn_stats_buffer(M, Cout, dev):
+    cp = -(-Cout // K.col_tile(Cout)) * K.col_tile(Cout)
+    return torch.zeros((K.row_blocks(M, Cout), cp, 4), dtype=torch.float32, device=dev), cp
+
+
+def gcn_backward(x, A32, XA, wg, bg, dg, dx, accumulate, dtype):
+    """Backward of gcn_forward given dg: dx (+)= A^T-mix(dg @ Wg), returns (dA fp32, dWg, dbg)."""
+    N, Cin, T, V = x.shape
+    P = A32.shape[-3]
+    Cout = wg.shape[0] // P
+    M = N * T * V
+    wgT = wg.detach().float().view(P, Cout, Cin).permute(0, 2, 1).reshape(1, P * Cin, Cout)
+    wgTp, cq, kq = K.pack_weight(wgT, dtype)
+    DW = K.conv_rows(dg, wgTp, Cout, P * Cin, cq, kq, T, T)
+    K.amix_trans(DW, A32, Cin, dx, accumulate=accumulate)
+    dA = K.amix_dA(x, DW, A32)
+    bgp = bg.detach().float().view(P, Cout)
+    # the conv bias pushed through A: dA[p][v][w] += sum_c b_p[c] S[w][c] (independent of v)
+    if A32.dim() == 4:
+        Sn = K.rowgroup_sum(dg, M, Cout, V, per_sample=True)            # [N][V(w)][Cout]
+        dA += torch.einsum("pc,nwc->npw", bgp, Sn).unsqueeze(2)
+        dbg = torch.einsum("npw,nwc->pc", A32.sum(dim=2), Sn).reshape(-1)
+    else:
+        S = K.rowgroup_sum(dg, M, Cout, V)                               # [V(w)][Cout]
+        dA += (bgp @ S.t()).unsqueeze(1)
+        dbg = (A32.sum(dim=1) @ S).reshape(-1)
+    dwg = K.conv_wgrad(XA, dg, P * Cin, Cout, T, T, Kt=1)                # [1][Cout][P*Cin]
+    dwg = dwg.view(Cout, P, Cin).permute(1, 0, 2).reshape(P * Cout, Cin, 1, 1)
+    return dA, dwg, dbg
+
+
 class StgcnLayerFunction(torch.autograd.Function):
     """Autograd node for the whole StgcnLayer (BN or LN variant)."""
 
@@ -388,14 +433,18 @@ class LayerNormFunction(torch.autograd.Function):
 
 
 class PoolFunction(torch.autograd.Function):
-    """F.avg_pool2d(x, x.size()[2:]) (stgcn.py:92) -> (N, C, 1, 1)."""
+    """F.avg_pool2d(x, x.size()[2:]) (stgcn.py:92) -> (N, C, 1, 1); joints_only=True is the RT head's
+    AvgPool2d((1, V)) (rtstgcn.py:127,149) -> (N, C, T, 1)."""
 
     @staticmethod
-    def forward(ctx, x, dtype):
+    def forward(ctx, x, dtype, joints_only=False):
         x = K.to_rows(x, dtype)
         N, C, T, V = x.shape
         ctx.shape = (N, C, T, V)
         ctx.dtype = dtype
+        ctx.joints_only = joints_only
+        if joints_only:
+            return K.pool_rows(x, N * T, V, C).reshape(N, T, 1, C).permute(0, 3, 1, 2)
         return K.pool_rows(x, N, T * V, C)
 
     @staticmethod
@@ -403,5 +452,154 @@ class PoolFunction(torch.autograd.Function):
         N, C, T, V = ctx.shape
         dp = K.to_rows(dp, ctx.dtype)
         dx = K.cl_empty(N, C, T, V, ctx.dtype, dp.device)
-        K.unpool_rows(dp, T * V, C, N * T * V, dx)
-        return dx, None
+        if ctx.joints_only:
+            dp = dp.permute(0, 2, 3, 1).reshape(N * T, 1, 1, C).permute(0, 3, 1, 2)
+            K.unpool_rows(dp, V, C, N * T * V, dx)
+        else:
+            K.unpool_rows(dp, T * V, C, N * T * V, dx)
+        return dx, None, None
+
+
+class AttentionFunction(torch.autograd.Function):
+    """C = softmax(theta^T phi) per (n, p) (models/aagcn/aagcn.py:142-145), theta/phi channels-last rows."""
+
+    @staticmethod
+    def forward(ctx, theta, phi, P, dtype):
+        theta = K.to_rows(theta, dtype)
+        phi = K.to_rows(phi, dtype)
+        C = K.attn_scores(theta, phi, P)
+        ctx.save_for_backward(theta, phi, C)
+        ctx.P = P
+        ctx.dtype = dtype
+        return C
+
+    @staticmethod
+    def backward(ctx, dC):
+        theta, phi, C = ctx.saved_tensors
+        dth, dph = K.attn_bwd(theta, phi, ctx.P, C, dC.float().contiguous())
+        return dth, dph, None, None
+
+
+class RtOfflineLayerFunction(torch.autograd.Function):
+    """OfflineLayer.forward (models/rtstgcn/rtstgcn.py:343-389) with the Toeplitz matmul it intends
+    (rtstgcn.py:366-379) evaluated as the causal K//S-tap box sum it is:
+
+        res = 0 | x | norm_r(conv1x1_nobias(x))
+        b   = boxsum_{K,S}( sum_p A_p-mix( conv1x1(x) ) )          (A = A_graph * edge_importance)
+        y   = relu(relu(norm(b)) + res)      (residual)     |     relu(norm(b))     (no residual)
+    """
+
+    @staticmethod
+    def forward(ctx, x, A, wc, bc, nw, nb, wr, nrw, nrb, cfg):
+        Kt, S, residual, norm, dtype = cfg
+        dev = x.device
+        x = K.to_rows(x, dtype)
+        N, Cin, L, V = x.shape
+        P = A.shape[-3]
+        Cout = wc.shape[0] // P
+        M = N * L * V
+        A32 = A.detach().float().contiguous()
+        res_conv = residual and not (Cin == Cout and S == 1)
+        XA, z, _ = gcn_forward(x, A32, wc, bc, dtype)
+        b = K.box_sum(z, Kt, S)
+        relu_mode = 3 if residual else 2
+        r = None
+        if res_conv:
+            wrp, cq, kq = K.pack_weight(wr.detach().float().view(1, Cout, Cin), dtype)
+            if norm == BN:
+                str_, _ = gcn_stats_buffer(M, Cout, dev)
+            r = K.conv_rows(x, wrp, Cin, Cout, cq, kq, L, L, stats=str_ if norm == BN else None)
+        if norm == BN:
+            part, nbk, _ = K.bn_stats_partial(b, M, Cout)
+            mr, sc, sh = K.bn_finalize(part, nbk, Cout, Cout, nw.detach().float(), nb.detach().float())
+            if res_conv:
+                mrr, scr, shr = K.bn_finalize(str_, str_.shape[0], str_.shape[1], Cout, nrw.detach().float(),
+                                              nrb.detach().float())
+                y = K.bn_apply(b, sc, sh, M, Cout, res_mode=2, r=r, rsc=scr, rsh=shr, relu=relu_mode)
+            else:
+                y = K.bn_apply(b, sc, sh, M, Cout, res_mode=1 if residual else 0, r=x if residual else None,
+                               relu=relu_mode)
+            st, stn = mr, (mrr if res_conv else None)
+        else:
+            st = K.ln_stats(b, N * L, V, Cout)
+            stn = None
+            if res_conv:
+                stn = K.ln_stats(r, N * L, V, Cout)
+                y = K.ln_apply(b, st, _flat_ln(nw), _flat_ln(nb), M, V, Cout, res_mode=2, r=r, rst=stn,
+                               rg=_flat_ln(nrw), rb=_flat_ln(nrb), relu=relu_mode)
+            else:
+                y = K.ln_apply(b, st, _flat_ln(nw), _flat_ln(nb), M, V, Cout, res_mode=1 if residual else 0,
+                               r=x if residual else None, relu=relu_mode)
+        ctx.cfg = cfg
+        ctx.dims = (N, Cin, Cout, L, V, P, res_conv)
+        ctx.in_dtype = A.dtype
+        saved = [x, A32, XA, b, y, st, wc, bc, nw, nb]
+        if norm == BN:
+            saved += [sc, sh]
+        if res_conv:
+            saved += [r, stn, wr, nrw, nrb]
+        ctx.save_for_backward(*saved)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        Kt, S, residual, norm, dtype = ctx.cfg
+        N, Cin, Cout, L, V, P, res_conv = ctx.dims
+        sv = list(ctx.saved_tensors)
+        x, A32, XA, b, y, st, wc, bc, nw, nb = sv[:10]
+        rest = sv[10:]
+        if norm == BN:
+            sc, sh = rest[:2]
+            rest = rest[2:]
+        if res_conv:
+            r, stn, wr, nrw, nrb = rest
+        dev = x.device
+        M = N * L * V
+        dy = K.to_rows(dy, dtype)
+        # dq = grad w.r.t. (relu(norm(b)) + res)
+        if residual:
+            dq = K.cl_empty(N, Cout, L, V, dtype, dev)
+            K.bn_bwd_apply(dy, M, Cout, dq, mask=1, mref=y)
+        else:
+            dq = dy
+        dx = K.cl_empty(N, Cin, L, V, dtype, dev)
+        dx_written = False
+        g = {}
+        if res_conv:
+            dr = K.cl_empty(N, Cout, L, V, dtype, dev)
+            if norm == BN:
+                sr = K.bn_bwd_reduce(dq, M, Cout, x=r, mean_rstd=stn)
+                K.bn_bwd_apply(dq, M, Cout, dr, x=r, mean_rstd=stn, gamma=nrw.detach().float(), sums=sr)
+                g["nrw"], g["nrb"] = sr[:, 1].clone(), sr[:, 0].clone()
+            else:
+                dgbr = torch.zeros((2, Cout * V), dtype=torch.float32, device=dev)
+                K.ln_bwd(dq, r, stn, _flat_ln(nrw), _flat_ln(nrb), N * L, V, Cout, dr, dgb=dgbr)
+                g["nrw"], g["nrb"] = dgbr[0].view(nrw.shape), dgbr[1].view(nrb.shape)
+            wrT, cq, kq = K.pack_weight(wr.detach().float().view(Cout, Cin).t().reshape(1, Cin, Cout), dtype)
+            K.conv_rows(dr, wrT, Cout, Cin, cq, kq, L, L, trans=True, out=dx)
+            dx_written = True
+            g["wr"] = K.conv_wgrad(x, dr, Cin, Cout, L, L).view(Cout, Cin, 1, 1)
+        elif residual:
+            K.bn_bwd_apply(dq, M, Cin, dx)  # dx = dq
+            dx_written = True
+        # through relu(norm(b))
+        db = K.cl_empty(N, Cout, L, V, dtype, dev)
+        if norm == BN:
+            s1 = K.bn_bwd_reduce(dq, M, Cout, mask=2, mref=b, msc=sc, msh=sh, x=b, mean_rstd=st)
+            K.bn_bwd_apply(dq, M, Cout, db, mask=2, mref=b, msc=sc, msh=sh, x=b, mean_rstd=st,
+                           gamma=nw.detach().float(), sums=s1)
+            g["nw"], g["nb"] = s1[:, 1].clone(), s1[:, 0].clone()
+        else:
+            dgb = torch.zeros((2, Cout * V), dtype=torch.float32, device=dev)
+            K.ln_bwd(dq, b, st, _flat_ln(nw), _flat_ln(nb), N * L, V, Cout, db, mask=2, dgb=dgb)
+            g["nw"], g["nb"] = dgb[0].view(nw.shape), dgb[1].view(nb.shape)
+        dz = K.box_sum(db, Kt, S, trans=True)
+        dA, dwc, dbc = gcn_backward(x, A32, XA, wc, bc, dz, dx, dx_written, dtype)
+
+        def gr(name, like):
+            v = g.get(name)
+            return None if v is None or like is None or not like.requires_grad else v.to(like.dtype).view(like.shape)
+
+        return (dx, dA.to(ctx.in_dtype), dwc.to(wc.dtype), dbc.to(bc.dtype), gr("nw", nw), gr("nb", nb),
+                gr("wr", wr if res_conv else None), gr("nrw", nrw if res_conv else None),
+                gr("nrb", nrb if res_conv else None), None)

@@ -219,7 +219,8 @@ def rowgroup_sum(x, M, C, G, per_sample=False):
     N = x.shape[0]
     S = torch.zeros(((N,) if per_sample else ()) + (G, C), dtype=torch.float32, device=x.device)
     period = M // N if per_sample else 0
-    L.check(L.lib().stgcn_rowgroup_sum(x.data_ptr(), rows_ld(x), M, C, G, period, S.data_ptr(),
+    work = torch.empty(L.lib().stgcn_rowgroup_sum_workspace(M, C, G, period), dtype=torch.float32, device=x.device)
+    L.check(L.lib().stgcn_rowgroup_sum(x.data_ptr(), rows_ld(x), M, C, G, period, S.data_ptr(), work.data_ptr(),
                                        L.dtype_code(x.dtype), L.stream()), "rowgroup_sum")
     return S
 
@@ -278,3 +279,24 @@ def rt_online_step(z, fifo, acc, idx, C, V, fifo_size, S, out):
     L.check(L.lib().stgcn_rt_online_step(z.data_ptr(), fifo.data_ptr(), acc.data_ptr(), idx.data_ptr(), C, V,
                                          fifo_size, S, out.data_ptr(), L.stream()), "rt_online_step")
     return out
+
+
+# ------------------------------------------------------------------------------------ AAGCN attention
+def attn_scores(theta, phi, P):
+    """C = softmax_w(theta_p^T phi_p) per (n, p): fp32 (N, P, V, V)."""
+    N, CH, T, V = theta.shape
+    C = torch.empty((N, P, V, V), dtype=torch.float32, device=theta.device)
+    L.check(L.lib().stgcn_attn_scores(theta.data_ptr(), phi.data_ptr(), rows_ld(theta), N, T, V, P, CH // P,
+                                      C.data_ptr(), L.dtype_code(theta.dtype), L.stream()), "attn_scores")
+    return C
+
+
+def attn_bwd(theta, phi, P, C, dC):
+    N, CH, T, V = theta.shape
+    dS = torch.empty_like(C)
+    dth = torch.empty_like(theta)
+    dph = torch.empty_like(phi)
+    L.check(L.lib().stgcn_attn_bwd(theta.data_ptr(), phi.data_ptr(), rows_ld(theta), N, T, V, P, CH // P,
+                                   C.data_ptr(), dC.data_ptr(), dS.data_ptr(), dth.data_ptr(), dph.data_ptr(),
+                                   L.dtype_code(theta.dtype), L.stream()), "attn_bwd")
+    return dth, dph

@@ -1,0 +1,232 @@
+"""RT-ST-GCN (models/rtstgcn/rtstgcn.py) on the HIP kernels.
+
+* ``OfflineLayer`` — training form (rtstgcn.py:220-389): the reference multiplies by an L x L Toeplitz
+  matrix and, in this snapshot, crashes on the never-assigned ``self.toeplitz`` (rtstgcn.py:379);
+  we evaluate the causal K//S-tap box sum that matrix encodes (rtstgcn.py:368-374), O(K) per output.
+* ``OnlineLayer`` + ``AggregateStgcn`` — per-frame inference form (rtstgcn.py:392-627) with the FIFO /
+  accumulator state in device buffers (the reference keeps them in CPU tensors, rtstgcn.py:576-579)
+  and the step as one HIP kernel (rt.hip).  State is non-persistent (not in the state_dict, exactly
+  like the reference's plain attributes).
+* ``Model`` — rtstgcn.py:8-217 incl. ``_swap_layers_for_inference`` (rtstgcn.py:160-187).
+
+Stride > 1: offline (K//S taps, dilation S) and online (FIFO of S*(K-1)+1 frames, S accumulators)
+diverge in the reference itself (SURVEY §7 hard parts); each form here reproduces its own reference
+form (tests/test_gpu_rt.py), and they agree at stride 1.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import layer_fn as LF
+from . import native as K
+from .graph import Graph
+from .modules import BatchNorm1d, LayerNorm, make_norm, resolve_dtype
+from .stgcn import IN_PAD
+
+
+class OfflineLayer(nn.Module):
+    def __init__(self, in_channels, out_channels, kernel_size, num_joints, stride, num_partitions, dropout,
+                 residual, importance, graph, normalization="LayerNorm"):
+        super().__init__()
+        assert kernel_size % 2 == 1
+        self.num_partitions = num_partitions
+        self.num_joints = num_joints
+        self.stride = stride
+        self.kernel_size = kernel_size
+        self.out_channels = out_channels
+        self.is_residual = residual
+        self.normalization = normalization
+        self.dropout = dropout
+        self.edge_importance = (nn.Parameter(torch.ones(num_partitions, num_joints, num_joints), requires_grad=True)
+                                if importance else 1)
+        self.conv = nn.Conv2d(in_channels, out_channels * num_partitions, kernel_size=1)
+        self.bn_relu = nn.Sequential(make_norm(normalization, out_channels, num_joints), nn.ReLU())
+        self.is_residual_conv = residual and not ((in_channels == out_channels) and (stride == 1))
+        if self.is_residual_conv:
+            self.residual = nn.Sequential(nn.Conv2d(in_channels, out_channels, kernel_size=1, bias=False),
+                                          make_norm(normalization, out_channels, num_joints))
+        self.do = nn.Sequential(nn.ReLU(), nn.Dropout(dropout)) if residual else nn.Dropout(dropout)
+        self.compute_dtype = torch.float32
+
+    def forward(self, x, A):
+        if self.dropout and self.training:
+            raise NotImplementedError("stgcn_amd: dropout > 0 in training is not implemented (reference configs use 0)")
+        A_eff = A * self.edge_importance
+        n = self.bn_relu[0]
+        if self.is_residual_conv:
+            wr, nrw, nrb = self.residual[0].weight, self.residual[1].weight, self.residual[1].bias
+        else:
+            wr = nrw = nrb = None
+        cfg = (self.kernel_size, self.stride, self.is_residual, self.normalization, self.compute_dtype)
+        return LF.RtOfflineLayerFunction.apply(x, A_eff, self.conv.weight, self.conv.bias, n.weight, n.bias, wr,
+                                               nrw, nrb, cfg)
+
+
+class AggregateStgcn(nn.Module):
+    """Spatial mix + FIFO temporal aggregation of one frame (rtstgcn.py:556-627).
+
+    forward(x (1, P*C, 1, V) conv output) -> (1, C, 1, V).  ``A`` is this layer's adjacency copy
+    (OnlineLayer.eval_ folds the edge importance into it, rtstgcn.py:522-525)."""
+
+    def __init__(self, graph, fifo_size, kernel_size, out_channels, stride):
+        super().__init__()
+        self.out_channels = out_channels
+        self.num_joints = graph.shape[1]
+        self.stride = stride
+        self.fifo_size = fifo_size
+        self.kernel_size = kernel_size
+        V = graph.size(1)
+        self.register_buffer("A", graph.clone().detach().float(), persistent=False)
+        self.register_buffer("fifo", torch.zeros(fifo_size, V, out_channels), persistent=False)
+        self.register_buffer("accumulator", torch.zeros(stride, V, out_channels), persistent=False)
+        self.register_buffer("idx", torch.zeros(2, dtype=torch.int32), persistent=False)  # (fifo_idx, acc_idx)
+
+    def reset(self):
+        self.fifo.zero_()
+        self.accumulator.zero_()
+        self.idx.zero_()
+
+    def step(self, z):
+        """z: (1, C, 1, V) channels-last fp32 frame (already A-mixed and summed over partitions)."""
+        out = K.cl_empty(1, self.out_channels, 1, self.num_joints, torch.float32, z.device)
+        K.rt_online_step(z, self.fifo, self.accumulator, self.idx, self.out_channels, self.num_joints,
+                         self.fifo_size, self.stride, out)
+        return out
+
+
+class OnlineLayer(nn.Module):
+    def __init__(self, in_channels, out_channels, kernel_size, num_joints, stride, num_partitions, dropout,
+                 residual, importance, graph, normalization="LayerNorm"):
+        super().__init__()
+        assert kernel_size % 2 == 1
+        fifo_size = stride * (kernel_size - 1) + 1
+        self.is_residual = residual
+        self.is_residual_conv = residual and not ((in_channels == out_channels) and (stride == 1))
+        self.normalization = normalization
+        self.edge_importance = (nn.Parameter(torch.ones(num_partitions, num_joints, num_joints), requires_grad=False)
+                                if importance else 1)
+        self.conv = nn.Conv2d(in_channels, out_channels * num_partitions, kernel_size=1)
+        self.aggregate = AggregateStgcn(graph, fifo_size, kernel_size, out_channels, stride)
+        self.bn_relu = nn.Sequential(make_norm(normalization, out_channels, num_joints), nn.ReLU())
+        if self.is_residual_conv:
+            self.residual = nn.Sequential(nn.Conv2d(in_channels, out_channels, kernel_size=1, bias=False),
+                                          make_norm(normalization, out_channels, num_joints))
+        else:
+            self.residual = nn.Identity()
+        self.do = nn.Sequential(nn.ReLU(), nn.Dropout(dropout)) if residual else nn.Dropout(dropout)
+
+    def eval_(self):
+        self.aggregate.A *= self.edge_importance
+        return
+
+    @torch.no_grad()
+    def forward(self, x, A):
+        x = K.to_rows(x, torch.float32)
+        if x.shape[0] != 1 or x.shape[2] != 1:
+            raise RuntimeError("OnlineLayer processes one frame of batch 1 (rtstgcn.py:607)")
+        V = x.shape[3]
+        Cout = self.aggregate.out_channels
+        P = self.aggregate.A.shape[0]
+        Cin = x.shape[1]
+        _, z, _ = LF.gcn_forward(x, self.aggregate.A.contiguous(), self.conv.weight, self.conv.bias, torch.float32)
+        a = self.aggregate.step(z)
+        n = self.bn_relu[0]
+        relu_mode = 3 if self.is_residual else 2
+        if self.is_residual_conv:
+            wrp, cq, kq = K.pack_weight(self.residual[0].weight.float().view(1, Cout, Cin), torch.float32)
+            r = K.conv_rows(x, wrp, Cin, Cout, cq, kq, 1, 1)
+        res_mode = 2 if self.is_residual_conv else (1 if self.is_residual else 0)
+        res = r if self.is_residual_conv else (x if self.is_residual else None)
+        if self.normalization == "LayerNorm":
+            st = K.ln_stats(a, 1, V, Cout)
+            rst = rg = rb = None
+            if self.is_residual_conv:
+                rst = K.ln_stats(r, 1, V, Cout)
+                rg, rb = LF._flat_ln(self.residual[1].weight), LF._flat_ln(self.residual[1].bias)
+            return K.ln_apply(a, st, LF._flat_ln(n.weight), LF._flat_ln(n.bias), V, V, Cout, res_mode=res_mode,
+                              r=res, rst=rst, rg=rg, rb=rb, relu=relu_mode)
+        # batch-statistics BatchNorm over the V joints of the frame
+        part, nb, _ = K.bn_stats_partial(a, V, Cout)
+        _, sc, sh = K.bn_finalize(part, nb, Cout, Cout, n.weight.float(), n.bias.float())
+        rsc = rsh = None
+        if self.is_residual_conv:
+            rpart, rnb, _ = K.bn_stats_partial(r, V, Cout)
+            _, rsc, rsh = K.bn_finalize(rpart, rnb, Cout, Cout, self.residual[1].weight.float(),
+                                        self.residual[1].bias.float())
+        return K.bn_apply(a, sc, sh, V, Cout, res_mode=res_mode, r=res, rsc=rsc, rsh=rsh, relu=relu_mode)
+
+
+class Model(nn.Module):
+    """rt-st-gcn (rtstgcn.py:8-217): forward(x (N, C, L, V)) -> (N, num_classes, L)."""
+
+    def __init__(self, rank=None, **kwargs):
+        super().__init__()
+        self.conf = kwargs["rt-st-gcn"]
+        self.graph = Graph(strategy=kwargs["strategy"], **kwargs["graph"])
+        A = torch.tensor(self.graph.A, dtype=torch.float32, requires_grad=False)
+        self.register_buffer("A", A)
+        self.normalization = kwargs["normalization"]
+        self.norm_in = (LayerNorm([kwargs["in_feat"], 1, A.size(1)]) if kwargs["normalization"] == "LayerNorm"
+                        else BatchNorm1d(kwargs["in_feat"] * A.size(1), track_running_stats=False))
+        self.fcn_in = nn.Conv2d(in_channels=self.conf["in_feat"], out_channels=self.conf["in_ch"][0], kernel_size=1)
+        self.st_gcn = nn.ModuleList([self._layer(OfflineLayer, i, kwargs["graph"]["num_node"])
+                                     for i in range(self.conf["layers"])])
+        self.avg_pool = nn.AvgPool2d(kernel_size=(1, kwargs["graph"]["num_node"]))
+        self.fcn_out = nn.Conv2d(in_channels=self.conf["out_ch"][-1], out_channels=kwargs["num_classes"],
+                                 kernel_size=1)
+        self.compute_dtype = torch.float32
+        self.online = False
+
+    def _layer(self, cls, i, V):
+        return cls(num_joints=V, in_channels=self.conf["in_ch"][i], out_channels=self.conf["out_ch"][i],
+                   kernel_size=self.conf["kernel"], stride=self.conf["stride"][i], num_partitions=self.A.shape[0],
+                   residual=not not self.conf["residual"][i], dropout=self.conf["dropout"][i],
+                   importance=self.conf["importance"], graph=self.A, normalization=self.normalization)
+
+    def set_compute_dtype(self, dtype):
+        dt = resolve_dtype(dtype)
+        self.compute_dtype = dt
+        for layer in self.st_gcn:
+            if hasattr(layer, "compute_dtype"):
+                layer.compute_dtype = dt
+        return self
+
+    def forward(self, x):
+        x = self.norm_in(x)
+        C = x.shape[1]
+        if C % IN_PAD:
+            x = F.pad(x.permute(0, 2, 3, 1), (0, IN_PAD - C % IN_PAD)).permute(0, 3, 1, 2)
+            w = F.pad(self.fcn_in.weight, (0, 0, 0, 0, 0, IN_PAD - C % IN_PAD))
+        else:
+            w = self.fcn_in.weight
+        dt = torch.float32 if self.online else self.compute_dtype
+        x = LF.Conv1x1Function.apply(x, w, self.fcn_in.bias, dt)
+        for gcn in self.st_gcn:
+            x = gcn(x, self.A)
+        x = LF.PoolFunction.apply(x, dt, True)
+        x = LF.Conv1x1Function.apply(x, self.fcn_out.weight, self.fcn_out.bias, dt)
+        return x.squeeze(-1).float()
+
+    def _swap_layers_for_inference(self):
+        """Replace OfflineLayers by OnlineLayers carrying the same parameters (rtstgcn.py:160-187)."""
+        V = self.A.shape[-1]
+        new = nn.ModuleList([self._layer(OnlineLayer, i, V) for i in range(self.conf["layers"])])
+        new.load_state_dict(self.st_gcn.state_dict(), strict=False)
+        self.st_gcn = new.to(self.A.device)
+        self.online = True
+        return
+
+    def reset_state(self):
+        for layer in self.st_gcn:
+            if isinstance(layer, OnlineLayer):
+                layer.aggregate.reset()
+
+    def prepare_benchmark(self, arch_conf):
+        """Intended semantics of rtstgcn.py:190-197 (which calls a missing method): swap to online layers
+        and fold the edge importance (OnlineLayer.eval_)."""
+        self._swap_layers_for_inference()
+        for module in self.st_gcn:
+            module.eval_()
+        return arch_conf
