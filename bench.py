@@ -105,8 +105,7 @@ def main():
     model = model.to(dev).set_compute_dtype(args.dtype)
     train_model = model
     if world > 1:
-        from torch.nn.parallel import DistributedDataParallel as DDP
-        train_model = DDP(model, device_ids=[local], bucket_cap_mb=16, gradient_as_bucket_view=True)
+        train_model = pkg.parallel.ddp(model, dev, bucket_cap_mb=16)  # RCCL all-reduce of fp32 grads
     opt = torch.optim.Adam(model.parameters(), lr=5e-4, foreach=True)
 
     gen = torch.Generator(device=dev).manual_seed(rank)
