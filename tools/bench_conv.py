@@ -1,0 +1,56 @@
+"""Micro-benchmark of the row-conv kernels on the config-2 shapes (HIP-event timing).
+Usage: python tools/bench_conv.py [reps]"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import __graft_entry__ as ge  # noqa: E402
+
+P = ge.load_package()
+K = P.native
+dev = "cuda:0"
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+dt = torch.bfloat16
+
+
+def timeit(fn):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+cases = [  # name, N, T, V, Cin, Cout, Kt, stride, trans, pro
+    ("tcn_fwd_c64", 64, 300, 25, 64, 64, 9, 1, False, 1),
+    ("tcn_dgrad_c64", 64, 300, 25, 64, 64, 9, 1, True, 0),
+    ("gcn_gemm_c64", 64, 300, 25, 192, 64, 1, 1, False, 0),
+    ("tcn_fwd_c128", 64, 150, 25, 128, 128, 9, 1, False, 1),
+    ("tcn_fwd_c256", 64, 75, 25, 256, 256, 9, 1, False, 1),
+    ("gcn_gemm_c256", 64, 75, 25, 768, 256, 1, 1, False, 0),
+]
+only = sys.argv[2] if len(sys.argv) > 2 else None
+for name, N, T, V, Cin, Cout, Kt, s, trans, pro in cases:
+    if only and name != only:
+        continue
+    pad = (Kt - 1) // 2
+    T_out = T if s == 1 else (T - 1) // s + 1
+    Ti, To = (T_out, T) if trans else (T, T_out)
+    x = torch.randn(N, Cin, Ti, V, device=dev).to(dt).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(Kt, Cout, Cin, device=dev) * 0.05
+    wp, cp, kp = K.pack_weight(w, dt)
+    sc = torch.rand(Cin, device=dev) + 0.5
+    sh = torch.randn(Cin, device=dev)
+    b = torch.randn(Cout, device=dev)
+    kw = dict(pro=1, pro_a=sc, pro_b=sh) if pro else {}
+    f = lambda: K.conv_rows(x, wp, Cin, Cout, cp, kp, Ti, To, Kt=Kt, stride=s, pad=pad, trans=trans, bias=b, **kw)
+    ms = timeit(f)
+    flops = 2.0 * N * To * V * Cin * Cout * Kt
+    byts = (N * Ti * V * Cin + N * To * V * Cout) * 2
+    print(f"{name:16s} {ms*1e3:9.1f} us  {flops/ms/1e9:8.1f} TFLOP/s  {byts/ms/1e6:8.1f} GB/s", flush=True)
