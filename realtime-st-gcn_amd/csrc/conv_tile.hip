@@ -1,0 +1,480 @@
+// Frame-tiled implicit-GEMM row convolution (v2) — the fast path of stgcn_conv_rows.
+//
+// Same contract as conv_rows.hip (stgcn_conv_desc; see that file for the math).  Handles
+//   * stride-1 Kt x 1 convs, forward and transposed (temporal conv fwd + data grad, stgcn.py:154-159)
+//   * stride-2 Kt x 1 convs, forward (the strided temporal conv / residual conv of layers 4 and 7)
+//   * flat 1x1 convs (gcn.conv on the A-mixed rows, fcn_in/out, 1x1 data grads)
+// and returns -1 for anything else (the caller falls back to conv_rows.hip).
+//
+// Why a second kernel: conv_rows.hip re-gathers a BM-row tile for every tap, re-applying the
+// BatchNorm+ReLU prologue Kt times per element and doing 64-bit address math and a validity test
+// per 16-B unit and tap (~48 VALU per MFMA measured, profiles/).  Here a block owns F whole frames
+// of ONE sample (F = floor(BM / V)), so
+//   * the block stages ONE halo of S*(F-1)+Kt frames per K-chunk (prologue applied once per element;
+//     frames outside [0, T_in) are written as zeros = the conv's zero padding AFTER the prologue),
+//   * tap dt of MFMA row r reads LDS row base(r) + q(dt)*V with q(dt) = dt (fwd) or Kt-1-dt
+//     (trans): no per-fragment masking, only a uniform offset per tap,
+//   * rows of the last, partial tile are simply not stored.
+// Flat mode (Kt = 1, stride 1) tiles BM consecutive rows across samples instead.
+//
+// Block: WM x WN waves, wave (wm, wn) owns TM x TN 32x32 MFMA tiles.  K is walked in chunks of
+// KC input channels; per chunk the A halo (register-staged: global -> regs -> prologue -> LDS,
+// padded rows of KC*sizeof(T)+16 B, conflict-free ds_read_b128) and the B tile of all Kt taps
+// (LDS-DMA global_load_lds_dwordx4, lane-linear image with the XOR swizzle applied on the source
+// address) are double-buffered: chunk c+1 is issued before chunk c's Kt*KC/16*TM*TN MFMAs and
+// written after them, one barrier per chunk.  blockIdx is remapped so consecutive tiles (which
+// share halo frames and, for several column tiles, the whole A halo) land on the same XCD.
+#include "common.h"
+#include "../../include/stgcn_amd.h"
+#include <stdlib.h>
+
+namespace {
+
+template <typename T, int KC>
+struct TL {
+  static constexpr int RB = KC * (int)sizeof(T);        // B row bytes (swizzled LDS-DMA image)
+  static constexpr int UPR = RB / 16;                    // 16-B units per row
+  static constexpr int RPB = RB >= 256 ? 1 : 256 / RB;   // rows per 256-B bank row
+  static constexpr int RS = RB + 16;                     // A row stride (padded)
+  static DEV int swz(int row) { return (row / RPB) & (UPR - 1); }
+};
+
+// 16-byte LDS-DMA: lane l writes lds_base + 16*l (device-only builtin)
+DEV void glds16(const void* src, char* lds_base) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+#endif
+}
+
+template <typename T>
+DEV typename Tr<T>::frag frag2(const char* p0, const char* p1) {
+  if constexpr (sizeof(T) == 2) {
+    (void)p1;
+    return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(p0));
+  } else {
+    const f32x4 a = __builtin_bit_cast(f32x4, *reinterpret_cast<const uint4*>(p0));
+    const f32x4 b = __builtin_bit_cast(f32x4, *reinterpret_cast<const uint4*>(p1));
+    f32x8 f;
+    f[0] = a[0]; f[1] = a[1]; f[2] = a[2]; f[3] = a[3];
+    f[4] = b[0]; f[5] = b[1]; f[6] = b[2]; f[7] = b[3];
+    return f;
+  }
+}
+
+struct TileGeom {
+  int F;        // output frames per tile (framed) ; 0 = flat mode
+  int tiles_n;  // tiles per sample (framed) or total row tiles (flat)
+  int HR;       // staged A rows per chunk
+  int ncol;     // column tiles
+  int nblk;     // total blocks
+};
+
+template <typename T, int WM, int WN, int TM, int TN, int KC, int KT, int S, int MINW>
+__global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stgcn_conv_desc a, const TileGeom g) {
+  typedef TL<T, KC> L;
+  constexpr int NW = WM * WN, NT = NW * 64;
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  constexpr int VEC = 16 / (int)sizeof(T);
+  constexpr int KS = KC / 16;
+  constexpr int HR_MAX = S * BM + (KT - S > 0 ? (KT - S) * 32 : 0);  // V <= 32 (checked at launch)
+  constexpr int A_MAX = (HR_MAX * L::UPR + NT - 1) / NT;
+  constexpr int B_BYTES = KT * BN * L::RB;
+  constexpr int B_PIECES = B_BYTES / 1024;
+  static_assert(B_BYTES % 1024 == 0, "B tile must be whole 1-KiB LDS-DMA pieces");
+  static_assert(NT % L::UPR == 0, "unit column must be fixed per thread");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int A_BYTES = (g.HR * L::RS + 1023) & ~1023;
+  const int STAGE = A_BYTES + B_BYTES;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int V = a.V;
+
+  // ---- XCD-aware tile order (bijective): blocks b, b+8, b+16, ... share an XCD -> give them
+  // consecutive tiles (same sample, neighbouring frames, all column tiles of a row tile).
+  int wg;
+  {
+    const int id = blockIdx.x, x = id & 7, q = g.nblk >> 3, r = g.nblk & 7;
+    wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (id >> 3);
+  }
+  const int ct = wg % g.ncol, rt = wg / g.ncol;
+  const int n0 = ct * BN;
+
+  // ---- tile geometry
+  long row0;       // first output row of the tile
+  int rows_valid;  // output rows of this tile
+  long src0;       // flat: first input row ; framed: first input row of sample n
+  int fi0 = 0;     // framed: first halo input frame
+  if (g.F) {
+    const int n = rt / g.tiles_n, f0 = (rt % g.tiles_n) * g.F;
+    const int fe = min(g.F, a.T_out - f0);
+    row0 = ((long)n * a.T_out + f0) * V;
+    rows_valid = fe * V;
+    src0 = (long)n * a.T_in * V;
+    fi0 = f0 * S - ((KT - 1) / 2) * (KT > 1);
+  } else {
+    row0 = (long)rt * BM;
+    const long M = (long)a.N * a.T_out * V;
+    rows_valid = (int)min((long)BM, M - row0);
+    src0 = row0;
+  }
+
+  const T* __restrict__ in = reinterpret_cast<const T*>(a.in);
+  const T* __restrict__ wp = reinterpret_cast<const T*>(a.w);
+
+  // ---- per-thread A staging units (row, unit column fixed per thread)
+  const int ucol = tid % L::UPR;
+  const int a_units = g.HR * L::UPR;
+  const T* a_ptr[A_MAX];  // chunk-0 source of each unit (nullptr = zero row)
+  int a_lds[A_MAX];       // LDS byte offset within the A stage
+  int a_src[A_MAX];       // source row index relative to src0 (LN prologue), -1 = zero
+#pragma unroll
+  for (int i = 0; i < A_MAX; ++i) {
+    const int id = tid + i * NT;
+    const int row = id / L::UPR;
+    a_ptr[i] = nullptr;
+    a_src[i] = -1;
+    a_lds[i] = row * L::RS + ucol * 16;
+    if (id < a_units) {
+      int sr;
+      bool ok;
+      if (g.F) {
+        const int fl = row / V, v = row - fl * V, fi = fi0 + fl;
+        ok = fi >= 0 && fi < a.T_in;
+        sr = fi * V + v;
+      } else {
+        sr = row;
+        ok = row < rows_valid;
+      }
+      if (ok) {
+        a_src[i] = sr;
+        a_ptr[i] = in + (src0 + sr) * a.in_ld + ucol * VEC;
+      }
+    } else {
+      a_lds[i] = -1;
+    }
+  }
+  const bool fast_ld = (a.in_ld % VEC) == 0 && (a.Cin % KC) == 0;
+
+  // ---- per-lane fragment offsets
+  int a_off[TM];  // byte offset of this lane's row (tap 0) within the A stage
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = (wm * TM + i) * 32 + lr;
+    int br;
+    if (g.F) {
+      if (r < g.F * V) {
+        const int fl = r / V;
+        br = (S * fl) * V + (r - fl * V);
+      } else {
+        br = 0;  // padding rows of the MFMA tile: read anything in range, never stored
+      }
+    } else {
+      br = r;
+    }
+    a_off[i] = br * L::RS + lh * 16 * (int)(sizeof(T) / 2);
+  }
+  int b_off[KS][2];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int f = L::swz(lr);  // rows dt*BN + j*32 + lr share lr's swizzle (BN, 32 multiples of RPB*UPR)
+    if constexpr (sizeof(T) == 2) {
+      b_off[ks][0] = lr * L::RB + (((2 * ks + lh) ^ f) << 4);
+      b_off[ks][1] = b_off[ks][0];
+    } else {
+      b_off[ks][0] = lr * L::RB + (((4 * ks + 2 * lh) ^ f) << 4);
+      b_off[ks][1] = lr * L::RB + (((4 * ks + 2 * lh + 1) ^ f) << 4);
+    }
+  }
+
+  const int nchunks = a.Cin_pad / KC;
+  uint4 ra[A_MAX];
+  float sc[VEC], sh[VEC];
+
+  auto load = [&](int c, int buf) {
+    const int cb = c * KC;
+#pragma unroll
+    for (int i = 0; i < A_MAX; ++i) {
+      ra[i] = make_uint4(0, 0, 0, 0);
+      if (a_ptr[i] != nullptr) {
+        const T* p = a_ptr[i] + cb;
+        const int ci = cb + ucol * VEC;
+        if (fast_ld) {
+          ra[i] = *reinterpret_cast<const uint4*>(p);
+        } else if (ci < a.Cin) {
+          float f[VEC];
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) f[j] = ci + j < a.Cin ? Tr<T>::to_f(p[j]) : 0.f;
+          ra[i] = pack16(f, (T*)nullptr);
+        }
+      }
+    }
+    if (a.pro == 1) {
+      const int ci = cb + ucol * VEC;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        sc[j] = ci + j < a.Cin ? a.pro_a[ci + j] : 0.f;
+        sh[j] = ci + j < a.Cin ? a.pro_b[ci + j] : 0.f;
+      }
+    }
+    char* B_ = smem + buf * STAGE + A_BYTES;
+#pragma unroll
+    for (int k = 0; k < (B_PIECES + NW - 1) / NW; ++k) {
+      const int piece = wave + k * NW;
+      if (piece < B_PIECES) {
+        const int byte = piece * 1024 + lane * 16;
+        const int br = byte / L::RB, pu = (byte % L::RB) >> 4;
+        const int u = pu ^ L::swz(br);
+        const int dt = br / BN, col = br % BN;
+        glds16(wp + ((long)dt * a.Cout_pad + n0 + col) * a.Cin_pad + cb + u * VEC, B_ + piece * 1024);
+      }
+    }
+  };
+
+  auto store = [&](int c, int buf) {
+    char* A_ = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < A_MAX; ++i) {
+      if (a_lds[i] >= 0) {
+        uint4 v = ra[i];
+        if (a.pro != 0 && a_src[i] >= 0) {
+          float f[VEC];
+          unpack16(v, f, (T*)nullptr);
+          if (a.pro == 1) {
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) f[j] = fmaxf(fmaf(f[j], sc[j], sh[j]), 0.f);
+          } else {
+            const long srow = src0 + a_src[i];
+            const float2 st = reinterpret_cast<const float2*>(a.pro_stats)[srow / V];
+            const int av = (int)(srow % V);
+            const int ci = c * KC + ucol * VEC;
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) {
+              const int gi = (ci + j) * V + av;
+              f[j] = ci + j < a.Cin ? fmaxf((f[j] - st.x) * st.y * a.pro_a[gi] + a.pro_b[gi], 0.f) : 0.f;
+            }
+          }
+          v = pack16(f, (T*)nullptr);
+        }
+        *reinterpret_cast<uint4*>(A_ + a_lds[i]) = v;
+      }
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  load(0, 0);
+  store(0, 0);
+  __syncthreads();
+  int cur = 0;
+  const int tap_stride = V * L::RS;
+  const bool rev = KT > 1 && a.trans;
+  constexpr int NSTEP = KT * KS;  // k-steps of 16 per chunk
+  typedef typename Tr<T>::frag Frag;
+  for (int c = 0; c < nchunks; ++c) {
+    const bool more = c + 1 < nchunks;
+    if (more) load(c + 1, cur ^ 1);
+    const char* A_ = smem + cur * STAGE;
+    const char* B_ = A_ + A_BYTES;
+    // fragments of k-step st+1 are read while the MFMAs of k-step st run (explicit double buffer;
+    // sched_barrier keeps the compiler from hoisting every tap's reads and blowing the VGPR budget)
+    Frag fa[2][TM], fb[2][TN];
+    auto rd = [&](int st, int b) {
+      const int dt = st / KS, ks = st % KS;
+      const int q = rev ? KT - 1 - dt : dt;
+      const char* At = A_ + q * tap_stride + ks * 16 * (int)sizeof(T);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[b][i] = frag2<T>(At + a_off[i], At + a_off[i] + 16);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const char* p = B_ + (dt * BN + (wn * TN + j) * 32) * L::RB;
+        fb[b][j] = frag2<T>(p + b_off[ks][0], p + b_off[ks][1]);
+      }
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int st = 0; st < NSTEP; ++st) {
+      if (st + 1 < NSTEP) rd(st + 1, (st + 1) & 1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) Tr<T>::mma(acc[i][j], fa[st & 1][i], fb[st & 1][j]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (more) store(c + 1, cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  // lane holds column col of rows lb(i) + (r&3) + 8*(r>>2) (32x32 C/D map); row offsets are
+  // compile-time multiples of the uniform out_ld.
+  T* __restrict__ out = reinterpret_cast<T*>(a.out);
+  const long ld = a.out_ld;
+  Welford ws[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + (wn * TN + j) * 32 + lr;
+    const bool cok = col < a.Cout;
+    const float b1 = (a.bias_mode == 1 && cok) ? a.bias[col] : 0.f;
+    float s = 0.f, cnt = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int lb = (wm * TM + i) * 32 + 4 * lh;
+      T* pb = out + (row0 + lb) * ld + col;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ro = (r & 3) + 8 * (r >> 2);
+        const bool ok = cok && lb + ro < rows_valid;
+        float v = acc[i][j][r] + b1;
+        if (a.bias_mode >= 2 && ok) {
+          const long m = row0 + lb + ro;
+          const long nt = m / V;
+          long bi = m - nt * V;
+          if (a.bias_mode == 3) bi += (nt / a.T_out) * V;
+          v += a.bias[bi * a.Cout + col];
+        }
+        if (ok) {
+          T* p = pb + ro * ld;
+          if (a.accumulate) v += Tr<T>::to_f(*p);
+          *p = Tr<T>::from_f(v);
+          s += v;
+          cnt += 1.f;
+        }
+        acc[i][j][r] = v;
+      }
+    }
+    Welford w;
+    w.n = cnt;
+    w.mean = cnt > 0.f ? s / cnt : 0.f;
+    float m2 = 0.f;
+    if (a.stats) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int lb = (wm * TM + i) * 32 + 4 * lh;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float d = acc[i][j][r] - w.mean;
+          if (cok && lb + (r & 3) + 8 * (r >> 2) < rows_valid) m2 += d * d;
+        }
+      }
+    }
+    w.m2 = m2;
+    ws[j] = w;
+  }
+  if (a.stats) {
+    __syncthreads();
+    float4* red = reinterpret_cast<float4*>(smem);  // [WM][BN]
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      Welford o;
+      o.n = __shfl_xor(ws[j].n, 32);
+      o.mean = __shfl_xor(ws[j].mean, 32);
+      o.m2 = __shfl_xor(ws[j].m2, 32);
+      const Welford w = welford_merge(ws[j], o);
+      if (lh == 0) red[wm * BN + (wn * TN + j) * 32 + lr] = make_float4(w.n, w.mean, w.m2, 0.f);
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += NT) {
+      const float4 f = red[c];
+      Welford w = {f.x, f.y, f.z};
+      for (int k = 1; k < WM; ++k) {
+        const float4 h = red[k * BN + c];
+        w = welford_merge(w, Welford{h.x, h.y, h.z});
+      }
+      if (n0 + c < a.Cout_pad)
+        reinterpret_cast<float4*>(a.stats)[(long)rt * a.Cout_pad + n0 + c] = make_float4(w.n, w.mean, w.m2, 0.f);
+    }
+  }
+}
+
+template <typename T, int WM, int WN, int TM, int TN, int KC, int KT, int S, int MINW = 2>
+int launch_tile(const stgcn_conv_desc& a, long max_row_blocks, hipStream_t s) {
+  typedef TL<T, KC> L;
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  constexpr int HR_MAX = S * BM + (KT - S > 0 ? (KT - S) * 32 : 0);
+  if (a.Cout_pad % BN || a.Cin_pad % KC) return -1;
+  TileGeom g;
+  const bool flat = KT == 1 && S == 1;
+  if (flat) {
+    const long M = (long)a.N * a.T_out * a.V;
+    g.F = 0;
+    g.tiles_n = (int)((M + BM - 1) / BM);
+    g.HR = BM;
+  } else {
+    if (a.V > 32 || a.V > BM) return -1;
+    g.F = BM / a.V;
+    g.tiles_n = (a.T_out + g.F - 1) / g.F;
+    g.HR = (S * (g.F - 1) + KT) * a.V;
+    if (g.HR > HR_MAX) return -1;
+  }
+  g.ncol = a.Cout_pad / BN;
+  const long rows_tiles = flat ? (long)g.tiles_n : (long)a.N * g.tiles_n;
+  if (a.stats && rows_tiles > max_row_blocks) return -1;
+  const long nblk = rows_tiles * g.ncol;
+  if (nblk <= 0 || nblk > 0x7fffffffL) return -1;
+  g.nblk = (int)nblk;
+  const int A_BYTES = (g.HR * L::RS + 1023) & ~1023;
+  size_t lds = 2 * (size_t)(A_BYTES + KT * BN * L::RB);
+  const size_t red = a.stats ? (size_t)WM * BN * 16 : 0;
+  if (red > lds) lds = red;
+  if (lds > 160 * 1024) return -1;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL((conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW>), dim3((unsigned)nblk), dim3(WM * WN * 64), lds,
+                     s, a, g);
+  return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
+}
+
+template <typename T, int KT, int S>
+int tile_dispatch(const stgcn_conv_desc& a, long mrb, hipStream_t s) {
+  // column tile follows conv_rows_bn_tile: 64 for Cout <= 64, else 128
+  static const int wide_cfg = getenv("STGCN_TILE_WIDE") ? atoi(getenv("STGCN_TILE_WIDE")) : 0;
+  const bool wide = a.Cout > 64;
+  if constexpr (sizeof(T) == 2) {
+    constexpr int KCB = (KT == 1 && S == 1) ? 32 : 16;  // flat GEMM: deeper chunks
+    if (!wide) return launch_tile<T, 4, 1, 2, 2, KCB, KT, S>(a, mrb, s);
+    if (wide_cfg == 1) return launch_tile<T, 2, 2, 4, 2, KCB, KT, S, 1>(a, mrb, s);
+    return launch_tile<T, 4, 2, 2, 2, KCB, KT, S>(a, mrb, s);
+  } else {
+    return wide ? launch_tile<T, 4, 2, 2, 2, 16, KT, S, 1>(a, mrb, s) : launch_tile<T, 4, 1, 2, 2, 16, KT, S, 1>(a, mrb, s);
+  }
+}
+
+}  // namespace
+
+long conv_rows_num_row_blocks(long M, int cout);
+
+// returns -1 when the shape is not handled here (caller falls back to conv_rows.hip)
+int conv_tile_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
+  const long mrb = conv_rows_num_row_blocks((long)a.N * a.T_out * a.V, a.Cout);
+  const int S = a.stride;
+  if (a.Kt == 1) {
+    if (a.pad != 0) return -1;
+    if (S == 1) {
+      if (a.T_in != a.T_out) return -1;
+      return dtype ? tile_dispatch<bf16, 1, 1>(a, mrb, s) : tile_dispatch<float, 1, 1>(a, mrb, s);
+    }
+    if (S == 2 && !a.trans && a.T_out == (a.T_in - 1) / 2 + 1)
+      return dtype ? tile_dispatch<bf16, 1, 2>(a, mrb, s) : tile_dispatch<float, 1, 2>(a, mrb, s);
+    return -1;
+  }
+  if (a.Kt != 9 || a.pad != 4) return -1;
+  if (S == 1 && a.T_out == a.T_in)
+    return dtype ? tile_dispatch<bf16, 9, 1>(a, mrb, s) : tile_dispatch<float, 9, 1>(a, mrb, s);
+  if (S == 2 && !a.trans && a.T_out == (a.T_in + 2 * 4 - 9) / 2 + 1)
+    return dtype ? tile_dispatch<bf16, 9, 2>(a, mrb, s) : tile_dispatch<float, 9, 2>(a, mrb, s);
+  return -1;
+}

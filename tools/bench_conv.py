@@ -34,6 +34,10 @@ cases = [  # name, N, T, V, Cin, Cout, Kt, stride, trans, pro
     ("tcn_fwd_c128", 64, 150, 25, 128, 128, 9, 1, False, 1),
     ("tcn_fwd_c256", 64, 75, 25, 256, 256, 9, 1, False, 1),
     ("gcn_gemm_c256", 64, 75, 25, 768, 256, 1, 1, False, 0),
+    ("tcn_dgrad_c128", 64, 150, 25, 128, 128, 9, 1, True, 0),
+    ("tcn_dgrad_c256", 64, 75, 25, 256, 256, 9, 1, True, 0),
+    ("tcn_fwd_s2_c128", 64, 300, 25, 128, 128, 9, 2, False, 1),
+    ("gcn_gemm_c128", 64, 150, 25, 384, 128, 1, 1, False, 0),
 ]
 only = sys.argv[2] if len(sys.argv) > 2 else None
 for name, N, T, V, Cin, Cout, Kt, s, trans, pro in cases:
@@ -49,6 +53,8 @@ for name, N, T, V, Cin, Cout, Kt, s, trans, pro in cases:
     sh = torch.randn(Cin, device=dev)
     b = torch.randn(Cout, device=dev)
     kw = dict(pro=1, pro_a=sc, pro_b=sh) if pro else {}
+    if not trans:  # forward convs feed a BatchNorm: epilogue partial statistics
+        kw["stats"] = torch.zeros((K.row_blocks(N * To * V, Cout), cp, 4), device=dev)
     f = lambda: K.conv_rows(x, wp, Cin, Cout, cp, kp, Ti, To, Kt=Kt, stride=s, pad=pad, trans=trans, bias=b, **kw)
     ms = timeit(f)
     flops = 2.0 * N * To * V * Cin * Cout * Kt
