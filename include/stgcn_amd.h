@@ -62,9 +62,13 @@ typedef struct {
   int N, T_in, T_out, V, Cin, Cout, Kt, stride, pad, pro;
   int in_ld, dy_ld;
   long rows_per_block; /* filled by the library */
+  void* work;          /* optional workspace (bf16 frame-tiled path: per-block fp32 partials) */
+  long work_bytes;     /* its size; stgcn_conv_wgrad_workspace() tells how much the fast path needs */
 } stgcn_wgrad_desc;
 
 int stgcn_conv_wgrad(const stgcn_wgrad_desc* d, int dtype, void* stream);
+/* workspace bytes for the deterministic frame-tiled path (0: shape/dtype served without one) */
+long stgcn_conv_wgrad_workspace(const stgcn_wgrad_desc* d, int dtype);
 
 /* Graph (joint-axis) mixing of ConvTemporalGraphical (models/utils/tgcn.py:58-79), A applied first.
  *   fwd  : XA[(n,t,w)][p*Cin+ci] = sum_v A[(n),p,v,w] x[(n,t,v)][ci]             (tgcn.py:76)

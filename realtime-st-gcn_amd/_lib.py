@@ -32,7 +32,8 @@ class WgradDesc(ctypes.Structure):
     _fields_ = [("in_", c_void_p), ("dy", c_void_p), ("dw", c_void_p), ("pro_a", c_void_p), ("pro_b", c_void_p),
                 ("pro_stats", c_void_p)] + \
                [(n, c_int) for n in ("N", "T_in", "T_out", "V", "Cin", "Cout", "Kt", "stride", "pad", "pro",
-                                     "in_ld", "dy_ld")] + [("rows_per_block", c_long)]
+                                     "in_ld", "dy_ld")] + [("rows_per_block", c_long), ("work", c_void_p),
+                                                           ("work_bytes", c_long)]
 
 
 class AmixDesc(ctypes.Structure):
@@ -47,6 +48,7 @@ _SIGS = {
     "stgcn_conv_rows_col_tile": (c_int, [c_int]),
     "stgcn_conv_rows_row_blocks": (c_long, [c_long, c_int]),
     "stgcn_conv_wgrad": (c_int, [ctypes.POINTER(WgradDesc), c_int, c_void_p]),
+    "stgcn_conv_wgrad_workspace": (c_long, [ctypes.POINTER(WgradDesc), c_int]),
     "stgcn_amix_fwd": (c_int, [ctypes.POINTER(AmixDesc), c_int, c_void_p]),
     "stgcn_amix_trans": (c_int, [ctypes.POINTER(AmixDesc), c_int, c_void_p]),
     "stgcn_amix_dA": (c_int, [ctypes.POINTER(AmixDesc), c_void_p, c_void_p, c_int, c_void_p]),

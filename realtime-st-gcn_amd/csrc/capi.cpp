@@ -17,6 +17,8 @@ int conv_rows_launch(const ConvArgs& a, int dtype, hipStream_t s);
 int conv_rows_bn_tile(int cout);
 long conv_rows_num_row_blocks(long M, int cout);
 int conv_wgrad_launch(WgradArgs a, int dtype, hipStream_t s);
+long wgrad_tile_workspace(const WgradArgs& a, int dtype);
+int wgrad_tile_launch(const WgradArgs& a, int dtype, hipStream_t s);
 int amix_fwd_launch(const AmixArgs& a, int dtype, hipStream_t s);
 int amix_trans_launch(const AmixArgs& a, int dtype, hipStream_t s);
 int amix_dA_launch(const AmixArgs& a, const void* dw, float* dA, int dtype, hipStream_t s);
@@ -81,10 +83,17 @@ int stgcn_conv_rows(const stgcn_conv_desc* d, int dtype, void* stream) {
 int stgcn_conv_rows_col_tile(int cout) { return conv_rows_bn_tile(cout); }
 long stgcn_conv_rows_row_blocks(long M, int cout) { return conv_rows_num_row_blocks(M, cout); }
 
+long stgcn_conv_wgrad_workspace(const stgcn_wgrad_desc* d, int dtype) {
+  if (!d || (dtype != 0 && dtype != 1)) return 0;
+  return wgrad_tile_workspace(*d, dtype);
+}
+
 int stgcn_conv_wgrad(const stgcn_wgrad_desc* d, int dtype, void* stream) {
   CHECK_DTYPE(dtype);
   if (!d || !d->in || !d->dy || !d->dw || d->N <= 0 || d->Kt <= 0 || d->stride <= 0) return STGCN_EBADSHAPE;
   if (d->pro && (!d->pro_a || !d->pro_b || (d->pro == 2 && !d->pro_stats))) return STGCN_EBADSHAPE;
+  const int r = wgrad_tile_launch(*d, dtype, STREAM(stream));  // bf16 frame-tiled path (needs work)
+  if (r >= 0) return r;
   return conv_wgrad_launch(*d, dtype, STREAM(stream));
 }
 

@@ -106,7 +106,12 @@ def conv_wgrad(x, dy, Cin, Cout, T_in, T_out, Kt=1, stride=1, pad=0, pro=0, pro_
     d.N, d.T_in, d.T_out, d.V, d.Cin, d.Cout, d.Kt, d.stride, d.pad, d.pro = \
         N, T_in, T_out, V, Cin, Cout, Kt, stride, pad, pro
     d.in_ld, d.dy_ld = rows_ld(x), rows_ld(dy)
-    L.check(L.lib().stgcn_conv_wgrad(d, L.dtype_code(x.dtype), L.stream()), "conv_wgrad")
+    code = L.dtype_code(x.dtype)
+    nbytes = L.lib().stgcn_conv_wgrad_workspace(d, code)
+    if nbytes > 0:  # per-block fp32 partials of the deterministic frame-tiled path
+        work = torch.empty(nbytes // 4, dtype=torch.float32, device=x.device)
+        d.work, d.work_bytes = work.data_ptr(), nbytes
+    L.check(L.lib().stgcn_conv_wgrad(d, code, L.stream()), "conv_wgrad")
     return dw
 
 

@@ -50,7 +50,9 @@ def test_conv_rows_fwd_and_trans(K, dtype, tol, cin, cout, kt, stride, T):
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 2e-2)])
 @pytest.mark.parametrize("cin,cout,kt,stride,T", [(64, 64, 9, 1, 37), (32, 128, 9, 2, 30), (16, 24, 1, 1, 11),
-                                                  (128, 64, 9, 1, 12), (24, 48, 9, 2, 11)])
+                                                  (128, 64, 9, 1, 12), (24, 48, 9, 2, 11), (64, 64, 1, 2, 21),
+                                                  (192, 64, 1, 1, 40), (256, 256, 9, 1, 10), (128, 256, 9, 2, 30),
+                                                  (128, 128, 1, 2, 9), (96, 40, 9, 1, 3)])
 def test_conv_wgrad(K, dtype, tol, cin, cout, kt, stride, T):
     torch.manual_seed(1)
     N, V = 3, 25
@@ -62,6 +64,32 @@ def test_conv_wgrad(K, dtype, tol, cin, cout, kt, stride, T):
     y.backward(dy)
     dw = K.conv_wgrad(cl(x, dtype), cl(dy, dtype), cin, cout, T, y.shape[2], Kt=kt, stride=stride, pad=pad)
     assert_close(dw.cpu().permute(1, 2, 0).unsqueeze(-1), w.grad, tol, "wgrad")
+
+
+@pytest.mark.parametrize("pro", [1, 2])
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 2e-2)])
+@pytest.mark.parametrize("stride", [1, 2])
+def test_conv_wgrad_prologue(K, pro, dtype, tol, stride):
+    """dW with the BatchNorm+ReLU (pro 1) or LayerNorm+ReLU (pro 2) prologue applied to the input."""
+    torch.manual_seed(5)
+    N, C, Co, T, V = 4, 64, 128, 33, 25
+    x = torch.randn(N, C, T, V) * 1.5 + 0.3
+    if pro == 1:
+        pa, pb = torch.rand(C) + 0.5, torch.randn(C)
+        h = torch.relu(x * pa.view(1, -1, 1, 1) + pb.view(1, -1, 1, 1))
+        kw = dict(pro_a=pa.to(DEV), pro_b=pb.to(DEV))
+    else:
+        mu, rs = torch.randn(N, T), torch.rand(N, T) + 0.5
+        pa, pb = torch.rand(C, V) + 0.5, torch.randn(C, V)
+        h = torch.relu((x - mu.view(N, 1, T, 1)) * rs.view(N, 1, T, 1) * pa.view(1, C, 1, V) + pb.view(1, C, 1, V))
+        kw = dict(pro_a=pa.reshape(-1).to(DEV), pro_b=pb.reshape(-1).to(DEV),
+                  pro_stats=torch.stack([mu, rs], -1).reshape(-1, 2).to(DEV).contiguous())
+    w = (torch.randn(Co, C, 9, 1) / 24).requires_grad_(True)
+    y = F.conv2d(h, w, None, stride=(stride, 1), padding=(4, 0))
+    dy = torch.randn(y.shape)
+    y.backward(dy)
+    dw = K.conv_wgrad(cl(x, dtype), cl(dy, dtype), C, Co, T, y.shape[2], Kt=9, stride=stride, pad=4, pro=pro, **kw)
+    assert_close(dw.cpu().permute(1, 2, 0).unsqueeze(-1), w.grad, tol, "wgrad+prologue")
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

@@ -60,3 +60,29 @@ for name, N, T, V, Cin, Cout, Kt, s, trans, pro in cases:
     flops = 2.0 * N * To * V * Cin * Cout * Kt
     byts = (N * Ti * V * Cin + N * To * V * Cout) * 2
     print(f"{name:16s} {ms*1e3:9.1f} us  {flops/ms/1e9:8.1f} TFLOP/s  {byts/ms/1e6:8.1f} GB/s", flush=True)
+
+wcases = [  # name, N, T, V, Cin, Cout, Kt, stride, pro
+    ("tcn_wgrad_c64", 64, 300, 25, 64, 64, 9, 1, 1),
+    ("tcn_wgrad_c128", 64, 150, 25, 128, 128, 9, 1, 1),
+    ("tcn_wgrad_c256", 64, 75, 25, 256, 256, 9, 1, 1),
+    ("tcn_wgrad_s2_c128", 64, 300, 25, 128, 128, 9, 2, 1),
+    ("gcn_wgrad_c64", 64, 300, 25, 192, 64, 1, 1, 0),
+    ("gcn_wgrad_c256", 64, 75, 25, 768, 256, 1, 1, 0),
+    ("res_wgrad_s2_c128", 64, 300, 25, 64, 128, 1, 2, 0),
+]
+for name, N, T, V, Cin, Cout, Kt, s, pro in wcases:
+    if only and name != only:
+        continue
+    pad = (Kt - 1) // 2
+    T_out = (T + 2 * pad - Kt) // s + 1
+    x = torch.randn(N, Cin, T, V, device=dev).to(dt).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(N, Cout, T_out, V, device=dev).to(dt).contiguous(memory_format=torch.channels_last)
+    sc = torch.rand(Cin, device=dev) + 0.5
+    sh = torch.randn(Cin, device=dev)
+    kw = dict(pro=1, pro_a=sc, pro_b=sh) if pro else {}
+    dw = torch.zeros((Kt, Cout, Cin), device=dev)
+    f = lambda: K.conv_wgrad(x, dy, Cin, Cout, T, T_out, Kt=Kt, stride=s, pad=pad, dw=dw, **kw)
+    ms = timeit(f)
+    flops = 2.0 * N * T_out * V * Cin * Cout * Kt
+    byts = (N * T * V * Cin + N * T_out * V * Cout) * 2
+    print(f"{name:18s} {ms*1e3:9.1f} us  {flops/ms/1e9:8.1f} TFLOP/s  {byts/ms/1e6:8.1f} GB/s", flush=True)
