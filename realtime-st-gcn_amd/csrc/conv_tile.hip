@@ -62,14 +62,17 @@ DEV typename Tr<T>::frag frag2(const char* p0, const char* p1) {
 }
 
 struct TileGeom {
-  int F;        // output frames per tile (framed) ; 0 = flat mode
-  int tiles_n;  // tiles per sample (framed) or total row tiles (flat)
-  int HR;       // staged A rows per chunk
-  int ncol;     // column tiles
-  int nblk;     // total blocks
+  int F;           // output frames per tile (framed) ; 0 = flat mode
+  int tiles_n;     // tiles per sample (framed) or total row tiles (flat)
+  int HR;          // staged A rows per chunk (max over tiles)
+  int ncol;        // column tiles
+  int nblk;        // total blocks
+  int parity;      // 1: stride-2 transposed conv, tiles hold output frames of one parity
+  int tiles_half;  // parity mode: tiles per (sample, parity)
+  float inv_v;     // 1 / V
 };
 
-template <typename T, int WM, int WN, int TM, int TN, int KC, int KT, int S, int MINW>
+template <typename T, int WM, int WN, int TM, int TN, int KC, int KT, int S, int MINW, bool PAR>
 __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stgcn_conv_desc a, const TileGeom g) {
   typedef TL<T, KC> L;
   constexpr int NW = WM * WN, NT = NW * 64;
@@ -102,18 +105,45 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stg
   const int ct = wg % g.ncol, rt = wg / g.ncol;
   const int n0 = ct * BN;
 
-  // ---- tile geometry
-  long row0;       // first output row of the tile
+  // ---- tile geometry.  Taps run as u = 0..nv-1 with weight tap dt(u) = da + db*u reading halo
+  // frame offset q(u) = qa + qb*u (frames relative to the tile's halo start fi0).
+  long row0;       // output row of the tile's local row 0
   int rows_valid;  // output rows of this tile
   long src0;       // flat: first input row ; framed: first input row of sample n
   int fi0 = 0;     // framed: first halo input frame
-  if (g.F) {
+  int nv = KT, qa = 0, qb = 1, da = 0, db = 1;
+  int rstep = S;   // halo frames per output frame (row base of MFMA row r)
+  if (PAR) {
+    // out frame f = 2i + par receives dy frame j = i + (par + pad - dt)/2 for taps with
+    // (par + pad - dt) even (the stride-2 transposed conv split into two stride-1 convs)
+    const int n = rt / g.tiles_n, tt = rt % g.tiles_n;
+    const int par = tt / g.tiles_half, i0 = (tt % g.tiles_half) * g.F;
+    const int Tp = (a.T_out - par + 1) / 2;
+    const int fe = max(0, min(g.F, Tp - i0));
+    const int dlo = (par + a.pad) & 1;
+    nv = dlo < KT ? (KT - 1 - dlo) / 2 + 1 : 0;
+    const int dhi = dlo + 2 * (nv - 1);
+    const int smax = (par + a.pad - dlo) / 2, smin = (par + a.pad - dhi) / 2;
+    row0 = ((long)n * a.T_out + 2 * i0 + par) * V;
+    rows_valid = fe * V;
+    src0 = (long)n * a.T_in * V;
+    fi0 = i0 + smin;
+    qa = smax - smin;
+    qb = -1;
+    da = dlo;
+    db = 2;
+    rstep = 1;
+  } else if (g.F) {
     const int n = rt / g.tiles_n, f0 = (rt % g.tiles_n) * g.F;
     const int fe = min(g.F, a.T_out - f0);
     row0 = ((long)n * a.T_out + f0) * V;
     rows_valid = fe * V;
     src0 = (long)n * a.T_in * V;
     fi0 = f0 * S - ((KT - 1) / 2) * (KT > 1);
+    if (KT > 1 && a.trans) {  // stride-1 transposed: frame t + pad - dt
+      qa = KT - 1;
+      qb = -1;
+    }
   } else {
     row0 = (long)rt * BM;
     const long M = (long)a.N * a.T_out * V;
@@ -167,7 +197,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stg
     if (g.F) {
       if (r < g.F * V) {
         const int fl = r / V;
-        br = (S * fl) * V + (r - fl * V);
+        br = (rstep * fl) * V + (r - fl * V);
       } else {
         br = 0;  // padding rows of the MFMA tile: read anything in range, never stored
       }
@@ -276,7 +306,6 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stg
   __syncthreads();
   int cur = 0;
   const int tap_stride = V * L::RS;
-  const bool rev = KT > 1 && a.trans;
   constexpr int NSTEP = KT * KS;  // k-steps of 16 per chunk
   typedef typename Tr<T>::frag Frag;
   for (int c = 0; c < nchunks; ++c) {
@@ -288,8 +317,8 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stg
     // sched_barrier keeps the compiler from hoisting every tap's reads and blowing the VGPR budget)
     Frag fa[2][TM], fb[2][TN];
     auto rd = [&](int st, int b) {
-      const int dt = st / KS, ks = st % KS;
-      const int q = rev ? KT - 1 - dt : dt;
+      const int u = st / KS, ks = st % KS;
+      const int q = qa + qb * u, dt = PAR ? da + db * u : u;
       const char* At = A_ + q * tap_stride + ks * 16 * (int)sizeof(T);
 #pragma unroll
       for (int i = 0; i < TM; ++i) fa[b][i] = frag2<T>(At + a_off[i], At + a_off[i] + 16);
@@ -299,14 +328,16 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stg
         fb[b][j] = frag2<T>(p + b_off[ks][0], p + b_off[ks][1]);
       }
     };
-    rd(0, 0);
+    if (!PAR || nv > 0) rd(0, 0);
 #pragma unroll
     for (int st = 0; st < NSTEP; ++st) {
-      if (st + 1 < NSTEP) rd(st + 1, (st + 1) & 1);
+      if (!PAR || st / KS < nv) {  // wave-uniform (parity mode runs fewer taps)
+        if (st + 1 < NSTEP && (!PAR || (st + 1) / KS < nv)) rd(st + 1, (st + 1) & 1);
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) Tr<T>::mma(acc[i][j], fa[st & 1][i], fb[st & 1][j]);
+          for (int j = 0; j < TN; ++j) Tr<T>::mma(acc[i][j], fa[st & 1][i], fb[st & 1][j]);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
     if (more) store(c + 1, cur ^ 1);
@@ -344,6 +375,10 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stg
         }
         if (ok) {
           T* p = pb + ro * ld;
+          if (PAR) {  // parity tiles: local frame fl sits at output frame 2*(i0+fl)+par
+            const int lrow = lb + ro, fl = (int)((lrow + 0.5f) * g.inv_v);
+            p = out + (row0 + lrow + (long)fl * V) * ld + col;
+          }
           if (a.accumulate) v += Tr<T>::to_f(*p);
           *p = Tr<T>::from_f(v);
           s += v;
@@ -404,6 +439,9 @@ int launch_tile(const stgcn_conv_desc& a, long max_row_blocks, hipStream_t s) {
   if (a.Cout_pad % BN || a.Cin_pad % KC) return -1;
   TileGeom g;
   const bool flat = KT == 1 && S == 1;
+  g.parity = (S == 2 && a.trans) ? 1 : 0;
+  g.inv_v = 1.f / (float)a.V;
+  g.tiles_half = 0;
   if (flat) {
     const long M = (long)a.N * a.T_out * a.V;
     g.F = 0;
@@ -412,8 +450,21 @@ int launch_tile(const stgcn_conv_desc& a, long max_row_blocks, hipStream_t s) {
   } else {
     if (a.V > 32 || a.V > BM) return -1;
     g.F = BM / a.V;
-    g.tiles_n = (a.T_out + g.F - 1) / g.F;
-    g.HR = (S * (g.F - 1) + KT) * a.V;
+    if (g.parity) {
+      // halo frames per parity: F + (smax - smin); smax - smin = 2*(nv-1)/2 = nv - 1
+      int hf = g.F;
+      for (int par = 0; par < 2; ++par) {
+        const int dlo = (par + a.pad) & 1;
+        const int nv = dlo < KT ? (KT - 1 - dlo) / 2 + 1 : 0;
+        hf = nv > 0 && g.F + nv - 1 > hf ? g.F + nv - 1 : hf;
+      }
+      g.tiles_half = ((a.T_out + 1) / 2 + g.F - 1) / g.F;
+      g.tiles_n = 2 * g.tiles_half;
+      g.HR = hf * a.V;
+    } else {
+      g.tiles_n = (a.T_out + g.F - 1) / g.F;
+      g.HR = (S * (g.F - 1) + KT) * a.V;
+    }
     if (g.HR > HR_MAX) return -1;
   }
   g.ncol = a.Cout_pad / BN;
@@ -429,24 +480,29 @@ int launch_tile(const stgcn_conv_desc& a, long max_row_blocks, hipStream_t s) {
   if (lds > 160 * 1024) return -1;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW>,
+    (void)hipFuncSetAttribute((const void*)conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, false>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (S == 2)
+      (void)hipFuncSetAttribute((const void*)conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, S == 2>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW>), dim3((unsigned)nblk), dim3(WM * WN * 64), lds,
-                     s, a, g);
+  if (g.parity)
+    hipLaunchKernelGGL((conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, S == 2>), dim3((unsigned)nblk),
+                       dim3(WM * WN * 64), lds, s, a, g);
+  else
+    hipLaunchKernelGGL((conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, false>), dim3((unsigned)nblk),
+                       dim3(WM * WN * 64), lds, s, a, g);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
 
 template <typename T, int KT, int S>
 int tile_dispatch(const stgcn_conv_desc& a, long mrb, hipStream_t s) {
   // column tile follows conv_rows_bn_tile: 64 for Cout <= 64, else 128
-  static const int wide_cfg = getenv("STGCN_TILE_WIDE") ? atoi(getenv("STGCN_TILE_WIDE")) : 0;
   const bool wide = a.Cout > 64;
   if constexpr (sizeof(T) == 2) {
     constexpr int KCB = (KT == 1 && S == 1) ? 32 : 16;  // flat GEMM: deeper chunks
     if (!wide) return launch_tile<T, 4, 1, 2, 2, KCB, KT, S>(a, mrb, s);
-    if (wide_cfg == 1) return launch_tile<T, 2, 2, 4, 2, KCB, KT, S, 1>(a, mrb, s);
     return launch_tile<T, 4, 2, 2, 2, KCB, KT, S>(a, mrb, s);
   } else {
     return wide ? launch_tile<T, 4, 2, 2, 2, 16, KT, S, 1>(a, mrb, s) : launch_tile<T, 4, 1, 2, 2, 16, KT, S, 1>(a, mrb, s);
@@ -467,14 +523,14 @@ int conv_tile_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
       if (a.T_in != a.T_out) return -1;
       return dtype ? tile_dispatch<bf16, 1, 1>(a, mrb, s) : tile_dispatch<float, 1, 1>(a, mrb, s);
     }
-    if (S == 2 && !a.trans && a.T_out == (a.T_in - 1) / 2 + 1)
-      return dtype ? tile_dispatch<bf16, 1, 2>(a, mrb, s) : tile_dispatch<float, 1, 2>(a, mrb, s);
+    const bool ok = S == 2 && (a.trans ? a.T_in == (a.T_out - 1) / 2 + 1 : a.T_out == (a.T_in - 1) / 2 + 1);
+    if (ok) return dtype ? tile_dispatch<bf16, 1, 2>(a, mrb, s) : tile_dispatch<float, 1, 2>(a, mrb, s);
     return -1;
   }
   if (a.Kt != 9 || a.pad != 4) return -1;
   if (S == 1 && a.T_out == a.T_in)
     return dtype ? tile_dispatch<bf16, 9, 1>(a, mrb, s) : tile_dispatch<float, 9, 1>(a, mrb, s);
-  if (S == 2 && !a.trans && a.T_out == (a.T_in + 2 * 4 - 9) / 2 + 1)
+  if (S == 2 && (a.trans ? a.T_in == (a.T_out + 2 * 4 - 9) / 2 + 1 : a.T_out == (a.T_in + 2 * 4 - 9) / 2 + 1))
     return dtype ? tile_dispatch<bf16, 9, 2>(a, mrb, s) : tile_dispatch<float, 9, 2>(a, mrb, s);
   return -1;
 }

@@ -267,25 +267,33 @@ __global__ __launch_bounds__(256, LN ? 1 : 2) void wgrad_tile_kernel(const stgcn
   }
 }
 
-// dw[e] += sum_r slab[r][e]  (deterministic order)
-__global__ void slab_reduce_kernel(const float* __restrict__ slab, int R, long E, float* __restrict__ dw) {
+// Deterministic two-level reduction of the per-block partials:
+//   level 1: part[s][e] = sum_{r = s, s+RS, ...} slab[r][e]     grid (E/1024, RS)
+//   level 2: dw[e]     += sum_s part[s][e]
+__global__ void slab_reduce1_kernel(const float* __restrict__ slab, int R, int RS, long E, float* __restrict__ part) {
+  const long e4 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const int sidx = blockIdx.y;
+  if (e4 >= E) return;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int r = sidx; r < R; r += RS) {
+    const float4 v = *reinterpret_cast<const float4*>(slab + (long)r * E + e4);
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  *reinterpret_cast<float4*>(part + (long)sidx * E + e4) = acc;
+}
+
+__global__ void slab_reduce2_kernel(const float* __restrict__ part, int RS, long E, float* __restrict__ dw) {
   const long e4 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (e4 >= E) return;
-  if (e4 + 4 <= E && (E % 4) == 0) {
-    float4 s = *reinterpret_cast<const float4*>(dw + e4);
-    for (int r = 0; r < R; ++r) {
-      const float4 v = *reinterpret_cast<const float4*>(slab + (long)r * E + e4);
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-    }
-    *reinterpret_cast<float4*>(dw + e4) = s;
-  } else {
-    for (long e = e4; e < E && e < e4 + 4; ++e) {
-      float s = dw[e];
-      for (int r = 0; r < R; ++r) s += slab[(long)r * E + e];
-      dw[e] = s;
-    }
+  float4 s = *reinterpret_cast<const float4*>(dw + e4);
+  for (int r = 0; r < RS; ++r) {
+    const float4 v = *reinterpret_cast<const float4*>(part + (long)r * E + e4);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
   }
+  *reinterpret_cast<float4*>(dw + e4) = s;
 }
+
+constexpr int RS_MAX = 16;
 
 struct Plan {
   bool ok;
@@ -337,7 +345,8 @@ Plan plan(const stgcn_wgrad_desc& a) {
   g.R = (g.ntiles + g.tpb - 1) / g.tpb;
   p.lds = 2 * (size_t)(2 * KM * PR + NB * (a.Kt >= S ? S : 1) * g.HRS * PR);
   if (p.lds > 160 * 1024) return p;
-  p.slab_elems = (long)g.R * a.Kt * a.Cout * a.Cin;
+  // slabs + level-1 partials; E % 4 == 0 holds since Cin % 8 == 0
+  p.slab_elems = (long)(g.R + RS_MAX) * a.Kt * a.Cout * a.Cin;
   p.ok = true;
   return p;
 }
@@ -389,7 +398,11 @@ int wgrad_tile_launch(const stgcn_wgrad_desc& a, int dtype, hipStream_t s) {
   if (rc < 0) return -1;
   if (rc != STGCN_OK) return rc;
   const long E = (long)a.Kt * a.Cout * a.Cin;
-  const unsigned blocks = (unsigned)((E / 4 + 1 + 255) / 256);
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3(blocks), dim3(256), 0, s, (const float*)p.g.slab, p.g.R, E, a.dw);
+  const int RS = p.g.R < RS_MAX ? p.g.R : RS_MAX;
+  float* part = p.g.slab + (long)p.g.R * E;
+  const unsigned blocks = (unsigned)((E / 4 + 255) / 256);
+  hipLaunchKernelGGL(slab_reduce1_kernel, dim3(blocks, RS), dim3(256), 0, s, (const float*)p.g.slab, p.g.R, RS, E,
+                     part);
+  hipLaunchKernelGGL(slab_reduce2_kernel, dim3(blocks), dim3(256), 0, s, (const float*)part, RS, E, a.dw);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }

@@ -49,8 +49,8 @@ def test_aagcn_model_golden(P):
     assert_grad_close(x.grad, d["dx"], TOL, "dx")
     grads = sub(d, "grad/")
     named = dict(m.named_parameters())
-    for k, g in grads.items():
-        assert_close(named[k].grad, g, TOL, k, grad_floor(grads, k))
+    for k, g in grads.items():  # deepest grads (norm_in) carry the same accumulation-order noise
+        assert_grad_close(named[k].grad, g, TOL, k, grad_floor(grads, k), reduction=True)
 
 
 def test_agcn_layer_vs_oracle_c64(P):

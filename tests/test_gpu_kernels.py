@@ -25,7 +25,8 @@ def cl(x, dtype=torch.float32):
 @pytest.mark.parametrize("cin,cout,kt,stride,T", [(64, 64, 9, 1, 37), (32, 128, 9, 2, 30), (16, 24, 1, 1, 11),
                                                   (128, 256, 9, 1, 12), (8, 64, 1, 1, 5), (64, 52, 1, 1, 1),
                                                   (24, 48, 9, 2, 11), (768, 256, 1, 1, 9), (256, 768, 1, 1, 9),
-                                                  (256, 256, 9, 1, 10), (4, 8, 9, 2, 9)])
+                                                  (256, 256, 9, 1, 10), (4, 8, 9, 2, 9), (64, 128, 1, 2, 21),
+                                                  (128, 128, 9, 2, 31), (128, 256, 1, 2, 8)])
 def test_conv_rows_fwd_and_trans(K, dtype, tol, cin, cout, kt, stride, T):
     torch.manual_seed(0)
     N, V = 3, 25

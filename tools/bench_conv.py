@@ -38,6 +38,8 @@ cases = [  # name, N, T, V, Cin, Cout, Kt, stride, trans, pro
     ("tcn_dgrad_c256", 64, 75, 25, 256, 256, 9, 1, True, 0),
     ("tcn_fwd_s2_c128", 64, 300, 25, 128, 128, 9, 2, False, 1),
     ("gcn_gemm_c128", 64, 150, 25, 384, 128, 1, 1, False, 0),
+    ("tcn_dgrad_s2_c128", 64, 300, 25, 128, 128, 9, 2, True, 0),
+    ("res_dgrad_s2_c128", 64, 300, 25, 128, 64, 1, 2, True, 0),
 ]
 only = sys.argv[2] if len(sys.argv) > 2 else None
 for name, N, T, V, Cin, Cout, Kt, s, trans, pro in cases:
