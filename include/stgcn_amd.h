@@ -90,6 +90,48 @@ int stgcn_amix_dA(const stgcn_amix_desc* d, const void* dw, float* dA, int dtype
 int stgcn_gcn_bias(const float* A, const float* b, float* out, int N, int P, int V, int C, int per_sample,
                    void* stream);
 
+/* Graph convolution as a joint-gathered GEMM for a batch-shared A (ConvTemporalGraphical,
+ * models/utils/tgcn.py:58-79; replaces the conv1x1 + einsum pair):
+ *   out[(i,a)][r] (+)= sum_{j<deg[a]} sum_c in[(i, nbr[a*J+j])][c] * w[a][j][r][c]  (+ bias[a][r]),
+ * i = n*T + t in [0, NT).  w = effective weights from stgcn_gconv_weights ([V][J][Cout_pad][Cin_pad]):
+ *   trans 0 (forward):   w[w][j][co][ci] = sum_p A[p][S(w)_j][w] * W[p*Cout+co][ci]
+ *   trans 1 (data grad): w[v][j][ci][co] = sum_p A[p][v][R(v)_j] * W[p*Cout+co][ci]
+ * with nbr = the support lists S (forward) or the reverse lists R (data grad).  Optional BN partial
+ * statistics per (row block, channel) as stgcn_conv_rows, row blocks <= stgcn_gconv_row_blocks. */
+typedef struct {
+  const void* in;
+  void* out;
+  const void* w;
+  const int* nbr;   /* [V][J] */
+  const int* deg;   /* [V] */
+  const float* bias; /* [V][Cout] or NULL */
+  float* stats;
+  int NT, V, J, Cin, Cout, Cin_pad, Cout_pad, in_ld, out_ld, accumulate;
+} stgcn_gconv_desc;
+
+int stgcn_gconv(const stgcn_gconv_desc* d, int dtype, void* stream);
+long stgcn_gconv_row_blocks(int NT, int V);
+int stgcn_gconv_weights(const float* A, const float* W, const int* nbr, const int* deg, int P, int V, int J, int Cout,
+                        int Cin, int trans, void* out, int rows_pad, int cols_pad, int dtype, void* stream);
+/* dweff[w][j][co][ci] += sum_i dy[(i,w)][co] * x[(i, nbr[w][j])][ci]   (fp32 [V][J][Cout][Cin]) */
+typedef struct {
+  const void* x;
+  const void* dy;
+  const int* nbr;
+  const int* deg;
+  float* dweff;
+  int NT, V, J, Cin, Cout, x_ld, dy_ld;
+  void* work;
+  long work_bytes;
+} stgcn_gconv_wgrad_desc;
+
+int stgcn_gconv_wgrad(const stgcn_gconv_wgrad_desc* d, int dtype, void* stream);
+long stgcn_gconv_wgrad_workspace(const stgcn_gconv_wgrad_desc* d, int dtype);
+/* dW[p*Cout+co][ci] += sum_{w,j} A[p][S(w)_j][w] dweff[w][j][co][ci]  (dW may be NULL);
+ * dA[p][S(w)_j][w] += sum_{co,ci} W[p*Cout+co][ci] dweff[w][j][co][ci]  (dA may be NULL) */
+int stgcn_gconv_wgrad_finish(const float* dweff, const float* A, const float* W, const int* nbr, const int* deg, int P,
+                             int V, int J, int Cout, int Cin, float* dW, float* dA, void* stream);
+
 /* BatchNorm with batch statistics (nn.BatchNorm2d(track_running_stats=False), stgcn.py:152,160,171;
  * BatchNorm1d input norm, models/utils/batchnorm.py:13-23 viewed as [N*T][V*C]).
  * Partials are float4 (count, mean, M2, 0) per (row block, channel); finalize merges them (fp64). */

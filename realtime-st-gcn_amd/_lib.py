@@ -41,6 +41,19 @@ class AmixDesc(ctypes.Structure):
                [(n, c_int) for n in ("N", "T", "V", "P", "Cin", "per_sample", "accumulate", "x_ld", "out_ld")]
 
 
+class GconvDesc(ctypes.Structure):
+    _fields_ = [("in_", c_void_p), ("out", c_void_p), ("w", c_void_p), ("nbr", c_void_p), ("deg", c_void_p),
+                ("bias", c_void_p), ("stats", c_void_p)] + \
+               [(n, c_int) for n in ("NT", "V", "J", "Cin", "Cout", "Cin_pad", "Cout_pad", "in_ld", "out_ld",
+                                     "accumulate")]
+
+
+class GconvWgradDesc(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("dy", c_void_p), ("nbr", c_void_p), ("deg", c_void_p), ("dweff", c_void_p)] + \
+               [(n, c_int) for n in ("NT", "V", "J", "Cin", "Cout", "x_ld", "dy_ld")] + \
+               [("work", c_void_p), ("work_bytes", c_long)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "stgcn_abi_version": (c_int, []),
@@ -49,6 +62,13 @@ _SIGS = {
     "stgcn_conv_rows_row_blocks": (c_long, [c_long, c_int]),
     "stgcn_conv_wgrad": (c_int, [ctypes.POINTER(WgradDesc), c_int, c_void_p]),
     "stgcn_conv_wgrad_workspace": (c_long, [ctypes.POINTER(WgradDesc), c_int]),
+    "stgcn_gconv": (c_int, [ctypes.POINTER(GconvDesc), c_int, c_void_p]),
+    "stgcn_gconv_row_blocks": (c_long, [c_int, c_int]),
+    "stgcn_gconv_weights": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 6 + [c_void_p, c_int, c_int,
+                                                                                           c_int, c_void_p]),
+    "stgcn_gconv_wgrad": (c_int, [ctypes.POINTER(GconvWgradDesc), c_int, c_void_p]),
+    "stgcn_gconv_wgrad_workspace": (c_long, [ctypes.POINTER(GconvWgradDesc), c_int]),
+    "stgcn_gconv_wgrad_finish": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_void_p, c_void_p, c_void_p]),
     "stgcn_amix_fwd": (c_int, [ctypes.POINTER(AmixDesc), c_int, c_void_p]),
     "stgcn_amix_trans": (c_int, [ctypes.POINTER(AmixDesc), c_int, c_void_p]),
     "stgcn_amix_dA": (c_int, [ctypes.POINTER(AmixDesc), c_void_p, c_void_p, c_int, c_void_p]),

@@ -20,6 +20,14 @@ int conv_wgrad_launch(WgradArgs a, int dtype, hipStream_t s);
 long wgrad_tile_workspace(const WgradArgs& a, int dtype);
 int wgrad_tile_launch(const WgradArgs& a, int dtype, hipStream_t s);
 int amix_fwd_launch(const AmixArgs& a, int dtype, hipStream_t s);
+long gconv_row_blocks(int NT, int V);
+int gconv_launch(const stgcn_gconv_desc& a, int dtype, hipStream_t s);
+int gconv_weights_launch(const float* A, const float* W, const int* nbr, const int* deg, int P, int V, int J, int Cout,
+                         int Cin, int trans, void* out, int R_pad, int C_pad, int dtype, hipStream_t s);
+long gconv_wgrad_workspace(const stgcn_gconv_wgrad_desc& a, int dtype);
+int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s);
+int gconv_wgrad_finish_launch(const float* dweff, const float* A, const float* W, const int* nbr, const int* deg,
+                              int P, int V, int J, int Cout, int Cin, float* dW, float* dA, hipStream_t s);
 int amix_trans_launch(const AmixArgs& a, int dtype, hipStream_t s);
 int amix_dA_launch(const AmixArgs& a, const void* dw, float* dA, int dtype, hipStream_t s);
 int gcn_bias_launch(const float* A, const float* b, float* out, int N, int P, int V, int C, int per_sample,
@@ -95,6 +103,42 @@ int stgcn_conv_wgrad(const stgcn_wgrad_desc* d, int dtype, void* stream) {
   const int r = wgrad_tile_launch(*d, dtype, STREAM(stream));  // bf16 frame-tiled path (needs work)
   if (r >= 0) return r;
   return conv_wgrad_launch(*d, dtype, STREAM(stream));
+}
+
+int stgcn_gconv(const stgcn_gconv_desc* d, int dtype, void* stream) {
+  CHECK_DTYPE(dtype);
+  if (!d || !d->in || !d->out || !d->w || !d->nbr || !d->deg || d->NT <= 0 || d->V <= 0 || d->J <= 0 ||
+      d->Cin <= 0 || d->Cout <= 0 || d->Cin_pad < d->Cin || d->Cout_pad < d->Cout || d->in_ld < d->Cin ||
+      d->out_ld < d->Cout)
+    return STGCN_EBADSHAPE;
+  return gconv_launch(*d, dtype, STREAM(stream));
+}
+long stgcn_gconv_row_blocks(int NT, int V) { return gconv_row_blocks(NT, V); }
+int stgcn_gconv_weights(const float* A, const float* W, const int* nbr, const int* deg, int P, int V, int J, int Cout,
+                        int Cin, int trans, void* out, int rows_pad, int cols_pad, int dtype, void* stream) {
+  CHECK_DTYPE(dtype);
+  if (!A || !W || !nbr || !deg || !out || P <= 0 || V <= 0 || J <= 0 || Cout <= 0 || Cin <= 0 ||
+      rows_pad < (trans ? Cin : Cout) || cols_pad < (trans ? Cout : Cin))
+    return STGCN_EBADSHAPE;
+  return gconv_weights_launch(A, W, nbr, deg, P, V, J, Cout, Cin, trans, out, rows_pad, cols_pad, dtype,
+                              STREAM(stream));
+}
+long stgcn_gconv_wgrad_workspace(const stgcn_gconv_wgrad_desc* d, int dtype) {
+  if (!d || (dtype != 0 && dtype != 1)) return 0;
+  return gconv_wgrad_workspace(*d, dtype);
+}
+int stgcn_gconv_wgrad(const stgcn_gconv_wgrad_desc* d, int dtype, void* stream) {
+  CHECK_DTYPE(dtype);
+  if (!d || !d->x || !d->dy || !d->nbr || !d->deg || !d->dweff || d->NT <= 0 || d->V <= 0 || d->J <= 0 ||
+      d->Cin <= 0 || d->Cout <= 0)
+    return STGCN_EBADSHAPE;
+  return gconv_wgrad_launch(*d, dtype, STREAM(stream));
+}
+int stgcn_gconv_wgrad_finish(const float* dweff, const float* A, const float* W, const int* nbr, const int* deg, int P,
+                             int V, int J, int Cout, int Cin, float* dW, float* dA, void* stream) {
+  if (!dweff || !A || !W || !nbr || !deg || P <= 0 || V <= 0 || J <= 0 || Cout <= 0 || Cin <= 0)
+    return STGCN_EBADSHAPE;
+  return gconv_wgrad_finish_launch(dweff, A, W, nbr, deg, P, V, J, Cout, Cin, dW, dA, STREAM(stream));
 }
 
 int stgcn_amix_fwd(const stgcn_amix_desc* d, int dtype, void* stream) {

@@ -1,0 +1,634 @@
+// Graph convolution of ST-GCN (ConvTemporalGraphical, models/utils/tgcn.py:58-79) as a
+// joint-gathered GEMM, for a graph shared by the batch.
+//
+// The reference computes  y = conv1x1(x) (P*Cout channels) ; g = einsum('nkctv,kvw->nctw', y, A).
+// Writing W_p = conv weight rows [p*Cout, (p+1)*Cout) and S(w) = {v : A_p[v][w] != 0 for some p}
+// (the joints feeding output joint w; <= 5 for the skeleton graphs), the same thing is
+//
+//   g[(i,w)][co] = sum_{j < |S(w)|} sum_ci x[(i, S(w)_j)][ci] * Weff[w][j][co][ci] + bias2d[w][co]
+//   Weff[w][j][co][ci] = sum_p A_p[S(w)_j][w] * W_p[co][ci]            (i = n*T + t)
+//
+// i.e. for every output joint w a GEMM over the frame rows i whose K axis gathers the |S(w)|
+// neighbour rows of the same frame.  Total MFMA work = sum_w |S(w)| * Cin * Cout per frame
+// (73 * Cin * Cout for the 25-joint graphs, vs P*V = 75 for the A-first form) and no A-mixed
+// intermediate ever touches HBM: the old path wrote and re-read an M x P*Cin tensor three times
+// (forward, data grad, weight grad).  The data gradient is the same kernel on dg with the
+// transposed effective weights  WeffT[v][j][ci][co] = sum_p A_p[v][R(v)_j] W_p[co][ci]  over the
+// reverse lists R(v) = {w : v in S(w)}; the weight/adjacency gradients come from
+//   dWeff[w][j][co][ci] = sum_i dg[(i,w)][co] * x[(i, S(w)_j)][ci]          (gconv_wgrad)
+//   dW_p[co][ci] = sum_{w,j} A_p[S(w)_j][w] dWeff[w][j][co][ci],
+//   dA_p[S(w)_j][w] = sum_{co,ci} W_p[co][ci] dWeff[w][j][co][ci]            (gconv_wgrad_finish)
+//
+// Kernel layout follows conv_tile.hip (flat mode): block = (row tile of BM frames, joint a, column
+// tile); A rows staged through registers into padded LDS rows, B (packed Weff) by LDS-DMA with the
+// XOR swizzle on the source, fragment double-buffering, BN partial statistics in the epilogue.
+#include "common.h"
+#include "../../include/stgcn_amd.h"
+
+namespace {
+
+template <typename T, int KC>
+struct GL {
+  static constexpr int RB = KC * (int)sizeof(T);
+  static constexpr int UPR = RB / 16;
+  static constexpr int RPB = RB >= 256 ? 1 : 256 / RB;
+  static constexpr int RS = RB + 16;
+  static DEV int swz(int row) { return (row / RPB) & (UPR - 1); }
+};
+
+DEV void glds16(const void* src, char* lds_base) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+#endif
+}
+
+template <typename T>
+DEV typename Tr<T>::frag frag2(const char* p0, const char* p1) {
+  if constexpr (sizeof(T) == 2) {
+    (void)p1;
+    return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(p0));
+  } else {
+    const f32x4 a = __builtin_bit_cast(f32x4, *reinterpret_cast<const uint4*>(p0));
+    const f32x4 b = __builtin_bit_cast(f32x4, *reinterpret_cast<const uint4*>(p1));
+    f32x8 f;
+    f[0] = a[0]; f[1] = a[1]; f[2] = a[2]; f[3] = a[3];
+    f[4] = b[0]; f[5] = b[1]; f[6] = b[2]; f[7] = b[3];
+    return f;
+  }
+}
+
+struct GGeom {
+  int ntile;  // row tiles
+  int ncol;   // column tiles
+  int nblk;
+};
+
+// ------------------------------------------------------------------ gather GEMM (fwd and data grad)
+template <typename T, int WM, int WN, int TM, int TN, int KC>
+__global__ __launch_bounds__(WM * WN * 64, 2) void gconv_kernel(const stgcn_gconv_desc a, const GGeom g) {
+  typedef GL<T, KC> L;
+  constexpr int NW = WM * WN, NT = NW * 64;
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  constexpr int VEC = 16 / (int)sizeof(T);
+  constexpr int KS = KC / 16;
+  constexpr int A_UNITS = BM * L::UPR / NT;
+  constexpr int A_BYTES = BM * L::RS;
+  constexpr int B_BYTES = BN * L::RB;
+  constexpr int B_PIECES = (B_BYTES + 1023) / 1024;
+  constexpr int STAGE = ((A_BYTES + B_BYTES) + 1023) & ~1023;
+  static_assert(BM * L::UPR % NT == 0, "A units");
+  static_assert(B_BYTES % 1024 == 0, "B pieces");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int V = a.V;
+
+  // XCD-aware order: consecutive ids (column tile fastest, then joint) share the row tile's x rows
+  int wg;
+  {
+    const int id = blockIdx.x, x = id & 7, q = g.nblk >> 3, r = g.nblk & 7;
+    wg = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (id >> 3);
+  }
+  const int ct = wg % g.ncol;
+  const int jt = (wg / g.ncol) % V;  // output joint
+  const int it = wg / (g.ncol * V);
+  const int n0 = ct * BN;
+  const int i0 = it * BM;
+  const int rows_valid = min(BM, a.NT - i0);
+  const int deg = a.deg[jt];
+
+  const T* __restrict__ in = reinterpret_cast<const T*>(a.in);
+  const T* __restrict__ wp = reinterpret_cast<const T*>(a.w);
+  const int ucol = tid % L::UPR;
+  long a_row[A_UNITS];  // element offset of frame row (i, joint 0) ; -1 = zero row
+  int a_lds[A_UNITS];
+#pragma unroll
+  for (int u = 0; u < A_UNITS; ++u) {
+    const int row = (tid + u * NT) / L::UPR;
+    a_lds[u] = row * L::RS + ucol * 16;
+    a_row[u] = row < rows_valid ? (long)(i0 + row) * V * a.in_ld + ucol * VEC : -1;
+  }
+  const bool fast_ld = (a.in_ld % VEC) == 0 && (a.Cin % KC) == 0;
+
+  int a_off[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) a_off[i] = ((wm * TM + i) * 32 + lr) * L::RS + lh * 16 * (int)(sizeof(T) / 2);
+  int b_off[KS][2];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int f = L::swz(lr);
+    if constexpr (sizeof(T) == 2) {
+      b_off[ks][0] = lr * L::RB + (((2 * ks + lh) ^ f) << 4);
+      b_off[ks][1] = b_off[ks][0];
+    } else {
+      b_off[ks][0] = lr * L::RB + (((4 * ks + 2 * lh) ^ f) << 4);
+      b_off[ks][1] = lr * L::RB + (((4 * ks + 2 * lh + 1) ^ f) << 4);
+    }
+  }
+
+  const int nch = a.Cin_pad / KC;
+  const int nk = deg * nch;  // K chunks: (neighbour j, channel chunk c)
+  uint4 ra[A_UNITS];
+
+  auto load = [&](int k, int buf) {
+    const int j = k / nch, c = k - j * nch;
+    const int src = a.nbr[jt * a.J + j];
+    const long joff = (long)src * a.in_ld + c * KC;
+    const int ci = c * KC + ucol * VEC;
+#pragma unroll
+    for (int u = 0; u < A_UNITS; ++u) {
+      ra[u] = make_uint4(0, 0, 0, 0);
+      if (a_row[u] >= 0) {
+        const T* p = in + a_row[u] + joff;
+        if (fast_ld) {
+          ra[u] = *reinterpret_cast<const uint4*>(p);
+        } else if (ci < a.Cin) {
+          float f[VEC];
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) f[e] = ci + e < a.Cin ? Tr<T>::to_f(p[e]) : 0.f;
+          ra[u] = pack16(f, (T*)nullptr);
+        }
+      }
+    }
+    char* B_ = smem + buf * STAGE + A_BYTES;
+    const T* wsrc = wp + ((long)(jt * a.J + j) * a.Cout_pad + n0) * a.Cin_pad + c * KC;
+#pragma unroll
+    for (int kk = 0; kk < (B_PIECES + NW - 1) / NW; ++kk) {
+      const int piece = wave + kk * NW;
+      if (piece < B_PIECES) {
+        const int byte = piece * 1024 + lane * 16;
+        const int br = byte / L::RB, pu = (byte % L::RB) >> 4;
+        glds16(wsrc + (long)br * a.Cin_pad + (pu ^ L::swz(br)) * VEC, B_ + piece * 1024);
+      }
+    }
+  };
+  auto store = [&](int buf) {
+    char* A_ = smem + buf * STAGE;
+#pragma unroll
+    for (int u = 0; u < A_UNITS; ++u) *reinterpret_cast<uint4*>(A_ + a_lds[u]) = ra[u];
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  typedef typename Tr<T>::frag Frag;
+  int cur = 0;
+  if (nk > 0) {
+    load(0, 0);
+    store(0);
+  }
+  __syncthreads();
+  for (int k = 0; k < nk; ++k) {
+    const bool more = k + 1 < nk;
+    if (more) load(k + 1, cur ^ 1);
+    const char* A_ = smem + cur * STAGE;
+    const char* B_ = A_ + A_BYTES;
+    Frag fa[2][TM], fb[2][TN];
+    auto rd = [&](int ks, int b) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const char* p = A_ + a_off[i] + ks * 16 * (int)sizeof(T);
+        fa[b][i] = frag2<T>(p, p + 16);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const char* p = B_ + ((wn * TN + j) * 32) * L::RB;
+        fb[b][j] = frag2<T>(p + b_off[ks][0], p + b_off[ks][1]);
+      }
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 1 < KS) rd(ks + 1, (ks + 1) & 1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) Tr<T>::mma(acc[i][j], fa[ks & 1][i], fb[ks & 1][j]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (more) store(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  T* __restrict__ out = reinterpret_cast<T*>(a.out);
+  const long ldv = (long)a.out_ld * V;  // row stride between consecutive frames of joint jt
+  Welford ws[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + (wn * TN + j) * 32 + lr;
+    const bool cok = col < a.Cout;
+    const float b1 = (a.bias && cok) ? a.bias[jt * a.Cout + col] : 0.f;
+    float s = 0.f, cnt = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int lb = (wm * TM + i) * 32 + 4 * lh;
+      T* pb = out + ((long)(i0 + lb) * V + jt) * a.out_ld + col;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ro = (r & 3) + 8 * (r >> 2);
+        const bool ok = cok && lb + ro < rows_valid;
+        float v = acc[i][j][r] + b1;
+        if (ok) {
+          T* p = pb + ro * ldv;
+          if (a.accumulate) v += Tr<T>::to_f(*p);
+          *p = Tr<T>::from_f(v);
+          s += v;
+          cnt += 1.f;
+        }
+        acc[i][j][r] = v;
+      }
+    }
+    Welford w;
+    w.n = cnt;
+    w.mean = cnt > 0.f ? s / cnt : 0.f;
+    float m2 = 0.f;
+    if (a.stats) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int lb = (wm * TM + i) * 32 + 4 * lh;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float d = acc[i][j][r] - w.mean;
+          if (cok && lb + (r & 3) + 8 * (r >> 2) < rows_valid) m2 += d * d;
+        }
+      }
+    }
+    w.m2 = m2;
+    ws[j] = w;
+  }
+  if (a.stats) {
+    __syncthreads();
+    float4* red = reinterpret_cast<float4*>(smem);  // [WM][BN]
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      Welford o;
+      o.n = __shfl_xor(ws[j].n, 32);
+      o.mean = __shfl_xor(ws[j].mean, 32);
+      o.m2 = __shfl_xor(ws[j].m2, 32);
+      const Welford w = welford_merge(ws[j], o);
+      if (lh == 0) red[wm * BN + (wn * TN + j) * 32 + lr] = make_float4(w.n, w.mean, w.m2, 0.f);
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += NT) {
+      const float4 f = red[c];
+      Welford w = {f.x, f.y, f.z};
+      for (int k = 1; k < WM; ++k) {
+        const float4 h = red[k * BN + c];
+        w = welford_merge(w, Welford{h.x, h.y, h.z});
+      }
+      if (n0 + c < a.Cout_pad)
+        reinterpret_cast<float4*>(a.stats)[((long)it * V + jt) * a.Cout_pad + n0 + c] =
+            make_float4(w.n, w.mean, w.m2, 0.f);
+    }
+  }
+}
+
+template <typename T, int WM, int WN, int TM, int TN, int KC>
+int launch_gconv(const stgcn_gconv_desc& a, hipStream_t s) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  typedef GL<T, KC> L;
+  if (a.Cout_pad % BN || a.Cin_pad % KC) return STGCN_EBADSHAPE;
+  GGeom g;
+  g.ntile = (a.NT + BM - 1) / BM;
+  g.ncol = a.Cout_pad / BN;
+  const long nblk = (long)g.ntile * a.V * g.ncol;
+  if (nblk <= 0 || nblk > 0x7fffffffL) return STGCN_EBADSHAPE;
+  g.nblk = (int)nblk;
+  const int STAGE = ((BM * L::RS + BN * L::RB) + 1023) & ~1023;
+  size_t lds = 2 * (size_t)STAGE;
+  const size_t red = a.stats ? (size_t)WM * BN * 16 : 0;
+  if (red > lds) lds = red;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gconv_kernel<T, WM, WN, TM, TN, KC>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gconv_kernel<T, WM, WN, TM, TN, KC>), dim3((unsigned)nblk), dim3(WM * WN * 64), lds, s, a, g);
+  return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
+}
+
+// ------------------------------------------------------------------ effective weights
+// out[a][j][r][c] (dtype, padded to [R_pad][C_pad]):
+//   trans 0: sum_p A[p][nbr[a][j]][a] * W[p*Cout + r][c]          (r = co < Cout, c = ci < Cin)
+//   trans 1: sum_p A[p][a][nbr[a][j]] * W[p*Cout + c][r]          (r = ci < Cin,  c = co < Cout)
+template <typename T>
+__global__ void gconv_weights_kernel(const float* __restrict__ A, const float* __restrict__ W, const int* nbr,
+                                     const int* deg, int P, int V, int J, int Cout, int Cin, int trans, T* out,
+                                     int R_pad, int C_pad) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)V * J * R_pad * C_pad;
+  if (idx >= total) return;
+  const int c = (int)(idx % C_pad);
+  const long t1 = idx / C_pad;
+  const int r = (int)(t1 % R_pad);
+  const long aj = t1 / R_pad;
+  const int j = (int)(aj % J), a = (int)(aj / J);
+  const int R = trans ? Cin : Cout, C = trans ? Cout : Cin;
+  float s = 0.f;
+  if (j < deg[a] && r < R && c < C) {
+    const int b = nbr[a * J + j];
+    for (int p = 0; p < P; ++p) {
+      const float coef = trans ? A[((long)p * V + a) * V + b] : A[((long)p * V + b) * V + a];
+      const float w = trans ? W[((long)p * Cout + c) * Cin + r] : W[((long)p * Cout + r) * Cin + c];
+      s += coef * w;
+    }
+  }
+  out[idx] = Tr<T>::from_f(s);
+}
+
+// ------------------------------------------------------------------ weight gradient (bf16 + fp32)
+// dWeff[w][j][co][ci] += sum_i dy[(i,w)][co] * x[(i, nbr[w][j])][ci].  Block = (pair (w,j), 64-co x
+// 64-ci block, row range); the 4 waves split the k-steps of each 128-row tile and are summed in LDS
+// at the end; per-block partials go to a slab and are reduced deterministically.
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+constexpr int WKM = 128;  // rows per tile
+constexpr int WPR = 64;   // bytes per bf16 panel row (32 channels)
+
+DEV bf16x8 trfrag(const char* panel, int row0, int lane) {
+  const int i = lane & 15, gq = lane >> 4;
+  const int q = i >> 2, p = i & 3, h = gq >> 1;
+  const char* a0 = panel + (row0 + 8 * h + q) * WPR + (16 * (gq & 1) + 4 * p) * 2;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * WPR));
+  s16x8 v;
+  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+struct WGG {
+  int ntile, tpb, R, nco, nci;
+  float* slab;  // [R][V*J][Cout][Cin]
+};
+
+__global__ __launch_bounds__(256, 2) void gconv_wgrad_kernel(const stgcn_gconv_wgrad_desc a, const WGG g) {
+  constexpr int PANEL = WKM * WPR;   // one 32-channel panel of a tile
+  constexpr int STAGE = 4 * PANEL;   // dy: 2 panels, x: 2 panels
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int V = a.V;
+  const int ngrp = g.nco * g.nci;
+  const int pair = blockIdx.x / (ngrp * g.R);
+  const int rem = blockIdx.x % (ngrp * g.R);
+  const int rr = rem / ngrp, grp = rem % ngrp;
+  const int w = pair / a.J, j = pair % a.J;
+  if (j >= a.deg[w]) return;  // unused (joint, neighbour) slot: block-uniform exit before any barrier
+  const int src = a.nbr[pair];
+  const int co0 = (grp % g.nco) * 64, ci0 = (grp / g.nco) * 64;
+  const int t0 = rr * g.tpb, t1 = min(g.ntile, t0 + g.tpb);
+
+  const bf16* __restrict__ dy = reinterpret_cast<const bf16*>(a.dy);
+  const bf16* __restrict__ x = reinterpret_cast<const bf16*>(a.x);
+  // staging: 128 rows x 8 units (64 channels) per operand -> 4 units per thread per operand
+  const int uc = tid & 7;
+  const int co = co0 + uc * 8, ci = ci0 + uc * 8;
+  uint4 ry[4], rx[4];
+  auto load = [&](int t) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int row = (tid >> 3) + u * 32;
+      const int i = t * WKM + row;
+      ry[u] = make_uint4(0, 0, 0, 0);
+      rx[u] = make_uint4(0, 0, 0, 0);
+      if (i < a.NT) {
+        if (co < a.Cout) ry[u] = *reinterpret_cast<const uint4*>(dy + ((long)i * V + w) * a.dy_ld + co);
+        if (ci < a.Cin) rx[u] = *reinterpret_cast<const uint4*>(x + ((long)i * V + src) * a.x_ld + ci);
+      }
+    }
+  };
+  auto store = [&](int buf) {
+    char* base = smem + buf * STAGE;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int row = (tid >> 3) + u * 32;
+      const int off = (uc >> 2) * PANEL + row * WPR + (uc & 3) * 16;
+      *reinterpret_cast<uint4*>(base + off) = ry[u];
+      *reinterpret_cast<uint4*>(base + 2 * PANEL + off) = rx[u];
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a2 = 0; a2 < 2; ++a2)
+#pragma unroll
+    for (int b2 = 0; b2 < 2; ++b2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a2][b2][r] = 0.f;
+
+  int cur = 0;
+  if (t0 < t1) {
+    load(t0);
+    store(0);
+  }
+  __syncthreads();
+  for (int t = t0; t < t1; ++t) {
+    const bool more = t + 1 < t1;
+    if (more) load(t + 1);
+    const char* base = smem + cur * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < WKM / 16 / 4; ++kk) {  // this wave's k-steps: ks = wave + 4*kk
+      const int ks = wave + 4 * kk;
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int a2 = 0; a2 < 2; ++a2) fa[a2] = trfrag(base + a2 * PANEL, ks * 16, lane);
+#pragma unroll
+      for (int b2 = 0; b2 < 2; ++b2) fb[b2] = trfrag(base + (2 + b2) * PANEL, ks * 16, lane);
+#pragma unroll
+      for (int a2 = 0; a2 < 2; ++a2)
+#pragma unroll
+        for (int b2 = 0; b2 < 2; ++b2)
+          acc[a2][b2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a2], fb[b2], acc[a2][b2], 0, 0, 0);
+    }
+    if (more) store(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // sum the 4 waves' accumulators (LDS), wave 0 writes this block's partial
+  float* red = reinterpret_cast<float*>(smem);  // [3][4 tiles][16][64]
+  if (wave > 0) {
+#pragma unroll
+    for (int a2 = 0; a2 < 2; ++a2)
+#pragma unroll
+      for (int b2 = 0; b2 < 2; ++b2)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) red[(((wave - 1) * 4 + a2 * 2 + b2) * 16 + r) * 64 + lane] = acc[a2][b2][r];
+  }
+  __syncthreads();
+  if (wave == 0) {
+    float* slab = g.slab + ((long)rr * V * a.J + pair) * a.Cout * a.Cin;
+#pragma unroll
+    for (int a2 = 0; a2 < 2; ++a2)
+#pragma unroll
+      for (int b2 = 0; b2 < 2; ++b2) {
+        const int cc = ci0 + b2 * 32 + (lane & 31);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float v = acc[a2][b2][r];
+          for (int k = 0; k < 3; ++k) v += red[((k * 4 + a2 * 2 + b2) * 16 + r) * 64 + lane];
+          const int oc = co0 + a2 * 32 + acc_row(r, lane);
+          if (oc < a.Cout && cc < a.Cin) slab[(long)oc * a.Cin + cc] = v;
+        }
+      }
+  }
+}
+
+// fp32 parity path of the gather wgrad: one thread per (pair, co, ci), loop over rows (small sizes)
+__global__ void gconv_wgrad_f32_kernel(const stgcn_gconv_wgrad_desc a) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)a.V * a.J * a.Cout * a.Cin;
+  if (idx >= total) return;
+  const int ci = (int)(idx % a.Cin);
+  const int co = (int)((idx / a.Cin) % a.Cout);
+  const int pair = (int)(idx / ((long)a.Cin * a.Cout));
+  const int w = pair / a.J, j = pair % a.J;
+  if (j >= a.deg[w]) return;
+  const int src = a.nbr[pair];
+  const float* dy = reinterpret_cast<const float*>(a.dy);
+  const float* x = reinterpret_cast<const float*>(a.x);
+  float s = 0.f;
+  for (int i = 0; i < a.NT; ++i)
+    s += dy[((long)i * a.V + w) * a.dy_ld + co] * x[((long)i * a.V + src) * a.x_ld + ci];
+  a.dweff[idx] += s;
+}
+
+// slab reduction (rows of the slab are whole [V*J][Cout][Cin] images): dweff[e] += sum_r slab[r][e]
+__global__ void gslab_reduce_kernel(const float* __restrict__ slab, int R, long E, float* __restrict__ out) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  float s = out[e];
+  for (int r = 0; r < R; ++r) s += slab[(long)r * E + e];
+  out[e] = s;
+}
+
+// dW[p*Cout+co][ci] (+)= sum_{w, j<deg} A[p][nbr[w][j]][w] * dWeff[w][j][co][ci]
+__global__ void gconv_dw_kernel(const float* __restrict__ dweff, const float* __restrict__ A, const int* nbr,
+                                const int* deg, int P, int V, int J, int Cout, int Cin, float* dW) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long E = (long)Cout * Cin;
+  if (idx >= (long)P * E) return;
+  const int p = (int)(idx / E);
+  const long e = idx % E;
+  float s = 0.f;
+  for (int w = 0; w < V; ++w)
+    for (int j = 0; j < deg[w]; ++j) s += A[((long)p * V + nbr[w * J + j]) * V + w] * dweff[(long)(w * J + j) * E + e];
+  dW[idx] += s;
+}
+
+// dA[p][nbr[w][j]][w] (+)= sum_{co,ci} W[p*Cout+co][ci] * dWeff[w][j][co][ci]; block per (pair, p)
+__global__ void gconv_dA_kernel(const float* __restrict__ dweff, const float* __restrict__ W, const int* nbr,
+                                const int* deg, int P, int V, int J, int Cout, int Cin, float* dA) {
+  const int pair = blockIdx.x, p = blockIdx.y;
+  const int w = pair / J, j = pair % J;
+  if (j >= deg[w]) return;
+  const long E = (long)Cout * Cin;
+  const float* d = dweff + (long)pair * E;
+  const float* wp = W + (long)p * E;
+  float s = 0.f;
+  for (long e = threadIdx.x; e < E; e += blockDim.x) s += wp[e] * d[e];
+  s = wave_sum(s);
+  __shared__ float part[4];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float t = part[0] + part[1] + part[2] + part[3];
+    dA[((long)p * V + nbr[w * J + j]) * V + w] += t;
+  }
+}
+
+WGG wplan(const stgcn_gconv_wgrad_desc& a) {
+  WGG g{};
+  g.ntile = (a.NT + WKM - 1) / WKM;
+  g.nco = (a.Cout + 63) / 64;
+  g.nci = (a.Cin + 63) / 64;
+  long used = 0;
+  // blocks of unused pairs exit at once; size R by the used pairs (<= V*J)
+  used = (long)a.V * a.J;
+  const long groups = used * g.nco * g.nci;
+  long R = (1024 + groups - 1) / groups;
+  if (R > g.ntile) R = g.ntile;
+  if (R < 1) R = 1;
+  g.tpb = (int)((g.ntile + R - 1) / R);
+  g.R = (g.ntile + g.tpb - 1) / g.tpb;
+  return g;
+}
+
+}  // namespace
+
+long gconv_row_blocks(int NT, int V) { return (long)((NT + 127) / 128) * V; }
+
+int gconv_launch(const stgcn_gconv_desc& a, int dtype, hipStream_t s) {
+  // column tile: 64 for Cout <= 64, else 128 (weights padded accordingly by stgcn_gconv_weights)
+  const bool wide = a.Cout > 64;
+  if (dtype == 1) return wide ? launch_gconv<bf16, 4, 2, 2, 2, 32>(a, s) : launch_gconv<bf16, 4, 1, 2, 2, 32>(a, s);
+  return wide ? launch_gconv<float, 4, 2, 2, 2, 16>(a, s) : launch_gconv<float, 4, 1, 2, 2, 16>(a, s);
+}
+
+int gconv_weights_launch(const float* A, const float* W, const int* nbr, const int* deg, int P, int V, int J, int Cout,
+                         int Cin, int trans, void* out, int R_pad, int C_pad, int dtype, hipStream_t s) {
+  const long total = (long)V * J * R_pad * C_pad;
+  const unsigned blocks = (unsigned)((total + 255) / 256);
+  if (dtype == 1)
+    hipLaunchKernelGGL(gconv_weights_kernel<bf16>, dim3(blocks), dim3(256), 0, s, A, W, nbr, deg, P, V, J, Cout, Cin,
+                       trans, (bf16*)out, R_pad, C_pad);
+  else
+    hipLaunchKernelGGL(gconv_weights_kernel<float>, dim3(blocks), dim3(256), 0, s, A, W, nbr, deg, P, V, J, Cout,
+                       Cin, trans, (float*)out, R_pad, C_pad);
+  return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
+}
+
+long gconv_wgrad_workspace(const stgcn_gconv_wgrad_desc& a, int dtype) {
+  if (dtype != 1) return 0;
+  const WGG g = wplan(a);
+  return (long)g.R * a.V * a.J * a.Cout * a.Cin * (long)sizeof(float);
+}
+
+int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s) {
+  const long E = (long)a.V * a.J * a.Cout * a.Cin;
+  if (dtype != 1) {
+    hipLaunchKernelGGL(gconv_wgrad_f32_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, a);
+    return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
+  }
+  if (a.Cin % 8 || a.Cout % 8 || a.x_ld % 8 || a.dy_ld % 8) return STGCN_EBADSHAPE;
+  WGG g = wplan(a);
+  if (!a.work || a.work_bytes < (long)g.R * E * (long)sizeof(float)) return STGCN_EBADSHAPE;
+  g.slab = reinterpret_cast<float*>(a.work);
+  // slots of unused pairs are never written by the kernel: clear the slab first
+  (void)hipMemsetAsync(g.slab, 0, (size_t)g.R * E * sizeof(float), s);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gconv_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr = true;
+  }
+  const long blocks = (long)a.V * a.J * g.nco * g.nci * g.R;
+  const size_t lds = 2 * 4 * WKM * WPR;  // >= the 48 KB cross-wave reduction buffer
+  hipLaunchKernelGGL(gconv_wgrad_kernel, dim3((unsigned)blocks), dim3(256), lds, s, a, g);
+  hipLaunchKernelGGL(gslab_reduce_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, (const float*)g.slab,
+                     g.R, E, a.dweff);
+  return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
+}
+
+int gconv_wgrad_finish_launch(const float* dweff, const float* A, const float* W, const int* nbr, const int* deg,
+                              int P, int V, int J, int Cout, int Cin, float* dW, float* dA, hipStream_t s) {
+  const long n = (long)P * Cout * Cin;
+  if (dW)
+    hipLaunchKernelGGL(gconv_dw_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dweff, A, nbr, deg, P, V,
+                       J, Cout, Cin, dW);
+  if (dA)
+    hipLaunchKernelGGL(gconv_dA_kernel, dim3((unsigned)(V * J), (unsigned)P), dim3(256), 0, s, dweff, W, nbr, deg, P,
+                       V, J, Cout, Cin, dA);
+  return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
+}

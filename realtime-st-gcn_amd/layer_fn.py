@@ -86,7 +86,7 @@ class StgcnLayerFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, A, wg, bg, n1w, n1b, wt, bt, n2w, n2b, wr, br, nrw, nrb, cfg):
-        kt, stride, residual, norm, dtype = cfg
+        kt, stride, residual, norm, dtype = cfg[:5]
         dev = x.device
         x = K.to_rows(x, dtype)
         N, Cin, T, V = x.shape
@@ -98,16 +98,27 @@ class StgcnLayerFunction(torch.autograd.Function):
         A32 = A.detach().float().contiguous()
         res_conv = residual and not (Cin == Cout and stride == 1)
 
-        # ---- graph convolution: g = sum_p (A_p-mix x) W_p + bias2d
-        XA = K.amix_fwd(x, A32)
-        wg3 = wg.detach().float().view(P, Cout, Cin).permute(1, 0, 2).reshape(1, Cout, P * Cin)
-        wgp, cpg, kpg = K.pack_weight(wg3, dtype)
+        # ---- graph convolution: g = sum_p A_p-mix(x) W_p + bias2d
+        sup = cfg[5] if len(cfg) > 5 else None
+        gather = sup is not None and A32.dim() == 3 and not sup.dense(P)
         bias2d = K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
-        bmode = 3 if A32.dim() == 4 else 2
-        if norm == BN:
-            st1 = torch.zeros((K.row_blocks(M1, Cout), cpg, 4), dtype=torch.float32, device=dev)
-        g = K.conv_rows(XA, wgp, P * Cin, Cout, cpg, kpg, T, T, bias=bias2d, bias_mode=bmode,
-                        stats=st1 if norm == BN else None)
+        if gather:  # joint-gathered GEMM over per-joint effective weights (gconv.hip), no XA in HBM
+            wg2 = wg.detach().float().reshape(P * Cout, Cin).contiguous()
+            wgp = K.gconv_weights(A32, wg2, sup, Cout, Cin, False, dtype)
+            cpg, kpg = wgp.shape[2], wgp.shape[3]
+            if norm == BN:
+                st1 = torch.zeros((K.gconv_row_blocks(N * T, V), cpg, 4), dtype=torch.float32, device=dev)
+            g = K.gconv(x, wgp, sup, Cin, Cout, bias=bias2d, stats=st1 if norm == BN else None)
+            XA = None
+        else:
+            XA = K.amix_fwd(x, A32)
+            wg3 = wg.detach().float().view(P, Cout, Cin).permute(1, 0, 2).reshape(1, Cout, P * Cin)
+            wgp, cpg, kpg = K.pack_weight(wg3, dtype)
+            bmode = 3 if A32.dim() == 4 else 2
+            if norm == BN:
+                st1 = torch.zeros((K.row_blocks(M1, Cout), cpg, 4), dtype=torch.float32, device=dev)
+            g = K.conv_rows(XA, wgp, P * Cin, Cout, cpg, kpg, T, T, bias=bias2d, bias_mode=bmode,
+                            stats=st1 if norm == BN else None)
         if norm == BN:
             mr1, sc1, sh1 = K.bn_finalize(st1, st1.shape[0], cpg, Cout, n1w.detach().float(), n1b.detach().float())
             pro1 = dict(pro=1, pro_a=sc1, pro_b=sh1)
@@ -156,6 +167,7 @@ class StgcnLayerFunction(torch.autograd.Function):
                                r=x if residual else None)
 
         ctx.cfg = cfg
+        ctx.sup = sup if gather else None
         ctx.dims = (N, Cin, Cout, T, T_out, V, P, pad, res_conv)
         ctx.packs = (cpg, kpg, cpt, kpt)
         saved = [x, A32, XA, g, u, y, wg, bg, wt, n1w, n1b, n2w, n2b]
@@ -171,7 +183,7 @@ class StgcnLayerFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        kt, stride, residual, norm, dtype = ctx.cfg
+        kt, stride, residual, norm, dtype = ctx.cfg[:5]
         N, Cin, Cout, T, T_out, V, P, pad, res_conv = ctx.dims
         sv = list(ctx.saved_tensors)
         x, A32, XA, g, u, y, wg, bg, wt, n1w, n1b, n2w, n2b = sv[:13]
@@ -250,13 +262,26 @@ class StgcnLayerFunction(torch.autograd.Function):
             grads["n1w"], grads["n1b"] = dgb1[0].view(n1w.shape), dgb1[1].view(n1b.shape)
 
         # ---- graph convolution backward
-        # DW[(n,t,w)][p*Cin+ci] = sum_c dg[(n,t,w)][c] Wg[p*Cout+c][ci]
-        wgT = wg.detach().float().view(P, Cout, Cin).permute(0, 2, 1).reshape(1, P * Cin, Cout)
-        wgTp, cq, kq = K.pack_weight(wgT, dtype)
-        DW = K.conv_rows(dg, wgTp, Cout, P * Cin, cq, kq, T, T)
-        K.amix_trans(DW, A32, Cin, dx, accumulate=dx_written)
-        dA = K.amix_dA(x, DW, A32)
         bgp = bg.detach().float().view(P, Cout)
+        if ctx.sup is not None:
+            # data grad: same gather GEMM on dg over the reverse lists with transposed effective weights;
+            # weight/adjacency grads from dWeff[w][j] = sum_i dg[(i,w)] x[(i,S(w)_j)]^T
+            sup = ctx.sup
+            wg2 = wg.detach().float().reshape(P * Cout, Cin).contiguous()
+            wgT = K.gconv_weights(A32, wg2, sup, Cout, Cin, True, dtype)
+            K.gconv(dg, wgT, sup, Cout, Cin, trans=True, out=dx, accumulate=dx_written)
+            dweff = K.gconv_wgrad(x, dg, sup, Cin, Cout)
+            dwg2, dA = K.gconv_finish(dweff, A32, wg2, sup, Cout, Cin)
+            grads["wg"] = dwg2.view(P * Cout, Cin, 1, 1)
+        else:
+            # DW[(n,t,w)][p*Cin+ci] = sum_c dg[(n,t,w)][c] Wg[p*Cout+c][ci]
+            wgT = wg.detach().float().view(P, Cout, Cin).permute(0, 2, 1).reshape(1, P * Cin, Cout)
+            wgTp, cq, kq = K.pack_weight(wgT, dtype)
+            DW = K.conv_rows(dg, wgTp, Cout, P * Cin, cq, kq, T, T)
+            K.amix_trans(DW, A32, Cin, dx, accumulate=dx_written)
+            dA = K.amix_dA(x, DW, A32)
+            dwg = K.conv_wgrad(XA, dg, P * Cin, Cout, T, T, Kt=1)              # [1][Cout][P*Cin]
+            grads["wg"] = dwg.view(Cout, P, Cin).permute(1, 0, 2).reshape(P * Cout, Cin, 1, 1)
         # bias pushed through A: dA[p][v][w] += sum_c b_p[c] S[w][c]  (independent of v)
         if A32.dim() == 4:
             Sn = K.rowgroup_sum(dg, M1, Cout, V, per_sample=True)            # [N][V(w)][Cout]
@@ -268,8 +293,6 @@ class StgcnLayerFunction(torch.autograd.Function):
             dA += (bgp @ S.t()).unsqueeze(1)
             colsum = A32.sum(dim=1)                                         # [P][W]
             grads["bg"] = (colsum @ S).reshape(-1)
-        dwg = K.conv_wgrad(XA, dg, P * Cin, Cout, T, T, Kt=1)              # [1][Cout][P*Cin]
-        grads["wg"] = dwg.view(Cout, P, Cin).permute(1, 0, 2).reshape(P * Cout, Cin, 1, 1)
 
         def gr(name, like):
             v = grads.get(name)

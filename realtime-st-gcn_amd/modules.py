@@ -11,10 +11,13 @@ parity path, bf16 (fp32 accumulate) for the perf path.  Activations are returned
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
 from . import layer_fn as F_
+from . import native as K
 
 _DTYPES = {"fp32": torch.float32, "bf16": torch.bfloat16, torch.float32: torch.float32,
            torch.bfloat16: torch.bfloat16}
@@ -108,6 +111,21 @@ class StgcnLayer(nn.Module):
         else:
             self.residual = nn.Identity()
         self.compute_dtype = torch.float32
+        self._gsup = None
+
+    def bind_graph(self, A):
+        """Cache the support lists of the static adjacency A (P, V, V) for the joint-gathered graph
+        conv.  Every A later passed to forward (A * edge_importance) must have its nonzeros inside
+        this support; a Model binds its graph buffer, a bare layer binds the first A it sees."""
+        s = self._gsup
+        if A.dim() == 3 and (s is None or s.V != A.shape[-1] or s.mask.device != A.device):
+            self._gsup = K.GraphSupport(A)
+
+    def graph_support(self, A):
+        if A.dim() != 3 or os.environ.get("STGCN_GCN_AFIRST"):
+            return None  # per-sample A (AAGCN) or forced A-first path
+        self.bind_graph(A)
+        return self._gsup
 
     def forward(self, x, A):
         if self.dropout and self.training:
@@ -122,7 +140,8 @@ class StgcnLayer(nn.Module):
             wr, br, nrw, nrb = rc.weight, rc.bias, rn.weight, rn.bias
         else:
             wr = br = nrw = nrb = None
-        cfg = (self.kernel_size[0], self.stride, self.is_residual, self.normalization, self.compute_dtype)
+        cfg = (self.kernel_size[0], self.stride, self.is_residual, self.normalization, self.compute_dtype,
+               self.graph_support(A))
         return F_.StgcnLayerFunction.apply(x, A, self.gcn.conv.weight, self.gcn.conv.bias, n1.weight, n1.bias,
                                            conv.weight, conv.bias, n2.weight, n2.bias, wr, br, nrw, nrb, cfg)
 

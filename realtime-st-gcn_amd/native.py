@@ -165,6 +165,105 @@ def gcn_bias(A, b, N, C):
     return out
 
 
+# ------------------------------------------------------------------------------ graph conv (gather GEMM)
+class GraphSupport:
+    """Support lists of a batch-shared adjacency A [P][V][V] for stgcn_gconv: S(w) = {v : A[:, v, w] != 0}
+    (forward) and R(v) = {w : A[:, v, w] != 0} (data grad), padded to J = max degree, on the device."""
+
+    def __init__(self, A):
+        import numpy as np
+        a = (A.detach().abs().sum(0) > 0).cpu().numpy()  # [v][w]
+        V = a.shape[0]
+        self.V = V
+        S = [np.nonzero(a[:, w])[0] for w in range(V)]
+        R = [np.nonzero(a[v, :])[0] for v in range(V)]
+        self.J = max(1, max(len(s) for s in S), max(len(r) for r in R))
+        self.nnz = int(a.sum())
+        self.mask = torch.as_tensor(a, device=A.device)
+
+        def pack(lists):
+            nb = np.full((V, self.J), 0, dtype=np.int32)
+            dg = np.zeros(V, dtype=np.int32)
+            for i, l in enumerate(lists):
+                nb[i, :len(l)] = l
+                dg[i] = len(l)
+            return torch.as_tensor(nb, device=A.device), torch.as_tensor(dg, device=A.device)
+
+        self.nbr, self.deg = pack(S)
+        self.rnbr, self.rdeg = pack(R)
+
+    def dense(self, P):
+        """A-first (amix) is cheaper when the support is denser than P entries per output joint."""
+        return self.nnz > P * self.V
+
+
+def gconv_weights(A, W, sup, Cout, Cin, trans, dtype):
+    """Effective weights [V][J][R_pad][C_pad]: trans 0 -> (Cout, Cin) from S lists, 1 -> (Cin, Cout) from R lists."""
+    P, V = A.shape[0], A.shape[-1]
+    R, C = (Cin, Cout) if trans else (Cout, Cin)
+    rp = -(-R // col_tile(R)) * col_tile(R)
+    cpad = -(-C // 32) * 32
+    out = torch.empty((V, sup.J, rp, cpad), dtype=dtype, device=A.device)
+    nbr, deg = (sup.rnbr, sup.rdeg) if trans else (sup.nbr, sup.deg)
+    L.check(L.lib().stgcn_gconv_weights(A.data_ptr(), W.data_ptr(), nbr.data_ptr(), deg.data_ptr(), P, V, sup.J,
+                                        Cout, Cin, int(trans), out.data_ptr(), rp, cpad, L.dtype_code(dtype),
+                                        L.stream()), "gconv_weights")
+    return out
+
+
+def gconv_row_blocks(NT: int, V: int) -> int:
+    return L.lib().stgcn_gconv_row_blocks(NT, V)
+
+
+def gconv(x, wpk, sup, Cin, Cout, trans=False, bias=None, stats=None, out=None, accumulate=False, tag=None):
+    """out rows (N, Cout, T, V) (+)= joint-gathered GEMM of x rows with packed effective weights."""
+    N, _, T, V = x.shape
+    if out is None:
+        out = cl_empty(N, Cout, T, V, x.dtype, x.device)
+    nbr, deg = (sup.rnbr, sup.rdeg) if trans else (sup.nbr, sup.deg)
+    d = L.GconvDesc()
+    d.in_, d.out, d.w = x.data_ptr(), out.data_ptr(), wpk.data_ptr()
+    d.nbr, d.deg, d.bias, d.stats = nbr.data_ptr(), deg.data_ptr(), L.ptr(bias), L.ptr(stats)
+    d.NT, d.V, d.J, d.Cin, d.Cout = N * T, V, sup.J, Cin, Cout
+    d.Cin_pad, d.Cout_pad = wpk.shape[3], wpk.shape[2]
+    d.in_ld, d.out_ld, d.accumulate = rows_ld(x), rows_ld(out), int(accumulate)
+    hook = EVENT_HOOK if tag is not None else None
+    if hook:
+        hook(tag, "start")
+    L.check(L.lib().stgcn_gconv(d, L.dtype_code(x.dtype), L.stream()), "gconv")
+    if hook:
+        hook(tag, "end")
+    return out
+
+
+def gconv_wgrad(x, dy, sup, Cin, Cout):
+    """dWeff [V][J][Cout][Cin] fp32 = sum_i dy[(i,w)] x[(i, S(w)_j)]^T."""
+    N, _, T, V = x.shape
+    dweff = torch.zeros((V, sup.J, Cout, Cin), dtype=torch.float32, device=x.device)
+    d = L.GconvWgradDesc()
+    d.x, d.dy, d.nbr, d.deg, d.dweff = x.data_ptr(), dy.data_ptr(), sup.nbr.data_ptr(), sup.deg.data_ptr(), \
+        dweff.data_ptr()
+    d.NT, d.V, d.J, d.Cin, d.Cout, d.x_ld, d.dy_ld = N * T, V, sup.J, Cin, Cout, rows_ld(x), rows_ld(dy)
+    code = L.dtype_code(x.dtype)
+    nbytes = L.lib().stgcn_gconv_wgrad_workspace(d, code)
+    if nbytes > 0:
+        work = torch.empty(nbytes // 4, dtype=torch.float32, device=x.device)
+        d.work, d.work_bytes = work.data_ptr(), nbytes
+    L.check(L.lib().stgcn_gconv_wgrad(d, code, L.stream()), "gconv_wgrad")
+    return dweff
+
+
+def gconv_finish(dweff, A, W, sup, Cout, Cin):
+    """(dW [P*Cout][Cin], dA [P][V][V]) fp32 from dWeff (stgcn_gconv_wgrad_finish)."""
+    P, V = A.shape[0], A.shape[-1]
+    dW = torch.zeros((P * Cout, Cin), dtype=torch.float32, device=A.device)
+    dA = torch.zeros((P, V, V), dtype=torch.float32, device=A.device)
+    L.check(L.lib().stgcn_gconv_wgrad_finish(dweff.data_ptr(), A.data_ptr(), W.data_ptr(), sup.nbr.data_ptr(),
+                                             sup.deg.data_ptr(), P, V, sup.J, Cout, Cin, dW.data_ptr(), dA.data_ptr(),
+                                             L.stream()), "gconv_finish")
+    return dW, dA
+
+
 # ------------------------------------------------------------------------------------ BatchNorm
 def bn_stat_blocks(M: int) -> int:
     return L.lib().stgcn_bn_stat_blocks(M)

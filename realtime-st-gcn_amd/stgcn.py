@@ -64,6 +64,7 @@ class Model(nn.Module):
             w = self.fcn_in.weight
         x = LF.Conv1x1Function.apply(x, w, self.fcn_in.bias, self.compute_dtype)   # stgcn.py:85
         for gcn, importance in zip(self.gcn_networks, self.edge_importance):       # stgcn.py:88-89
+            gcn.bind_graph(self.A)  # support of the static graph (cached; no sync after the first call)
             x = gcn(x, self.A * importance)
         x = LF.PoolFunction.apply(x, self.compute_dtype)                            # stgcn.py:92
         x = LF.Conv1x1Function.apply(x, self.fcn_out.weight, self.fcn_out.bias, self.compute_dtype)  # :95

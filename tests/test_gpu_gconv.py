@@ -1,0 +1,64 @@
+"""Joint-gathered graph conv (gconv.hip) vs the reference's conv1x1 -> einsum(A) formulation
+(models/utils/tgcn.py:71-79) in plain PyTorch fp32: forward, data grad, weight and adjacency grads."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import assert_close
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def K(pkg):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return pkg.native
+
+
+def cl(x, dtype=torch.float32):
+    return x.to(DEV, dtype).contiguous(memory_format=torch.channels_last)
+
+
+def ref_gcn(x, A, W, b):
+    P, V = A.shape[0], A.shape[-1]
+    y = F.conv2d(x, W.view(W.shape[0], -1, 1, 1), b)
+    n, kc, t, v = y.shape
+    return torch.einsum("nkctv,kvw->nctw", y.view(n, P, kc // P, t, v), A)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 2e-2)])
+@pytest.mark.parametrize("Cin,Cout,N,T", [(64, 64, 3, 37), (128, 256, 2, 19), (8, 64, 2, 11), (256, 128, 2, 7),
+                                          (24, 40, 3, 5)])
+def test_gconv_fwd_bwd(K, pkg, dtype, tol, Cin, Cout, N, T):
+    torch.manual_seed(3)
+    A0 = torch.tensor(pkg.Graph(**pkg.PKU_MMD).A, dtype=torch.float32)
+    imp = torch.rand(A0.shape) + 0.5
+    A = (A0 * imp).requires_grad_(True)
+    P, V = A.shape[0], A.shape[-1]
+    x = torch.randn(N, Cin, T, V, requires_grad=True)
+    W = (torch.randn(P * Cout, Cin) / Cin ** 0.5).requires_grad_(True)
+    b = torch.randn(P * Cout)
+    ref = ref_gcn(x, A, W, torch.zeros_like(b))
+    dy = torch.randn(ref.shape)
+    ref.backward(dy)
+
+    sup = K.GraphSupport(A0.to(DEV))
+    Ad, Wd = A.detach().to(DEV).contiguous(), W.detach().to(DEV).contiguous()
+    wpk = K.gconv_weights(Ad, Wd, sup, Cout, Cin, False, dtype)
+    bias2d = K.gcn_bias(Ad, b.to(DEV), N, Cout)
+    st = torch.zeros((K.gconv_row_blocks(N * T, V), wpk.shape[2], 4), device=DEV)
+    g = K.gconv(cl(x.detach(), dtype), wpk, sup, Cin, Cout, bias=bias2d, stats=st)
+    ref_b = ref_gcn(x.detach(), A.detach(), W.detach(), b)
+    assert_close(g.float(), ref_b, tol, "gconv fwd")
+    mr, _, _ = K.bn_finalize(st, st.shape[0], wpk.shape[2], Cout, None, None)
+    assert_close(mr[:, 0].cpu(), ref_b.mean(dim=(0, 2, 3)), 1e-4 if dtype == torch.float32 else 2e-3, "stats mean")
+
+    wT = K.gconv_weights(Ad, Wd, sup, Cout, Cin, True, dtype)
+    dx = K.gconv(cl(dy, dtype), wT, sup, Cout, Cin, trans=True)
+    assert_close(dx.float(), x.grad, tol, "gconv dgrad")
+    dweff = K.gconv_wgrad(cl(x.detach(), dtype), cl(dy, dtype), sup, Cin, Cout)
+    dW, dA = K.gconv_finish(dweff, Ad, Wd, sup, Cout, Cin)
+    assert_close(dW, W.grad, tol, "gconv dW")
+    assert_close(dA, A.grad, tol, "gconv dA")
