@@ -273,6 +273,12 @@ class StgcnLayerFunction(torch.autograd.Function):
             dweff = K.gconv_wgrad(x, dg, sup, Cin, Cout)
             dwg2, dA = K.gconv_finish(dweff, A32, wg2, sup, Cout, Cin)
             grads["wg"] = dwg2.view(P * Cout, Cin, 1, 1)
+            if ctx.cfg[6] and ctx.needs_input_grad[1]:
+                # caller-owned A: the reference's dA is dense (also off the graph's support), so take
+                # it from the A-first factorisation dA_p[v][w] = sum x[(i,v)] . (dg W_p)[(i,w)]
+                wgTd = wg.detach().float().view(P, Cout, Cin).permute(0, 2, 1).reshape(1, P * Cin, Cout)
+                wgTp, cq, kq = K.pack_weight(wgTd, dtype)
+                dA = K.amix_dA(x, K.conv_rows(dg, wgTp, Cout, P * Cin, cq, kq, T, T), A32)
         else:
             # DW[(n,t,w)][p*Cin+ci] = sum_c dg[(n,t,w)][c] Wg[p*Cout+c][ci]
             wgT = wg.detach().float().view(P, Cout, Cin).permute(0, 2, 1).reshape(1, P * Cin, Cout)

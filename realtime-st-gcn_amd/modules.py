@@ -112,19 +112,23 @@ class StgcnLayer(nn.Module):
             self.residual = nn.Identity()
         self.compute_dtype = torch.float32
         self._gsup = None
+        self._graph_bound = False
 
-    def bind_graph(self, A):
+    def bind_graph(self, A, masked=True):
         """Cache the support lists of the static adjacency A (P, V, V) for the joint-gathered graph
-        conv.  Every A later passed to forward (A * edge_importance) must have its nonzeros inside
-        this support; a Model binds its graph buffer, a bare layer binds the first A it sees."""
+        conv.  Every A later passed to forward must have its nonzeros inside this support.  A Model
+        binds its graph buffer (``masked``: it passes A * edge_importance, so the gradient of A off the
+        support is multiplied by zero and never needed); a bare layer binds the first A it sees and
+        keeps the reference's dense dA."""
         s = self._gsup
         if A.dim() == 3 and (s is None or s.V != A.shape[-1] or s.mask.device != A.device):
             self._gsup = K.GraphSupport(A)
+        self._graph_bound = self._graph_bound or masked
 
     def graph_support(self, A):
         if A.dim() != 3 or os.environ.get("STGCN_GCN_AFIRST"):
             return None  # per-sample A (AAGCN) or forced A-first path
-        self.bind_graph(A)
+        self.bind_graph(A, masked=False)
         return self._gsup
 
     def forward(self, x, A):
@@ -141,7 +145,7 @@ class StgcnLayer(nn.Module):
         else:
             wr = br = nrw = nrb = None
         cfg = (self.kernel_size[0], self.stride, self.is_residual, self.normalization, self.compute_dtype,
-               self.graph_support(A))
+               self.graph_support(A), not self._graph_bound)
         return F_.StgcnLayerFunction.apply(x, A, self.gcn.conv.weight, self.gcn.conv.bias, n1.weight, n1.bias,
                                            conv.weight, conv.bias, n2.weight, n2.bias, wr, br, nrw, nrb, cfg)
 
