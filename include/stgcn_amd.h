@@ -139,6 +139,35 @@ long stgcn_bn_stat_blocks(long M);
 int stgcn_bn_stats_partial(const void* x, int ld, long M, int C, void* part_f4, int dtype, void* stream);
 int stgcn_bn_finalize(const void* part_f4, int nblocks, int ld_part, int C, const float* gamma, const float* beta,
                       float eps, void* mean_rstd_f2, float* scale, float* shift, void* stream);
+/* Fused BatchNorm backward (two row passes), see bn_fused.hip:
+ *   reduce: dz = dy*mask; sums[c] = (sum dz, sum dz*xhat1, sum dz*xhat2, 0)
+ *   apply : out1 = g1*rstd1*(dz - S0/M - xhat1*S1/M) (or dz when x1 == NULL);
+ *           out2 (+)= g2*rstd2*(dz - S0/M - xhat2*S2/M) (or dz when x2 == NULL);  osum[c] = (sum out1,
+ *           sum out2) — the conv-bias gradients.  mask: 0 none | 1 mref > 0 | 2 mref*msc + msh > 0.
+ * Replaces: autograd of stgcn.py:160,171,191-193 (BN2 / residual BN / ReLU / add) and :152-153. */
+typedef struct {
+  const void* dy;
+  const void* mref;
+  const void* x1;
+  const void* x2;
+  const float* msc;
+  const float* msh;
+  const float* mean_rstd1; /* float2 [C] */
+  const float* mean_rstd2;
+  const float* gamma1;
+  const float* gamma2;
+  float* sums;  /* float4 [C] */
+  void* out1;
+  void* out2;
+  float* osum;  /* optional float4 [C] */
+  float* work;  /* float4 [blocks][C], stgcn_bn_bwd_fused_workspace() floats */
+  long M;
+  int C, mask, lddy, ldm, ldx1, ldx2, ldo1, ldo2, acc2;
+} stgcn_bn_bwd_desc;
+
+long stgcn_bn_bwd_fused_workspace(long M, int C, int dtype);
+int stgcn_bn_bwd_fused_reduce(const stgcn_bn_bwd_desc* d, int dtype, void* stream);
+int stgcn_bn_bwd_fused_apply(const stgcn_bn_bwd_desc* d, int dtype, void* stream);
 /* y = act(u*sc + sh + res), res_mode 0 none | 1 r | 2 r*rsc + rsh  (stgcn.py:191-193, rtstgcn.py:386-389);
  * relu bit 0: ReLU after the residual add; bit 1: ReLU on the normalised branch before the add. */
 int stgcn_bn_apply(const void* u, int ldu, const float* sc, const float* sh, int res_mode, const void* r, int ldr,

@@ -54,6 +54,13 @@ class GconvWgradDesc(ctypes.Structure):
                [("work", c_void_p), ("work_bytes", c_long)]
 
 
+class BnBwdDesc(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in ("dy", "mref", "x1", "x2", "msc", "msh", "mean_rstd1", "mean_rstd2",
+                                        "gamma1", "gamma2", "sums", "out1", "out2", "osum", "work")] + \
+               [("M", c_long)] + [(n, c_int) for n in ("C", "mask", "lddy", "ldm", "ldx1", "ldx2", "ldo1", "ldo2",
+                                                       "acc2")]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "stgcn_abi_version": (c_int, []),
@@ -63,6 +70,9 @@ _SIGS = {
     "stgcn_conv_wgrad": (c_int, [ctypes.POINTER(WgradDesc), c_int, c_void_p]),
     "stgcn_conv_wgrad_workspace": (c_long, [ctypes.POINTER(WgradDesc), c_int]),
     "stgcn_gconv": (c_int, [ctypes.POINTER(GconvDesc), c_int, c_void_p]),
+    "stgcn_bn_bwd_fused_workspace": (c_long, [c_long, c_int, c_int]),
+    "stgcn_bn_bwd_fused_reduce": (c_int, [ctypes.POINTER(BnBwdDesc), c_int, c_void_p]),
+    "stgcn_bn_bwd_fused_apply": (c_int, [ctypes.POINTER(BnBwdDesc), c_int, c_void_p]),
     "stgcn_gconv_row_blocks": (c_long, [c_int, c_int]),
     "stgcn_gconv_weights": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 6 + [c_void_p, c_int, c_int,
                                                                                            c_int, c_void_p]),

@@ -21,6 +21,9 @@ long wgrad_tile_workspace(const WgradArgs& a, int dtype);
 int wgrad_tile_launch(const WgradArgs& a, int dtype, hipStream_t s);
 int amix_fwd_launch(const AmixArgs& a, int dtype, hipStream_t s);
 long gconv_row_blocks(int NT, int V);
+long bn_bwd_fused_work_floats(long M, int C, int dtype);
+int bn_bwd_fused_reduce_launch(const stgcn_bn_bwd_desc& a, int dtype, hipStream_t s);
+int bn_bwd_fused_apply_launch(const stgcn_bn_bwd_desc& a, int dtype, hipStream_t s);
 int gconv_launch(const stgcn_gconv_desc& a, int dtype, hipStream_t s);
 int gconv_weights_launch(const float* A, const float* W, const int* nbr, const int* deg, int P, int V, int J, int Cout,
                          int Cin, int trans, void* out, int R_pad, int C_pad, int dtype, hipStream_t s);
@@ -103,6 +106,25 @@ int stgcn_conv_wgrad(const stgcn_wgrad_desc* d, int dtype, void* stream) {
   const int r = wgrad_tile_launch(*d, dtype, STREAM(stream));  // bf16 frame-tiled path (needs work)
   if (r >= 0) return r;
   return conv_wgrad_launch(*d, dtype, STREAM(stream));
+}
+
+long stgcn_bn_bwd_fused_workspace(long M, int C, int dtype) {
+  if (M <= 0 || C <= 0 || (dtype != 0 && dtype != 1)) return 0;
+  return bn_bwd_fused_work_floats(M, C, dtype);
+}
+int stgcn_bn_bwd_fused_reduce(const stgcn_bn_bwd_desc* d, int dtype, void* stream) {
+  CHECK_DTYPE(dtype);
+  if (!d || !d->dy || d->M <= 0 || d->C <= 0 || (d->mask && !d->mref) || (d->mask == 2 && (!d->msc || !d->msh)) ||
+      (d->x1 && !d->mean_rstd1) || (d->x2 && !d->mean_rstd2))
+    return STGCN_EBADSHAPE;
+  return bn_bwd_fused_reduce_launch(*d, dtype, STREAM(stream));
+}
+int stgcn_bn_bwd_fused_apply(const stgcn_bn_bwd_desc* d, int dtype, void* stream) {
+  CHECK_DTYPE(dtype);
+  if (!d || !d->dy || d->M <= 0 || d->C <= 0 || (d->mask && !d->mref) || (d->mask == 2 && (!d->msc || !d->msh)) ||
+      (d->x1 && !d->mean_rstd1) || (d->x2 && !d->mean_rstd2))
+    return STGCN_EBADSHAPE;
+  return bn_bwd_fused_apply_launch(*d, dtype, STREAM(stream));
 }
 
 int stgcn_gconv(const stgcn_gconv_desc* d, int dtype, void* stream) {

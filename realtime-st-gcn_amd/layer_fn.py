@@ -205,7 +205,26 @@ class StgcnLayerFunction(torch.autograd.Function):
         du = K.cl_empty(N, Cout, T_out, V, dtype, dev)
         dx = K.cl_empty(N, Cin, T, V, dtype, dev)
         dx_written = False
-        if norm == BN:
+        fused = norm == BN and K.bn_fused_ok(Cout, dtype)
+        bt_done = False
+        if fused:
+            # one reduce + one apply pass: du, the residual branch's dr (or dx = dz), and the conv-bias
+            # gradients (column sums of du / dr) together
+            kw = dict(mask=1, mref=y, x1=u, mr1=mr2, g1=n2w.detach().float(), out1=du, bias_sums=True)
+            if res_conv:
+                dr = K.cl_empty(N, Cout, T_out, V, dtype, dev)
+                kw.update(x2=r, mr2=strr, g2=nrw.detach().float(), out2=dr)
+            elif residual:
+                kw.update(out2=dx)
+                dx_written = True
+            sums2, osum2 = K.bn_bwd_fused(dy, M2, Cout, **kw)
+            grads["n2w"], grads["n2b"] = sums2[:, 1].clone(), sums2[:, 0].clone()
+            grads["bt"] = osum2[:, 0].clone()
+            bt_done = True
+            if res_conv:
+                grads["nrw"], grads["nrb"] = sums2[:, 2].clone(), sums2[:, 0].clone()
+                grads["br"] = osum2[:, 1].clone()
+        elif norm == BN:
             s2 = K.bn_bwd_reduce(dy, M2, Cout, mask=1, mref=y, x=u, mean_rstd=mr2)
             K.bn_bwd_apply(dy, M2, Cout, du, mask=1, mref=y, x=u, mean_rstd=mr2, gamma=n2w.detach().float(), sums=s2)
             grads["n2w"], grads["n2b"] = s2[:, 1].clone(), s2[:, 0].clone()
@@ -215,25 +234,26 @@ class StgcnLayerFunction(torch.autograd.Function):
             grads["n2w"], grads["n2b"] = dgb2[0].view(n2w.shape), dgb2[1].view(n2b.shape)
 
         if res_conv:
-            dr = K.cl_empty(N, Cout, T_out, V, dtype, dev)
-            if norm == BN:
-                sr = K.bn_bwd_reduce(dy, M2, Cout, mask=1, mref=y, x=r, mean_rstd=strr)
-                K.bn_bwd_apply(dy, M2, Cout, dr, mask=1, mref=y, x=r, mean_rstd=strr, gamma=nrw.detach().float(),
-                               sums=sr)
-                grads["nrw"], grads["nrb"] = sr[:, 1].clone(), sr[:, 0].clone()
-            else:
-                dgbr = torch.zeros((2, Cout * V), dtype=torch.float32, device=dev)
-                K.ln_bwd(dy, r, strr, _flat_ln(nrw), _flat_ln(nrb), N * T_out, V, Cout, dr, mask=1, mref=y,
-                         dgb=dgbr)
-                grads["nrw"], grads["nrb"] = dgbr[0].view(nrw.shape), dgbr[1].view(nrb.shape)
-            # residual conv (1x1, stride s, bias): data grad (transposed), weight grad, bias grad
+            if not fused:
+                dr = K.cl_empty(N, Cout, T_out, V, dtype, dev)
+                if norm == BN:
+                    sr = K.bn_bwd_reduce(dy, M2, Cout, mask=1, mref=y, x=r, mean_rstd=strr)
+                    K.bn_bwd_apply(dy, M2, Cout, dr, mask=1, mref=y, x=r, mean_rstd=strr,
+                                   gamma=nrw.detach().float(), sums=sr)
+                    grads["nrw"], grads["nrb"] = sr[:, 1].clone(), sr[:, 0].clone()
+                else:
+                    dgbr = torch.zeros((2, Cout * V), dtype=torch.float32, device=dev)
+                    K.ln_bwd(dy, r, strr, _flat_ln(nrw), _flat_ln(nrb), N * T_out, V, Cout, dr, mask=1, mref=y,
+                             dgb=dgbr)
+                    grads["nrw"], grads["nrb"] = dgbr[0].view(nrw.shape), dgbr[1].view(nrb.shape)
+                grads["br"] = K.bn_bwd_reduce(dr, M2, Cout)[:, 0].clone()
+            # residual conv (1x1, stride s, bias): data grad (transposed), weight grad
             wrT = wr.detach().float().view(Cout, Cin).t().reshape(1, Cin, Cout)
             wrTp, cq, kq = K.pack_weight(wrT, dtype)
             K.conv_rows(dr, wrTp, Cout, Cin, cq, kq, T_out, T, Kt=1, stride=stride, pad=0, trans=True, out=dx)
             dx_written = True
             grads["wr"] = K.conv_wgrad(x, dr, Cin, Cout, T, T_out, Kt=1, stride=stride, pad=0).view(Cout, Cin, 1, 1)
-            grads["br"] = K.bn_bwd_reduce(dr, M2, Cout)[:, 0].clone()
-        elif residual:
+        elif residual and not fused:
             K.bn_bwd_apply(dy, M2, Cin, dx, mask=1, mref=y)  # dx = dz
             dx_written = True
 
@@ -247,11 +267,16 @@ class StgcnLayerFunction(torch.autograd.Function):
             pro1 = dict(pro=2, pro_a=_flat_ln(n1w), pro_b=_flat_ln(n1b), pro_stats=ls1)
         dwt = K.conv_wgrad(g, du, Cout, Cout, T, T_out, Kt=kt, stride=stride, pad=pad, **pro1)
         grads["wt"] = dwt.permute(1, 2, 0).unsqueeze(-1)  # [Kt][co][ci] -> (co, ci, Kt, 1)
-        grads["bt"] = K.bn_bwd_reduce(du, M2, Cout)[:, 0].clone()
+        if not bt_done:
+            grads["bt"] = K.bn_bwd_reduce(du, M2, Cout)[:, 0].clone()
 
         # ---- through relu(norm1(g))
         dg = K.cl_empty(N, Cout, T, V, dtype, dev)
-        if norm == BN:
+        if fused:
+            s1, _ = K.bn_bwd_fused(dh, M1, Cout, mask=2, mref=g, msc=sc1, msh=sh1, x1=g, mr1=mr1,
+                                   g1=n1w.detach().float(), out1=dg)
+            grads["n1w"], grads["n1b"] = s1[:, 1].clone(), s1[:, 0].clone()
+        elif norm == BN:
             s1 = K.bn_bwd_reduce(dh, M1, Cout, mask=2, mref=g, msc=sc1, msh=sh1, x=g, mean_rstd=mr1)
             K.bn_bwd_apply(dh, M1, Cout, dg, mask=2, mref=g, msc=sc1, msh=sh1, x=g, mean_rstd=mr1,
                            gamma=n1w.detach().float(), sums=s1)

@@ -318,6 +318,39 @@ def bn_bwd_apply(dy, M, C, out, mask=0, mref=None, msc=None, msh=None, x=None, m
     return out
 
 
+def bn_fused_ok(C: int, dtype) -> bool:
+    vec = 8 if dtype == torch.bfloat16 else 4
+    return C % vec == 0 and C // vec <= 256
+
+
+def bn_bwd_fused(dy, M, C, mask=0, mref=None, msc=None, msh=None, x1=None, mr1=None, g1=None, out1=None,
+                 x2=None, mr2=None, g2=None, out2=None, acc2=False, bias_sums=False):
+    """Fused BN backward (stgcn_bn_bwd_fused_*).  Returns (sums [C,4] = (sum dz, sum dz*xhat1, sum dz*xhat2),
+    osum [C,4] = (sum out1, sum out2) or None).  out1 / out2 are written in place."""
+    code = L.dtype_code(dy.dtype)
+    dev = dy.device
+    work = torch.empty(L.lib().stgcn_bn_bwd_fused_workspace(M, C, code), dtype=torch.float32, device=dev)
+    sums = torch.empty((C, 4), dtype=torch.float32, device=dev)
+    osum = torch.empty((C, 4), dtype=torch.float32, device=dev) if bias_sums else None
+    d = L.BnBwdDesc()
+    d.dy, d.mref, d.x1, d.x2 = dy.data_ptr(), L.ptr(mref), L.ptr(x1), L.ptr(x2)
+    d.msc, d.msh, d.mean_rstd1, d.mean_rstd2 = L.ptr(msc), L.ptr(msh), L.ptr(mr1), L.ptr(mr2)
+    d.gamma1, d.gamma2, d.sums = L.ptr(g1), L.ptr(g2), sums.data_ptr()
+    d.out1, d.out2, d.osum, d.work = L.ptr(out1), L.ptr(out2), L.ptr(osum), work.data_ptr()
+    d.M, d.C, d.mask = M, C, mask
+    d.lddy = rows_ld(dy)
+    d.ldm = rows_ld(mref) if mref is not None else 0
+    d.ldx1 = rows_ld(x1) if x1 is not None else 0
+    d.ldx2 = rows_ld(x2) if x2 is not None else 0
+    d.ldo1 = rows_ld(out1) if out1 is not None else 0
+    d.ldo2 = rows_ld(out2) if out2 is not None else 0
+    d.acc2 = int(acc2)
+    L.check(L.lib().stgcn_bn_bwd_fused_reduce(d, code, L.stream()), "bn_bwd_fused_reduce")
+    if out1 is not None:
+        L.check(L.lib().stgcn_bn_bwd_fused_apply(d, code, L.stream()), "bn_bwd_fused_apply")
+    return sums, osum
+
+
 def rowgroup_sum(x, M, C, G, per_sample=False):
     """[G][C] (or [N][G][C] per sample) sums of rows grouped by m % G."""
     N = x.shape[0]

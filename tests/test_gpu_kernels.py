@@ -198,3 +198,61 @@ def test_box_sum(K):
         for i in range(Kt // S):
             adj[:, :, :T - i * S] += x[:, :, i * S:]
         assert_close(K.box_sum(cl(x), Kt, S, trans=True).cpu(), adj, 1e-6, "box sum adjoint")
+
+
+def _bn_ref(x, w, b):
+    mu = x.mean(dim=(0, 2, 3), keepdim=True)
+    var = x.var(dim=(0, 2, 3), unbiased=False, keepdim=True)
+    return (x - mu) / torch.sqrt(var + 1e-5) * w.view(1, -1, 1, 1) + b.view(1, -1, 1, 1)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 2e-2)])
+@pytest.mark.parametrize("mode", ["conv_res", "identity", "none", "bn1"])
+def test_bn_bwd_fused(K, dtype, tol, mode):
+    """Fused BN backward vs autograd of relu(BN2(u) + res) (stgcn.py:160-193) / relu(BN1(g)) (:152-153)."""
+    torch.manual_seed(9)
+    N, C, T, V = 3, 64, 21, 25
+    M = N * T * V
+    rnd = lambda t: t.to(dtype).float()  # inputs as the kernels store them (masks then agree exactly)
+    u = rnd(torch.randn(N, C, T, V) * 2 + 0.5).requires_grad_(True)
+    r = rnd(torch.randn(N, C, T, V) - 0.3).requires_grad_(True)
+    x = rnd(torch.randn(N, C, T, V)).requires_grad_(True)
+    w2, b2, wr, brr = torch.rand(C) + 0.5, torch.randn(C), torch.rand(C) + 0.5, torch.randn(C)
+    if mode == "bn1":
+        y = torch.relu(_bn_ref(u, w2, b2))
+    else:
+        res = {"conv_res": _bn_ref(r, wr, brr), "identity": x, "none": 0}[mode]
+        y = torch.relu(_bn_ref(u, w2, b2) + res)
+    dy = torch.randn(y.shape)
+    y.backward(dy)
+
+    def stats(t):
+        return torch.stack([t.mean(dim=(0, 2, 3)), 1 / torch.sqrt(t.var(dim=(0, 2, 3), unbiased=False) + 1e-5)],
+                           -1).to(DEV).contiguous()
+
+    ud, rd = cl(u.detach(), dtype), cl(r.detach(), dtype)
+    # the mask reference as the kernels see it: the stored (rounded) forward output
+    yd = cl(y.detach(), dtype)
+    du = torch.empty_like(ud)
+    kw = dict(x1=ud, mr1=stats(u.detach()), g1=w2.to(DEV), out1=du, bias_sums=True)
+    if mode == "bn1":
+        mr = stats(u.detach())
+        sc = (w2.to(DEV) * mr[:, 1])
+        sh = (b2.to(DEV) - mr[:, 0] * sc)
+        kw.update(mask=2, mref=ud, msc=sc.contiguous(), msh=sh.contiguous())
+    else:
+        kw.update(mask=1, mref=yd)
+    out2 = None
+    if mode == "conv_res":
+        out2 = torch.empty_like(rd)
+        kw.update(x2=rd, mr2=stats(r.detach()), g2=wr.to(DEV), out2=out2)
+    elif mode == "identity":
+        out2 = torch.empty_like(ud)
+        kw.update(out2=out2)
+    sums, osum = K.bn_bwd_fused(cl(dy, dtype), M, C, **kw)
+    assert_close(du.float(), u.grad, tol, "du")
+    assert_close(osum[:, 0].cpu(), u.grad.sum(dim=(0, 2, 3)), tol, "sum du", u.grad.abs().sum(dim=(0, 2, 3)).max())
+    if mode == "conv_res":
+        assert_close(out2.float(), r.grad, tol, "dr")
+    if mode == "identity":
+        assert_close(out2.float(), x.grad, tol, "dx")
