@@ -6,8 +6,10 @@ One step = forward of the whole model on one (64, 3, 300, 25) batch + the refere
 WindowSegment.mask_segment) + backward + Adam step.  Inputs are resident in HBM before timing.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
-N > 1: launched by torch.distributed.run, one process per GPU, RCCL (backend "nccl") DDP gradient
-all-reduce; each rank processes its own 64-window batch (weak scaling).
+Kernels are launched eagerly from Python (the GPU stays busy: launch cost < kernel time); --graph
+captures the step into HIP graphs (torch.cuda.CUDAGraph) and replays them instead.
+N > 1: launched by torch.distributed.run, one process per GPU, DistributedDataParallel over RCCL
+(backend "nccl"); each rank processes its own 64-window batch (weak scaling).
 Rank 0 prints ONE JSON line (metric/value/..., roofline, cpu_baseline).
 """
 from __future__ import annotations
@@ -84,6 +86,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the step into HIP graphs and replay them (measured slower than eager here)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -103,37 +107,95 @@ def main():
     model = pkg.MODELS["st-gcn"](rank=None, **dict(ARCH, graph=pkg.PKU_MMD))
     cpu_sd = {k: v.clone() for k, v in model.state_dict().items()}
     model = model.to(dev).set_compute_dtype(args.dtype)
+    params = [p for p in model.parameters() if p.requires_grad]
     train_model = model
-    if world > 1:
-        train_model = pkg.parallel.ddp(model, dev, bucket_cap_mb=16)  # RCCL all-reduce of fp32 grads
-    opt = torch.optim.Adam(model.parameters(), lr=5e-4, foreach=True)
+    if world > 1 and not args.graph:
+        train_model = pkg.parallel.ddp(model, dev, bucket_cap_mb=16)  # RCCL all-reduce overlapped with bwd
+    elif world > 1:  # identical replicas (DistributedDataParallel's broadcast from rank 0)
+        for p in params:
+            torch.distributed.broadcast(p.data, 0)
+    opt = torch.optim.Adam(params, lr=5e-4, foreach=True, capturable=args.graph)
 
     gen = torch.Generator(device=dev).manual_seed(rank)
     x = torch.randn(N_BATCH, 3, T_LEN, V_J, device=dev, generator=gen)
     labels = torch.randint(0, CLASSES, (1, N_BATCH), device=dev, generator=gen)
     weight = (1 - torch.rand(CLASSES, device=dev, generator=gen) / CLASSES)
 
-    def step():
+    # Gradient exchange (N > 1): eager mode uses DistributedDataParallel (RCCL all-reduce of 16 MB
+    # buckets overlapped with backward); graph mode all-reduces one flat fp32 buffer between the
+    # backward graph and the optimizer graph.  BatchNorm statistics stay per replica in both.
+    numels = [p.numel() for p in params]
+    flat = torch.zeros(sum(numels), device=dev) if world > 1 and args.graph else None
+
+    def fwd_bwd():
         y = train_model(x)
         loss = loss_fn(y, labels, weight)
         loss.backward()
+        if flat is not None:
+            torch.cat([p.grad.reshape(-1) for p in params], out=flat)
+        return loss
+
+    def opt_step():
+        if flat is not None:
+            for p, g in zip(params, torch.split(flat, numels)):
+                p.grad.copy_(g.view_as(p.grad)).div_(world)
         opt.step()
-        opt.zero_grad(set_to_none=True)
 
-    for _ in range(args.warmup):
-        step()
+    def eager_step():
+        opt.zero_grad(set_to_none=False)
+        fwd_bwd()
+        if flat is not None:
+            torch.distributed.all_reduce(flat)
+        opt_step()
 
-    # live timing of the dominant kernel (temporal-conv forward of the C=64 layers) on its stream
+    # live timing of the dominant kernel (temporal-conv forward of the C=64 layers): HIP events on
+    # the stream the kernel is launched on.  ROCm refuses timing events inside a captured graph, so in
+    # graph mode the events bracket the launches of one eager step run right after the timed region.
     events = []
+    timing = {"on": False}
 
     def hook(tag, phase):
-        if tag != "tcn_fwd_c64":
+        if tag != "tcn_fwd_c64" or not timing["on"]:
             return
         ev = torch.cuda.Event(enable_timing=True)
         ev.record(torch.cuda.current_stream())
         events.append(ev)
 
     K.EVENT_HOOK = hook
+    for _ in range(max(args.warmup, 2)):
+        eager_step()
+    torch.cuda.synchronize()
+
+    graphs = None
+    if args.graph:
+        # capture: [zero grads, fwd, loss, bwd (+ flatten)] and [unflatten/average, Adam]; grads keep
+        # their addresses, so replays overwrite them in place
+        opt.zero_grad(set_to_none=False)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1):
+                for p in params:
+                    p.grad.zero_()
+                fwd_bwd()
+            with torch.cuda.graph(g2):
+                opt_step()
+        torch.cuda.current_stream().wait_stream(s)
+        graphs = (g1, g2)
+
+        def step():
+            g1.replay()
+            if flat is not None:
+                torch.distributed.all_reduce(flat)
+            g2.replay()
+        for _ in range(2):
+            step()
+    else:
+        step = eager_step
+
+    if not args.graph:
+        timing["on"] = True
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -144,12 +206,18 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
+    if args.graph:
+        timing["on"] = True
+        eager_step()
+        torch.cuda.synchronize()
+    timing["on"] = False
     K.EVENT_HOOK = None
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = t.item()
 
+    # eager mode: every launch of the timed region; graph mode: the 6 launches of the step after it
     kt = [events[i].elapsed_time(events[i + 1]) for i in range(0, len(events) - 1, 2)]
     k_ms = sum(kt) / len(kt) if kt else float("nan")
     achieved = tcn_flops_c64() / (k_ms * 1e-3) / 1e12 if kt else None
@@ -173,14 +241,17 @@ def main():
             "data": "synthetic (randn skeletons, random labels/class weights), random-init weights",
             "config": {"workload": "config 2: as_is st-gcn (fcn_in + 9 StgcnLayer, BatchNorm, Kt=9), fwd + loss + "
                                    "bwd + Adam", "global_batch": N_BATCH * world, "seq_len": T_LEN, "joints": V_J,
-                       "parallelism": f"dp{world}" if world > 1 else "single"},
-            "roofline": {"kernel": "conv_rows_kernel (temporal conv fwd, C=64, Kt=9, stride 1)", "bound": "mfma",
-                         "achieved": round(achieved, 2) if achieved else None, "peak": BF16_DENSE_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4) if achieved else None,
+                       "parallelism": f"dp{world}" if world > 1 else "single",
+                       "launch": "eager" if not args.graph else "hip-graph replay (fwd+bwd | allreduce | Adam)"},
+            "roofline": {"kernel": "conv_tile_kernel (frame-tiled temporal conv fwd, C=64, Kt=9, stride 1)",
+                         "bound": "mfma", "achieved": round(achieved, 2) if achieved else None,
+                         "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4) if achieved else None,
                          "traffic": traffic, "avg_launch_ms": round(k_ms, 4), "launches_timed": len(kt)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
+    del graphs
     if world > 1:
         torch.distributed.destroy_process_group()
 
