@@ -70,7 +70,7 @@ def cpu_baseline(pkg, model_cpu_sd):
 
     step(2)  # warm-up (allocator, oneDNN primitives)
     t0 = time.perf_counter()
-    reps = 2
+    reps = 3
     for _ in range(reps):
         step(n_sample)
     dt = time.perf_counter() - t0
