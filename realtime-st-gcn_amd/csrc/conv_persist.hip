@@ -3,34 +3,40 @@
 // and its data gradient).
 //
 // Why: at C = 64 the K axis is only Kt*64 = 576 deep, so the frame-tiled kernel (conv_tile.hip)
-// spends more time fetching the 74 KB weight tile (all 9 taps) into every block and waiting on
-// each short K-chunk than it spends in MFMA (measured ~10 % of peak).  Here one block per CU
-//   * loads the whole packed weight [9][64 co][64 ci] into LDS ONCE (LDS-DMA, XOR-swizzled 128-B
+// spends more time fetching the 74 KB weight tile into every block and waiting on each short
+// K-chunk than in MFMA, and its VALU work (prologue, epilogue) runs in lock-step with the MFMAs
+// of the same waves.  Here one block per CU
+//   * loads the whole packed weight [9][64 co][64 ci] into LDS once (LDS-DMA, XOR-swizzled 128-B
 //     rows, conflict-free ds_read_b128),
-//   * walks a contiguous range of F-frame tiles of the same samples (F = floor(128/V): 5 frames at
-//     V = 25), staging each tile's halo of F+8 frames x 64 channels (BN1+ReLU prologue applied once
-//     per element; frames outside [0,T) zero) into a double-buffered, XOR-swizzled LDS ring while
-//     the previous tile computes,
-//   * runs 8 waves = 4 row groups (32 rows) x 2 column tiles (32 cols): per k-step one A and one B
-//     fragment per MFMA, tap dt reading halo rows r + q(dt)*V (q = dt fwd, 8-dt transposed),
-//   * accumulates the BatchNorm partial statistics (Welford) of all its tiles in registers and
-//     writes one partial row per block.
+//   * walks a contiguous range of F-frame tiles (F = floor(128/V): 5 frames at V = 25) through a
+//     ring of RS = 2F+8 frame slots in LDS (rows padded to 144 B): a tile reads frames
+//     f0-4 .. f0+F+3 and only the F newest are not in the ring already — each frame is fetched and
+//     transformed (BN1+ReLU prologue; zero padding outside [0,T)) once per block,
+//   * splits its 8 waves into two groups of 4 that alternate roles every phase: group (k & 1)
+//     computes tile k (4 waves x 64 rows x 32 cols, 72 MFMAs each) while the other group runs the
+//     epilogue of tile k-1 (bias, bf16 store, BatchNorm Welford partials), writes tile k+1's new
+//     frames into the ring from registers and issues the global loads for tile k+3.  Waves w and
+//     w+4 share a SIMD, so every SIMD always has one MFMA wave and one VALU/memory wave,
+//   * tap dt reads frame slot (f0 + fl + q(dt)) mod RS, q = dt (fwd) or 8 - dt (transposed = data
+//     gradient); a tile that starts a new sample is staged in an extra synchronous phase.
 #include "common.h"
 #include "../../include/stgcn_amd.h"
 
 namespace {
 
 constexpr int KT = 9;
-constexpr int C = 64;            // Cin_pad = Cout_pad = 64
-constexpr int RB = C * 2;        // bytes per row (bf16)
-constexpr int NWAVE = 8, NT = NWAVE * 64;
-constexpr int ROWS = 128;        // MFMA rows per tile (4 row groups x 32)
+constexpr int PADT = (KT - 1) / 2;
+constexpr int C = 64;                  // Cin_pad = Cout_pad = 64
+constexpr int RB = C * 2;              // bytes per weight row (bf16)
+constexpr int RS_A = RB + 16;          // bytes per activation row in the ring (padded)
+constexpr int NWAVE = 8, NT = NWAVE * 64, GT = NT / 2;  // two groups of 4 waves
+constexpr int ROWS = 128;              // MFMA rows per tile (2 row groups x 64)
+constexpr int TM = 2;                  // 32-row MFMA tiles per wave
 constexpr int B_BYTES = KT * C * RB;   // 73 728
-constexpr int HR_MAX = 352;      // halo rows per stage: (F + 8) * V <= 352
-constexpr int A_BYTES = HR_MAX * RB;   // 45 056
-constexpr int A_MAX = (HR_MAX * 8 + NT - 1) / NT;  // 16-B units per thread per tile (6)
+constexpr int LDS_MAX = 160 * 1024;
+constexpr int RA = ROWS * 8 / GT;      // steady-state units per thread of a group: F*V <= 128 rows -> 4
 
-DEV int swz(int row) { return (row >> 1) & 7; }  // 128-B rows: 2 rows per 256-B bank row
+DEV int swz(int row) { return (row >> 1) & 7; }  // weight rows: 2 rows per 256-B bank row
 
 DEV void glds16(const void* src, char* lds_base) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -39,28 +45,26 @@ DEV void glds16(const void* src, char* lds_base) {
 }
 
 struct PGeom {
-  int F;         // frames per tile
-  int tiles_n;   // tiles per sample
-  int ntiles;    // total tiles
-  int tpb;       // tiles per block
-  int HR;        // halo rows
+  int F;        // frames per tile
+  int RSL;      // ring slots (frames)
+  int tiles_n;  // tiles per sample
+  int ntiles;   // total tiles
+  int tpb;      // tiles per block
 };
 
 __global__ __launch_bounds__(NT, 1) void conv_persist_kernel(const stgcn_conv_desc a, const PGeom g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* sB = smem;
-  char* sA0 = smem + B_BYTES;
+  char* sR = smem + B_BYTES;  // ring: slot s, joint v at (s*V + v) * RS_A
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave & 3, wc = wave >> 2;
+  const int grp = wave >> 2, gw = wave & 3, gtid = tid & (GT - 1);
+  const int wr = gw & 1, wc = gw >> 1;  // rows [64 wr, +64) x cols [32 wc, +32)
   const int lr = lane & 31, lh = lane >> 5;
   const int V = a.V;
   const int t_begin = blockIdx.x * g.tpb;
-  const int t_end = min(g.ntiles, t_begin + g.tpb);
-  if (t_begin >= t_end) {
-    // no tiles: still publish an empty statistics row (the caller zero-fills, nothing to do)
-    return;
-  }
+  const int K = min(g.ntiles, t_begin + g.tpb) - t_begin;
+  if (K <= 0) return;
 
   const bf16* __restrict__ in = reinterpret_cast<const bf16*>(a.in);
   const bf16* __restrict__ wp = reinterpret_cast<const bf16*>(a.w);
@@ -72,164 +76,233 @@ __global__ __launch_bounds__(NT, 1) void conv_persist_kernel(const stgcn_conv_de
     const int dt = br >> 6, co = br & 63;
     glds16(wp + ((long)dt * a.Cout_pad + co) * a.Cin_pad + (pu ^ swz(br)) * 8, sB + piece * 1024);
   }
+  float* s_aff = reinterpret_cast<float*>(sR + g.RSL * V * RS_A);  // [2][64] BN1 scale / shift
+  if (tid < 2 * C) s_aff[tid] = a.pro == 1 ? (tid < C ? a.pro_a[tid] : a.pro_b[tid - C]) : (tid < C ? 1.f : 0.f);
 
-  // ---- per-thread staging units: unit id = tid + i*NT -> (halo row, 16-B column)
+  // ---- staging helpers; a unit = 16 B (8 channels) of one joint row of one frame
   const int ucol = tid & 7;
-  float sc[8], sh[8];
+  auto transform = [&](uint4 v) -> uint4 {
+    if (a.pro != 1) return v;
+    const float4* sa = reinterpret_cast<const float4*>(s_aff + ucol * 8);
+    const float4* sb = reinterpret_cast<const float4*>(s_aff + C + ucol * 8);
+    const float4 a0 = sa[0], a1 = sa[1], b0 = sb[0], b1 = sb[1];
+    const float sc[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const float sh[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    float f[8];
+    unpack16(v, f, (bf16*)nullptr);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int ci = ucol * 8 + j;
-    sc[j] = (a.pro == 1 && ci < a.Cin) ? a.pro_a[ci] : 1.f;
-    sh[j] = (a.pro == 1 && ci < a.Cin) ? a.pro_b[ci] : 0.f;
-  }
-  int u_fl[A_MAX], u_v[A_MAX], u_lds[A_MAX];
-#pragma unroll
-  for (int i = 0; i < A_MAX; ++i) {
-    const int row = (tid + i * NT) >> 3;
-    u_fl[i] = row / V;
-    u_v[i] = row - u_fl[i] * V;
-    u_lds[i] = row < g.HR ? row * RB + ((ucol ^ swz(row)) << 4) : -1;
-  }
-  const int pad = (KT - 1) / 2;
-  uint4 ra[A_MAX];
-  unsigned zm = 0;  // bit i: unit i of the staged tile is a zero-padding row (frame outside [0, T))
-
-  auto load = [&](int t) {
-    const int n = t / g.tiles_n, f0 = (t - n * g.tiles_n) * g.F;
+    for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], sc[j], sh[j]), 0.f);
+    return pack16(f, (bf16*)nullptr);
+  };
+  auto put = [&](uint4 v, int f, int vj) {  // frame f -> ring slot (f + PADT) mod RS
+    const int slot = (f + PADT) % g.RSL;
+    *reinterpret_cast<uint4*>(sR + (slot * V + vj) * RS_A + ucol * 16) = v;
+  };
+  auto fetch = [&](long base, int f, int vj) -> uint4 {
+    if (f < 0 || f >= a.T_in) return make_uint4(0, 0, 0, 0);
+    return *reinterpret_cast<const uint4*>(in + ((base + f) * V + vj) * a.in_ld + ucol * 8);
+  };
+  auto tile_nf = [&](int k, int& n, int& f0) {
+    const int t = t_begin + k;
+    n = t / g.tiles_n;
+    f0 = (t - n * g.tiles_n) * g.F;
+  };
+  // fresh halo of tile k (frames f0-4 .. f0+F+3), all 512 threads, synchronous
+  auto stage_fresh = [&](int k) {
+    int n, f0;
+    tile_nf(k, n, f0);
     const long base = (long)n * a.T_in;
-    zm = 0;
-#pragma unroll
-    for (int i = 0; i < A_MAX; ++i) {
-      ra[i] = make_uint4(0, 0, 0, 0);
-      const int fi = f0 - pad + u_fl[i];
-      if (u_lds[i] >= 0 && fi >= 0 && fi < a.T_in)
-        ra[i] = *reinterpret_cast<const uint4*>(in + ((base + fi) * V + u_v[i]) * a.in_ld + ucol * 8);
-      else
-        zm |= 1u << i;
+    const int rows = (g.F + KT - 1) * V;
+    for (int r = tid >> 3; r < rows; r += NT / 8) {
+      const int j = r / V, vj = r - j * V;
+      const int f = f0 - PADT + j;
+      const uint4 v = fetch(base, f, vj);
+      put((f < 0 || f >= a.T_in) ? v : transform(v), f, vj);
     }
   };
-  auto store = [&](int buf) {
-    char* A_ = sA0 + buf * A_BYTES;
+  // steady state: tile k's F new frames f0+4 .. f0+F+3, by one group (256 threads, <= 4 units each)
+  uint4 ra[RA];
+  auto prefetch = [&](int k) {
+    int n, f0;
+    tile_nf(k, n, f0);
+    const long base = (long)n * a.T_in;
 #pragma unroll
-    for (int i = 0; i < A_MAX; ++i) {
-      if (u_lds[i] < 0) continue;
-      const bool zero = (zm >> i) & 1u;
-      uint4 v = ra[i];
-      if (zero) {
-        v = make_uint4(0, 0, 0, 0);
-      } else if (a.pro == 1) {
-        float f[8];
-        unpack16(v, f, (bf16*)nullptr);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], sc[j], sh[j]), 0.f);
-        v = pack16(f, (bf16*)nullptr);
-      }
-      *reinterpret_cast<uint4*>(A_ + u_lds[i]) = v;
+    for (int i = 0; i < RA; ++i) {
+      const int r = (gtid >> 3) + i * (GT / 8);
+      const int j = r / V, vj = r - j * V;
+      ra[i] = j < g.F ? fetch(base, f0 + PADT + j, vj) : make_uint4(0, 0, 0, 0);
     }
+  };
+  auto commit = [&](int k) {
+    int n, f0;
+    tile_nf(k, n, f0);
+#pragma unroll
+    for (int i = 0; i < RA; ++i) {
+      const int r = (gtid >> 3) + i * (GT / 8);
+      const int j = r / V, vj = r - j * V;
+      if (j < g.F) {
+        const int f = f0 + PADT + j;
+        put((f < 0 || f >= a.T_in) ? ra[i] : transform(ra[i]), f, vj);
+      }
+    }
+  };
+  auto fresh = [&](int k) {  // tile k starts a sample (or the block's range)
+    int n, f0;
+    tile_nf(k, n, f0);
+    return k == 0 || f0 == 0;
   };
 
-  // ---- fragment addressing
-  int a_base;  // halo row of this lane's MFMA row at tap offset 0
-  {
-    const int r = wr * 32 + lr;
-    const int rr = r < g.F * V ? r : 0;  // padding rows of the tile read anything in range
-    const int fl = rr / V;
-    a_base = fl * V + (rr - fl * V);
+  // ---- MFMA fragment addressing (two 32-row tiles per wave)
+  int fl[TM], a_lane[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r_l = wr * 64 + i * 32 + lr;
+    const int rr = r_l < g.F * V ? r_l : 0;  // padding rows of the tile read anything in range
+    fl[i] = rr / V;
+    a_lane[i] = (rr - fl[i] * V) * RS_A + lh * 16;  // + slot * V * RS_A + ks * 32
   }
-  const int b_lane = (wc * 32 + lr) * RB;  // + dt*64*RB ; unit (2ks+lh) ^ swz(lr)
-  const int b_sw = swz(lr);
+  const int slot_stride = V * RS_A;
+  int boff[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) boff[ks] = (wc * 32 + lr) * RB + (((2 * ks + lh) ^ swz(lr)) << 4);
   const bool rev = a.trans != 0;
 
-  const float bias_c = (a.bias_mode == 1 && wc * 32 + lr < a.Cout) ? a.bias[wc * 32 + lr] : 0.f;
   const int col = wc * 32 + lr;
   const bool cok = col < a.Cout;
+  const float bias_c = (a.bias_mode == 1 && cok) ? a.bias[col] : 0.f;
   bf16* __restrict__ out = reinterpret_cast<bf16*>(a.out);
   const long ld = a.out_ld;
   Welford run = {0.f, 0.f, 0.f};
+  f32x16 acc[TM];
 
-  __builtin_amdgcn_s_waitcnt(0);  // weights landed (vmcnt) before the first barrier
-  load(t_begin);
-  store(0);
-  __syncthreads();
-  int cur = 0;
-  for (int t = t_begin; t < t_end; ++t) {
-    const bool more = t + 1 < t_end;
-    if (more) load(t + 1);
-    const char* A_ = sA0 + cur * A_BYTES;
-    f32x16 acc;
+  auto compute = [&](int k) {
+    int n, f0;
+    tile_nf(k, n, f0);
+    const int f0m = f0 % g.RSL;  // the lane's frame at tap offset q: slot (f0 + fl + q) mod RS
+    int sb[TM];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    bf16x8 fa[2], fb[2];
+    for (int i = 0; i < TM; ++i) {
+      sb[i] = f0m + fl[i];
+      sb[i] = sb[i] >= g.RSL ? sb[i] - g.RSL : sb[i];
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+    bf16x8 fa[3][TM], fb[3];
+    int base[TM];
     auto rd = [&](int st, int b) {
       const int dt = st >> 2, ks = st & 3;
-      const int q = rev ? KT - 1 - dt : dt;
-      const int row = a_base + q * V;
-      fa[b] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(
-                                             A_ + row * RB + (((2 * ks + lh) ^ swz(row)) << 4)));
-      fb[b] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(
-                                             sB + dt * C * RB + b_lane + (((2 * ks + lh) ^ b_sw) << 4)));
+      if (ks == 0) {
+        const int q = rev ? KT - 1 - dt : dt;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          int s = sb[i] + q;
+          s = s >= g.RSL ? s - g.RSL : s;
+          base[i] = s * slot_stride + a_lane[i];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[b][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sR + base[i] + ks * 32));
+      fb[b] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sB + dt * C * RB + boff[ks]));
     };
     rd(0, 0);
+    rd(1, 1);
 #pragma unroll
     for (int st = 0; st < KT * 4; ++st) {
-      if (st + 1 < KT * 4) rd(st + 1, (st + 1) & 1);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[st & 1], fb[st & 1], acc, 0, 0, 0);
+      if (st + 2 < KT * 4) rd(st + 2, (st + 2) % 3);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[st % 3][i], fb[st % 3], acc[i], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
+  };
 
-    // ---- epilogue of tile t: rows r = wr*32 + acc_row(i) of the tile
-    const int n = t / g.tiles_n, f0 = (t - n * g.tiles_n) * g.F;
+  auto epilogue = [&](int k) {
+    int n, f0;
+    tile_nf(k, n, f0);
     const int fe = min(g.F, a.T_out - f0);
     const int rows_valid = fe * V;
     const long row0 = ((long)n * a.T_out + f0) * V;
-    const int lb = wr * 32 + 4 * lh;
-    bf16* pb = out + (row0 + lb) * ld + col;
     float s = 0.f, cnt = 0.f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int ro = (r & 3) + 8 * (r >> 2);
-      const bool ok = cok && lb + ro < rows_valid;
-      float v = acc[r] + bias_c;
-      if (ok) {
-        bf16* p = pb + ro * ld;
-        if (a.accumulate) v += (float)*p;
-        *p = (bf16)v;
-        s += v;
-        cnt += 1.f;
+    for (int i = 0; i < TM; ++i) {
+      const int lb = wr * 64 + i * 32 + 4 * lh;
+      bf16* pb = out + (row0 + lb) * ld + col;
+      const bool full = cok && wr * 64 + i * 32 + 32 <= rows_valid;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ro = (r & 3) + 8 * (r >> 2);
+        const bool ok = full || (cok && lb + ro < rows_valid);
+        float v = acc[i][r] + bias_c;
+        if (ok) {
+          bf16* p = pb + ro * ld;
+          if (a.accumulate) v += (float)*p;
+          *p = (bf16)v;
+          s += v;
+          cnt += 1.f;
+        }
+        acc[i][r] = v;
       }
-      acc[r] = v;
     }
     if (a.stats && cnt > 0.f) {
       const float mean = s / cnt;
       float m2 = 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float d = acc[r] - mean;
-        if (cok && lb + (r & 3) + 8 * (r >> 2) < rows_valid) m2 += d * d;
+      for (int i = 0; i < TM; ++i) {
+        const int lb = wr * 64 + i * 32 + 4 * lh;
+        const bool full = cok && wr * 64 + i * 32 + 32 <= rows_valid;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float d = acc[i][r] - mean;
+          if (full || (cok && lb + (r & 3) + 8 * (r >> 2) < rows_valid)) m2 += d * d;
+        }
       }
       run = welford_merge(run, Welford{cnt, mean, m2});
     }
+  };
 
-    if (more) store(cur ^ 1);
+  // ---- prologue: weights + BN table, tile 0 staged by everyone, groups prefetch tiles 1 / 2
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  stage_fresh(0);
+  if (grp == 1 && K > 1 && !fresh(1)) prefetch(1);
+  if (grp == 0 && K > 2 && !fresh(2)) prefetch(2);
+  __syncthreads();
+
+  // ---- phases: group (p & 1) computes tile p; the other group finishes tile p-1, commits tile
+  // p+1's frames (its own next tile) and prefetches tile p+3 (its tile after that)
+  for (int p = 0; p <= K; ++p) {
+    if (grp == (p & 1)) {
+      if (p < K) compute(p);
+    } else {
+      if (p >= 1) epilogue(p - 1);
+      if (p + 1 < K && !fresh(p + 1)) commit(p + 1);
+      if (p + 3 < K && !fresh(p + 3)) prefetch(p + 3);
+    }
     __syncthreads();
-    cur ^= 1;
+    if (p + 1 < K && fresh(p + 1)) {  // a new sample: its halo overwrites slots of tile p
+      stage_fresh(p + 1);
+      __syncthreads();
+    }
   }
 
   if (a.stats) {
-    // merge lane halves (same column), then the 4 row-group waves of each column tile via LDS
+    // merge lane halves (same column), then the 2 row groups x 2 wave groups per column via LDS
     Welford o;
     o.n = __shfl_xor(run.n, 32);
     o.mean = __shfl_xor(run.mean, 32);
     o.m2 = __shfl_xor(run.m2, 32);
     run = welford_merge(run, o);
-    float4* red = reinterpret_cast<float4*>(smem);  // [4 row groups][64 cols]; LDS is free now
-    if (lh == 0) red[wr * C + col] = make_float4(run.n, run.mean, run.m2, 0.f);
+    float4* red = reinterpret_cast<float4*>(smem);  // [4][64]; LDS is free now
+    if (lh == 0) red[(grp * 2 + wr) * C + col] = make_float4(run.n, run.mean, run.m2, 0.f);
     __syncthreads();
     if (tid < C) {
       float4 f = red[tid];
       Welford w = {f.x, f.y, f.z};
-      for (int k = 1; k < 4; ++k) {
-        const float4 h = red[k * C + tid];
+      for (int kk = 1; kk < 4; ++kk) {
+        const float4 h = red[kk * C + tid];
         w = welford_merge(w, Welford{h.x, h.y, h.z});
       }
       reinterpret_cast<float4*>(a.stats)[(long)blockIdx.x * a.Cout_pad + tid] = make_float4(w.n, w.mean, w.m2, 0.f);
@@ -243,13 +316,15 @@ long conv_rows_num_row_blocks(long M, int cout);
 
 // -1: shape not handled (caller tries the next kernel)
 int conv_persist_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
-  if (dtype != 1 || a.Kt != KT || a.stride != 1 || a.pad != 4 || a.T_in != a.T_out) return -1;
+  if (dtype != 1 || a.Kt != KT || a.stride != 1 || a.pad != PADT || a.T_in != a.T_out) return -1;
   if (a.Cin_pad != C || a.Cout_pad != C || a.Cin != C || a.in_ld % 8 || a.pro > 1) return -1;
   if (a.bias_mode > 1 || a.V > 32) return -1;
   PGeom g;
   g.F = ROWS / a.V;
-  g.HR = (g.F + KT - 1) * a.V;
-  if (g.HR > HR_MAX || g.F < 1) return -1;
+  if (g.F < 1) return -1;
+  g.RSL = 2 * g.F + KT - 1;
+  const size_t lds = B_BYTES + (size_t)g.RSL * a.V * RS_A + 2 * C * sizeof(float);
+  if (lds > (size_t)LDS_MAX) return -1;
   g.tiles_n = (a.T_out + g.F - 1) / g.F;
   const long nt = (long)a.N * g.tiles_n;
   if (nt > 0x7fffffffL) return -1;
@@ -261,15 +336,13 @@ int conv_persist_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     if (ncu <= 0) ncu = 256;
   }
-  int grid = ncu;
-  g.tpb = (g.ntiles + grid - 1) / grid;
-  grid = (g.ntiles + g.tpb - 1) / g.tpb;
+  g.tpb = (g.ntiles + ncu - 1) / ncu;
+  const int grid = (g.ntiles + g.tpb - 1) / g.tpb;
   if (a.stats && grid > conv_rows_num_row_blocks((long)a.N * a.T_out * a.V, a.Cout)) return -1;
-  const size_t lds = B_BYTES + 2 * (size_t)A_BYTES;  // 163 840
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)conv_persist_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
+                              LDS_MAX);
     attr = true;
   }
   hipLaunchKernelGGL(conv_persist_kernel, dim3(grid), dim3(NT), lds, s, a, g);

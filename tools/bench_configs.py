@@ -1,0 +1,141 @@
+"""SURVEY §8(d) configs 3 and 5 on one MI355X (synthetic data, random-init weights).
+
+config 3: RT-ST-GCN online inference (config/pku-mmd/ln/rtstgcn_local.json: LN, K=9, 9 layers),
+          one (1, 3, 1, 25) frame at a time through OnlineLayer FIFOs; per-frame latency p50/p99
+          eager (one Python-launched kernel sequence per frame) and as a replayed HIP graph (the
+          per-frame step captured once; FIFO state and indices are device buffers, so replays
+          advance the stream correctly).  Parity of the two against each other is checked.
+config 5: AAGCN (config/pku-mmd/as_is/aagcn_local.json: 2 streams, BN, 9 layers) fwd+bwd, bf16,
+          N=64 T=300 V=25: skeleton-frames/s.
+
+    python tools/bench_configs.py [--frames 2000] [--steps 10]
+Prints one JSON line per config.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import __graft_entry__ as ge  # noqa: E402
+
+LAYERS = {"layers": 9, "kernel": 9, "in_ch": [64, 64, 64, 64, 128, 128, 128, 256, 256],
+          "out_ch": [64, 64, 64, 128, 128, 128, 256, 256, 256], "stride": [1, 1, 1, 2, 1, 1, 2, 1, 1],
+          "residual": [1] * 9, "dropout": [0.0] * 9}
+RT_ARCH = {"strategy": "spatial", "in_feat": 3, "stages": 1, "kernel": 9, "output_type": "logits",
+           "normalization": "LayerNorm", "segment": 500, "num_classes": 52,
+           "rt-st-gcn": dict(LAYERS, latency=False, importance=True, in_feat=3, buffer=1, stages=1)}
+AAGCN_ARCH = {"strategy": "spatial", "receptive_field": 50, "in_feat": 3, "stages": 1, "output_type": "softmax",
+              "normalization": "BatchNorm", "num_classes": 52,
+              "aa-gcn": dict(LAYERS, latency=False, importance=True, in_feat=3, stages=1)}
+
+
+def pct(xs, q):
+    xs = sorted(xs)
+    return xs[min(len(xs) - 1, int(q * len(xs)))]
+
+
+def config3(P, dev, frames):
+    torch.manual_seed(0)
+    m = P.MODELS["rt-st-gcn"](rank=None, **dict(RT_ARCH, graph=P.PKU_MMD)).to(dev)
+    m.eval()
+    m.prepare_benchmark(RT_ARCH)
+    gen = torch.Generator(device=dev).manual_seed(3)
+    stream = torch.randn(frames + 64, 1, 3, 1, 25, device=dev, generator=gen)
+    out = {}
+    with torch.no_grad():
+        # eager: every kernel launched from Python per frame
+        m.reset_state()
+        lat, ys = [], []
+        for i in range(frames):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            y = m(stream[i])
+            torch.cuda.synchronize()
+            lat.append(time.perf_counter() - t0)
+            if i < 64:
+                ys.append(y.clone())
+        warm = lat[32:]
+        out["eager"] = {"p50_ms": round(1e3 * pct(warm, 0.5), 4), "p99_ms": round(1e3 * pct(warm, 0.99), 4)}
+        # HIP graph: capture one per-frame step on a static input buffer, replay per frame
+        m.reset_state()
+        x_static = torch.zeros_like(stream[0])
+        for i in range(3):  # warm-up launches (attribute setup, allocator) on the real stream
+            x_static.copy_(stream[i])
+            m(x_static)
+        m.reset_state()
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g):
+                y_static = m(x_static)
+        torch.cuda.current_stream().wait_stream(s)
+        m.reset_state()  # the capture itself does not run the step
+        lat, err = [], 0.0
+        for i in range(frames):
+            x_static.copy_(stream[i])
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            g.replay()
+            torch.cuda.synchronize()
+            lat.append(time.perf_counter() - t0)
+            if i < 64:
+                err = max(err, float((y_static - ys[i]).abs().max() / ys[i].abs().max().clamp_min(1e-12)))
+        warm = lat[32:]
+        out["graph"] = {"p50_ms": round(1e3 * pct(warm, 0.5), 4), "p99_ms": round(1e3 * pct(warm, 0.99), 4),
+                        "max_rel_diff_vs_eager": err}
+    return {"config": "3: rt-st-gcn online (ln/rtstgcn_local.json, LN, K=9, 9 layers), 1 frame (1,3,1,25)",
+            "metric": "per-frame latency", "unit": "ms", "frames": frames, "dtype": "fp32",
+            "reference_cpu": "2.7 ms/frame (SURVEY §8(a12), 9 layers)", **out}
+
+
+def config5(P, dev, steps, warmup):
+    torch.manual_seed(1538574472)
+    m = P.MODELS["aa-gcn"](rank=None, **dict(AAGCN_ARCH, graph=P.PKU_MMD)).to(dev).set_compute_dtype("bf16")
+    opt = torch.optim.Adam(m.parameters(), lr=5e-4, foreach=True)
+    gen = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(64, 3, 300, 25, device=dev, generator=gen)
+    labels = torch.randint(0, 52, (64,), device=dev, generator=gen)
+
+    def step():
+        y = m(x)
+        loss = torch.nn.functional.nll_loss(torch.log(y.reshape(64, 52).clamp_min(1e-12)), labels)
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"config": "5: aa-gcn (as_is/aagcn_local.json, 2 streams, BN, 9 layers) fwd+bwd+Adam, bf16, "
+                      "N=64 T=300 V=25", "metric": "skeleton-frames/s", "value": round(steps * 64 * 300 / dt, 1),
+            "ms_per_step": round(1e3 * dt / steps, 3), "steps": steps, "data": "synthetic"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=2000)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--only", default=None)
+    args = ap.parse_args()
+    P = ge.load_package()
+    dev = torch.device("cuda", 0)
+    if args.only in (None, "3"):
+        print(json.dumps(config3(P, dev, args.frames)), flush=True)
+    if args.only in (None, "5"):
+        print(json.dumps(config5(P, dev, args.steps, args.warmup)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
