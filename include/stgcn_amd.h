@@ -45,6 +45,10 @@ typedef struct {
 } stgcn_conv_desc;
 
 int stgcn_conv_rows(const stgcn_conv_desc* d, int dtype, void* stream);
+/* Pack an fp32 weight given as any strided [Kt][Cout][Cin] view (element (k,co,ci) at src[k*s0+co*s1+ci*s2])
+ * into the zero-padded contiguous [Kt][Cout_pad][Cin_pad] dtype image stgcn_conv_rows reads. */
+int stgcn_pack_weight(const float* src, long s0, long s1, long s2, int Kt, int Cout, int Cin, void* dst, int Cout_pad,
+                      int Cin_pad, int dtype, void* stream);
 /* column tile the packed weights must be padded to (Cout_pad % tile == 0) */
 int stgcn_conv_rows_col_tile(int cout);
 /* upper bound on row blocks (first dim of the BN partial-stat buffer, which the caller zero-fills) */
@@ -86,7 +90,15 @@ typedef struct {
 
 int stgcn_amix_fwd(const stgcn_amix_desc* d, int dtype, void* stream);
 int stgcn_amix_trans(const stgcn_amix_desc* d, int dtype, void* stream);
-int stgcn_amix_dA(const stgcn_amix_desc* d, const void* dw, float* dA, int dtype, void* stream);
+/* dA (+)= sum over frames of x (x) DW.  work: stgcn_amix_dA_workspace() bytes -> per-block partials summed
+   in a fixed order (bit-reproducible); NULL -> fp32 atomics (run-to-run order noise). */
+long stgcn_amix_dA_workspace(const stgcn_amix_desc* d);
+int stgcn_amix_dA(const stgcn_amix_desc* d, const void* dw, float* dA, void* work, int dtype, void* stream);
+/* Shared-A gradients of the graph-conv bias (autograd of tgcn.py:71-79 through the bias), from
+ * S[w][c] = sum of dg over the rows of joint w (stgcn_rowgroup_sum):
+ *   dA[p][v][w] += sum_c b[p*C+c] S[w][c];   db[p*C+c] = sum_w (sum_v A[p][v][w]) S[w][c] */
+int stgcn_gcn_bias_bwd(const float* A, const float* b, const float* S, int P, int V, int C, float* dA, float* db,
+                       void* stream);
 int stgcn_gcn_bias(const float* A, const float* b, float* out, int N, int P, int V, int C, int per_sample,
                    void* stream);
 
@@ -113,7 +125,8 @@ int stgcn_gconv(const stgcn_gconv_desc* d, int dtype, void* stream);
 long stgcn_gconv_row_blocks(int NT, int V);
 int stgcn_gconv_weights(const float* A, const float* W, const int* nbr, const int* deg, int P, int V, int J, int Cout,
                         int Cin, int trans, void* out, int rows_pad, int cols_pad, int dtype, void* stream);
-/* dweff[w][j][co][ci] += sum_i dy[(i,w)][co] * x[(i, nbr[w][j])][ci]   (fp32 [V][J][Cout][Cin]) */
+/* dweff[w][j][co][ci] = sum_i dy[(i,w)][co] * x[(i, nbr[w][j])][ci]   (fp32 [V][J][Cout][Cin], written
+ * whole: 0 for the unused slots j >= deg[w]) */
 typedef struct {
   const void* x;
   const void* dy;
@@ -128,9 +141,12 @@ typedef struct {
 int stgcn_gconv_wgrad(const stgcn_gconv_wgrad_desc* d, int dtype, void* stream);
 long stgcn_gconv_wgrad_workspace(const stgcn_gconv_wgrad_desc* d, int dtype);
 /* dW[p*Cout+co][ci] += sum_{w,j} A[p][S(w)_j][w] dweff[w][j][co][ci]  (dW may be NULL);
- * dA[p][S(w)_j][w] += sum_{co,ci} W[p*Cout+co][ci] dweff[w][j][co][ci]  (dA may be NULL) */
+ * dA[p][S(w)_j][w] += sum_{co,ci} W[p*Cout+co][ci] dweff[w][j][co][ci]  (dA may be NULL)
+ * work: stgcn_gconv_wgrad_finish_workspace() bytes (chunked dA partials, fixed-order reduce) or NULL
+ * (slower per-partition path).  Deterministic either way. */
+long stgcn_gconv_wgrad_finish_workspace(int P, int V, int J, int Cout, int Cin);
 int stgcn_gconv_wgrad_finish(const float* dweff, const float* A, const float* W, const int* nbr, const int* deg, int P,
-                             int V, int J, int Cout, int Cin, float* dW, float* dA, void* stream);
+                             int V, int J, int Cout, int Cin, float* dW, float* dA, void* work, void* stream);
 
 /* BatchNorm with batch statistics (nn.BatchNorm2d(track_running_stats=False), stgcn.py:152,160,171;
  * BatchNorm1d input norm, models/utils/batchnorm.py:13-23 viewed as [N*T][V*C]).
@@ -156,10 +172,10 @@ typedef struct {
   const float* mean_rstd2;
   const float* gamma1;
   const float* gamma2;
-  float* sums;  /* float4 [C] */
+  float* sums;  /* float4 [C], then the same planar: float [3][C] (7*C floats) */
   void* out1;
   void* out2;
-  float* osum;  /* optional float4 [C] */
+  float* osum;  /* optional, layout as sums */
   float* work;  /* float4 [blocks][C], stgcn_bn_bwd_fused_workspace() floats */
   long M;
   int C, mask, lddy, ldm, ldx1, ldx2, ldo1, ldo2, acc2;
@@ -217,8 +233,10 @@ int stgcn_rt_online_step(const void* z_f32, float* fifo, float* acc, int* idx, i
 /* AAGCN attention adjacency (models/aagcn/aagcn.py:142-145): C[n,p] = softmax_w(theta_p^T phi_p) over
  * K = T*ce, theta/phi rows [N][T][V][ld] (channel p*ce+c).  C: fp32 [N][P][V][V].  Backward writes
  * dS (scratch, fp32 like C) and dtheta/dphi (rows like theta/phi). */
+/* work: stgcn_attn_scores_workspace() bytes (deterministic T-chunk reduction) or NULL (atomics). */
+long stgcn_attn_scores_workspace(int N, int T, int V, int P);
 int stgcn_attn_scores(const void* theta, const void* phi, int ld, int N, int T, int V, int P, int ce, float* C,
-                      int dtype, void* stream);
+                      void* work, int dtype, void* stream);
 int stgcn_attn_bwd(const void* theta, const void* phi, int ld, int N, int T, int V, int P, int ce, const float* C,
                    const float* dC, float* dS, void* dtheta, void* dphi, int dtype, void* stream);
 

@@ -78,10 +78,15 @@ _SIGS = {
                                                                                            c_int, c_void_p]),
     "stgcn_gconv_wgrad": (c_int, [ctypes.POINTER(GconvWgradDesc), c_int, c_void_p]),
     "stgcn_gconv_wgrad_workspace": (c_long, [ctypes.POINTER(GconvWgradDesc), c_int]),
-    "stgcn_gconv_wgrad_finish": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_void_p, c_void_p, c_void_p]),
+    "stgcn_gconv_wgrad_finish_workspace": (ctypes.c_long, [c_int] * 5),
+    "stgcn_gconv_wgrad_finish": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_void_p, c_void_p, c_void_p, c_void_p]),
     "stgcn_amix_fwd": (c_int, [ctypes.POINTER(AmixDesc), c_int, c_void_p]),
     "stgcn_amix_trans": (c_int, [ctypes.POINTER(AmixDesc), c_int, c_void_p]),
-    "stgcn_amix_dA": (c_int, [ctypes.POINTER(AmixDesc), c_void_p, c_void_p, c_int, c_void_p]),
+    "stgcn_gcn_bias_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "stgcn_pack_weight": (c_int, [c_void_p, ctypes.c_long, ctypes.c_long, ctypes.c_long, c_int, c_int, c_int,
+                                  c_void_p, c_int, c_int, c_int, c_void_p]),
+    "stgcn_amix_dA_workspace": (ctypes.c_long, [ctypes.POINTER(AmixDesc)]),
+    "stgcn_amix_dA": (c_int, [ctypes.POINTER(AmixDesc), c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "stgcn_gcn_bias": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     "stgcn_bn_stat_blocks": (c_long, [c_long]),
     "stgcn_bn_stats_partial": (c_int, [c_void_p, c_int, c_long, c_int, c_void_p, c_int, c_void_p]),
@@ -108,8 +113,9 @@ _SIGS = {
                               c_int, c_int, c_void_p]),
     "stgcn_rt_online_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                                      c_void_p]),
-    "stgcn_attn_scores": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int,
-                                  c_void_p]),
+    "stgcn_attn_scores_workspace": (ctypes.c_long, [c_int, c_int, c_int, c_int]),
+    "stgcn_attn_scores": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                  c_int, c_void_p]),
     "stgcn_attn_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
 }

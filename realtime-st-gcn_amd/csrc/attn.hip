@@ -9,12 +9,16 @@
 // (8 consecutive channels per lane = 16 B); blocks split T and add fp32 partials.
 #include "common.h"
 
+void slab_sum_launch(const float* in, long B, long R, long E, float* tmp, float* out, int accumulate, hipStream_t s);
+long slab_sum_tmp_floats(long B, long R, long E);
+
 namespace {
 constexpr int VMAX = 32;
 
 template <typename T>
 __global__ __launch_bounds__(256) void attn_scores_kernel(const T* __restrict__ th, const T* __restrict__ ph,
-                                                          int ld, int T_, int V, int P, int ce, int tpb, float* S) {
+                                                          int ld, int T_, int V, int P, int ce, int tpb, float* S,
+                                                          float* work) {
   constexpr int VEC = 16 / sizeof(T);
   __shared__ float red[4][VMAX * VMAX];
   const int n = blockIdx.z, p = blockIdx.y;
@@ -69,10 +73,12 @@ __global__ __launch_bounds__(256) void attn_scores_kernel(const T* __restrict__ 
 #pragma unroll
   for (int i = 0; i < 16; ++i) red[wave][acc_row(i, lane) * VMAX + r] = acc[i];
   __syncthreads();
-  float* dst = S + ((long)n * P + p) * V * V;
+  // work: partial of T-chunk blockIdx.x in slab row ((n*P + p) * chunks + chunk) (ordered sum afterwards)
+  float* dst = work ? work + (((long)n * P + p) * gridDim.x + blockIdx.x) * V * V : S + ((long)n * P + p) * V * V;
   for (int i = threadIdx.x; i < V * V; i += 256) {
     const int v = i / V, w = i % V;
-    atomicAdd(dst + i, red[0][v * VMAX + w] + red[1][v * VMAX + w] + red[2][v * VMAX + w] + red[3][v * VMAX + w]);
+    const float s = red[0][v * VMAX + w] + red[1][v * VMAX + w] + red[2][v * VMAX + w] + red[3][v * VMAX + w];
+    if (work) dst[i] = s; else atomicAdd(dst + i, s);
   }
 }
 
@@ -130,19 +136,35 @@ __global__ __launch_bounds__(256) void attn_mix_kernel(const T* __restrict__ in,
 }
 }  // namespace
 
-int attn_scores_launch(const void* th, const void* ph, int ld, int N, int T_, int V, int P, int ce, float* S,
-                       int dtype, hipStream_t s) {
-  if (V > VMAX || P > 4) return STGCN_EBADSHAPE;
-  (void)hipMemsetAsync(S, 0, sizeof(float) * N * P * V * V, s);
+namespace {
+int attn_chunks(int N, int T_, int P, int* tpb_out) {
   int tpb = (int)(((long)T_ * N * P + 1023) / 1024);  // ~1024 blocks
   if (tpb < 8) tpb = 8;
-  dim3 grid((T_ + tpb - 1) / tpb, P, N);
+  if (tpb_out) *tpb_out = tpb;
+  return (T_ + tpb - 1) / tpb;
+}
+}  // namespace
+
+long attn_scores_workspace(int N, int T_, int V, int P) {
+  const long chunks = attn_chunks(N, T_, P, nullptr), E = (long)V * V;
+  return (long)sizeof(float) * ((long)N * P * chunks * E + slab_sum_tmp_floats((long)N * P, chunks, E));
+}
+
+int attn_scores_launch(const void* th, const void* ph, int ld, int N, int T_, int V, int P, int ce, float* S,
+                       void* work, int dtype, hipStream_t s) {
+  if (V > VMAX || P > 4) return STGCN_EBADSHAPE;
+  int tpb;
+  const int chunks = attn_chunks(N, T_, P, &tpb);
+  float* w = reinterpret_cast<float*>(work);
+  if (!w) (void)hipMemsetAsync(S, 0, sizeof(float) * N * P * V * V, s);
+  dim3 grid(chunks, P, N);
   if (dtype)
     hipLaunchKernelGGL(attn_scores_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)th, (const bf16*)ph, ld, T_, V,
-                       P, ce, tpb, S);
+                       P, ce, tpb, S, w);
   else
     hipLaunchKernelGGL(attn_scores_kernel<float>, grid, dim3(256), 0, s, (const float*)th, (const float*)ph, ld, T_,
-                       V, P, ce, tpb, S);
+                       V, P, ce, tpb, S, w);
+  if (w) slab_sum_launch(w, (long)N * P, chunks, (long)V * V, w + (long)N * P * chunks * V * V, S, 0, s);
   const long rows = (long)N * P * V;
   hipLaunchKernelGGL(attn_softmax_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, S, rows, V);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;

@@ -105,7 +105,9 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_fused_kernel(const stgcn_bn
   }
 }
 
-// column sums of float4 partials [nb][C] -> out [C] (fp64 accumulation); one block per channel
+// column sums of float4 partials [nb][C] -> out [C] (fp64 accumulation); one block per channel.
+// The same values also go planar to ((float*)(out + C))[k*C + c], k < 3, so per-channel parameter
+// gradients are contiguous views (no gather copies on the host side).
 __global__ __launch_bounds__(256) void sum4_kernel(const float4* part, int nb, int C, float4* out) {
   __shared__ double sx[256], sy[256], sz[256];
   const int c = blockIdx.x;
@@ -124,7 +126,14 @@ __global__ __launch_bounds__(256) void sum4_kernel(const float4* part, int nb, i
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) out[c] = make_float4((float)sx[0], (float)sy[0], (float)sz[0], 0.f);
+  if (threadIdx.x == 0) {
+    const float4 r = make_float4((float)sx[0], (float)sy[0], (float)sz[0], 0.f);
+    out[c] = r;
+    float* pl = reinterpret_cast<float*>(out + C);
+    pl[c] = r.x;
+    pl[C + c] = r.y;
+    pl[2 * C + c] = r.z;
+  }
 }
 
 template <typename T, int VEC, int MASK, int O2, bool OSUM>

@@ -15,6 +15,8 @@ typedef stgcn_amix_desc AmixArgs;
 // launchers (defined in the .hip translation units)
 int conv_rows_launch(const ConvArgs& a, int dtype, hipStream_t s);
 int conv_rows_bn_tile(int cout);
+int pack_weight_launch(const float* src, long s0, long s1, long s2, int Kt, int Co, int Ci, void* dst, int cp, int kp,
+                       int dtype, hipStream_t s);
 long conv_rows_num_row_blocks(long M, int cout);
 int conv_wgrad_launch(WgradArgs a, int dtype, hipStream_t s);
 long wgrad_tile_workspace(const WgradArgs& a, int dtype);
@@ -30,9 +32,13 @@ int gconv_weights_launch(const float* A, const float* W, const int* nbr, const i
 long gconv_wgrad_workspace(const stgcn_gconv_wgrad_desc& a, int dtype);
 int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s);
 int gconv_wgrad_finish_launch(const float* dweff, const float* A, const float* W, const int* nbr, const int* deg,
-                              int P, int V, int J, int Cout, int Cin, float* dW, float* dA, hipStream_t s);
+                              int P, int V, int J, int Cout, int Cin, float* dW, float* dA, void* work, hipStream_t s);
+long gconv_wgrad_finish_workspace(int P, int V, int J, int Cout, int Cin);
 int amix_trans_launch(const AmixArgs& a, int dtype, hipStream_t s);
-int amix_dA_launch(const AmixArgs& a, const void* dw, float* dA, int dtype, hipStream_t s);
+int amix_dA_launch(const AmixArgs& a, const void* dw, float* dA, void* work, int dtype, hipStream_t s);
+long amix_dA_workspace(const AmixArgs& a);
+int gcn_bias_bwd_launch(const float* A, const float* b, const float* S, int P, int V, int C, float* dA, float* db,
+                        hipStream_t s);
 int gcn_bias_launch(const float* A, const float* b, float* out, int N, int P, int V, int C, int per_sample,
                     hipStream_t s);
 long norm_stats_num_blocks(long M);
@@ -67,7 +73,8 @@ int rt_online_launch(const float* z, float* fifo, float* acc, int* idx, int C, i
                      float* out, hipStream_t s);
 
 int attn_scores_launch(const void* th, const void* ph, int ld, int N, int T_, int V, int P, int ce, float* S,
-                       int dtype, hipStream_t s);
+                       void* work, int dtype, hipStream_t s);
+long attn_scores_workspace(int N, int T_, int V, int P);
 int attn_bwd_launch(const void* th, const void* ph, int ld, int N, int T_, int V, int P, int ce, const float* C,
                     const float* dC, float* dS, void* dth, void* dph, int dtype, hipStream_t s);
 
@@ -92,6 +99,12 @@ int stgcn_conv_rows(const stgcn_conv_desc* d, int dtype, void* stream) {
 }
 
 int stgcn_conv_rows_col_tile(int cout) { return conv_rows_bn_tile(cout); }
+int stgcn_pack_weight(const float* src, long s0, long s1, long s2, int Kt, int Co, int Ci, void* dst, int Cout_pad,
+                      int Cin_pad, int dtype, void* stream) {
+  CHECK_DTYPE(dtype);
+  if (!src || !dst || Kt <= 0 || Co <= 0 || Ci <= 0 || Cout_pad < Co || Cin_pad < Ci) return STGCN_EBADSHAPE;
+  return pack_weight_launch(src, s0, s1, s2, Kt, Co, Ci, dst, Cout_pad, Cin_pad, dtype, STREAM(stream));
+}
 long stgcn_conv_rows_row_blocks(long M, int cout) { return conv_rows_num_row_blocks(M, cout); }
 
 long stgcn_conv_wgrad_workspace(const stgcn_wgrad_desc* d, int dtype) {
@@ -156,11 +169,14 @@ int stgcn_gconv_wgrad(const stgcn_gconv_wgrad_desc* d, int dtype, void* stream) 
     return STGCN_EBADSHAPE;
   return gconv_wgrad_launch(*d, dtype, STREAM(stream));
 }
+long stgcn_gconv_wgrad_finish_workspace(int P, int V, int J, int Cout, int Cin) {
+  return gconv_wgrad_finish_workspace(P, V, J, Cout, Cin);
+}
 int stgcn_gconv_wgrad_finish(const float* dweff, const float* A, const float* W, const int* nbr, const int* deg, int P,
-                             int V, int J, int Cout, int Cin, float* dW, float* dA, void* stream) {
+                             int V, int J, int Cout, int Cin, float* dW, float* dA, void* work, void* stream) {
   if (!dweff || !A || !W || !nbr || !deg || P <= 0 || V <= 0 || J <= 0 || Cout <= 0 || Cin <= 0)
     return STGCN_EBADSHAPE;
-  return gconv_wgrad_finish_launch(dweff, A, W, nbr, deg, P, V, J, Cout, Cin, dW, dA, STREAM(stream));
+  return gconv_wgrad_finish_launch(dweff, A, W, nbr, deg, P, V, J, Cout, Cin, dW, dA, work, STREAM(stream));
 }
 
 int stgcn_amix_fwd(const stgcn_amix_desc* d, int dtype, void* stream) {
@@ -173,10 +189,16 @@ int stgcn_amix_trans(const stgcn_amix_desc* d, int dtype, void* stream) {
   if (!d || !d->x || !d->out || !d->A) return STGCN_EBADSHAPE;
   return amix_trans_launch(*d, dtype, STREAM(stream));
 }
-int stgcn_amix_dA(const stgcn_amix_desc* d, const void* dw, float* dA, int dtype, void* stream) {
+long stgcn_amix_dA_workspace(const stgcn_amix_desc* d) { return d ? amix_dA_workspace(*d) : 0; }
+int stgcn_amix_dA(const stgcn_amix_desc* d, const void* dw, float* dA, void* work, int dtype, void* stream) {
   CHECK_DTYPE(dtype);
   if (!d || !d->x || !dw || !dA) return STGCN_EBADSHAPE;
-  return amix_dA_launch(*d, dw, dA, dtype, STREAM(stream));
+  return amix_dA_launch(*d, dw, dA, work, dtype, STREAM(stream));
+}
+int stgcn_gcn_bias_bwd(const float* A, const float* b, const float* S, int P, int V, int C, float* dA, float* db,
+                       void* stream) {
+  if (!A || !b || !S || !dA || !db || P <= 0 || V <= 0 || C <= 0) return STGCN_EBADSHAPE;
+  return gcn_bias_bwd_launch(A, b, S, P, V, C, dA, db, STREAM(stream));
 }
 int stgcn_gcn_bias(const float* A, const float* b, float* out, int N, int P, int V, int C, int per_sample,
                    void* stream) {
@@ -262,11 +284,12 @@ int stgcn_rt_online_step(const void* z, float* fifo, float* acc, int* idx, int C
   return rt_online_launch((const float*)z, fifo, acc, idx, C, V, fifo_size, S, out, STREAM(stream));
 }
 
-int stgcn_attn_scores(const void* th, const void* ph, int ld, int N, int T, int V, int P, int ce, float* C, int dtype,
-                      void* stream) {
+long stgcn_attn_scores_workspace(int N, int T, int V, int P) { return attn_scores_workspace(N, T, V, P); }
+int stgcn_attn_scores(const void* th, const void* ph, int ld, int N, int T, int V, int P, int ce, float* C, void* work,
+                      int dtype, void* stream) {
   CHECK_DTYPE(dtype);
   if (!th || !ph || !C || ld < P * ce) return STGCN_EBADSHAPE;
-  return attn_scores_launch(th, ph, ld, N, T, V, P, ce, C, dtype, STREAM(stream));
+  return attn_scores_launch(th, ph, ld, N, T, V, P, ce, C, work, dtype, STREAM(stream));
 }
 int stgcn_attn_bwd(const void* th, const void* ph, int ld, int N, int T, int V, int P, int ce, const float* C,
                    const float* dC, float* dS, void* dth, void* dph, int dtype, void* stream) {
@@ -276,3 +299,7 @@ int stgcn_attn_bwd(const void* th, const void* ph, int ld, int N, int T, int V, 
 }
 
 }  // extern "C"
+
+// diagnostic (not part of include/stgcn_amd.h): phase timers of the persistent conv kernel
+int persist_debug_read(long long* host, long n);
+extern "C" int stgcn_debug_persist_timers(long long* host, long n) { return persist_debug_read(host, n); }

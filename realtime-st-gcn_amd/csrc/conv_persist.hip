@@ -21,6 +21,7 @@
 //     gradient); a tile that starts a new sample is staged in an extra synchronous phase.
 #include "common.h"
 #include "../../include/stgcn_amd.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -45,6 +46,8 @@ DEV void glds16(const void* src, char* lds_base) {
 }
 
 struct PGeom {
+  long long* dbg;  // diagnostic build only: per-block phase timers (s_memtime), else nullptr
+  int dmode;       // diagnostic: bit0 skip output stores, bit1 skip stats, bit2 skip scratch writes
   int F;        // frames per tile
   int RSL;      // ring slots (frames)
   int tiles_n;  // tiles per sample
@@ -120,29 +123,38 @@ __global__ __launch_bounds__(NT, 1) void conv_persist_kernel(const stgcn_conv_de
       put((f < 0 || f >= a.T_in) ? v : transform(v), f, vj);
     }
   };
-  // steady state: tile k's F new frames f0+4 .. f0+F+3, by one group (256 threads, <= 4 units each)
+  // steady state: tile k's F new frames f0+4 .. f0+F+3, by one group (256 threads, <= 4 units each).
+  // The (frame j, joint v) of each unit and its ring-row offset are tile-invariant: precomputed.
   uint4 ra[RA];
+  int u_j[RA], u_r[RA], u_row[RA];  // frame in the new range (>= F: unused); row in it; LDS offset in a slot
+#pragma unroll
+  for (int i = 0; i < RA; ++i) {
+    u_r[i] = (gtid >> 3) + i * (GT / 8);
+    u_j[i] = u_r[i] / V;
+    u_row[i] = (u_r[i] - u_j[i] * V) * RS_A + ucol * 16;
+  }
   auto prefetch = [&](int k) {
     int n, f0;
     tile_nf(k, n, f0);
-    const long base = (long)n * a.T_in;
+    const bf16* src = in + ((long)n * a.T_in + f0 + PADT) * V * a.in_ld + ucol * 8;
 #pragma unroll
     for (int i = 0; i < RA; ++i) {
-      const int r = (gtid >> 3) + i * (GT / 8);
-      const int j = r / V, vj = r - j * V;
-      ra[i] = j < g.F ? fetch(base, f0 + PADT + j, vj) : make_uint4(0, 0, 0, 0);
+      const int f = f0 + PADT + u_j[i];
+      ra[i] = (u_j[i] < g.F && f < a.T_in) ? *reinterpret_cast<const uint4*>(src + (long)u_r[i] * a.in_ld)
+                                            : make_uint4(0, 0, 0, 0);
     }
   };
   auto commit = [&](int k) {
     int n, f0;
     tile_nf(k, n, f0);
+    const int s0 = (f0 + 2 * PADT) % g.RSL;  // slot of frame f0 + PADT (block-uniform)
 #pragma unroll
     for (int i = 0; i < RA; ++i) {
-      const int r = (gtid >> 3) + i * (GT / 8);
-      const int j = r / V, vj = r - j * V;
-      if (j < g.F) {
-        const int f = f0 + PADT + j;
-        put((f < 0 || f >= a.T_in) ? ra[i] : transform(ra[i]), f, vj);
+      if (u_j[i] < g.F) {
+        const int f = f0 + PADT + u_j[i];
+        int slot = s0 + u_j[i];
+        slot = slot >= g.RSL ? slot - g.RSL : slot;
+        *reinterpret_cast<uint4*>(sR + slot * (V * RS_A) + u_row[i]) = f < a.T_in ? transform(ra[i]) : ra[i];
       }
     }
   };
@@ -219,6 +231,10 @@ __global__ __launch_bounds__(NT, 1) void conv_persist_kernel(const stgcn_conv_de
     }
   };
 
+  // Epilogue: bias, BatchNorm partials from the fp32 accumulators (lane = column: in-lane Welford),
+  // then the bf16 tile goes through a per-wave LDS scratch [64 rows][32 cols] so that the global
+  // stores are 16 B per lane (4 per wave) instead of 32 scattered 2-byte stores.
+  char* scratch = sR + g.RSL * V * RS_A + 2 * C * sizeof(float) + gw * (64 * 64);
   auto epilogue = [&](int k) {
     int n, f0;
     tile_nf(k, n, f0);
@@ -229,24 +245,40 @@ __global__ __launch_bounds__(NT, 1) void conv_persist_kernel(const stgcn_conv_de
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int lb = wr * 64 + i * 32 + 4 * lh;
-      bf16* pb = out + (row0 + lb) * ld + col;
       const bool full = cok && wr * 64 + i * 32 + 32 <= rows_valid;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int ro = (r & 3) + 8 * (r >> 2);
-        const bool ok = full || (cok && lb + ro < rows_valid);
-        float v = acc[i][r] + bias_c;
-        if (ok) {
-          bf16* p = pb + ro * ld;
-          if (a.accumulate) v += (float)*p;
-          *p = (bf16)v;
+        const float v = acc[i][r] + bias_c;
+        acc[i][r] = v;
+        if (!(g.dmode & 4)) *reinterpret_cast<bf16*>(scratch + (i * 32 + 4 * lh + ro) * 64 + lr * 2) = (bf16)v;
+        if (full || (cok && lb + ro < rows_valid)) {
           s += v;
           cnt += 1.f;
         }
-        acc[i][r] = v;
       }
     }
-    if (a.stats && cnt > 0.f) {
+    // rows of this wave: wr*64 + lrow, 16 B units u = 0..3 of its 32 columns
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (g.dmode & 1) break;
+      const int lrow = q * 16 + (lane >> 2), u = lane & 3;
+      uint4 v = *reinterpret_cast<const uint4*>(scratch + lrow * 64 + u * 16);
+      const int trow = wr * 64 + lrow;
+      if (trow < rows_valid) {
+        bf16* p = out + (row0 + trow) * ld + wc * 32 + u * 8;
+        if (a.accumulate) {
+          float f[8], o[8];
+          unpack16(v, f, (bf16*)nullptr);
+          unpack16(*reinterpret_cast<const uint4*>(p), o, (bf16*)nullptr);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] += o[e];
+          v = pack16(f, (bf16*)nullptr);
+        }
+        if (wc * 32 + u * 8 < a.Cout) *reinterpret_cast<uint4*>(p) = v;
+      }
+    }
+    if (a.stats && cnt > 0.f && !(g.dmode & 2)) {
       const float mean = s / cnt;
       float m2 = 0.f;
 #pragma unroll
@@ -263,6 +295,15 @@ __global__ __launch_bounds__(NT, 1) void conv_persist_kernel(const stgcn_conv_de
     }
   };
 
+  // Phase barrier: LDS traffic retired (lgkmcnt) + s_barrier, WITHOUT draining vmcnt — the
+  // prefetched global loads and the epilogue's global stores stay in flight across phases
+  // (__syncthreads() would wait for all of them every phase).
+  auto bar = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
   // ---- prologue: weights + BN table, tile 0 staged by everyone, groups prefetch tiles 1 / 2
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
@@ -273,21 +314,43 @@ __global__ __launch_bounds__(NT, 1) void conv_persist_kernel(const stgcn_conv_de
 
   // ---- phases: group (p & 1) computes tile p; the other group finishes tile p-1, commits tile
   // p+1's frames (its own next tile) and prefetches tile p+3 (its tile after that)
+  long long tc = 0, te = 0, tcm = 0, tp = 0, t0 = g.dbg ? (long long)__builtin_amdgcn_s_memtime() : 0;
+  auto stamp = [&](long long& acc_t) {
+    if (g.dbg) {
+      const long long t1 = (long long)__builtin_amdgcn_s_memtime();
+      acc_t += t1 - t0;
+      t0 = t1;
+    }
+  };
+  long long tb = 0;
   for (int p = 0; p <= K; ++p) {
     if (grp == (p & 1)) {
       if (p < K) compute(p);
+      stamp(tc);
     } else {
       if (p >= 1) epilogue(p - 1);
+      stamp(te);
       if (p + 1 < K && !fresh(p + 1)) commit(p + 1);
+      stamp(tcm);
       if (p + 3 < K && !fresh(p + 3)) prefetch(p + 3);
+      stamp(tp);
     }
-    __syncthreads();
+    bar();
+    stamp(tb);
     if (p + 1 < K && fresh(p + 1)) {  // a new sample: its halo overwrites slots of tile p
       stage_fresh(p + 1);
-      __syncthreads();
+      bar();
     }
   }
 
+  if (g.dbg && lane == 0 && (wave == 0 || wave == 4)) {
+    long long* d = g.dbg + (long)blockIdx.x * 8 + (wave ? 4 : 0);
+    d[0] = tc;
+    d[1] = te;
+    d[2] = tcm;
+    d[3] = tp;
+    (void)tb;
+  }
   if (a.stats) {
     // merge lane halves (same column), then the 2 row groups x 2 wave groups per column via LDS
     Welford o;
@@ -313,17 +376,35 @@ __global__ __launch_bounds__(NT, 1) void conv_persist_kernel(const stgcn_conv_de
 }  // namespace
 
 long conv_rows_num_row_blocks(long M, int cout);
+long long* persist_dbg_ptr = nullptr;
+
+// copy the diagnostic timers (8 per block) of the last persistent launch to the host
+int persist_debug_read(long long* host, long n) {
+  if (!persist_dbg_ptr) return 1;
+  (void)hipDeviceSynchronize();
+  return hipMemcpy(host, persist_dbg_ptr, n * sizeof(long long), hipMemcpyDeviceToHost) == hipSuccess ? 0 : 3;
+}
 
 // -1: shape not handled (caller tries the next kernel)
 int conv_persist_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
   if (dtype != 1 || a.Kt != KT || a.stride != 1 || a.pad != PADT || a.T_in != a.T_out) return -1;
   if (a.Cin_pad != C || a.Cout_pad != C || a.Cin != C || a.in_ld % 8 || a.pro > 1) return -1;
-  if (a.bias_mode > 1 || a.V > 32) return -1;
+  if (a.bias_mode > 1 || a.V > 32 || a.out_ld % 8 || a.Cout % 8) return -1;
   PGeom g;
+  g.dbg = nullptr;
+  static const int dmode = getenv("STGCN_PERSIST_MODE") ? atoi(getenv("STGCN_PERSIST_MODE")) : 0;
+  g.dmode = dmode;
+  static long long* dbg = nullptr;
+  static const bool want_dbg = getenv("STGCN_PERSIST_DBG") != nullptr;
+  if (want_dbg) {
+    if (!dbg) (void)hipMalloc(&dbg, 8 * 4096 * sizeof(long long));
+    g.dbg = dbg;
+    persist_dbg_ptr = dbg;
+  }
   g.F = ROWS / a.V;
   if (g.F < 1) return -1;
   g.RSL = 2 * g.F + KT - 1;
-  const size_t lds = B_BYTES + (size_t)g.RSL * a.V * RS_A + 2 * C * sizeof(float);
+  const size_t lds = B_BYTES + (size_t)g.RSL * a.V * RS_A + 2 * C * sizeof(float) + 4 * 64 * 64;
   if (lds > (size_t)LDS_MAX) return -1;
   g.tiles_n = (a.T_out + g.F - 1) / g.F;
   const long nt = (long)a.N * g.tiles_n;

@@ -315,7 +315,35 @@ int launch_conv(const ConvArgs& a, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
 
+// dst[k][co][ci] = src[k*s0 + co*s1 + ci*s2] (0 in the padding), cast to T: any strided view of the
+// fp32 parameter (permuted / transposed) packs in one pass
+template <typename T>
+__global__ void pack_weight_kernel(const float* __restrict__ src, long s0, long s1, long s2, int Co, int Ci, int cp,
+                                   int kp, long total, T* __restrict__ dst) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int ci = (int)(i % kp);
+  const long r = i / kp;
+  const int co = (int)(r % cp);
+  const long k = r / cp;
+  const float v = (co < Co && ci < Ci) ? src[k * s0 + co * s1 + ci * s2] : 0.f;
+  dst[i] = Tr<T>::from_f(v);
+}
+
 }  // namespace
+
+int pack_weight_launch(const float* src, long s0, long s1, long s2, int Kt, int Co, int Ci, void* dst, int cp, int kp,
+                       int dtype, hipStream_t s) {
+  const long total = (long)Kt * cp * kp;
+  const unsigned blocks = (unsigned)((total + 255) / 256);
+  if (dtype == 1)
+    hipLaunchKernelGGL(pack_weight_kernel<bf16>, dim3(blocks), dim3(256), 0, s, src, s0, s1, s2, Co, Ci, cp, kp, total,
+                       (bf16*)dst);
+  else
+    hipLaunchKernelGGL(pack_weight_kernel<float>, dim3(blocks), dim3(256), 0, s, src, s0, s1, s2, Co, Ci, cp, kp,
+                       total, (float*)dst);
+  return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
+}
 
 // Column tile = 64 for Cout <= 64, 128 otherwise; weights are packed to a multiple of it.
 int conv_rows_bn_tile(int cout) { return cout <= 64 ? 64 : 128; }

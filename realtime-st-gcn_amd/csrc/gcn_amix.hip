@@ -163,7 +163,8 @@ __global__ __launch_bounds__(256) void amix_trans_kernel(const AmixArgs a, int f
 // cols w, both 8-consecutive-ci per lane => plain 16B loads).  One wave per frame stream; waves of
 // a block reduce through LDS, then one atomicAdd per element per block.
 template <typename T>
-__global__ __launch_bounds__(256) void amix_dA_kernel(const AmixArgs a, const void* dwp, float* dA, int frames_per_block) {
+__global__ __launch_bounds__(256) void amix_dA_kernel(const AmixArgs a, const void* dwp, float* dA, float* work,
+                                                      int frames_per_block) {
   constexpr int VEC = 16 / sizeof(T);
   __shared__ float red[4][VMAX * VMAX];
   const int n = blockIdx.y;
@@ -217,30 +218,96 @@ __global__ __launch_bounds__(256) void amix_dA_kernel(const AmixArgs a, const vo
 #pragma unroll
     for (int i = 0; i < 16; ++i) red[wave][acc_row(i, lane) * VMAX + r] = acc[i];
     __syncthreads();
-    float* dst = dA + ((a.per_sample ? (long)n * a.P : 0) + p) * a.V * a.V;
+    // work: this block's partial in slab row (n * gridDim.x + blockIdx.x) of width P*V*V (fixed-order
+    // reduction afterwards -> deterministic); no work: atomics
+    float* dst = work ? work + ((long)n * gridDim.x + blockIdx.x) * a.P * a.V * a.V + (long)p * a.V * a.V
+                      : dA + ((a.per_sample ? (long)n * a.P : 0) + p) * a.V * a.V;
     for (int i = threadIdx.x; i < a.V * a.V; i += 256) {
       const int v = i / a.V, w = i % a.V;
       const float s = red[0][v * VMAX + w] + red[1][v * VMAX + w] + red[2][v * VMAX + w] + red[3][v * VMAX + w];
-      atomicAdd(dst + i, s);
+      if (work) dst[i] = s; else atomicAdd(dst + i, s);
     }
     __syncthreads();
   }
 }
 
-__global__ void gcn_bias_kernel(const float* A, const float* b, float* out, int P, int V, int C, int per_sample) {
-  // out[(n), w, c] = sum_p b[p*C + c] * sum_v A[(n), p, v, w]
+// out[b][r2][e] (+)= sum_{r in group r2} in[b][r][e], rows summed in a fixed order (deterministic).
+// Block: 64 columns x 4 row-interleaved waves, LDS combine in wave order.
+__global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ in, long R, long E, int rpb,
+                                                       float* out, int accumulate) {
+  const int g = threadIdx.x >> 6;
+  const long e = (long)blockIdx.x * 64 + (threadIdx.x & 63);
+  const long b = blockIdx.z;
+  const long r0 = (long)blockIdx.y * rpb, r1 = min(R, r0 + rpb);
+  const float* src = in + b * R * E + e;
+  float acc = 0.f;
+  if (e < E)
+    for (long r = r0 + g; r < r1; r += 4) acc += src[r * E];
+  __shared__ float part[4][64];
+  part[g][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (g == 0 && e < E) {
+    const int l = threadIdx.x;
+    const float t = ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
+    float* o = out + (b * gridDim.y + blockIdx.y) * E + e;
+    *o = accumulate ? *o + t : t;
+  }
+}
+
+__global__ __launch_bounds__(256) void gcn_bias_kernel(const float* A, const float* b, float* out, int P, int V, int C,
+                                                       int per_sample) {
+  // out[(n), w, c] = sum_p b[p*C + c] * colsum_p[w],  colsum_p[w] = sum_v A[(n), p, v, w] (staged in LDS)
+  __shared__ float cs[4 * VMAX];
   const int n = blockIdx.y;
   const float* An = A + (per_sample ? (long)n * P * V * V : 0);
+  for (int i = threadIdx.x; i < P * V; i += blockDim.x) {
+    const int p = i / V, w = i % V;
+    float t = 0.f;
+    for (int v = 0; v < V; ++v) t += An[(p * V + v) * V + w];
+    cs[i] = t;
+  }
+  __syncthreads();
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < V * C; i += gridDim.x * blockDim.x) {
     const int w = i / C, c = i % C;
     float s = 0.f;
-    for (int p = 0; p < P; ++p) {
-      float cs = 0.f;
-      for (int v = 0; v < V; ++v) cs += An[(p * V + v) * V + w];
-      s += b[p * C + c] * cs;
-    }
+    for (int p = 0; p < P; ++p) s += b[p * C + c] * cs[p * V + w];
     out[(long)n * V * C + i] = s;
   }
+}
+
+// Gradients of the conv bias pushed through a shared A, from S[w][c] = sum over rows of joint w of dg:
+//   dA[p][v][w] += sum_c b[p][c] S[w][c]   (independent of v)
+//   db[p][c]     = sum_w colsum_p[w] S[w][c]
+// Block x < P*V: one (p, w) dot over c, broadcast along v; blocks >= P*V: db columns.
+__global__ __launch_bounds__(256) void gcn_bias_bwd_kernel(const float* A, const float* b, const float* S, int P, int V,
+                                                           int C, float* dA, float* db) {
+  const int bx = blockIdx.x;
+  if (bx < P * V) {
+    const int p = bx / V, w = bx % V;
+    float t = 0.f;
+    for (int c = threadIdx.x; c < C; c += 256) t += b[p * C + c] * S[w * C + c];
+    t = wave_sum(t);
+    __shared__ float red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+    __syncthreads();
+    const float tot = ((red[0] + red[1]) + red[2]) + red[3];
+    for (int v = threadIdx.x; v < V; v += 256) dA[(p * V + v) * V + w] += tot;
+    return;
+  }
+  __shared__ float cs[4 * VMAX];
+  for (int i = threadIdx.x; i < P * V; i += 256) {
+    const int p = i / V, w = i % V;
+    float t = 0.f;
+    for (int v = 0; v < V; ++v) t += A[(p * V + v) * V + w];
+    cs[i] = t;
+  }
+  __syncthreads();
+  const int i = (bx - P * V) * 256 + threadIdx.x;  // (p, c)
+  if (i >= P * C) return;
+  const int p = i / C, c = i % C;
+  float t = 0.f;
+  for (int w = 0; w < V; ++w) t += cs[p * V + w] * S[w * C + c];
+  db[i] = t;
 }
 
 // frames per block so that a block has ~16 work items per thread
@@ -284,21 +351,69 @@ int amix_trans_launch(const AmixArgs& a0, int dtype, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
 
-int amix_dA_launch(const AmixArgs& a, const void* dw, float* dA, int dtype, hipStream_t s) {
-  if (a.V > VMAX || a.P > 4) return STGCN_EBADSHAPE;
+namespace {
+constexpr int SLAB_RPB = 32;  // rows per block of a slab_sum level
+int amix_dA_chunks(const AmixArgs& a, int* fpb_out) {
   // ~1024 blocks overall
   int fpb = (int)(((long)a.N * a.T + 1023) / 1024);
   if (fpb < 8) fpb = 8;
-  dim3 grid((a.T + fpb - 1) / fpb, a.N);
+  if (fpb_out) *fpb_out = fpb;
+  return (a.T + fpb - 1) / fpb;
+}
+}  // namespace
+
+// Deterministic fixed-order sum of a slab in[B][R][E] into out[B][E] (+=: accumulate); two levels when R
+// is large.  tmp: ceil(R / SLAB_RPB) * B * E floats (only when R > SLAB_RPB).
+void slab_sum_launch(const float* in, long B, long R, long E, float* tmp, float* out, int accumulate, hipStream_t s) {
+  const unsigned cb = (unsigned)((E + 63) / 64);
+  if (R > SLAB_RPB) {
+    const long R2 = (R + SLAB_RPB - 1) / SLAB_RPB;
+    hipLaunchKernelGGL(slab_sum_kernel, dim3(cb, (unsigned)R2, (unsigned)B), dim3(256), 0, s, in, R, E, SLAB_RPB, tmp, 0);
+    in = tmp;
+    R = R2;
+  }
+  hipLaunchKernelGGL(slab_sum_kernel, dim3(cb, 1, (unsigned)B), dim3(256), 0, s, in, R, E, (int)R, out, accumulate);
+}
+
+long slab_sum_tmp_floats(long B, long R, long E) { return R > SLAB_RPB ? ((R + SLAB_RPB - 1) / SLAB_RPB) * B * E : 0; }
+
+long amix_dA_workspace(const AmixArgs& a) {
+  if (a.V > VMAX || a.P > 4) return 0;
+  const long rows = (long)a.N * amix_dA_chunks(a, nullptr);
+  const long E = (long)a.P * a.V * a.V;
+  const long B = a.per_sample ? a.N : 1, R = a.per_sample ? rows / a.N : rows;
+  return (long)sizeof(float) * (rows * E + slab_sum_tmp_floats(B, R, E));
+}
+
+int amix_dA_launch(const AmixArgs& a, const void* dw, float* dA, void* work, int dtype, hipStream_t s) {
+  if (a.V > VMAX || a.P > 4) return STGCN_EBADSHAPE;
+  int fpb;
+  const int chunks = amix_dA_chunks(a, &fpb);
+  dim3 grid(chunks, a.N);
+  float* w = reinterpret_cast<float*>(work);
   if (dtype)
-    hipLaunchKernelGGL(amix_dA_kernel<bf16>, grid, dim3(256), 0, s, a, dw, dA, fpb);
+    hipLaunchKernelGGL(amix_dA_kernel<bf16>, grid, dim3(256), 0, s, a, dw, dA, w, fpb);
   else
-    hipLaunchKernelGGL(amix_dA_kernel<float>, grid, dim3(256), 0, s, a, dw, dA, fpb);
+    hipLaunchKernelGGL(amix_dA_kernel<float>, grid, dim3(256), 0, s, a, dw, dA, w, fpb);
+  if (w) {
+    const long E = (long)a.P * a.V * a.V;
+    const long B = a.per_sample ? a.N : 1, R = a.per_sample ? chunks : (long)a.N * chunks;
+    slab_sum_launch(w, B, R, E, w + (long)a.N * chunks * E, dA, 1, s);
+  }
+  return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
+}
+
+int gcn_bias_bwd_launch(const float* A, const float* b, const float* S, int P, int V, int C, float* dA, float* db,
+                        hipStream_t s) {
+  if (V > VMAX || P > 4) return STGCN_EBADSHAPE;
+  hipLaunchKernelGGL(gcn_bias_bwd_kernel, dim3((unsigned)(P * V + (P * C + 255) / 256)), dim3(256), 0, s, A, b, S, P,
+                     V, C, dA, db);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
 
 int gcn_bias_launch(const float* A, const float* b, float* out, int N, int P, int V, int C, int per_sample,
                     hipStream_t s) {
+  if (V > VMAX || P > 4) return STGCN_EBADSHAPE;
   dim3 grid((V * C + 255) / 256, per_sample ? N : 1);
   hipLaunchKernelGGL(gcn_bias_kernel, grid, dim3(256), 0, s, A, b, out, P, V, C, per_sample);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;

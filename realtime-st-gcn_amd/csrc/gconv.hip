@@ -494,22 +494,28 @@ __global__ void gconv_wgrad_f32_kernel(const stgcn_gconv_wgrad_desc a) {
   const int co = (int)((idx / a.Cin) % a.Cout);
   const int pair = (int)(idx / ((long)a.Cin * a.Cout));
   const int w = pair / a.J, j = pair % a.J;
-  if (j >= a.deg[w]) return;
+  if (j >= a.deg[w]) {
+    a.dweff[idx] = 0.f;
+    return;
+  }
   const int src = a.nbr[pair];
   const float* dy = reinterpret_cast<const float*>(a.dy);
   const float* x = reinterpret_cast<const float*>(a.x);
   float s = 0.f;
   for (int i = 0; i < a.NT; ++i)
     s += dy[((long)i * a.V + w) * a.dy_ld + co] * x[((long)i * a.V + src) * a.x_ld + ci];
-  a.dweff[idx] += s;
+  a.dweff[idx] = s;
 }
 
-// slab reduction (rows of the slab are whole [V*J][Cout][Cin] images): dweff[e] += sum_r slab[r][e]
-__global__ void gslab_reduce_kernel(const float* __restrict__ slab, int R, long E, float* __restrict__ out) {
+// slab reduction (rows of the slab are whole [V*J][Cout][Cin] images): dweff[e] = sum_r slab[r][e]
+__global__ void gslab_reduce_kernel(const float* __restrict__ slab, int R, long E, long EC, const int* deg, int J,
+                                    float* __restrict__ out) {
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= E) return;
-  float s = out[e];
-  for (int r = 0; r < R; ++r) s += slab[(long)r * E + e];
+  const int pair = (int)(e / EC);
+  float s = 0.f;
+  if (pair % J < deg[pair / J])  // slab slots of unused pairs are never written (nor read)
+    for (int r = 0; r < R; ++r) s += slab[(long)r * E + e];
   out[e] = s;
 }
 
@@ -546,6 +552,79 @@ __global__ void gconv_dA_kernel(const float* __restrict__ dweff, const float* __
     const float t = part[0] + part[1] + part[2] + part[3];
     dA[((long)p * V + nbr[w * J + j]) * V + w] += t;
   }
+}
+
+constexpr int PMAX = 4;
+// dW[p][e] += sum_{pairs} A[p][v][w] dWeff[pair][e] for all p in one pass (dWeff read once).
+// Block = 64 e-columns x 4 groups over target joints w (w = g, g+4, ...); fixed-order LDS combine.
+__global__ __launch_bounds__(256) void gconv_dw_all_kernel(const float* __restrict__ dweff, const float* __restrict__ A,
+                                                           const int* nbr, const int* deg, int P, int V, int J, long E,
+                                                           float* dW) {
+  const int g = threadIdx.x >> 6;
+  const long e = (long)blockIdx.x * 64 + (threadIdx.x & 63);
+  float acc[PMAX] = {0.f, 0.f, 0.f, 0.f};
+  if (e < E) {
+    for (int w = g; w < V; w += 4) {
+      const int dg = deg[w];
+      for (int j = 0; j < dg; ++j) {
+        const int v = nbr[w * J + j];
+        const float d = dweff[(long)(w * J + j) * E + e];
+#pragma unroll
+        for (int p = 0; p < PMAX; ++p)
+          if (p < P) acc[p] += A[((long)p * V + v) * V + w] * d;
+      }
+    }
+  }
+  __shared__ float part[4][PMAX][64];
+#pragma unroll
+  for (int p = 0; p < PMAX; ++p) part[g][p][threadIdx.x & 63] = acc[p];
+  __syncthreads();
+  if (threadIdx.x < 64 && e < E) {
+    const int l = threadIdx.x;
+#pragma unroll
+    for (int p = 0; p < PMAX; ++p)
+      if (p < P) dW[(long)p * E + e] += ((part[0][p][l] + part[1][p][l]) + part[2][p][l]) + part[3][p][l];
+  }
+}
+
+// dA[p][v][w] += <W_p, dWeff[pair]> for all p, in two deterministic steps: block (pair, chunk) writes the
+// P partial dots of its DA_CHUNK-element slice to part[pair][chunk][p]; gconv_dA_reduce sums the chunks in
+// order.  (pair, chunk) grid keeps >= ~1000 blocks in flight even for C = 64.
+constexpr int DA_CHUNK = 2048;
+__global__ __launch_bounds__(256) void gconv_dA_part_kernel(const float* __restrict__ dweff, const float* __restrict__ W,
+                                                            const int* deg, int P, int J, long E, float* part) {
+  const int pair = blockIdx.x, c = blockIdx.y, nch = gridDim.y;
+  if (pair % J >= deg[pair / J]) return;
+  const float* d = dweff + (long)pair * E;
+  float acc[PMAX] = {0.f, 0.f, 0.f, 0.f};
+  const long e1 = min(E, (long)(c + 1) * DA_CHUNK);
+  for (long e = (long)c * DA_CHUNK + threadIdx.x; e < e1; e += 256) {
+    const float dv = d[e];
+#pragma unroll
+    for (int p = 0; p < PMAX; ++p)
+      if (p < P) acc[p] += W[(long)p * E + e] * dv;
+  }
+  __shared__ float red[4][PMAX];
+#pragma unroll
+  for (int p = 0; p < PMAX; ++p) {
+    const float t = wave_sum(acc[p]);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][p] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < P)
+    part[((long)pair * nch + c) * PMAX + threadIdx.x] =
+        ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+}
+
+__global__ void gconv_dA_reduce_kernel(const float* __restrict__ part, const int* nbr, const int* deg, int P, int V,
+                                       int J, int nch, float* dA) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // (pair, p)
+  if (i >= V * J * P) return;
+  const int pair = i / P, p = i % P, w = pair / J, j = pair % J;
+  if (j >= deg[w]) return;
+  float s = 0.f;
+  for (int c = 0; c < nch; ++c) s += part[((long)pair * nch + c) * PMAX + p];
+  dA[((long)p * V + nbr[w * J + j]) * V + w] += s;
 }
 
 WGG wplan(const stgcn_gconv_wgrad_desc& a) {
@@ -605,8 +684,6 @@ int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s
   WGG g = wplan(a);
   if (!a.work || a.work_bytes < (long)g.R * E * (long)sizeof(float)) return STGCN_EBADSHAPE;
   g.slab = reinterpret_cast<float*>(a.work);
-  // slots of unused pairs are never written by the kernel: clear the slab first
-  (void)hipMemsetAsync(g.slab, 0, (size_t)g.R * E * sizeof(float), s);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gconv_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -617,18 +694,38 @@ int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s
   const size_t lds = 2 * 4 * WKM * WPR;  // >= the 48 KB cross-wave reduction buffer
   hipLaunchKernelGGL(gconv_wgrad_kernel, dim3((unsigned)blocks), dim3(256), lds, s, a, g);
   hipLaunchKernelGGL(gslab_reduce_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, (const float*)g.slab,
-                     g.R, E, a.dweff);
+                     g.R, E, (long)a.Cout * a.Cin, a.deg, a.J, a.dweff);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
 
+long gconv_wgrad_finish_workspace(int P, int V, int J, int Cout, int Cin) {
+  const long E = (long)Cout * Cin;
+  return P > PMAX ? 0 : (long)V * J * ((E + DA_CHUNK - 1) / DA_CHUNK) * PMAX * (long)sizeof(float);
+}
+
 int gconv_wgrad_finish_launch(const float* dweff, const float* A, const float* W, const int* nbr, const int* deg,
-                              int P, int V, int J, int Cout, int Cin, float* dW, float* dA, hipStream_t s) {
-  const long n = (long)P * Cout * Cin;
-  if (dW)
-    hipLaunchKernelGGL(gconv_dw_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dweff, A, nbr, deg, P, V,
-                       J, Cout, Cin, dW);
-  if (dA)
-    hipLaunchKernelGGL(gconv_dA_kernel, dim3((unsigned)(V * J), (unsigned)P), dim3(256), 0, s, dweff, W, nbr, deg, P,
-                       V, J, Cout, Cin, dA);
+                              int P, int V, int J, int Cout, int Cin, float* dW, float* dA, void* work, hipStream_t s) {
+  const long E = (long)Cout * Cin;
+  if (P > PMAX || (dA && !work)) {  // generic per-partition path (dA via atomics-free per-(pair,p) blocks)
+    const long n = (long)P * E;
+    if (dW)
+      hipLaunchKernelGGL(gconv_dw_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dweff, A, nbr, deg, P,
+                         V, J, Cout, Cin, dW);
+    if (dA)
+      hipLaunchKernelGGL(gconv_dA_kernel, dim3((unsigned)(V * J), (unsigned)P), dim3(256), 0, s, dweff, W, nbr, deg,
+                         P, V, J, Cout, Cin, dA);
+  } else {  // one pass over dWeff per output, all partitions at once
+    if (dW)
+      hipLaunchKernelGGL(gconv_dw_all_kernel, dim3((unsigned)((E + 63) / 64)), dim3(256), 0, s, dweff, A, nbr, deg,
+                         P, V, J, E, dW);
+    if (dA) {
+      const int nch = (int)((E + DA_CHUNK - 1) / DA_CHUNK);
+      float* part = reinterpret_cast<float*>(work);
+      hipLaunchKernelGGL(gconv_dA_part_kernel, dim3((unsigned)(V * J), (unsigned)nch), dim3(256), 0, s, dweff, W,
+                         deg, P, J, E, part);
+      hipLaunchKernelGGL(gconv_dA_reduce_kernel, dim3((unsigned)((V * J * P + 255) / 256)), dim3(256), 0, s, part,
+                         nbr, deg, P, V, J, nch, dA);
+    }
+  }
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }

@@ -363,16 +363,6 @@ __global__ __launch_bounds__(256) void rowgroup_sum_kernel(const T* __restrict__
   }
 }
 
-// S[s][e] += sum_b part[s][b][e]  (deterministic reduction of the per-block partial slabs)
-__global__ __launch_bounds__(256) void sum_slabs_kernel(const float* part, int nb, int E, float* S) {
-  const int s = blockIdx.y;
-  for (int e = blockIdx.x * 256 + threadIdx.x; e < E; e += gridDim.x * 256) {
-    float acc = 0.f;
-    const float* p = part + (long)s * nb * E + e;
-    for (int b = 0; b < nb; ++b) acc += p[(long)b * E];
-    S[(long)s * E + e] += acc;
-  }
-}
 
 // ------------------------------------------------------------------ LayerNorm([C,1,V])
 // one wave per frame: frame = V rows x C channels (row stride ld)
@@ -615,16 +605,20 @@ static void rowgroup_geometry(long M, int G, long period, long& F, long& fps, lo
   fps = period > 0 ? period / G : 0;
   nsamp = period > 0 ? M / period : 1;
   const long span = period > 0 ? fps : F;
-  fpb = (span + 63) / 64;  // <= 64 partial slabs per sample
-  if (fpb < 16) fpb = 16;
+  // ~1024 blocks over the whole tensor (enough loads in flight to stream it at HBM rate)
+  fpb = (span * nsamp + 1023) / 1024;
+  if (fpb < 4) fpb = 4;
   nb = (int)((span + fpb - 1) / fpb);
 }
+
+void slab_sum_launch(const float* in, long B, long R, long E, float* tmp, float* out, int accumulate, hipStream_t s);
+long slab_sum_tmp_floats(long B, long R, long E);
 
 long rowgroup_sum_workspace(long M, int C, int G, long period) {
   long F, fps, nsamp, fpb;
   int nb;
   rowgroup_geometry(M, G, period, F, fps, nsamp, fpb, nb);
-  return (long)nb * nsamp * G * C;
+  return (long)nb * nsamp * G * C + slab_sum_tmp_floats(nsamp, nb, (long)G * C);
 }
 
 int rowgroup_sum_launch(const void* x, int ld, long M, int C, int G, long period, float* S, float* work, int dtype,
@@ -635,8 +629,8 @@ int rowgroup_sum_launch(const void* x, int ld, long M, int C, int G, long period
   rowgroup_geometry(M, G, period, F, fps, nsamp, fpb, nb);
   DISPATCH_VEC(dtype, C, hipLaunchKernelGGL((rowgroup_sum_kernel<T, VEC>), dim3(nb, (unsigned)nsamp), dim3(256), 0, s,
                                             (const T*)x, ld, F, C, G, fpb, fps, work));
-  const int E = G * C;
-  hipLaunchKernelGGL(sum_slabs_kernel, dim3((E + 255) / 256, (unsigned)nsamp), dim3(256), 0, s, work, nb, E, S);
+  const long E = (long)G * C;
+  slab_sum_launch(work, nsamp, nb, E, work + (long)nb * nsamp * E, S, 1, s);  // fixed-order, two levels
   RET_HIP;
 }
 

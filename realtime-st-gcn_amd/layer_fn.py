@@ -102,12 +102,19 @@ class StgcnLayerFunction(torch.autograd.Function):
         sup = cfg[5] if len(cfg) > 5 else None
         gather = sup is not None and A32.dim() == 3 and not sup.dense(P)
         bias2d = K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
+        if norm == BN:  # all BatchNorm partial-statistics buffers of the layer from one zero fill
+            cpo = -(-Cout // K.col_tile(Cout)) * K.col_tile(Cout)
+            st_shapes = [(K.gconv_row_blocks(N * T, V) if gather else K.row_blocks(M1, Cout), cpo, 4),
+                         (K.row_blocks(M2, Cout), cpo, 4)] + ([(K.row_blocks(M2, Cout), cpo, 4)] if res_conv else [])
+            st_all = K.zeros_arena(dev, *st_shapes)
+            st1, st2 = st_all[0], st_all[1]
+            str_ = st_all[2] if res_conv else None
         if gather:  # joint-gathered GEMM over per-joint effective weights (gconv.hip), no XA in HBM
             wg2 = wg.detach().float().reshape(P * Cout, Cin).contiguous()
             wgp = K.gconv_weights(A32, wg2, sup, Cout, Cin, False, dtype)
             cpg, kpg = wgp.shape[2], wgp.shape[3]
             if norm == BN:
-                st1 = torch.zeros((K.gconv_row_blocks(N * T, V), cpg, 4), dtype=torch.float32, device=dev)
+                assert cpg == cpo
             g = K.gconv(x, wgp, sup, Cin, Cout, bias=bias2d, stats=st1 if norm == BN else None)
             XA = None
         else:
@@ -115,8 +122,6 @@ class StgcnLayerFunction(torch.autograd.Function):
             wg3 = wg.detach().float().view(P, Cout, Cin).permute(1, 0, 2).reshape(1, Cout, P * Cin)
             wgp, cpg, kpg = K.pack_weight(wg3, dtype)
             bmode = 3 if A32.dim() == 4 else 2
-            if norm == BN:
-                st1 = torch.zeros((K.row_blocks(M1, Cout), cpg, 4), dtype=torch.float32, device=dev)
             g = K.conv_rows(XA, wgp, P * Cin, Cout, cpg, kpg, T, T, bias=bias2d, bias_mode=bmode,
                             stats=st1 if norm == BN else None)
         if norm == BN:
@@ -130,8 +135,6 @@ class StgcnLayerFunction(torch.autograd.Function):
         # ---- temporal conv on relu(norm1(g)) (norm applied in the prologue)
         wt3 = wt.detach().float().squeeze(-1).permute(2, 0, 1)  # [Kt][Cout][Cin]
         wtp, cpt, kpt = K.pack_weight(wt3, dtype)
-        if norm == BN:
-            st2 = torch.zeros((K.row_blocks(M2, Cout), cpt, 4), dtype=torch.float32, device=dev)
         u = K.conv_rows(g, wtp, Cout, Cout, cpt, kpt, T, T_out, Kt=kt, stride=stride, pad=pad,
                         bias=bt.detach().float().contiguous(), stats=st2 if norm == BN else None,
                         tag=f"tcn_fwd_c{Cout}" if stride == 1 else None, **pro1)
@@ -141,8 +144,6 @@ class StgcnLayerFunction(torch.autograd.Function):
         if res_conv:
             wr3 = wr.detach().float().view(1, Cout, Cin)
             wrp, cpr, kpr = K.pack_weight(wr3, dtype)
-            if norm == BN:
-                str_ = torch.zeros((K.row_blocks(M2, Cout), cpr, 4), dtype=torch.float32, device=dev)
             r = K.conv_rows(x, wrp, Cin, Cout, cpr, kpr, T, T_out, Kt=1, stride=stride, pad=0,
                             bias=br.detach().float().contiguous(), stats=str_ if norm == BN else None)
 
@@ -200,6 +201,10 @@ class StgcnLayerFunction(torch.autograd.Function):
         dy = K.to_rows(dy, dtype)
         M1, M2 = N * T * V, N * T_out * V
         grads = {}
+        # every fp32 accumulation target of this backward from one zero fill
+        zshapes = [(kt, Cout, Cout), (1, Cout, Cin), (P * Cout, Cin), (P, V, V),
+                   ((N, V, Cout) if A32.dim() == 4 else (V, Cout))]
+        z_dwt, z_dwr, z_dwg, z_dA, z_S = K.zeros_arena(dev, *zshapes)
 
         # ---- through relu(norm2(u) + res): dz = dy * [y > 0]
         du = K.cl_empty(N, Cout, T_out, V, dtype, dev)
@@ -218,12 +223,12 @@ class StgcnLayerFunction(torch.autograd.Function):
                 kw.update(out2=dx)
                 dx_written = True
             sums2, osum2 = K.bn_bwd_fused(dy, M2, Cout, **kw)
-            grads["n2w"], grads["n2b"] = sums2[:, 1].clone(), sums2[:, 0].clone()
-            grads["bt"] = osum2[:, 0].clone()
+            grads["n2w"], grads["n2b"] = sums2[1], sums2[0]
+            grads["bt"] = osum2[0]
             bt_done = True
-            if res_conv:
-                grads["nrw"], grads["nrb"] = sums2[:, 2].clone(), sums2[:, 0].clone()
-                grads["br"] = osum2[:, 1].clone()
+            if res_conv:  # nrb == n2b numerically; own storage so no two parameters share a grad tensor
+                grads["nrw"], grads["nrb"] = sums2[2], sums2[0].clone()
+                grads["br"] = osum2[1]
         elif norm == BN:
             s2 = K.bn_bwd_reduce(dy, M2, Cout, mask=1, mref=y, x=u, mean_rstd=mr2)
             K.bn_bwd_apply(dy, M2, Cout, du, mask=1, mref=y, x=u, mean_rstd=mr2, gamma=n2w.detach().float(), sums=s2)
@@ -252,7 +257,8 @@ class StgcnLayerFunction(torch.autograd.Function):
             wrTp, cq, kq = K.pack_weight(wrT, dtype)
             K.conv_rows(dr, wrTp, Cout, Cin, cq, kq, T_out, T, Kt=1, stride=stride, pad=0, trans=True, out=dx)
             dx_written = True
-            grads["wr"] = K.conv_wgrad(x, dr, Cin, Cout, T, T_out, Kt=1, stride=stride, pad=0).view(Cout, Cin, 1, 1)
+            grads["wr"] = K.conv_wgrad(x, dr, Cin, Cout, T, T_out, Kt=1, stride=stride, pad=0,
+                                       dw=z_dwr).view(Cout, Cin, 1, 1)
         elif residual and not fused:
             K.bn_bwd_apply(dy, M2, Cin, dx, mask=1, mref=y)  # dx = dz
             dx_written = True
@@ -265,7 +271,7 @@ class StgcnLayerFunction(torch.autograd.Function):
             pro1 = dict(pro=1, pro_a=sc1, pro_b=sh1)
         else:
             pro1 = dict(pro=2, pro_a=_flat_ln(n1w), pro_b=_flat_ln(n1b), pro_stats=ls1)
-        dwt = K.conv_wgrad(g, du, Cout, Cout, T, T_out, Kt=kt, stride=stride, pad=pad, **pro1)
+        dwt = K.conv_wgrad(g, du, Cout, Cout, T, T_out, Kt=kt, stride=stride, pad=pad, dw=z_dwt, **pro1)
         grads["wt"] = dwt.permute(1, 2, 0).unsqueeze(-1)  # [Kt][co][ci] -> (co, ci, Kt, 1)
         if not bt_done:
             grads["bt"] = K.bn_bwd_reduce(du, M2, Cout)[:, 0].clone()
@@ -275,7 +281,7 @@ class StgcnLayerFunction(torch.autograd.Function):
         if fused:
             s1, _ = K.bn_bwd_fused(dh, M1, Cout, mask=2, mref=g, msc=sc1, msh=sh1, x1=g, mr1=mr1,
                                    g1=n1w.detach().float(), out1=dg)
-            grads["n1w"], grads["n1b"] = s1[:, 1].clone(), s1[:, 0].clone()
+            grads["n1w"], grads["n1b"] = s1[1], s1[0]
         elif norm == BN:
             s1 = K.bn_bwd_reduce(dh, M1, Cout, mask=2, mref=g, msc=sc1, msh=sh1, x=g, mean_rstd=mr1)
             K.bn_bwd_apply(dh, M1, Cout, dg, mask=2, mref=g, msc=sc1, msh=sh1, x=g, mean_rstd=mr1,
@@ -296,7 +302,7 @@ class StgcnLayerFunction(torch.autograd.Function):
             wgT = K.gconv_weights(A32, wg2, sup, Cout, Cin, True, dtype)
             K.gconv(dg, wgT, sup, Cout, Cin, trans=True, out=dx, accumulate=dx_written)
             dweff = K.gconv_wgrad(x, dg, sup, Cin, Cout)
-            dwg2, dA = K.gconv_finish(dweff, A32, wg2, sup, Cout, Cin)
+            dwg2, dA = K.gconv_finish(dweff, A32, wg2, sup, Cout, Cin, dW=z_dwg, dA=z_dA)
             grads["wg"] = dwg2.view(P * Cout, Cin, 1, 1)
             if ctx.cfg[6] and ctx.needs_input_grad[1]:
                 # caller-owned A: the reference's dA is dense (also off the graph's support), so take
@@ -315,15 +321,15 @@ class StgcnLayerFunction(torch.autograd.Function):
             grads["wg"] = dwg.view(Cout, P, Cin).permute(1, 0, 2).reshape(P * Cout, Cin, 1, 1)
         # bias pushed through A: dA[p][v][w] += sum_c b_p[c] S[w][c]  (independent of v)
         if A32.dim() == 4:
-            Sn = K.rowgroup_sum(dg, M1, Cout, V, per_sample=True)            # [N][V(w)][Cout]
+            Sn = K.rowgroup_sum(dg, M1, Cout, V, per_sample=True, out=z_S)   # [N][V(w)][Cout]
             dA += torch.einsum("pc,nwc->npw", bgp, Sn).unsqueeze(2)
             colsum = A32.sum(dim=2)                                         # [N][P][W]
             grads["bg"] = torch.einsum("npw,nwc->pc", colsum, Sn).reshape(-1)
         else:
-            S = K.rowgroup_sum(dg, M1, Cout, V)                               # [V(w)][Cout]
-            dA += (bgp @ S.t()).unsqueeze(1)
-            colsum = A32.sum(dim=1)                                         # [P][W]
-            grads["bg"] = (colsum @ S).reshape(-1)
+            S = K.rowgroup_sum(dg, M1, Cout, V, out=z_S)                      # [V(w)][Cout]
+            if not dA.is_contiguous():
+                dA = dA.contiguous()
+            grads["bg"] = K.gcn_bias_bwd(A32, bg.detach().float().contiguous(), S, dA, Cout)
 
         def gr(name, like):
             v = grads.get(name)

@@ -61,8 +61,12 @@ def pack_weight(w3: torch.Tensor, dtype) -> tuple:
     Kt, Co, Ci = w3.shape
     cp = -(-Co // col_tile(Co)) * col_tile(Co)
     kp = -(-Ci // 32) * 32
-    out = torch.zeros((Kt, cp, kp), dtype=dtype, device=w3.device)
-    out[:, :Co, :Ci] = w3
+    out = torch.empty((Kt, cp, kp), dtype=dtype, device=w3.device)
+    if w3.dtype != torch.float32:
+        w3 = w3.float()
+    s0, s1, s2 = w3.stride()
+    L.check(L.lib().stgcn_pack_weight(w3.data_ptr(), s0, s1, s2, Kt, Co, Ci, out.data_ptr(), cp, kp,
+                                      L.dtype_code(dtype), L.stream()), "pack_weight")
     return out, cp, kp
 
 
@@ -145,14 +149,43 @@ def amix_trans(dw, A, Cin, out, accumulate):
     return out
 
 
+def zeros_arena(device, *shapes):
+    """Zeroed fp32 tensors of the given shapes carved from ONE allocation (one fill launch instead of one
+    per buffer); every view starts 256-B aligned."""
+    sizes = [int(torch.Size(sh).numel()) for sh in shapes]
+    offs, tot = [], 0
+    for n in sizes:
+        offs.append(tot)
+        tot += -(-n // 64) * 64
+    buf = torch.zeros(max(tot, 1), dtype=torch.float32, device=device)
+    return [buf[o:o + n].view(sh) for o, n, sh in zip(offs, sizes, shapes)]
+
+
+def _workspace(nbytes, device):
+    """fp32 scratch of at least nbytes (>= 1 element so data_ptr is valid)."""
+    return torch.empty(max(1, (nbytes + 3) // 4), dtype=torch.float32, device=device)
+
+
 def amix_dA(x, dw, A):
     """dA (fp32, shape of A) = sum x (x) DW (stgcn_amix_dA)."""
     N, Cin, T, V = x.shape
     P = A.shape[-3]
     dA = torch.zeros(A.shape, dtype=torch.float32, device=x.device)
     d = _amix_desc(x, None, A, N, T, V, P, Cin)
-    L.check(L.lib().stgcn_amix_dA(d, dw.data_ptr(), dA.data_ptr(), L.dtype_code(x.dtype), L.stream()), "amix_dA")
+    # per-block partials + fixed-order reduction: bit-reproducible (no atomics)
+    work = _workspace(L.lib().stgcn_amix_dA_workspace(d), x.device)
+    L.check(L.lib().stgcn_amix_dA(d, dw.data_ptr(), dA.data_ptr(), work.data_ptr(), L.dtype_code(x.dtype),
+                                  L.stream()), "amix_dA")
     return dA
+
+
+def gcn_bias_bwd(A, b, S, dA, C):
+    """Shared A: dA += bias-through-A term (in place), returns db [P*C] (stgcn_gcn_bias_bwd)."""
+    P, V = A.shape[0], A.shape[-1]
+    db = torch.empty(P * C, dtype=torch.float32, device=A.device)
+    L.check(L.lib().stgcn_gcn_bias_bwd(A.data_ptr(), b.data_ptr(), S.data_ptr(), P, V, C, dA.data_ptr(),
+                                       db.data_ptr(), L.stream()), "gcn_bias_bwd")
+    return db
 
 
 def gcn_bias(A, b, N, C):
@@ -239,7 +272,7 @@ def gconv(x, wpk, sup, Cin, Cout, trans=False, bias=None, stats=None, out=None, 
 def gconv_wgrad(x, dy, sup, Cin, Cout):
     """dWeff [V][J][Cout][Cin] fp32 = sum_i dy[(i,w)] x[(i, S(w)_j)]^T."""
     N, _, T, V = x.shape
-    dweff = torch.zeros((V, sup.J, Cout, Cin), dtype=torch.float32, device=x.device)
+    dweff = torch.empty((V, sup.J, Cout, Cin), dtype=torch.float32, device=x.device)
     d = L.GconvWgradDesc()
     d.x, d.dy, d.nbr, d.deg, d.dweff = x.data_ptr(), dy.data_ptr(), sup.nbr.data_ptr(), sup.deg.data_ptr(), \
         dweff.data_ptr()
@@ -253,14 +286,17 @@ def gconv_wgrad(x, dy, sup, Cin, Cout):
     return dweff
 
 
-def gconv_finish(dweff, A, W, sup, Cout, Cin):
-    """(dW [P*Cout][Cin], dA [P][V][V]) fp32 from dWeff (stgcn_gconv_wgrad_finish)."""
+def gconv_finish(dweff, A, W, sup, Cout, Cin, dW=None, dA=None):
+    """(dW [P*Cout][Cin], dA [P][V][V]) fp32 (+)= from dWeff (stgcn_gconv_wgrad_finish); zeroed if not given."""
     P, V = A.shape[0], A.shape[-1]
-    dW = torch.zeros((P * Cout, Cin), dtype=torch.float32, device=A.device)
-    dA = torch.zeros((P, V, V), dtype=torch.float32, device=A.device)
+    if dW is None:
+        dW = torch.zeros((P * Cout, Cin), dtype=torch.float32, device=A.device)
+    if dA is None:
+        dA = torch.zeros((P, V, V), dtype=torch.float32, device=A.device)
+    work = _workspace(L.lib().stgcn_gconv_wgrad_finish_workspace(P, V, sup.J, Cout, Cin), A.device)
     L.check(L.lib().stgcn_gconv_wgrad_finish(dweff.data_ptr(), A.data_ptr(), W.data_ptr(), sup.nbr.data_ptr(),
                                              sup.deg.data_ptr(), P, V, sup.J, Cout, Cin, dW.data_ptr(), dA.data_ptr(),
-                                             L.stream()), "gconv_finish")
+                                             work.data_ptr(), L.stream()), "gconv_finish")
     return dW, dA
 
 
@@ -325,13 +361,13 @@ def bn_fused_ok(C: int, dtype) -> bool:
 
 def bn_bwd_fused(dy, M, C, mask=0, mref=None, msc=None, msh=None, x1=None, mr1=None, g1=None, out1=None,
                  x2=None, mr2=None, g2=None, out2=None, acc2=False, bias_sums=False):
-    """Fused BN backward (stgcn_bn_bwd_fused_*).  Returns (sums [C,4] = (sum dz, sum dz*xhat1, sum dz*xhat2),
-    osum [C,4] = (sum out1, sum out2) or None).  out1 / out2 are written in place."""
+    """Fused BN backward (stgcn_bn_bwd_fused_*).  Returns (sums [3, C] = (sum dz, sum dz*xhat1, sum dz*xhat2),
+    osum [3, C] = (sum out1, sum out2, -) or None), contiguous rows.  out1 / out2 are written in place."""
     code = L.dtype_code(dy.dtype)
     dev = dy.device
     work = torch.empty(L.lib().stgcn_bn_bwd_fused_workspace(M, C, code), dtype=torch.float32, device=dev)
-    sums = torch.empty((C, 4), dtype=torch.float32, device=dev)
-    osum = torch.empty((C, 4), dtype=torch.float32, device=dev) if bias_sums else None
+    sums = torch.empty(7 * C, dtype=torch.float32, device=dev)
+    osum = torch.empty(7 * C, dtype=torch.float32, device=dev) if bias_sums else None
     d = L.BnBwdDesc()
     d.dy, d.mref, d.x1, d.x2 = dy.data_ptr(), L.ptr(mref), L.ptr(x1), L.ptr(x2)
     d.msc, d.msh, d.mean_rstd1, d.mean_rstd2 = L.ptr(msc), L.ptr(msh), L.ptr(mr1), L.ptr(mr2)
@@ -348,13 +384,14 @@ def bn_bwd_fused(dy, M, C, mask=0, mref=None, msc=None, msh=None, x1=None, mr1=N
     L.check(L.lib().stgcn_bn_bwd_fused_reduce(d, code, L.stream()), "bn_bwd_fused_reduce")
     if out1 is not None:
         L.check(L.lib().stgcn_bn_bwd_fused_apply(d, code, L.stream()), "bn_bwd_fused_apply")
-    return sums, osum
+    return sums[4 * C:].view(3, C), (osum[4 * C:].view(3, C) if osum is not None else None)
 
 
-def rowgroup_sum(x, M, C, G, per_sample=False):
-    """[G][C] (or [N][G][C] per sample) sums of rows grouped by m % G."""
+def rowgroup_sum(x, M, C, G, per_sample=False, out=None):
+    """[G][C] (or [N][G][C] per sample) sums of rows grouped by m % G (+= into a zeroed ``out`` if given)."""
     N = x.shape[0]
-    S = torch.zeros(((N,) if per_sample else ()) + (G, C), dtype=torch.float32, device=x.device)
+    S = out if out is not None else \
+        torch.zeros(((N,) if per_sample else ()) + (G, C), dtype=torch.float32, device=x.device)
     period = M // N if per_sample else 0
     work = torch.empty(L.lib().stgcn_rowgroup_sum_workspace(M, C, G, period), dtype=torch.float32, device=x.device)
     L.check(L.lib().stgcn_rowgroup_sum(x.data_ptr(), rows_ld(x), M, C, G, period, S.data_ptr(), work.data_ptr(),
@@ -423,8 +460,10 @@ def attn_scores(theta, phi, P):
     """C = softmax_w(theta_p^T phi_p) per (n, p): fp32 (N, P, V, V)."""
     N, CH, T, V = theta.shape
     C = torch.empty((N, P, V, V), dtype=torch.float32, device=theta.device)
+    work = _workspace(L.lib().stgcn_attn_scores_workspace(N, T, V, P), theta.device)
     L.check(L.lib().stgcn_attn_scores(theta.data_ptr(), phi.data_ptr(), rows_ld(theta), N, T, V, P, CH // P,
-                                      C.data_ptr(), L.dtype_code(theta.dtype), L.stream()), "attn_scores")
+                                      C.data_ptr(), work.data_ptr(), L.dtype_code(theta.dtype), L.stream()),
+            "attn_scores")
     return C
 
 

@@ -76,3 +76,20 @@ def test_agcn_layer_vs_oracle_c64(P):
     grads = {k: v.grad for k, v in sd.items() if v.grad is not None}
     for k, g in grads.items():
         assert_grad_close(named[k].grad, g, TOL, k, grad_floor(grads, k), reduction=True)
+
+
+def test_aagcn_model_bit_reproducible(P):
+    """Attention scores and per-sample dA reduce their T-chunk partials in a fixed order (no atomics):
+    two identical fwd+bwd runs give bit-identical outputs and input gradients."""
+    d = load_golden("model_aagcn_bn_narrow")
+    m = P.MODELS["aa-gcn"](rank=None, **d["arch"])
+    m.load_state_dict(sub(d, "sd/"), strict=True)
+    m = m.to(DEV)
+    outs = []
+    for _ in range(2):
+        x = d["x"].to(DEV).requires_grad_(True)
+        y = m(x)
+        y.backward(d["dy"].to(DEV))
+        outs.append((y.detach().clone(), x.grad.clone()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])

@@ -218,6 +218,8 @@ def test_bn_bwd_fused(K, dtype, tol, mode):
     r = rnd(torch.randn(N, C, T, V) - 0.3).requires_grad_(True)
     x = rnd(torch.randn(N, C, T, V)).requires_grad_(True)
     w2, b2, wr, brr = torch.rand(C) + 0.5, torch.randn(C), torch.rand(C) + 0.5, torch.randn(C)
+    w2.requires_grad_(True)
+    b2.requires_grad_(True)
     if mode == "bn1":
         y = torch.relu(_bn_ref(u, w2, b2))
     else:
@@ -234,11 +236,11 @@ def test_bn_bwd_fused(K, dtype, tol, mode):
     # the mask reference as the kernels see it: the stored (rounded) forward output
     yd = cl(y.detach(), dtype)
     du = torch.empty_like(ud)
-    kw = dict(x1=ud, mr1=stats(u.detach()), g1=w2.to(DEV), out1=du, bias_sums=True)
+    kw = dict(x1=ud, mr1=stats(u.detach()), g1=w2.detach().to(DEV), out1=du, bias_sums=True)
     if mode == "bn1":
         mr = stats(u.detach())
-        sc = (w2.to(DEV) * mr[:, 1])
-        sh = (b2.to(DEV) - mr[:, 0] * sc)
+        sc = (w2.detach().to(DEV) * mr[:, 1])
+        sh = (b2.detach().to(DEV) - mr[:, 0] * sc)
         kw.update(mask=2, mref=ud, msc=sc.contiguous(), msh=sh.contiguous())
     else:
         kw.update(mask=1, mref=yd)
@@ -251,7 +253,10 @@ def test_bn_bwd_fused(K, dtype, tol, mode):
         kw.update(out2=out2)
     sums, osum = K.bn_bwd_fused(cl(dy, dtype), M, C, **kw)
     assert_close(du.float(), u.grad, tol, "du")
-    assert_close(osum[:, 0].cpu(), u.grad.sum(dim=(0, 2, 3)), tol, "sum du", u.grad.abs().sum(dim=(0, 2, 3)).max())
+    assert_close(osum[0].cpu(), u.grad.sum(dim=(0, 2, 3)), tol, "sum du", u.grad.abs().sum(dim=(0, 2, 3)).max())
+    # the BN parameter gradients: sum dz = d beta2, sum dz*xhat1 = d gamma2
+    assert_close(sums[0].cpu(), b2.grad, tol, "dbeta", b2.grad.abs().max() + 1e-3)
+    assert_close(sums[1].cpu(), w2.grad, tol, "dgamma", w2.grad.abs().max() + 1e-3)
     if mode == "conv_res":
         assert_close(out2.float(), r.grad, tol, "dr")
     if mode == "identity":
