@@ -70,9 +70,21 @@ struct TileGeom {
   int parity;      // 1: stride-2 transposed conv, tiles hold output frames of one parity
   int tiles_half;  // parity mode: tiles per (sample, parity)
   float inv_v;     // 1 / V
+  long long* dbg;  // diagnostic (STGCN_TILE_DBG): per-block phase cycles of wave 0, else nullptr
 };
 
-template <typename T, int WM, int WN, int TM, int TN, int KC, int KT, int S, int MINW, bool PAR>
+// s_waitcnt vmcnt(n) lgkmcnt(0) (gfx9 encoding: vmcnt[3:0] | expcnt[6:4]=7 | lgkmcnt[11:8] | vmcnt[5:4]<<14)
+template <int N>
+DEV void wait_vm_lgkm0() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | ((N >> 4) << 14));
+}
+
+// NBS: B-tile LDS stages.  2: chunk c+1 is prefetched while chunk c computes (one __syncthreads per
+// chunk).  3: chunk c+2 is prefetched (A halo into a second register set, B by LDS-DMA into the third
+// stage) and the chunk barrier waits only for chunk c+1's loads (explicit vmcnt), so ~2 chunks of MFMA
+// time cover the global-load latency instead of one.
+template <typename T, int WM, int WN, int TM, int TN, int KC, int KT, int S, int MINW, bool PAR, int NBS>
 __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stgcn_conv_desc a, const TileGeom g) {
   typedef TL<T, KC> L;
   constexpr int NW = WM * WN, NT = NW * 64;
@@ -88,7 +100,8 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stg
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int A_BYTES = (g.HR * L::RS + 1023) & ~1023;
-  const int STAGE = A_BYTES + B_BYTES;
+  char* const Abase = smem;                    // A halo stages [2]
+  char* const Bbase = smem + 2 * A_BYTES;      // B stages [NBS]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -220,28 +233,37 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stg
   }
 
   const int nchunks = a.Cin_pad / KC;
-  uint4 ra[A_MAX];
-  float sc[VEC], sh[VEC];
+  // BatchNorm prologue (pro 1) scale/shift for all input channels staged once in LDS
+  const bool pro_lds = a.pro == 1 && fast_ld;
+  float* const sPro = reinterpret_cast<float*>(Bbase + NBS * B_BYTES);  // [2][Cin_pad]
+  if (pro_lds)
+    for (int i = tid; i < a.Cin_pad; i += NT) {
+      sPro[i] = i < a.Cin ? a.pro_a[i] : 0.f;
+      sPro[a.Cin_pad + i] = i < a.Cin ? a.pro_b[i] : 0.f;
+    }
+  uint4 ra[2][A_MAX];
+  float sc[VEC], sh[VEC];  // pro 1 without pro_lds (ragged channels)
 
-  auto load = [&](int c, int buf) {
+  // A halo units of chunk c -> registers (fast path: unconditional 16-B loads, zero rows masked at store)
+  auto issue_A = [&](int c, uint4(&r)[A_MAX]) {
     const int cb = c * KC;
 #pragma unroll
     for (int i = 0; i < A_MAX; ++i) {
-      ra[i] = make_uint4(0, 0, 0, 0);
-      if (a_ptr[i] != nullptr) {
-        const T* p = a_ptr[i] + cb;
+      if (fast_ld) {
+        r[i] = *reinterpret_cast<const uint4*>((a_ptr[i] != nullptr ? a_ptr[i] : in) + cb);
+      } else {
+        r[i] = make_uint4(0, 0, 0, 0);
         const int ci = cb + ucol * VEC;
-        if (fast_ld) {
-          ra[i] = *reinterpret_cast<const uint4*>(p);
-        } else if (ci < a.Cin) {
+        if (a_ptr[i] != nullptr && ci < a.Cin) {
+          const T* p = a_ptr[i] + cb;
           float f[VEC];
 #pragma unroll
           for (int j = 0; j < VEC; ++j) f[j] = ci + j < a.Cin ? Tr<T>::to_f(p[j]) : 0.f;
-          ra[i] = pack16(f, (T*)nullptr);
+          r[i] = pack16(f, (T*)nullptr);
         }
       }
     }
-    if (a.pro == 1) {
+    if (a.pro == 1 && !pro_lds) {
       const int ci = cb + ucol * VEC;
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
@@ -249,26 +271,42 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stg
         sh[j] = ci + j < a.Cin ? a.pro_b[ci + j] : 0.f;
       }
     }
-    char* B_ = smem + buf * STAGE + A_BYTES;
-#pragma unroll
-    for (int k = 0; k < (B_PIECES + NW - 1) / NW; ++k) {
-      const int piece = wave + k * NW;
-      if (piece < B_PIECES) {
-        const int byte = piece * 1024 + lane * 16;
-        const int br = byte / L::RB, pu = (byte % L::RB) >> 4;
-        const int u = pu ^ L::swz(br);
-        const int dt = br / BN, col = br % BN;
-        glds16(wp + ((long)dt * a.Cout_pad + n0 + col) * a.Cin_pad + cb + u * VEC, B_ + piece * 1024);
-      }
-    }
   };
 
-  auto store = [&](int c, int buf) {
-    char* A_ = smem + buf * STAGE;
+  // B tile of chunk c (all KT taps x BN columns x KC channels) -> LDS stage bb by LDS-DMA; whole rounds of
+  // NW pieces first, then the wave-uniform tail (vmcnt bookkeeping counts B_PIECES / NW per wave)
+  constexpr int B_FULL = B_PIECES / NW, B_TAIL = B_PIECES % NW;
+  auto issue_B = [&](int c, int bb) {
+    const int cb = c * KC;
+    char* B_ = Bbase + bb * B_BYTES;
+    auto piece_load = [&](int piece) {
+      const int byte = piece * 1024 + lane * 16;
+      const int br = byte / L::RB, pu = (byte % L::RB) >> 4;
+      const int u = pu ^ L::swz(br);
+      const int dt = br / BN, col = br % BN;
+      glds16(wp + ((long)dt * a.Cout_pad + n0 + col) * a.Cin_pad + cb + u * VEC, B_ + piece * 1024);
+    };
+#pragma unroll
+    for (int k = 0; k < B_FULL; ++k) piece_load(wave + k * NW);
+    if (B_TAIL && wave < B_TAIL) piece_load(B_FULL * NW + wave);
+  };
+
+  auto store = [&](int c, int ab, const uint4(&r)[A_MAX]) {
+    char* A_ = Abase + ab * A_BYTES;
+    if (pro_lds) {
+      const int ci = c * KC + ucol * VEC;
+#pragma unroll
+      for (int j = 0; j < VEC; j += 4) {
+        const float4 s4 = *reinterpret_cast<const float4*>(sPro + ci + j);
+        const float4 h4 = *reinterpret_cast<const float4*>(sPro + a.Cin_pad + ci + j);
+        sc[j] = s4.x; sc[j + 1] = s4.y; sc[j + 2] = s4.z; sc[j + 3] = s4.w;
+        sh[j] = h4.x; sh[j + 1] = h4.y; sh[j + 2] = h4.z; sh[j + 3] = h4.w;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < A_MAX; ++i) {
       if (a_lds[i] >= 0) {
-        uint4 v = ra[i];
+        uint4 v = a_src[i] >= 0 ? r[i] : make_uint4(0, 0, 0, 0);
         if (a.pro != 0 && a_src[i] >= 0) {
           float f[VEC];
           unpack16(v, f, (T*)nullptr);
@@ -301,18 +339,12 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stg
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  load(0, 0);
-  store(0, 0);
-  __syncthreads();
-  int cur = 0;
   const int tap_stride = V * L::RS;
   constexpr int NSTEP = KT * KS;  // k-steps of 16 per chunk
   typedef typename Tr<T>::frag Frag;
-  for (int c = 0; c < nchunks; ++c) {
-    const bool more = c + 1 < nchunks;
-    if (more) load(c + 1, cur ^ 1);
-    const char* A_ = smem + cur * STAGE;
-    const char* B_ = A_ + A_BYTES;
+  auto compute = [&](int ab, int bb) {
+    const char* A_ = Abase + ab * A_BYTES;
+    const char* B_ = Bbase + bb * B_BYTES;
     // fragments of k-step st+1 are read while the MFMAs of k-step st run (explicit double buffer;
     // sched_barrier keeps the compiler from hoisting every tap's reads and blowing the VGPR budget)
     Frag fa[2][TM], fb[2][TN];
@@ -340,9 +372,99 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stg
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (more) store(c + 1, cur ^ 1);
+  };
+
+  long long tl = 0, tcp = 0, tst = 0, tbar = 0, tk0 = g.dbg ? (long long)__builtin_amdgcn_s_memtime() : 0;
+  long long q0 = 0, q1 = 0, q2 = 0, q3 = 0;
+  auto stamp = [&](long long& q) {
+    if (g.dbg) q = (long long)__builtin_amdgcn_s_memtime();
+  };
+  auto account = [&]() {
+    if (g.dbg) {
+      const long long q4 = (long long)__builtin_amdgcn_s_memtime();
+      tl += q1 - q0;
+      tcp += q2 - q1;
+      tst += q3 - q2;
+      tbar += q4 - q3;
+    }
+  };
+
+  if constexpr (NBS == 2) {
+    issue_A(0, ra[0]);
+    issue_B(0, 0);
+    store(0, 0, ra[0]);
     __syncthreads();
-    cur ^= 1;
+    for (int c = 0; c < nchunks; ++c) {
+      const bool more = c + 1 < nchunks;
+      stamp(q0);
+      if (more) {
+        issue_A(c + 1, ra[0]);
+        issue_B(c + 1, (c + 1) & 1);
+      }
+      stamp(q1);
+      compute(c & 1, c & 1);
+      stamp(q2);
+      if (more) store(c + 1, (c + 1) & 1, ra[0]);
+      stamp(q3);
+      __syncthreads();
+      account();
+    }
+  } else {
+    // VMEM instructions a wave issues for one chunk (fast path: A_MAX loads + the whole B rounds)
+    constexpr int VM_CHUNK = A_MAX + B_FULL;
+    issue_B(0, 0);
+    issue_A(0, ra[0]);
+    if (nchunks > 1) {
+      issue_B(1, 1);
+      issue_A(1, ra[1]);
+    }
+    store(0, 0, ra[0]);
+    if (nchunks > 1) wait_vm_lgkm0<VM_CHUNK>(); else wait_vm_lgkm0<0>();
+    __builtin_amdgcn_s_barrier();
+    int b0 = 0;  // B stage of chunk c
+    for (int c = 0; c < nchunks; c += 2) {
+      // even chunk c: A regs set 0 is free (chunk c was stored last step), B stage (c+2)%3 too
+      const int b2 = b0 == 0 ? 2 : b0 - 1;  // (c+2) % 3
+      stamp(q0);
+      if (c + 2 < nchunks) {
+        issue_B(c + 2, b2);
+        issue_A(c + 2, ra[0]);
+      }
+      stamp(q1);
+      compute(0, b0);
+      stamp(q2);
+      if (c + 1 < nchunks) store(c + 1, 1, ra[1]);
+      stamp(q3);
+      if (c + 2 < nchunks) wait_vm_lgkm0<VM_CHUNK>(); else wait_vm_lgkm0<0>();
+      __builtin_amdgcn_s_barrier();
+      account();
+      if (c + 1 >= nchunks) break;
+      // odd chunk c+1
+      const int b1 = b0 == 2 ? 0 : b0 + 1;  // (c+1) % 3
+      stamp(q0);
+      if (c + 3 < nchunks) {
+        issue_B(c + 3, b0);  // (c+3) % 3 == c % 3
+        issue_A(c + 3, ra[1]);
+      }
+      stamp(q1);
+      compute(1, b1);
+      stamp(q2);
+      if (c + 2 < nchunks) store(c + 2, 0, ra[0]);
+      stamp(q3);
+      if (c + 3 < nchunks) wait_vm_lgkm0<VM_CHUNK>(); else wait_vm_lgkm0<0>();
+      __builtin_amdgcn_s_barrier();
+      account();
+      b0 = b2;  // (c+2) % 3
+    }
+  }
+  if (g.dbg && tid == 0) {
+    long long* d = g.dbg + (long)blockIdx.x * 8;
+    d[0] = tl;
+    d[1] = tcp;
+    d[2] = tst;
+    d[3] = tbar;
+    d[4] = (long long)__builtin_amdgcn_s_memtime() - tk0;
+    d[5] = nchunks;
   }
 
   // ---------------------------------------------------------------- epilogue
@@ -431,6 +553,14 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stg
   }
 }
 
+long long* tile_dbg_ptr = nullptr;
+long long* tile_dbg_buffer() {
+  static const bool want = getenv("STGCN_TILE_DBG") != nullptr;
+  if (!want) return nullptr;
+  if (!tile_dbg_ptr) (void)hipMalloc(&tile_dbg_ptr, 8 * 65536 * sizeof(long long));
+  return tile_dbg_ptr;
+}
+
 template <typename T, int WM, int WN, int TM, int TN, int KC, int KT, int S, int MINW = 2>
 int launch_tile(const stgcn_conv_desc& a, long max_row_blocks, hipStream_t s) {
   typedef TL<T, KC> L;
@@ -438,6 +568,7 @@ int launch_tile(const stgcn_conv_desc& a, long max_row_blocks, hipStream_t s) {
   constexpr int HR_MAX = S * BM + (KT - S > 0 ? (KT - S) * 32 : 0);
   if (a.Cout_pad % BN || a.Cin_pad % KC) return -1;
   TileGeom g;
+  g.dbg = tile_dbg_buffer();
   const bool flat = KT == 1 && S == 1;
   g.parity = (S == 2 && a.trans) ? 1 : 0;
   g.inv_v = 1.f / (float)a.V;
@@ -474,24 +605,42 @@ int launch_tile(const stgcn_conv_desc& a, long max_row_blocks, hipStream_t s) {
   if (nblk <= 0 || nblk > 0x7fffffffL) return -1;
   g.nblk = (int)nblk;
   const int A_BYTES = (g.HR * L::RS + 1023) & ~1023;
-  size_t lds = 2 * (size_t)(A_BYTES + KT * BN * L::RB);
+  const size_t B_BYTES = (size_t)KT * BN * L::RB;
+  const size_t pro_bytes = a.pro == 1 ? 2 * sizeof(float) * (size_t)a.Cin_pad : 0;
   const size_t red = a.stats ? (size_t)WM * BN * 16 : 0;
+  // 3 B stages (prefetch distance 2) for the bf16 stride-1 framed convs when they fit the 160 KB LDS
+  // and every chunk is loaded by the unconditional fast path
+  constexpr bool CAN3 = sizeof(T) == 2 && S == 1 && KT > 1;
+  const bool fast = (a.in_ld % (16 / (int)sizeof(T))) == 0 && (a.Cin % KC) == 0;
+  size_t lds3 = 2 * (size_t)A_BYTES + 3 * B_BYTES + pro_bytes;
+  if (red > lds3) lds3 = red;
+  // measured: no gain over 2 stages on the config-2 shapes (the chunk barriers, not load latency, bound
+  // this kernel), so the 3-stage pipeline is opt-in (STGCN_TILE_NB3=1) for experiments
+  static const bool want3 = getenv("STGCN_TILE_NB3") != nullptr;
+  const bool use3 = want3 && CAN3 && fast && a.pro != 2 && !g.parity && lds3 <= 160 * 1024;
+  size_t lds = 2 * ((size_t)A_BYTES + B_BYTES) + pro_bytes;
   if (red > lds) lds = red;
-  if (lds > 160 * 1024) return -1;
+  if (!use3 && lds > 160 * 1024) return -1;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, false>,
+    (void)hipFuncSetAttribute((const void*)conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, false, 2>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (S == 2)
-      (void)hipFuncSetAttribute((const void*)conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, S == 2>,
+      (void)hipFuncSetAttribute((const void*)conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, S == 2, 2>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (CAN3)
+      (void)hipFuncSetAttribute((const void*)conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, false, CAN3 ? 3 : 2>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
   if (g.parity)
-    hipLaunchKernelGGL((conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, S == 2>), dim3((unsigned)nblk),
+    hipLaunchKernelGGL((conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, S == 2, 2>), dim3((unsigned)nblk),
                        dim3(WM * WN * 64), lds, s, a, g);
+  else if (use3)
+    hipLaunchKernelGGL((conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, false, CAN3 ? 3 : 2>),
+                       dim3((unsigned)nblk), dim3(WM * WN * 64), lds3, s, a, g);
   else
-    hipLaunchKernelGGL((conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, false>), dim3((unsigned)nblk),
+    hipLaunchKernelGGL((conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, false, 2>), dim3((unsigned)nblk),
                        dim3(WM * WN * 64), lds, s, a, g);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
@@ -512,6 +661,12 @@ int tile_dispatch(const stgcn_conv_desc& a, long mrb, hipStream_t s) {
 }  // namespace
 
 long conv_rows_num_row_blocks(long M, int cout);
+
+int tile_debug_read(long long* host, long n) {
+  if (!tile_dbg_ptr) return 1;
+  (void)hipDeviceSynchronize();
+  return hipMemcpy(host, tile_dbg_ptr, n * sizeof(long long), hipMemcpyDeviceToHost) == hipSuccess ? 0 : 3;
+}
 
 // returns -1 when the shape is not handled here (caller falls back to conv_rows.hip)
 int conv_persist_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s);

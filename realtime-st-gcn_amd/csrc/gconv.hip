@@ -64,7 +64,9 @@ struct GGeom {
 };
 
 // ------------------------------------------------------------------ gather GEMM (fwd and data grad)
-template <typename T, int WM, int WN, int TM, int TN, int KC>
+// ACCV: accumulate (out +=) through the vectorised LDS-scratch epilogue; a separate instantiation so
+// the plain-store kernel keeps its register budget (<= 128 VGPRs: 2 blocks per CU)
+template <typename T, int WM, int WN, int TM, int TN, int KC, bool ACCV>
 __global__ __launch_bounds__(WM * WN * 64, 2) void gconv_kernel(const stgcn_gconv_desc a, const GGeom g) {
   typedef GL<T, KC> L;
   constexpr int NW = WM * WN, NT = NW * 64;
@@ -219,32 +221,77 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gconv_kernel(const stgcn_gcon
   }
 
   // ---------------------------------------------------------------- epilogue
+  // bias + BN partials on the fp32 accumulators.  accumulate: the values go through a per-wave LDS
+  // scratch (one 32x32 tile at a time) so that every lane read-modify-writes 16-B units of an output
+  // row instead of scattered 2/4-byte elements (a dependent load per element before its store).  The main loop's last barrier
+  // retired every read of the stage buffers, which the scratch reuses.
   T* __restrict__ out = reinterpret_cast<T*>(a.out);
   const long ldv = (long)a.out_ld * V;  // row stride between consecutive frames of joint jt
+  constexpr int SROW = 32 * (int)sizeof(T) + 16;  // padded scratch row (bytes)
+  constexpr int UR = 32 * (int)sizeof(T) / 16;     // 16-B units per 32-column row
+  char* scratch = smem + wave * 32 * SROW;
+  // measured: the scratch path pays off for the read-modify-write (accumulate) case only; plain stores
+  // stay scattered (fewer LDS round trips, lower register pressure)
+  constexpr bool vec_out = ACCV;  // launcher: ACCV only with accumulate and 16-B aligned rows
   Welford ws[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int col = n0 + (wn * TN + j) * 32 + lr;
+    const int c0 = n0 + (wn * TN + j) * 32;
+    const int col = c0 + lr;
     const bool cok = col < a.Cout;
     const float b1 = (a.bias && cok) ? a.bias[jt * a.Cout + col] : 0.f;
     float s = 0.f, cnt = 0.f;
+    if constexpr (!vec_out) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int lb = (wm * TM + i) * 32 + 4 * lh;
-      T* pb = out + ((long)(i0 + lb) * V + jt) * a.out_ld + col;
+      for (int i = 0; i < TM; ++i) {
+        const int lb = (wm * TM + i) * 32 + 4 * lh;
+        T* pb = out + ((long)(i0 + lb) * V + jt) * a.out_ld + col;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ro = (r & 3) + 8 * (r >> 2);
-        const bool ok = cok && lb + ro < rows_valid;
-        float v = acc[i][j][r] + b1;
-        if (ok) {
-          T* p = pb + ro * ldv;
-          if (a.accumulate) v += Tr<T>::to_f(*p);
-          *p = Tr<T>::from_f(v);
-          s += v;
-          cnt += 1.f;
+        for (int r = 0; r < 16; ++r) {
+          const int ro = (r & 3) + 8 * (r >> 2);
+          const bool ok = cok && lb + ro < rows_valid;
+          float v = acc[i][j][r] + b1;
+          if (ok) {
+            T* p = pb + ro * ldv;
+            if (a.accumulate) v += Tr<T>::to_f(*p);
+            *p = Tr<T>::from_f(v);
+            s += v;
+            cnt += 1.f;
+          }
+          acc[i][j][r] = v;
         }
-        acc[i][j][r] = v;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int rb = (wm * TM + i) * 32;  // tile's first row (frame index within the row tile)
+        const int lb = rb + 4 * lh;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ro = (r & 3) + 8 * (r >> 2);
+          const float v = acc[i][j][r] + b1;
+          acc[i][j][r] = v;
+          if (cok && lb + ro < rows_valid) {
+            s += v;
+            cnt += 1.f;
+          }
+          *reinterpret_cast<T*>(scratch + (4 * lh + ro) * SROW + lr * (int)sizeof(T)) = Tr<T>::from_f(v);
+        }
+        // 32 rows x UR units, lane -> (row, unit): 16-B read-modify-write of the output (wave-private
+        // scratch: no block barrier needed)
+#pragma unroll
+        for (int q = 0; q < 32 * UR / 64; ++q) {
+          const int idx = q * 64 + lane, row = idx / UR, u = idx % UR;
+          if (rb + row < rows_valid && c0 + u * VEC < a.Cout) {
+            T* p = out + ((long)(i0 + rb + row) * V + jt) * a.out_ld + c0 + u * VEC;
+            float f[VEC], o[VEC];
+            unpack16(*reinterpret_cast<const uint4*>(scratch + row * SROW + u * 16), f, (T*)nullptr);
+            unpack16(*reinterpret_cast<const uint4*>(p), o, (T*)nullptr);
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) f[e] += o[e];
+            *reinterpret_cast<uint4*>(p) = pack16(f, (T*)nullptr);
+          }
+        }
       }
     }
     Welford w;
@@ -294,6 +341,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gconv_kernel(const stgcn_gcon
 
 template <typename T, int WM, int WN, int TM, int TN, int KC>
 int launch_gconv(const stgcn_gconv_desc& a, hipStream_t s) {
+  constexpr int VEC = 16 / (int)sizeof(T);
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   typedef GL<T, KC> L;
   if (a.Cout_pad % BN || a.Cin_pad % KC) return STGCN_EBADSHAPE;
@@ -309,11 +357,19 @@ int launch_gconv(const stgcn_gconv_desc& a, hipStream_t s) {
   if (red > lds) lds = red;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gconv_kernel<T, WM, WN, TM, TN, KC>,
+    (void)hipFuncSetAttribute((const void*)gconv_kernel<T, WM, WN, TM, TN, KC, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)gconv_kernel<T, WM, WN, TM, TN, KC, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((gconv_kernel<T, WM, WN, TM, TN, KC>), dim3((unsigned)nblk), dim3(WM * WN * 64), lds, s, a, g);
+  const bool accv = a.accumulate && (a.out_ld % VEC) == 0 && (a.Cout % VEC) == 0;
+  if (accv)
+    hipLaunchKernelGGL((gconv_kernel<T, WM, WN, TM, TN, KC, true>), dim3((unsigned)nblk), dim3(WM * WN * 64), lds, s,
+                       a, g);
+  else
+    hipLaunchKernelGGL((gconv_kernel<T, WM, WN, TM, TN, KC, false>), dim3((unsigned)nblk), dim3(WM * WN * 64), lds,
+                       s, a, g);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
 

@@ -88,3 +88,29 @@ for name, N, T, V, Cin, Cout, Kt, s, pro in wcases:
     flops = 2.0 * N * T_out * V * Cin * Cout * Kt
     byts = (N * T * V * Cin + N * T_out * V * Cout) * 2
     print(f"{name:18s} {ms*1e3:9.1f} us  {flops/ms/1e9:8.1f} TFLOP/s  {byts/ms/1e6:8.1f} GB/s", flush=True)
+
+# joint-gathered graph conv (gconv.hip) on the PKU-MMD graph: fwd (S lists) and data grad (R lists),
+# algorithmic flops = 2 * N*T * nnz(support) * Cin * Cout
+A0 = torch.tensor(P.Graph(**P.PKU_MMD).A, dtype=torch.float32, device=dev)
+sup = K.GraphSupport(A0)
+gcases = [("gconv_fwd_c64", 64, 300, 64, 64), ("gconv_fwd_c128", 64, 150, 128, 128),
+          ("gconv_fwd_c256", 64, 75, 256, 256), ("gconv_fwd_64to128", 64, 300, 64, 128)]
+for name, N, T, Cin, Cout in gcases:
+    if only and not name.startswith(only):
+        continue
+    Pp, V = A0.shape[0], A0.shape[-1]
+    W = torch.randn(Pp * Cout, Cin, device=dev) / Cin ** 0.5
+    x = torch.randn(N, Cin, T, V, device=dev).to(dt).contiguous(memory_format=torch.channels_last)
+    dg = torch.randn(N, Cout, T, V, device=dev).to(dt).contiguous(memory_format=torch.channels_last)
+    wpk = K.gconv_weights(A0, W, sup, Cout, Cin, False, dt)
+    wT = K.gconv_weights(A0, W, sup, Cout, Cin, True, dt)
+    b2 = K.gcn_bias(A0, torch.randn(Pp * Cout, device=dev), N, Cout)
+    st = torch.zeros((K.gconv_row_blocks(N * T, V), wpk.shape[2], 4), device=dev)
+    flops = 2.0 * N * T * sup.nnz * Cin * Cout
+    byts = (N * T * V * (Cin + Cout)) * 2
+    for tag, f in (("", lambda: K.gconv(x, wpk, sup, Cin, Cout, bias=b2, stats=st)),
+                   ("_dgrad", lambda: K.gconv(dg, wT, sup, Cout, Cin, trans=True))):
+        ms = timeit(f)
+        print(f"{name + tag:22s} {ms*1e3:9.1f} us  {flops/ms/1e9:8.1f} TFLOP/s  {byts/ms/1e6:8.1f} GB/s", flush=True)
+    ms = timeit(lambda: K.gconv_wgrad(x, dg, sup, Cin, Cout))
+    print(f"{name.replace('fwd', 'wgrad'):22s} {ms*1e3:9.1f} us  {flops/ms/1e9:8.1f} TFLOP/s", flush=True)
