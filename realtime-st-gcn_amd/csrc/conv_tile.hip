@@ -671,10 +671,16 @@ int tile_debug_read(long long* host, long n) {
 // returns -1 when the shape is not handled here (caller falls back to conv_rows.hip)
 int conv_persist_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s);
 
+int conv_wide_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s);
+
 int conv_tile_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
   static const bool no_persist = getenv("STGCN_NO_PERSIST") != nullptr;  // A/B switch
   if (!no_persist) {  // weight-resident persistent kernel for the 64-channel Kt=9 convs
     const int r = conv_persist_launch(a, dtype, s);
+    if (r >= 0) return r;
+  }
+  {  // persistent register-tiled kernel for the >= 128-channel Kt=9 stride-1 convs (conv_wide.hip)
+    const int r = conv_wide_launch(a, dtype, s);
     if (r >= 0) return r;
   }
   const long mrb = conv_rows_num_row_blocks((long)a.N * a.T_out * a.V, a.Cout);

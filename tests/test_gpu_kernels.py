@@ -261,3 +261,32 @@ def test_bn_bwd_fused(K, dtype, tol, mode):
         assert_close(out2.float(), r.grad, tol, "dr")
     if mode == "identity":
         assert_close(out2.float(), x.grad, tol, "dx")
+
+
+@pytest.mark.parametrize("cin,cout,T,N", [(128, 128, 37, 3), (256, 256, 23, 2), (128, 256, 16, 3), (256, 128, 150, 2)])
+def test_conv_wide_prologue_stats(K, cin, cout, T, N):
+    """The >= 128-channel Kt=9 stride-1 convs (conv_wide.hip, bf16): BN1+ReLU prologue, bias, BN2 partial
+    statistics, and the transposed conv (data gradient), against torch fp32."""
+    torch.manual_seed(3)
+    V = 25
+    x = torch.randn(N, cin, T, V) * 1.5 + 0.5
+    sc, sh = torch.rand(cin) + 0.5, torch.randn(cin)
+    w = torch.randn(cout, cin, 9, 1) / (cin * 9) ** 0.5
+    b = torch.randn(cout)
+    h = torch.relu(x * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1))
+    ref = F.conv2d(h, w, b, padding=(4, 0))
+    wp, cp, kp = K.pack_weight(w.squeeze(-1).permute(2, 0, 1).to(DEV), torch.bfloat16)
+    st = torch.zeros((K.row_blocks(N * T * V, cout), cp, 4), device=DEV)
+    y = K.conv_rows(cl(x, torch.bfloat16), wp, cin, cout, cp, kp, T, T, Kt=9, pad=4, bias=b.to(DEV), pro=1,
+                    pro_a=sc.to(DEV), pro_b=sh.to(DEV), stats=st)
+    assert_close(y.float(), ref, 2e-2, "wide conv+prologue")
+    mr, _, _ = K.bn_finalize(st, st.shape[0], cp, cout, None, None)
+    yr = y.float().cpu()
+    assert_close(mr[:, 0].cpu(), yr.mean(dim=(0, 2, 3)), 2e-3, "bn mean")
+    assert_close(mr[:, 1].cpu(), 1 / torch.sqrt(yr.var(dim=(0, 2, 3), unbiased=False) + 1e-5), 2e-3, "bn rstd")
+    dy = torch.randn(ref.shape)
+    xr = x.clone().requires_grad_(True)
+    F.conv2d(xr, w, None, padding=(4, 0)).backward(dy)
+    wtp, cq, kq = K.pack_weight(w.squeeze(-1).permute(2, 1, 0).to(DEV), torch.bfloat16)
+    dx = K.conv_rows(cl(dy, torch.bfloat16), wtp, cout, cin, cq, kq, T, T, Kt=9, pad=4, trans=True)
+    assert_close(dx.float(), xr.grad, 2e-2, "wide conv trans")
