@@ -42,6 +42,8 @@ typedef struct {
   int N, T_in, T_out, V, Cin, Cout, Cin_pad, Cout_pad;
   int Kt, stride, pad, trans, pro, bias_mode, accumulate;
   int in_ld, out_ld;
+  const void* w_frag;     /* optional: the same weights as an MFMA-fragment image (stgcn_pack_weight_frag);
+                           * the wide-channel Kt = 9 kernel runs only when it is given (NULL: other kernels) */
 } stgcn_conv_desc;
 
 int stgcn_conv_rows(const stgcn_conv_desc* d, int dtype, void* stream);
@@ -49,6 +51,11 @@ int stgcn_conv_rows(const stgcn_conv_desc* d, int dtype, void* stream);
  * into the zero-padded contiguous [Kt][Cout_pad][Cin_pad] dtype image stgcn_conv_rows reads. */
 int stgcn_pack_weight(const float* src, long s0, long s1, long s2, int Kt, int Cout, int Cin, void* dst, int Cout_pad,
                       int Cin_pad, int dtype, void* stream);
+/* stgcn_pack_weight plus the MFMA-fragment image dst_frag (same element count; Cout_pad % 32 == 0,
+ * Cin_pad % 16 == 0): 1-KiB blocks [k][co/32][ci/16], lane (ci%16)/8*32 + co%32 holding 8 consecutive ci,
+ * so one 32x32x16 B fragment is one contiguous wave load (conv_wide.hip). */
+int stgcn_pack_weight_frag(const float* src, long s0, long s1, long s2, int Kt, int Cout, int Cin, void* dst,
+                           void* dst_frag, int Cout_pad, int Cin_pad, int dtype, void* stream);
 /* column tile the packed weights must be padded to (Cout_pad % tile == 0) */
 int stgcn_conv_rows_col_tile(int cout);
 /* upper bound on row blocks (first dim of the BN partial-stat buffer, which the caller zero-fills) */

@@ -25,7 +25,8 @@ class ConvDesc(ctypes.Structure):
     _fields_ = [("in_", c_void_p), ("out", c_void_p), ("w", c_void_p), ("bias", c_void_p), ("pro_a", c_void_p),
                 ("pro_b", c_void_p), ("pro_stats", c_void_p), ("stats", c_void_p)] + \
                [(n, c_int) for n in ("N", "T_in", "T_out", "V", "Cin", "Cout", "Cin_pad", "Cout_pad", "Kt", "stride",
-                                     "pad", "trans", "pro", "bias_mode", "accumulate", "in_ld", "out_ld")]
+                                     "pad", "trans", "pro", "bias_mode", "accumulate", "in_ld", "out_ld")] + \
+               [("w_frag", c_void_p)]
 
 
 class WgradDesc(ctypes.Structure):
@@ -85,6 +86,8 @@ _SIGS = {
     "stgcn_gcn_bias_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "stgcn_pack_weight": (c_int, [c_void_p, ctypes.c_long, ctypes.c_long, ctypes.c_long, c_int, c_int, c_int,
                                   c_void_p, c_int, c_int, c_int, c_void_p]),
+    "stgcn_pack_weight_frag": (c_int, [c_void_p, ctypes.c_long, ctypes.c_long, ctypes.c_long, c_int, c_int, c_int,
+                                       c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "stgcn_amix_dA_workspace": (ctypes.c_long, [ctypes.POINTER(AmixDesc)]),
     "stgcn_amix_dA": (c_int, [ctypes.POINTER(AmixDesc), c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "stgcn_gcn_bias": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p]),

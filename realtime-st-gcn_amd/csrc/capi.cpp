@@ -16,7 +16,7 @@ typedef stgcn_amix_desc AmixArgs;
 int conv_rows_launch(const ConvArgs& a, int dtype, hipStream_t s);
 int conv_rows_bn_tile(int cout);
 int pack_weight_launch(const float* src, long s0, long s1, long s2, int Kt, int Co, int Ci, void* dst, int cp, int kp,
-                       int dtype, hipStream_t s);
+                       int dtype, hipStream_t s, void* dst_frag);
 long conv_rows_num_row_blocks(long M, int cout);
 int conv_wgrad_launch(WgradArgs a, int dtype, hipStream_t s);
 long wgrad_tile_workspace(const WgradArgs& a, int dtype);
@@ -103,7 +103,13 @@ int stgcn_pack_weight(const float* src, long s0, long s1, long s2, int Kt, int C
                       int Cin_pad, int dtype, void* stream) {
   CHECK_DTYPE(dtype);
   if (!src || !dst || Kt <= 0 || Co <= 0 || Ci <= 0 || Cout_pad < Co || Cin_pad < Ci) return STGCN_EBADSHAPE;
-  return pack_weight_launch(src, s0, s1, s2, Kt, Co, Ci, dst, Cout_pad, Cin_pad, dtype, STREAM(stream));
+  return pack_weight_launch(src, s0, s1, s2, Kt, Co, Ci, dst, Cout_pad, Cin_pad, dtype, STREAM(stream), nullptr);
+}
+int stgcn_pack_weight_frag(const float* src, long s0, long s1, long s2, int Kt, int Co, int Ci, void* dst,
+                           void* dst_frag, int Cout_pad, int Cin_pad, int dtype, void* stream) {
+  CHECK_DTYPE(dtype);
+  if (!src || !dst || !dst_frag || Kt <= 0 || Co <= 0 || Ci <= 0 || Cout_pad < Co || Cin_pad < Ci) return STGCN_EBADSHAPE;
+  return pack_weight_launch(src, s0, s1, s2, Kt, Co, Ci, dst, Cout_pad, Cin_pad, dtype, STREAM(stream), dst_frag);
 }
 long stgcn_conv_rows_row_blocks(long M, int cout) { return conv_rows_num_row_blocks(M, cout); }
 
@@ -305,3 +311,5 @@ int persist_debug_read(long long* host, long n);
 extern "C" int stgcn_debug_persist_timers(long long* host, long n) { return persist_debug_read(host, n); }
 int tile_debug_read(long long* host, long n);
 extern "C" int stgcn_debug_tile_timers(long long* host, long n) { return tile_debug_read(host, n); }
+int wide_debug_read(long long* host, long n);
+extern "C" int stgcn_debug_wide_timers(long long* host, long n) { return wide_debug_read(host, n); }

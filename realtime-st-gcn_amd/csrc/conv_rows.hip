@@ -319,7 +319,7 @@ int launch_conv(const ConvArgs& a, hipStream_t s) {
 // fp32 parameter (permuted / transposed) packs in one pass
 template <typename T>
 __global__ void pack_weight_kernel(const float* __restrict__ src, long s0, long s1, long s2, int Co, int Ci, int cp,
-                                   int kp, long total, T* __restrict__ dst) {
+                                   int kp, long total, T* __restrict__ dst, T* __restrict__ dst_frag) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const int ci = (int)(i % kp);
@@ -328,20 +328,28 @@ __global__ void pack_weight_kernel(const float* __restrict__ src, long s0, long 
   const long k = r / cp;
   const float v = (co < Co && ci < Ci) ? src[k * s0 + co * s1 + ci * s2] : 0.f;
   dst[i] = Tr<T>::from_f(v);
+  if (dst_frag) {
+    // MFMA-fragment image (conv_wide.hip): 1-KiB blocks [k][co/32][ci/16], lane l = (ci%16)/8*32 + co%32
+    // holding 8 consecutive ci: a wave's B fragment is one contiguous 1-KiB load
+    const long blk = ((long)k * (cp / 32) + co / 32) * (kp / 16) + ci / 16;
+    const int l = ((ci & 15) >> 3) * 32 + (co & 31);
+    dst_frag[blk * 512 + l * 8 + (ci & 7)] = Tr<T>::from_f(v);
+  }
 }
 
 }  // namespace
 
 int pack_weight_launch(const float* src, long s0, long s1, long s2, int Kt, int Co, int Ci, void* dst, int cp, int kp,
-                       int dtype, hipStream_t s) {
+                       int dtype, hipStream_t s, void* dst_frag) {
   const long total = (long)Kt * cp * kp;
   const unsigned blocks = (unsigned)((total + 255) / 256);
+  if (dst_frag && (cp % 32 || kp % 16)) return STGCN_EBADSHAPE;
   if (dtype == 1)
     hipLaunchKernelGGL(pack_weight_kernel<bf16>, dim3(blocks), dim3(256), 0, s, src, s0, s1, s2, Co, Ci, cp, kp, total,
-                       (bf16*)dst);
+                       (bf16*)dst, (bf16*)dst_frag);
   else
     hipLaunchKernelGGL(pack_weight_kernel<float>, dim3(blocks), dim3(256), 0, s, src, s0, s1, s2, Co, Ci, cp, kp,
-                       total, (float*)dst);
+                       total, (float*)dst, (float*)dst_frag);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
 

@@ -40,8 +40,8 @@ constexpr int WM = 2, WN = 2, TM = 4;
 constexpr int RSA = KG * 2 + 16;     // padded halo row bytes (144)
 constexpr int HR_CAP = 456;          // max halo rows per item (V = 25: 18 frames x 25 = 450)
 constexpr int NA = (HR_CAP * 8 + NT - 1) / NT;  // 16-B halo units per thread (15)
-constexpr int RSO = 128 * 2 + 16;                 // epilogue tile image row bytes (BN = 128 bf16, padded)
-constexpr int ABYTES_MIN = 256 * RSO;             // LDS halo buffer (>= NA*32 halo rows of RSA bytes) = tile image
+constexpr int CSO = 256 * 2 + 8;                  // column bytes of the column-major output tile image (256 rows)
+constexpr int ABYTES_MIN = (128 * CSO > NA * 32 * RSA ? 128 * CSO : NA * 32 * RSA);  // halo buffer / tile image
 constexpr int LDS_MAX = 160 * 1024;
 
 // compile-time loop: f.template operator()<I>() for I = 0..N-1 (guaranteed unrolled; register arrays
@@ -65,6 +65,7 @@ struct WGeom {
   int G;        // 64-channel items per tile (even)
   int HR;       // halo rows per item ((F + 8) * V)
   int abytes;   // bytes per LDS halo buffer
+  long long* dbg;  // DBG & 4: per-block phase cycles [block][16]
 };
 
 struct TileInfo {
@@ -81,22 +82,27 @@ DEV TileInfo tile_info(int tile, const WGeom& g, int T_out) {
   return ti;
 }
 
-// DBG (diagnostic instantiations, STGCN_WIDE_DBG=<bits>, results wrong): bit0 contiguous 1-KiB B fragments
-// (layout probe), bit1 no halo LDS writes, bit2 no epilogue
+// Block = 8 waves in two roles (wave-uniform branch; both roles execute the same barrier sequence):
+//   MMA waves 0-3 (wm = w>>1, wn = w&1): B-fragment ring + LDS A fragments + MFMAs only, so their
+//     vmcnt never waits on anything but L2-resident weights;
+//   helper waves 4-7: stage the NEXT item's halo (global loads -> prologue -> LDS) and drain finished
+//     output tiles (LDS image -> 16-B row stores, BN partials -> global), i.e. all HBM traffic.
+// Per item k (buffer b = k & 1): MMA computes item k from buf b while the helpers fill buf b^1 with
+// item k+1; barrier E_k.  At a tile end the MMA waves dump acc (+ bias) as a column-major bf16 image
+// into buf b (8-B ds_write_b64 per 4 rows) and their Welford partials into sRed; barrier I_k; the
+// helpers drain that image during item k+1 before they overwrite buf b with item k+2's halo.
+// DBG (diagnostic instantiations, STGCN_WIDE_DBG=<bits>): bit1 no helper work (results wrong), bit2 phase
+// timers (s_memtime of MMA wave 0 / helper wave 4 into g.dbg)
 template <int BN, int NBUF, int PRO, int DBG = 0>
-__global__ __launch_bounds__(NT, 1) void conv_wide_kernel(const stgcn_conv_desc a, const WGeom g) {
+__global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_desc a, const WGeom g) {
   constexpr int TN = BN / 64;
   constexpr int LEAD = NBUF - 1;
   constexpr int PAIR = 2 * SPI;  // k-steps per item pair
   static_assert(PAIR % NBUF == 0, "B register ring must divide the pair");
-  constexpr int SA = LEAD + 2;   // first k-step that writes the next halo (its loads issued at k-step 0)
-  constexpr int NST = 5;         // k-steps the halo writes are spread over
-  constexpr int UPS = (NA + NST - 1) / NST;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int lr = lane & 31, lh = lane >> 5;
+  const bool mma = wave < 4;
   const int V = a.V;
   const int grid = gridDim.x;
   const int ntile_b = (g.ntiles - (int)blockIdx.x + grid - 1) / grid;
@@ -104,93 +110,188 @@ __global__ __launch_bounds__(NT, 1) void conv_wide_kernel(const stgcn_conv_desc 
   const int nitems = ntile_b * g.G;
 
   const bf16* __restrict__ in = reinterpret_cast<const bf16*>(a.in);
-  const bf16* __restrict__ wp = reinterpret_cast<const bf16*>(a.w);
+  const bf16* __restrict__ wp = reinterpret_cast<const bf16*>(a.w_frag);
   char* const sA0 = smem;
   char* const sA1 = smem + g.abytes;
   float4* const sRed = reinterpret_cast<float4*>(smem + 2 * g.abytes);  // [WM][BN]
 
-  // Items past the block's last one are clamped to it: their loads are issued (keeps the unrolled
-  // k-step body branch-free) and their halo writes land in a buffer nobody reads again.
-  auto item_tile = [&](int w, int& gi) {
+  auto item_tile = [&](int w, int& gi) {  // items past the block's last one are clamped to it
     w = min(w, nitems - 1);
     const int tl = w / g.G;
     gi = w - tl * g.G;
     return (int)blockIdx.x + tl * grid;
   };
+  auto tile_end = [&](int w) { return w < nitems && (w % g.G) == g.G - 1; };
+  long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
+  auto tmark = [&](int slot) {  // accumulate cycles since the previous mark into slot
+    if constexpr ((DBG & 4) != 0) {
+      const long long t = (long long)__builtin_amdgcn_s_memtime();
+      if (slot >= 0) tacc[slot] += t - tlast;
+      tlast = t;
+    }
+  };
+  auto tflush = [&](int base) {
+    if constexpr ((DBG & 4) != 0) {
+      if ((tid & 63) == 0)
+        for (int q = 0; q < 8; ++q) g.dbg[(long)blockIdx.x * 16 + base + q] = tacc[q];
+    }
+  };
 
-  // ---- B fragment addressing: lane (lr, lh) of frag j at k-step (t, ks) of item (ct, gi) reads
-  // w[t][ct*BN + (wn*TN + j)*32 + lr][gi*64 + ks*16 + lh*8 .. +8]
-  const int kcc = a.Cout_pad * a.Cin_pad;
-  const int wlane = (DBG & 1) ? lane * 8 + wn * 4096 : ((wn * TN) * 32 + lr) * a.Cin_pad + lh * 8;
+  if (!mma) {
+    // =============================== helper waves ===============================
+    const int htid = tid - NT;
+    const int ucol = htid & 7, row0u = htid >> 3;
+    int a_lo = 0, a_hi = 0;
+    uint4 ra[NA];
+    float sc[8], sh[8];
+    auto issue_A = [&](int w) {  // item w's halo units -> registers
+      int gi;
+      const int tile = item_tile(w, gi);
+      const TileInfo ti = tile_info(tile, g, a.T_out);
+      const int fi0 = ti.f0 - (KT - 1) / 2;
+      a_lo = max(0, -fi0) * V;
+      a_hi = min(g.HR, (a.T_in - fi0) * V);
+      const bf16* base = in + ((long)ti.n * a.T_in + fi0) * V * a.in_ld + gi * KG + ucol * 8;
+      static_for<NA>([&]<int i>() {
+        const int row = min(max(row0u + 32 * i, a_lo), a_hi - 1);
+        ra[i] = *reinterpret_cast<const uint4*>(base + row * a.in_ld);
+      });
+      if (PRO == 1) {
+        const int c = gi * KG + ucol * 8;
+        const float4 s0 = *reinterpret_cast<const float4*>(a.pro_a + c);
+        const float4 s1 = *reinterpret_cast<const float4*>(a.pro_a + c + 4);
+        const float4 h0 = *reinterpret_cast<const float4*>(a.pro_b + c);
+        const float4 h1 = *reinterpret_cast<const float4*>(a.pro_b + c + 4);
+        sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
+        sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+        sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w;
+        sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
+      }
+    };
+    auto store_A = [&](char* buf) {  // prologue (BN1 scale/shift + ReLU) + zero rows -> LDS halo buffer
+      static_for<NA>([&]<int i>() {
+        const int row = row0u + 32 * i;
+        uint4 v = ra[i];
+        if (PRO == 1) {
+          float f[8];
+          unpack16(v, f, (bf16*)nullptr);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], sc[j], sh[j]), 0.f);
+          v = pack16(f, (bf16*)nullptr);
+        }
+        const bool ok = row >= a_lo && row < a_hi;
+        v.x = ok ? v.x : 0u;
+        v.y = ok ? v.y : 0u;
+        v.z = ok ? v.z : 0u;
+        v.w = ok ? v.w : 0u;
+        *reinterpret_cast<uint4*>(buf + row * RSA + ucol * 16) = v;
+      });
+    };
+    // finished tile image (column-major [BN][CSO bytes]) -> global rows; BN partials -> global
+    auto drain = [&](int w, const char* img) {
+      int gi;
+      const int tile = item_tile(w, gi);
+      const TileInfo ti = tile_info(tile, g, a.T_out);
+      const int rows_valid = ti.fe * V;
+      const int n0 = ti.ct * BN;
+      if (a.stats) {
+        const int rt = tile / g.ncol;
+        for (int c = htid; c < BN; c += NT) {
+          const float4 f0 = sRed[c], f1 = sRed[BN + c];
+          const Welford wv = welford_merge(Welford{f0.x, f0.y, f0.z}, Welford{f1.x, f1.y, f1.z});
+          if (n0 + c < a.Cout_pad)
+            reinterpret_cast<float4*>(a.stats)[(long)rt * a.Cout_pad + n0 + c] = make_float4(wv.n, wv.mean, wv.m2, 0.f);
+        }
+      }
+      // lane = row quad (4 rows), helper wave h = 8-channel units 4h..4h+3: per unit, 8 conflict-free
+      // ds_read_b64 (4 rows of one column each) are transposed in registers into 4 row units of 16 B
+      bf16* __restrict__ outb = reinterpret_cast<bf16*>(a.out) + ((long)ti.n * a.T_out + ti.f0) * V * (long)a.out_ld;
+      const int rq = htid & 63, hw = htid >> 6;
+      if (4 * rq >= rows_valid) return;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int cu = hw * 4 + k;
+        if (n0 + cu * 8 >= a.Cout) continue;
+        uint2 col[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) col[c] = *reinterpret_cast<const uint2*>(img + (cu * 8 + c) * CSO + rq * 8);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int rl = 4 * rq + e;
+          if (rl >= rows_valid) break;
+          // row e of the quad: low/high halves of dword e>>1 of each column
+          const unsigned sel = (e & 1) ? 0x07060302u : 0x05040100u;
+          uint4 u;
+          u.x = __builtin_amdgcn_perm((e >> 1) ? col[1].y : col[1].x, (e >> 1) ? col[0].y : col[0].x, sel);
+          u.y = __builtin_amdgcn_perm((e >> 1) ? col[3].y : col[3].x, (e >> 1) ? col[2].y : col[2].x, sel);
+          u.z = __builtin_amdgcn_perm((e >> 1) ? col[5].y : col[5].x, (e >> 1) ? col[4].y : col[4].x, sel);
+          u.w = __builtin_amdgcn_perm((e >> 1) ? col[7].y : col[7].x, (e >> 1) ? col[6].y : col[6].x, sel);
+          bf16* p = outb + (long)rl * a.out_ld + n0 + cu * 8;
+          if (a.accumulate) {
+            float f[8], o[8];
+            unpack16(u, f, (bf16*)nullptr);
+            unpack16(*reinterpret_cast<const uint4*>(p), o, (bf16*)nullptr);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) f[q] += o[q];
+            u = pack16(f, (bf16*)nullptr);
+          }
+          *reinterpret_cast<uint4*>(p) = u;
+        }
+      }
+    };
+
+    // loads run one item ahead of the LDS writes: item w+2's halo is requested right after item w+1's
+    // is written (window w), so a whole item of MMA time covers its HBM latency
+    issue_A(0);
+    store_A(sA0);
+    if (nitems > 1) issue_A(1);
+    lds_barrier();  // P
+    tmark(-1);
+    for (int w = 0; w < nitems; ++w) {
+      char* const nb = (w & 1) ? sA0 : sA1;  // buffer of item w + 1
+      if ((DBG & 2) == 0) {
+        if (w > 0 && tile_end(w - 1)) drain(w - 1, nb);
+        tmark(0);
+        if (w + 1 < nitems) store_A(nb);
+        tmark(1);
+        if (w + 2 < nitems) issue_A(w + 2);
+        tmark(2);
+      }
+      lds_barrier();  // E_w
+      tmark(3);
+      if (tile_end(w)) lds_barrier();  // I_w
+      tmark(4);
+    }
+    if ((DBG & 2) == 0) drain(nitems - 1, ((nitems - 1) & 1) ? sA1 : sA0);
+    tmark(5);
+    if (wave == 4) tflush(8);
+    return;
+  }
+
+  // =============================== MMA waves ===============================
+  const int wm = wave >> 1, wn = wave & 1;
+  const int lr = lane & 31, lh = lane >> 5;
+  // B fragment j at k-step (t, ks) of item (ct, gi): the contiguous 1-KiB block
+  // [t][c32 = ct*BN/32 + wn*TN + j][k16 = gi*4 + ks] of the fragment image (stgcn_pack_weight_frag)
+  const int c32n = a.Cout_pad / 32, k16n = a.Cin_pad / 16;
+  const int kcc = c32n * k16n * 512;  // elements per tap
+  const int wnu = __builtin_amdgcn_readfirstlane(wn);
+  const int wlane = lane * 8;
   auto item_woff = [&](int w) {
     int gi;
     const int tile = item_tile(w, gi);
-    return (tile % g.ncol) * BN * a.Cin_pad + gi * KG;
+    return ((tile % g.ncol) * (BN / 32) + wnu * TN) * k16n * 512 + gi * KS * 512;
   };
   bf16x8 fb[NBUF][TN];
-  auto load_B = [&](bf16x8 (&dst)[TN], int hs, int woff, int wl, int kc, int cinp) {
+  auto load_B = [&](bf16x8 (&dst)[TN], int hs, int woff, int wl, int kc, int k16) {
     const int t = hs / KS, ks = hs % KS;
-    const bf16* p = wp + (t * kc + woff + ks * 16) + wl;
+    const bf16* p = wp + (t * kc + woff + ks * 512) + wl;
 #pragma unroll
     for (int j = 0; j < TN; ++j)
-      dst[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(p + j * 32 * cinp));
+      dst[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(p + j * k16 * 512));
   };
-
-  // ---- halo staging of the NEXT item: unit i of this thread = halo row tid/8 + 32 i, 16-B column tid%8.
-  // Rows outside [lo, hi) (frames outside [0, T_in), rows past the halo) are written as zeros; their
-  // load address is clamped into the valid range.
-  const int ucol = tid & 7, row0u = tid >> 3;
-  const bf16* a_base = in;  // element (row 0 of the halo, channel 0) of the staged item
-  int a_lo = 0, a_hi = 0;
-  uint4 ra[NA];
-  float sc[8], sh[8];
-  auto issue_A = [&](int w) {
-    int gi;
-    const int tile = item_tile(w, gi);
-    const TileInfo ti = tile_info(tile, g, a.T_out);
-    const int fi0 = ti.f0 - (KT - 1) / 2;
-    a_lo = max(0, -fi0) * V;
-    a_hi = min(g.HR, (a.T_in - fi0) * V);
-    a_base = in + ((long)ti.n * a.T_in + fi0) * V * a.in_ld + gi * KG + ucol * 8;
-    static_for<NA>([&]<int i>() {
-      const int row = min(max(row0u + 32 * i, a_lo), a_hi - 1);
-      ra[i] = *reinterpret_cast<const uint4*>(a_base + row * a.in_ld);
-    });
-    if (PRO == 1) {
-      const int c = gi * KG + ucol * 8;
-      const float4 s0 = *reinterpret_cast<const float4*>(a.pro_a + c);
-      const float4 s1 = *reinterpret_cast<const float4*>(a.pro_a + c + 4);
-      const float4 h0 = *reinterpret_cast<const float4*>(a.pro_b + c);
-      const float4 h1 = *reinterpret_cast<const float4*>(a.pro_b + c + 4);
-      sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
-      sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
-      sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w;
-      sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
-    }
-  };
-  auto store_A = [&]<int i0, int i1>(char* buf) {  // units [i0, i1) -> LDS halo buffer
-    static_for<NA>([&]<int i>() {
-      if constexpr (i < i0 || i >= i1) return;
-      const int row = row0u + 32 * i;
-      uint4 v = ra[i];
-      if (PRO == 1) {
-        float f[8];
-        unpack16(v, f, (bf16*)nullptr);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], sc[j], sh[j]), 0.f);
-        v = pack16(f, (bf16*)nullptr);
-      }
-      const bool ok = row >= a_lo && row < a_hi;
-      v.x = ok ? v.x : 0u;
-      v.y = ok ? v.y : 0u;
-      v.z = ok ? v.z : 0u;
-      v.w = ok ? v.w : 0u;
-      *reinterpret_cast<uint4*>(buf + row * RSA + ucol * 16) = v;
-    });
-  };
-
-  // ---- A fragment rows: MFMA row r = (wm*TM + i)*32 + lr reads halo row r + q(dt)*V (padding rows of
-  // the 256-row MFMA tile past F*V read row 0: in range, never stored)
+  // A fragment rows: MFMA row r = (wm*TM + i)*32 + lr reads halo row r + q(dt)*V (padding rows of the
+  // 256-row MFMA tile past F*V read row 0: in range, never stored)
   int a_frag[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -207,95 +308,76 @@ __global__ __launch_bounds__(NT, 1) void conv_wide_kernel(const stgcn_conv_desc 
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  // ---- epilogue of a finished tile (called after a barrier; the halo buffer sA1 is free): acc + bias
-  // -> bf16 tile image in sA1 (rows of BN channels, padded) -> 16-B row stores; BatchNorm Welford
-  // partials per (tile, channel) from the fp32 values (two passes over the registers).
-  auto epilogue = [&](int tile) {
+  // tile end: acc + bias -> column-major bf16 image (4 consecutive rows of one column per ds_write_b64)
+  // and per-column Welford partials of the fp32 values -> sRed; acc reset
+  // bias of the current tile's columns, loaded at its first pair (a load issued in the dump itself
+  // would wait behind the whole in-flight B ring: loads retire in order)
+  float bias_r[TN];
+  auto load_bias = [&](int w) {
+    int gi;
+    const int n0 = (item_tile(w, gi) % g.ncol) * BN;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + (wn * TN + j) * 32 + lr;
+      bias_r[j] = (a.bias_mode == 1 && col < a.Cout) ? a.bias[col] : 0.f;
+    }
+  };
+  auto dump = [&](int w, char* img) {
+    int gi;
+    const int tile = item_tile(w, gi);
     const TileInfo ti = tile_info(tile, g, a.T_out);
     const int rows_valid = ti.fe * V;
     const int n0 = ti.ct * BN;
-    Welford ws[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int cl = (wn * TN + j) * 32 + lr;  // column within the tile
+      const int cl = (wn * TN + j) * 32 + lr;
       const bool cok = n0 + cl < a.Cout;
-      const float b1 = (a.bias_mode == 1 && cok) ? a.bias[n0 + cl] : 0.f;
-      float sum = 0.f, cnt = 0.f;
-      int lim1 = cok ? rows_valid - 4 * lh : 0;
-      asm volatile("" : "+v"(lim1));
+      const float b1 = bias_r[j];
+      // single pass: statistics of v = acc + b1 shifted by b1 (s1 = sum acc, s2 = sum acc^2 over valid
+      // rows); row masks only in the 32-row blocks that cross rows_valid (wave-uniform test)
+      float s1 = 0.f, s2 = 0.f, cnt = 0.f;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int rl = (wm * TM + i) * 32 + 4 * lh + (r & 3) + 8 * (r >> 2);
-          const float v = acc[i][j][r] + b1;
-          acc[i][j][r] = v;
-          const bool ok = (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) < lim1;
-          sum += ok ? v : 0.f;
-          cnt += ok ? 1.f : 0.f;
-          *reinterpret_cast<bf16*>(sA1 + rl * RSO + cl * 2) = (bf16)v;
-        }
-      }
-      Welford w;
-      w.n = cnt;
-      w.mean = cnt > 0.f ? sum / cnt : 0.f;
-      float m2 = 0.f;
-      if (a.stats) {
-        // row limit re-derived per lane (opaque to CSE: the 16 x TM row masks of the first pass
-        // would otherwise be kept alive in SGPR pairs and spill)
-        int lim = cok ? rows_valid - 4 * lh : 0;
-        asm volatile("" : "+v"(lim));
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
+        const int rb = (wm * TM + i) * 32;
+        if (rb + 32 <= rows_valid) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const int rr = (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2);
-            const float d = acc[i][j][r] - w.mean;
-            m2 += rr < lim ? d * d : 0.f;
+            s1 += acc[i][j][r];
+            s2 = fmaf(acc[i][j][r], acc[i][j][r], s2);
+          }
+          cnt += 16.f;
+        } else if (rb < rows_valid) {
+          const int lim = rows_valid - rb - 4 * lh;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const bool ok = (r & 3) + 8 * (r >> 2) < lim;
+            const float d = ok ? acc[i][j][r] : 0.f;
+            s1 += d;
+            s2 = fmaf(d, d, s2);
+            cnt += ok ? 1.f : 0.f;
           }
         }
-      }
-      w.m2 = m2;
-      ws[j] = w;
-    }
-    if (a.stats) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
+        for (int q = 0; q < 4; ++q) {
+          bf16x4 pk;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) pk[e] = (bf16)(acc[i][j][4 * q + e] + b1);
+          *reinterpret_cast<bf16x4*>(img + cl * CSO + (rb + 4 * lh + 8 * q) * 2) = pk;
+        }
+      }
+      if (a.stats) {
+        Welford wv;
+        wv.n = cok ? cnt : 0.f;
+        const float mu = wv.n > 0.f ? s1 / wv.n : 0.f;
+        wv.mean = b1 + mu;
+        wv.m2 = wv.n > 0.f ? fmaxf(s2 - s1 * mu, 0.f) : 0.f;
         Welford o;
-        o.n = __shfl_xor(ws[j].n, 32);
-        o.mean = __shfl_xor(ws[j].mean, 32);
-        o.m2 = __shfl_xor(ws[j].m2, 32);
-        const Welford w = welford_merge(ws[j], o);
-        if (lh == 0) sRed[wm * BN + (wn * TN + j) * 32 + lr] = make_float4(w.n, w.mean, w.m2, 0.f);
+        o.n = __shfl_xor(wv.n, 32);
+        o.mean = __shfl_xor(wv.mean, 32);
+        o.m2 = __shfl_xor(wv.m2, 32);
+        const Welford m = welford_merge(wv, o);
+        if (lh == 0) sRed[wm * BN + cl] = make_float4(m.n, m.mean, m.m2, 0.f);
       }
-    }
-    __syncthreads();
-    if (a.stats) {
-      const int rt = tile / g.ncol;
-      for (int c = tid; c < BN; c += NT) {
-        const float4 f0 = sRed[c], f1 = sRed[BN + c];
-        const Welford w = welford_merge(Welford{f0.x, f0.y, f0.z}, Welford{f1.x, f1.y, f1.z});
-        if (n0 + c < a.Cout_pad)
-          reinterpret_cast<float4*>(a.stats)[(long)rt * a.Cout_pad + n0 + c] = make_float4(w.n, w.mean, w.m2, 0.f);
-      }
-    }
-    // rows -> global: 16 threads per row (16 B each), 16 rows per pass
-    bf16* __restrict__ outb = reinterpret_cast<bf16*>(a.out) + ((long)ti.n * a.T_out + ti.f0) * V * (long)a.out_ld;
-    const int cu = tid & 15, r0 = tid >> 4;
-    const bool cvalid = n0 + cu * 8 < a.Cout;
-    for (int rl = r0; rl < rows_valid; rl += NT / 16) {
-      uint4 v = *reinterpret_cast<const uint4*>(sA1 + rl * RSO + cu * 16);
-      bf16* p = outb + (long)rl * a.out_ld + n0 + cu * 8;
-      if (!cvalid) continue;
-      if (a.accumulate) {
-        float f[8], o[8];
-        unpack16(v, f, (bf16*)nullptr);
-        unpack16(*reinterpret_cast<const uint4*>(p), o, (bf16*)nullptr);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] += o[e];
-        v = pack16(f, (bf16*)nullptr);
-      }
-      *reinterpret_cast<uint4*>(p) = v;
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -305,15 +387,12 @@ __global__ __launch_bounds__(NT, 1) void conv_wide_kernel(const stgcn_conv_desc 
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   };
 
-  // ---- prologue: halo of item 0 staged synchronously; B of its first LEAD k-steps in flight
-  issue_A(0);
-  store_A.template operator()<0, NA>(sA0);
   {
     const int w0 = item_woff(0);
 #pragma unroll
-    for (int hs = 0; hs < LEAD; ++hs) load_B(fb[hs % NBUF], hs, w0, wlane, kcc, a.Cin_pad);
+    for (int hs = 0; hs < LEAD; ++hs) load_B(fb[hs % NBUF], hs, w0, wlane, kcc, k16n);
   }
-  __syncthreads();
+  lds_barrier();  // P
 
   const int qsign = a.trans ? -1 : 1;
   const int qbase = a.trans ? KT - 1 : 0;
@@ -329,7 +408,7 @@ __global__ __launch_bounds__(NT, 1) void conv_wide_kernel(const stgcn_conv_desc 
     }
     int wl = wlane;
     asm volatile("" : "+v"(wl));
-    int tbytes = tap_bytes, kcc_l = kcc, cinp_l = a.Cin_pad;
+    int tbytes = tap_bytes, kcc_l = kcc, cinp_l = k16n;
     asm volatile("" : "+s"(tbytes));
     asm volatile("" : "+s"(kcc_l));
     asm volatile("" : "+s"(cinp_l));
@@ -338,58 +417,64 @@ __global__ __launch_bounds__(NT, 1) void conv_wide_kernel(const stgcn_conv_desc 
     auto step = [&]<int hs>() {
       constexpr int h = hs / SPI, s = hs % SPI, t = s / KS, ks = s % KS;
       char* const cur = h == 0 ? sA0 : sA1;
-      char* const nxt = h == 0 ? sA1 : sA0;
-      // 1. B fragments LEAD k-steps ahead (may belong to the next item or the next pair)
-      {
-        const int hn = hs + LEAD;
+      {  // B fragments LEAD k-steps ahead (may belong to the next item or the next pair)
+        constexpr int hn = hs + LEAD;
         const int woff = hn < SPI ? woff0 : (hn < PAIR ? woff1 : woff2);
         load_B(fb[hn % NBUF], hn % SPI, woff, wl, kcc_l, cinp_l);
       }
-      // 2. next item's halo: loads at the item's first k-step, LDS writes spread over NST k-steps
-      if constexpr (s == 0) issue_A(w + h + 1);
-      if constexpr ((DBG & 2) == 0 && s >= SA && s < SA + NST) store_A.template operator()<(s - SA) * UPS, (s - SA + 1) * UPS>(nxt);
-      // 3. A fragments (read one k-step ahead inside an item)
       if constexpr (s == 0) {
         const int tb = (qbase + qsign * t) * tbytes + ks * 32;
 #pragma unroll
         for (int i = 0; i < TM; ++i)
           fa[hs & 1][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(cur + af[i] + tb));
       }
-      if constexpr (s + 1 < SPI) {
-        const int t1 = (s + 1) / KS, ks1 = (s + 1) % KS;
+      if constexpr (s + 1 < SPI) {  // A fragments one k-step ahead inside an item
+        constexpr int t1 = (s + 1) / KS, ks1 = (s + 1) % KS;
         const int tb1 = (qbase + qsign * t1) * tbytes + ks1 * 32;
 #pragma unroll
         for (int i = 0; i < TM; ++i)
           fa[(hs + 1) & 1][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(cur + af[i] + tb1));
       }
-      // 4. MFMAs
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[hs & 1][i], fb[hs % NBUF][j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (hs == SPI - 1) lds_barrier();
+      if constexpr (s == SPI - 1) {
+        tmark(3);
+        lds_barrier();  // E_{w+h}
+        tmark(4);
+      }
     };
-    [&]<int... I>(std::integer_sequence<int, I...>) { (step.template operator()<I>(), ...); }(
-        std::make_integer_sequence<int, PAIR>{});
-    const int tl = w / g.G;
-    if ((DBG & 4) != 0 && a.N < 0) epilogue(0);  // never runs: keeps the MFMAs alive
-    if ((DBG & 4) == 0 && (w + 1) - tl * g.G == g.G - 1) {
-      lds_barrier();  // every wave done reading sA1 (item w + 1's halo)
-      epilogue((int)blockIdx.x + tl * grid);
+    if (w % g.G == 0) load_bias(w);
+    tmark(-1);
+    static_for<PAIR>(step);
+    tmark(0);
+    if (tile_end(w + 1)) {
+      dump(w + 1, sA1);
+      tmark(1);
+      lds_barrier();  // I_{w+1}
+      tmark(2);
     }
-    lds_barrier();
   }
+  if (wave == 0) tflush(0);
 }
 
 }  // namespace
+
+long long* wide_dbg_ptr = nullptr;
+int wide_debug_read(long long* host, long n) {
+  if (!wide_dbg_ptr) return 1;
+  (void)hipDeviceSynchronize();
+  return hipMemcpy(host, wide_dbg_ptr, n * sizeof(long long), hipMemcpyDeviceToHost) == hipSuccess ? 0 : 3;
+}
 
 long conv_rows_num_row_blocks(long M, int cout);
 
 int conv_wide_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
   static const bool off = getenv("STGCN_NO_WIDE") != nullptr;  // A/B switch
-  if (off || dtype != 1) return -1;
+  if (off || dtype != 1 || !a.w_frag) return -1;
   if (a.Kt != KT || a.pad != (KT - 1) / 2 || a.stride != 1 || a.T_in != a.T_out) return -1;
   if (a.pro != 0 && a.pro != 1) return -1;
   if (a.bias_mode != 0 && a.bias_mode != 1) return -1;
@@ -398,6 +483,7 @@ int conv_wide_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
   const int BN = 128;  // BN = 256 (acc 256 + B ring) does not fit the register file without spills
   if (a.Cout_pad % BN) return -1;
   WGeom g;
+  g.dbg = nullptr;
   g.F = 256 / a.V;
   g.HR = (g.F + KT - 1) * a.V;
   if (g.HR > HR_CAP || g.F < 1) return -1;
@@ -426,14 +512,16 @@ int conv_wide_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
     (void)hipFuncSetAttribute((const void*)conv_wide_kernel<128, 6, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     attr = true;
   }
-  const dim3 gd((unsigned)grid), bd(NT);
+  const dim3 gd((unsigned)grid), bd(2 * NT), bd2(2 * NT);
   static const int dbg = getenv("STGCN_WIDE_DBG") ? atoi(getenv("STGCN_WIDE_DBG")) : 0;
   if (dbg) {
-    auto* k = dbg == 1 ? conv_wide_kernel<128, 6, 1, 1> : dbg == 2 ? conv_wide_kernel<128, 6, 1, 2>
-            : dbg == 4 ? conv_wide_kernel<128, 6, 1, 4> : dbg == 6 ? conv_wide_kernel<128, 6, 1, 6>
-                       : conv_wide_kernel<128, 6, 1, 7>;
+    static long long* dbuf = nullptr;
+    if (!dbuf) (void)hipMalloc(&dbuf, 16 * 4096 * sizeof(long long));
+    wide_dbg_ptr = dbuf;
+    g.dbg = dbuf;
+    auto* k = dbg == 2 ? conv_wide_kernel<128, 6, 1, 2> : conv_wide_kernel<128, 6, 1, 4>;
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-    hipLaunchKernelGGL(k, gd, bd, lds, s, a, g);
+    hipLaunchKernelGGL(k, gd, bd2, lds, s, a, g);
     return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
   }
   if (a.pro) hipLaunchKernelGGL((conv_wide_kernel<128, 6, 1>), gd, bd, lds, s, a, g);
