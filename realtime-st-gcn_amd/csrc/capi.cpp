@@ -20,6 +20,8 @@ int pack_weight_launch(const float* src, long s0, long s1, long s2, int Kt, int 
 long conv_rows_num_row_blocks(long M, int cout);
 int conv_wgrad_launch(WgradArgs a, int dtype, hipStream_t s);
 long wgrad_tile_workspace(const WgradArgs& a, int dtype);
+long wgrad_wide_workspace(const WgradArgs& a, int dtype);
+int wgrad_wide_launch(const WgradArgs& a, int dtype, hipStream_t s);
 int wgrad_tile_launch(const WgradArgs& a, int dtype, hipStream_t s);
 int amix_fwd_launch(const AmixArgs& a, int dtype, hipStream_t s);
 long gconv_row_blocks(int NT, int V);
@@ -115,13 +117,16 @@ long stgcn_conv_rows_row_blocks(long M, int cout) { return conv_rows_num_row_blo
 
 long stgcn_conv_wgrad_workspace(const stgcn_wgrad_desc* d, int dtype) {
   if (!d || (dtype != 0 && dtype != 1)) return 0;
-  return wgrad_tile_workspace(*d, dtype);
+  const long w = wgrad_wide_workspace(*d, dtype);  // >= 128-channel Kt=9 stride-1 path first
+  return w > 0 ? w : wgrad_tile_workspace(*d, dtype);
 }
 
 int stgcn_conv_wgrad(const stgcn_wgrad_desc* d, int dtype, void* stream) {
   CHECK_DTYPE(dtype);
   if (!d || !d->in || !d->dy || !d->dw || d->N <= 0 || d->Kt <= 0 || d->stride <= 0) return STGCN_EBADSHAPE;
   if (d->pro && (!d->pro_a || !d->pro_b || (d->pro == 2 && !d->pro_stats))) return STGCN_EBADSHAPE;
+  const int rw = wgrad_wide_launch(*d, dtype, STREAM(stream));  // bf16 >= 128-channel ring path (needs work)
+  if (rw >= 0) return rw;
   const int r = wgrad_tile_launch(*d, dtype, STREAM(stream));  // bf16 frame-tiled path (needs work)
   if (r >= 0) return r;
   return conv_wgrad_launch(*d, dtype, STREAM(stream));

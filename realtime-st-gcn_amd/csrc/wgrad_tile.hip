@@ -375,6 +375,15 @@ int launch_w(const stgcn_wgrad_desc& a, const Plan& p, hipStream_t s) {
 
 }  // namespace
 
+// deterministic two-level sum of R fp32 slabs [R][E] into dw (+=); part holds RS_MAX * E floats
+int slab_reduce_launch(const float* slab, int R, long E, float* part, float* dw, hipStream_t s) {
+  const int RS = R < RS_MAX ? R : RS_MAX;
+  const unsigned blocks = (unsigned)((E / 4 + 255) / 256);
+  hipLaunchKernelGGL(slab_reduce1_kernel, dim3(blocks, RS), dim3(256), 0, s, slab, R, RS, E, part);
+  hipLaunchKernelGGL(slab_reduce2_kernel, dim3(blocks), dim3(256), 0, s, (const float*)part, RS, E, dw);
+  return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
+}
+
 // bytes of workspace the tile path needs (0 = shape not covered: conv_wgrad.hip handles it)
 long wgrad_tile_workspace(const stgcn_wgrad_desc& a, int dtype) {
   if (dtype != 1) return 0;

@@ -1,0 +1,310 @@
+// Weight gradient of the Kt = 9, stride-1 temporal convs with >= 128 output channels (bf16): the
+// convolution_backward weight path of tcn.2 (stgcn.py:154-159, the reference's top CPU op) at the
+// config-2 layer 4, 5, 7, 8 shapes.
+//
+//   dW[dt][co][ci] += sum_m dY[m][co] * pro(in[m + (dt - 4) V][ci])        (rows m of one sample)
+//
+// A GEMM with M = co, N = (dt, ci), K = output rows.  wgrad_tile.hip gives each block a 64-co x 32-ci
+// output block, so every dY element is staged Cin/32 times and the input halo of 5+8 frames is
+// staged for every 5-frame tile (2.6x).  Here:
+//   * a block (8 waves, two per SIMD) owns a 128-co x 64-ci x 9-tap output block (wave (wc, wi):
+//     32 co x 32 ci x 9 taps = 9 accumulators of 32 x 32) and walks a contiguous range of tiles of
+//     F = floor(128 / V) frames (5 at V = 25): dY is staged Cin/64 times, the input Cout/128 times;
+//   * the input lives in a frame RING of RS = 2F + 8 slots plus a MIRROR of its first F + 7 slots
+//     (every frame written to slot f mod RS, and again to slot f mod RS + RS when that is < RS + F + 7):
+//     a tile's window (frames f0-4 .. f0+F+3) is then always LDS-contiguous, the next tile's F new
+//     frames land in slots the current tile does not read, and each input frame is staged (BatchNorm1
+//     scale/shift + ReLU prologue applied, zero frames outside [0, T)) exactly once per block, with
+//     one barrier per tile;
+//   * both operands are read with the transposing ds_read_b64_tr_b16 from 32-channel panels of 64-B
+//     rows (8 consecutive K rows per lane), the input fragment of tap dt at a uniform offset dt*V rows;
+//     fragments are read two tap-steps ahead of their MFMAs;
+//   * the next tile's dY rows and new frames are loaded into registers while the current tile computes;
+//   * the fp32 block result goes to a slab [range][9][Cout][Cin], summed deterministically into dW by
+//     slab_reduce (wgrad_tile.hip).
+#include "common.h"
+#include "../../include/stgcn_amd.h"
+#include <stdlib.h>
+#include <utility>
+
+namespace {
+
+constexpr int KT = 9, PADT = 4;
+constexpr int NT = 512;              // 8 waves
+constexpr int KM = 128;              // K rows per tile (F*V <= 128, rest zero rows)
+constexpr int PR = 64;               // bytes per panel row (32 bf16 channels)
+constexpr int COB = 128, CIB = 64;   // output block
+constexpr int DY_PANEL = KM * PR;    // 8 KB
+constexpr int DY_BYTES = (COB / 32) * DY_PANEL;  // 32 KB per buffer
+constexpr int DY_U = KM * (COB / 8) / NT;        // 16-B dY units per thread per tile (4)
+constexpr int X_U = (KM * (CIB / 8) + NT - 1) / NT;  // input units per thread per batch of <= 128 rows (2)
+constexpr int LDS_MAX = 160 * 1024;
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+template <int N, typename F>
+DEV void static_for(F&& f) {
+  [&]<int... I>(std::integer_sequence<int, I...>) { (f.template operator()<I>(), ...); }(
+      std::make_integer_sequence<int, N>{});
+}
+
+DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// two ds_read_b64_tr_b16 (rows lo and lo + 4 of a 64-B-row panel) -> one MFMA fragment: lane
+// (c = column, h) receives rows 8h .. 8h+7 of its column
+DEV bf16x8 trpair(const char* lo) {
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)lo);
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lo + 4 * PR));
+  s16x8 v;
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+  v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+struct WWGeom {
+  int F;         // output frames per tile
+  int RS;        // ring slots (frames)
+  int MS;        // ring + mirror slots
+  int nco, nci;  // output blocks along co (128) and ci (64)
+  int tiles_n;   // tiles per sample
+  int tpb;       // tiles per block (contiguous range of the sample-major tile sequence)
+  int R;         // row-range blocks per output block (slab count)
+  float* slab;   // [R][KT][Cout][Cin]
+};
+
+template <int PRO>
+__global__ __launch_bounds__(NT, 1) void wgrad_wide_kernel(const stgcn_wgrad_desc a, const WWGeom g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int V = a.V, F = g.F;
+  const int XP = g.MS * V * PR;                 // bytes per input panel (ring + mirror)
+  char* const sX = smem;                        // input panel p (ci 32p ..) at p * XP
+  char* const sY = smem + 2 * XP;               // dY buffers [2][4 panels][KM rows]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wc = wave >> 1, wi = wave & 1;      // co tile (32), ci tile (32)
+  const int ob = blockIdx.x % (g.nco * g.nci), rg = blockIdx.x / (g.nco * g.nci);
+  const int co0 = (ob % g.nco) * COB, ci0 = (ob / g.nco) * CIB;
+  const int tiles_n = g.tiles_n;
+  const int k_begin = rg * g.tpb, k_end = min(a.N * tiles_n, k_begin + g.tpb);
+
+  const bf16* __restrict__ xin = reinterpret_cast<const bf16*>(a.in);
+  const bf16* __restrict__ dy = reinterpret_cast<const bf16*>(a.dy);
+
+  // ---- staging: dY unit (row tid/16 + 32 i, 8 co at 8*(tid%16)); input unit (row tid/8 + 64 i, 8 ci at 8*(tid%8))
+  const int ycu = tid & 15, xcu = tid & 7;
+  float sc[8], sh[8];
+  if (PRO == 1) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = ci0 + xcu * 8 + j;
+      sc[j] = c < a.Cin ? a.pro_a[c] : 0.f;
+      sh[j] = c < a.Cin ? a.pro_b[c] : 0.f;
+    }
+  }
+  uint4 ry[DY_U], rx[X_U];
+  auto load_dy = [&](int n, int f0) {  // rows of output frames f0 .. f0+F-1 (zero past T_out / F*V)
+    const int rows_valid = min(F, a.T_out - f0) * V;
+    const bf16* base = dy + ((long)n * a.T_out + f0) * V * a.dy_ld + co0 + ycu * 8;
+    const bool cok = co0 + ycu * 8 < a.Cout;
+    static_for<DY_U>([&]<int i>() {
+      const int r = (tid >> 4) + 32 * i;
+      ry[i] = make_uint4(0, 0, 0, 0);
+      if (cok && r < rows_valid) ry[i] = *reinterpret_cast<const uint4*>(base + (long)r * a.dy_ld);
+    });
+  };
+  auto store_dy = [&](int buf) {
+    char* p = sY + buf * DY_BYTES + (ycu >> 2) * DY_PANEL + (ycu & 3) * 16;
+    static_for<DY_U>([&]<int i>() {
+      const int r = (tid >> 4) + 32 * i;
+      *reinterpret_cast<uint4*>(p + r * PR) = ry[i];
+    });
+  };
+  // input frames [fa, fa + nf) of sample n (nf * V <= 128) -> registers
+  auto load_x = [&](int n, int fa, int nf) {
+    const bool cok = ci0 + xcu * 8 < a.Cin;
+    static_for<X_U>([&]<int i>() {
+      const int r = (tid >> 3) + 64 * i;
+      rx[i] = make_uint4(0, 0, 0, 0);
+      if (r < nf * V) {
+        const int fl = r / V, v = r - fl * V, f = fa + fl;
+        if (cok && f >= 0 && f < a.T_in)
+          rx[i] = *reinterpret_cast<const uint4*>(xin + (((long)n * a.T_in + f) * V + v) * a.in_ld + ci0 + xcu * 8);
+      }
+    });
+  };
+  auto store_x = [&](int fa, int nf) {  // slot f mod RS and its mirror
+    static_for<X_U>([&]<int i>() {
+      const int r = (tid >> 3) + 64 * i;
+      if (r < nf * V) {
+        const int fl = r / V, v = r - fl * V, f = fa + fl;
+        uint4 u = rx[i];
+        if (PRO == 1 && f >= 0 && f < a.T_in) {
+          float e[8];
+          unpack16(u, e, (bf16*)nullptr);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) e[j] = fmaxf(fmaf(e[j], sc[j], sh[j]), 0.f);
+          u = pack16(e, (bf16*)nullptr);
+        }
+        int slot = f % g.RS;
+        slot += slot < 0 ? g.RS : 0;
+        char* p = sX + (xcu >> 2) * XP + (xcu & 3) * 16 + v * PR;
+        *reinterpret_cast<uint4*>(p + slot * V * PR) = u;
+        if (slot + g.RS < g.MS) *reinterpret_cast<uint4*>(p + (slot + g.RS) * V * PR) = u;
+      }
+    });
+  };
+  // the whole window of a range's / sample's first tile (F + 8 frames) in batches of F frames
+  auto stage_window = [&](int n, int f0) {
+    for (int fb = f0 - PADT; fb < f0 + F + PADT; fb += F) {
+      const int nf = min(F, f0 + F + PADT - fb);
+      load_x(n, fb, nf);
+      store_x(fb, nf);
+    }
+  };
+
+  // ---- fragments: lane (i = lane&15, gq = lane>>4): row 8h + q (+4), column 16(gq&1) + 4p
+  const int li = lane & 15, gq = lane >> 4;
+  const int colb = (16 * (gq & 1) + 4 * (li & 3)) * 2;
+  const int rlo = 8 * (gq >> 1) + (li >> 2);
+
+  f32x16 acc[KT];
+#pragma unroll
+  for (int t = 0; t < KT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  // zero the input panels once: K padding rows of a tile read past the window (finite values needed)
+  for (int o = tid * 16; o < 2 * XP; o += NT * 16) *reinterpret_cast<uint4*>(sX + o) = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+
+  const int tapb = V * PR;  // bytes between taps
+  for (int k = k_begin; k < k_end; ++k) {
+    const int n = k / tiles_n, tt = k - n * tiles_n, f0 = tt * F;
+    if (tt == 0 || k == k_begin) {  // range/sample start: dY of this tile and the whole input window
+      __syncthreads();
+      load_dy(n, f0);
+      store_dy(k & 1);
+      stage_window(n, f0);
+      __syncthreads();
+    }
+    // prefetch tile k+1 (same sample only: a new sample restages above)
+    const bool pre = k + 1 < k_end && tt + 1 < tiles_n;
+    if (pre) {
+      load_dy(n, f0 + F);
+      load_x(n, f0 + F + PADT, F);
+    }
+    // ---- compute tile k: 72 tap-steps u = (ks, t), fragments read D steps ahead
+    int s0 = (f0 - PADT) % g.RS;
+    s0 += s0 < 0 ? g.RS : 0;
+    const char* Y = sY + (k & 1) * DY_BYTES + wc * DY_PANEL + colb + rlo * PR;
+    const char* X = sX + wi * XP + colb + (s0 * V + rlo) * PR;
+    int tb = tapb;
+    asm volatile("" : "+s"(tb));
+    constexpr int NU = (KM / 16) * KT, D = 2;
+    bf16x8 fx[D + 1], fy[2];
+    auto rd = [&]<int u>() {
+      constexpr int ks = u / KT, t = u % KT;
+      if constexpr (t == 0) fy[ks & 1] = trpair(Y + 16 * ks * PR);
+      fx[u % (D + 1)] = trpair(X + t * tb + 16 * ks * PR);
+    };
+    static_for<D>([&]<int u>() { rd.template operator()<u>(); });
+    static_for<NU>([&]<int u>() {
+      if constexpr (u + D < NU) rd.template operator()<u + D>();
+      constexpr int ks = u / KT, t = u % KT;
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fy[ks & 1], fx[u % (D + 1)], acc[t], 0, 0, 0);
+    });
+    // ---- hand the prefetched tile to LDS (ring slots / dY buffer not read by tile k)
+    if (pre) {
+      store_dy((k + 1) & 1);
+      store_x(f0 + F + PADT, F);
+    }
+    lds_barrier();
+  }
+
+  // ---- block partial -> slab [rg][t][co][ci]: lane holds ci = ci0 + 32 wi + (lane&31), co rows acc_row
+  float* __restrict__ out = g.slab + (long)rg * KT * a.Cout * a.Cin;
+  const int ci = ci0 + 32 * wi + (lane & 31);
+#pragma unroll
+  for (int t = 0; t < KT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = co0 + 32 * wc + acc_row(r, lane);
+      if (co < a.Cout && ci < a.Cin) out[((long)t * a.Cout + co) * a.Cin + ci] = acc[t][r];
+    }
+}
+
+struct WPlan {
+  bool ok;
+  WWGeom g;
+  size_t lds;
+  long slab_elems;
+};
+
+constexpr int RS_PART = 16;  // level-1 partials of slab_reduce
+
+WPlan wplan(const stgcn_wgrad_desc& a) {
+  WPlan p{};
+  p.ok = false;
+  static const bool off = getenv("STGCN_NO_WGRAD_WIDE") != nullptr;  // A/B switch
+  if (off) return p;
+  if (a.Kt != KT || a.pad != PADT || a.stride != 1 || a.T_in != a.T_out) return p;
+  if (a.pro != 0 && a.pro != 1) return p;
+  if (a.Cout < COB || a.Cin < CIB || a.Cout % 8 || a.Cin % 8 || a.in_ld % 8 || a.dy_ld % 8 || a.V > 32) return p;
+  WWGeom& g = p.g;
+  g.F = KM / a.V;
+  g.RS = 2 * g.F + 2 * PADT;
+  g.MS = g.RS + g.F + 2 * PADT - 1;  // a window starting at slot RS-1 ends at slot MS-1
+  if (g.F < 1 || g.F * a.V > KM || g.F * a.V > 64 * X_U) return p;
+  g.nco = (a.Cout + COB - 1) / COB;
+  g.nci = (a.Cin + CIB - 1) / CIB;
+  const int nob = g.nco * g.nci;
+  g.tiles_n = (a.T_out + g.F - 1) / g.F;
+  const long total = (long)a.N * g.tiles_n;
+  if (total > 0x7fffffffL) return p;
+  // one block per CU (LDS): split the tile sequence so that nob * R ~ 256 blocks
+  int R = 256 / nob;
+  if (R < 1) R = 1;
+  if (R > total) R = (int)total;
+  g.tpb = (int)((total + R - 1) / R);
+  g.R = (int)((total + g.tpb - 1) / g.tpb);
+  // K padding rows of the window's last tap read up to KM - F*V rows past slot MS: keep them inside
+  // the allocation (they land in the dY buffers; finite, multiplied by zero dY rows)
+  p.lds = 2 * (size_t)g.MS * a.V * PR + 2 * (size_t)DY_BYTES;
+  if (p.lds > LDS_MAX || (size_t)(KM - g.F * a.V) * PR > 2 * (size_t)DY_BYTES) return p;
+  p.slab_elems = (long)(g.R + RS_PART) * KT * a.Cout * a.Cin;
+  p.ok = true;
+  return p;
+}
+
+}  // namespace
+
+int slab_reduce_launch(const float* slab, int R, long E, float* part, float* dw, hipStream_t s);
+
+long wgrad_wide_workspace(const stgcn_wgrad_desc& a, int dtype) {
+  if (dtype != 1) return 0;
+  const WPlan p = wplan(a);
+  return p.ok ? p.slab_elems * (long)sizeof(float) : 0;
+}
+
+// -1: not handled here
+int wgrad_wide_launch(const stgcn_wgrad_desc& a, int dtype, hipStream_t s) {
+  if (dtype != 1 || a.work == nullptr) return -1;
+  WPlan p = wplan(a);
+  if (!p.ok || a.work_bytes < p.slab_elems * (long)sizeof(float)) return -1;
+  p.g.slab = reinterpret_cast<float*>(a.work);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)wgrad_wide_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)wgrad_wide_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  const unsigned grid = (unsigned)(p.g.nco * p.g.nci * p.g.R);
+  if (a.pro == 1)
+    hipLaunchKernelGGL(wgrad_wide_kernel<1>, dim3(grid), dim3(NT), p.lds, s, a, p.g);
+  else
+    hipLaunchKernelGGL(wgrad_wide_kernel<0>, dim3(grid), dim3(NT), p.lds, s, a, p.g);
+  if (hipGetLastError() != hipSuccess) return STGCN_EHIP;
+  const long E = (long)KT * a.Cout * a.Cin;
+  return slab_reduce_launch(p.g.slab, p.g.R, E, p.g.slab + (long)p.g.R * E, a.dw, s);
+}

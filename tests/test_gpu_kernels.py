@@ -290,3 +290,21 @@ def test_conv_wide_prologue_stats(K, cin, cout, T, N):
     wtp, cq, kq = K.pack_weight(w.squeeze(-1).permute(2, 1, 0).to(DEV), torch.bfloat16)
     dx = K.conv_rows(cl(dy, torch.bfloat16), wtp, cout, cin, cq, kq, T, T, Kt=9, pad=4, trans=True)
     assert_close(dx.float(), xr.grad, 2e-2, "wide conv trans")
+
+
+@pytest.mark.parametrize("cin,cout,T,N", [(128, 128, 37, 3), (256, 256, 23, 2), (64, 256, 16, 3), (256, 128, 150, 2)])
+def test_wgrad_wide_prologue(K, cin, cout, T, N):
+    """>= 128-output-channel Kt=9 stride-1 weight gradient (wgrad_wide.hip, frame ring, bf16) with the
+    BN1+ReLU prologue, against torch fp32."""
+    torch.manual_seed(7)
+    V = 25
+    x = torch.randn(N, cin, T, V) * 1.5 + 0.3
+    pa, pb = torch.rand(cin) + 0.5, torch.randn(cin)
+    h = torch.relu(x * pa.view(1, -1, 1, 1) + pb.view(1, -1, 1, 1))
+    w = (torch.randn(cout, cin, 9, 1) / (9 * cin) ** 0.5).requires_grad_(True)
+    y = F.conv2d(h, w, None, padding=(4, 0))
+    dy = torch.randn(y.shape)
+    y.backward(dy)
+    dw = K.conv_wgrad(cl(x, torch.bfloat16), cl(dy, torch.bfloat16), cin, cout, T, T, Kt=9, pad=4, pro=1,
+                      pro_a=pa.to(DEV), pro_b=pb.to(DEV))
+    assert_close(dw.cpu().permute(1, 2, 0).unsqueeze(-1), w.grad, 2e-2, "wide wgrad+prologue")
