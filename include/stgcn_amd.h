@@ -42,8 +42,9 @@ typedef struct {
   int N, T_in, T_out, V, Cin, Cout, Cin_pad, Cout_pad;
   int Kt, stride, pad, trans, pro, bias_mode, accumulate;
   int in_ld, out_ld;
-  const void* w_frag;     /* optional: the same weights as an MFMA-fragment image (stgcn_pack_weight_frag);
-                           * the wide-channel Kt = 9 kernel runs only when it is given (NULL: other kernels) */
+  const void* w_frag;     /* optional MFMA-fragment image of the weights for the wide-channel Kt = 9 kernel
+                           * (NULL: other kernels): stride 1 -> stgcn_pack_weight_frag's image of w;
+                           * stride 2 -> stgcn_pack_weight_s2frag's parity-folded image (trans to match) */
 } stgcn_conv_desc;
 
 int stgcn_conv_rows(const stgcn_conv_desc* d, int dtype, void* stream);
@@ -56,6 +57,13 @@ int stgcn_pack_weight(const float* src, long s0, long s1, long s2, int Kt, int C
  * so one 32x32x16 B fragment is one contiguous wave load (conv_wide.hip). */
 int stgcn_pack_weight_frag(const float* src, long s0, long s1, long s2, int Kt, int Cout, int Cin, void* dst,
                            void* dst_frag, int Cout_pad, int Cin_pad, int dtype, void* stream);
+/* Parity-folded MFMA-fragment image of a stride-2 Kt = 9 weight src [9][Cout][Cin] (fp32, element
+ * (k,co,ci) at src[k*s0+co*s1+ci*s2]) — the w_frag a stride-2 stgcn_conv_rows call takes: the 5-tap
+ * conv over frame pairs (forward: W'[t][co][par*Cin+ci] = W[2t+par][co][ci]; trans = 1, the data grad:
+ * W'[t][par*Cout+co][ci] = W[8-2t+par][co][ci]), dst_frag holding 5 * 2 * Cout * Cin bf16.
+ * Replaces: the strided tcn.2 of layers with stride 2 (models/stgcn/stgcn.py:154-159) and its input grad. */
+int stgcn_pack_weight_s2frag(const float* src, long s0, long s1, long s2, int Cout, int Cin, void* dst_frag, int trans,
+                             int dtype, void* stream);
 /* column tile the packed weights must be padded to (Cout_pad % tile == 0) */
 int stgcn_conv_rows_col_tile(int cout);
 /* upper bound on row blocks (first dim of the BN partial-stat buffer, which the caller zero-fills) */

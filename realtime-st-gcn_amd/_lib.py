@@ -86,6 +86,8 @@ _SIGS = {
     "stgcn_gcn_bias_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "stgcn_pack_weight": (c_int, [c_void_p, ctypes.c_long, ctypes.c_long, ctypes.c_long, c_int, c_int, c_int,
                                   c_void_p, c_int, c_int, c_int, c_void_p]),
+    "stgcn_pack_weight_s2frag": (c_int, [c_void_p, ctypes.c_long, ctypes.c_long, ctypes.c_long, c_int, c_int,
+                                         c_void_p, c_int, c_int, c_void_p]),
     "stgcn_pack_weight_frag": (c_int, [c_void_p, ctypes.c_long, ctypes.c_long, ctypes.c_long, c_int, c_int, c_int,
                                        c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "stgcn_amix_dA_workspace": (ctypes.c_long, [ctypes.POINTER(AmixDesc)]),

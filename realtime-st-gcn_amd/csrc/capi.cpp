@@ -19,6 +19,8 @@ int pack_weight_launch(const float* src, long s0, long s1, long s2, int Kt, int 
                        int dtype, hipStream_t s, void* dst_frag);
 long conv_rows_num_row_blocks(long M, int cout);
 int conv_wgrad_launch(WgradArgs a, int dtype, hipStream_t s);
+int pack_s2frag_launch(const float* src, long s0, long s1, long s2, int Co, int Ci, void* dst, int trans,
+                       hipStream_t s);
 long wgrad_tile_workspace(const WgradArgs& a, int dtype);
 long wgrad_wide_workspace(const WgradArgs& a, int dtype);
 int wgrad_wide_launch(const WgradArgs& a, int dtype, hipStream_t s);
@@ -106,6 +108,12 @@ int stgcn_pack_weight(const float* src, long s0, long s1, long s2, int Kt, int C
   CHECK_DTYPE(dtype);
   if (!src || !dst || Kt <= 0 || Co <= 0 || Ci <= 0 || Cout_pad < Co || Cin_pad < Ci) return STGCN_EBADSHAPE;
   return pack_weight_launch(src, s0, s1, s2, Kt, Co, Ci, dst, Cout_pad, Cin_pad, dtype, STREAM(stream), nullptr);
+}
+int stgcn_pack_weight_s2frag(const float* src, long s0, long s1, long s2, int Co, int Ci, void* dst_frag, int trans,
+                             int dtype, void* stream) {
+  if (dtype != 1) return STGCN_EDTYPE;
+  if (!src || !dst_frag || Co <= 0 || Ci <= 0) return STGCN_EBADSHAPE;
+  return pack_s2frag_launch(src, s0, s1, s2, Co, Ci, dst_frag, trans ? 1 : 0, STREAM(stream));
 }
 int stgcn_pack_weight_frag(const float* src, long s0, long s1, long s2, int Kt, int Co, int Ci, void* dst,
                            void* dst_frag, int Cout_pad, int Cin_pad, int dtype, void* stream) {

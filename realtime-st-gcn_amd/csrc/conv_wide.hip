@@ -31,10 +31,8 @@
 
 namespace {
 
-constexpr int KT = 9;
 constexpr int KG = 64;               // input channels per item
 constexpr int KS = KG / 16;          // MFMA k-steps per tap
-constexpr int SPI = KT * KS;         // k-steps per item (36)
 constexpr int NT = 256;              // 4 waves
 constexpr int WM = 2, WN = 2, TM = 4;
 constexpr int RSA = KG * 2 + 16;     // padded halo row bytes (144)
@@ -63,8 +61,12 @@ struct WGeom {
   int ncol;     // column tiles (Cout_pad / BN)
   int ntiles;   // N * tiles_n * ncol
   int G;        // 64-channel items per tile (even)
-  int HR;       // halo rows per item ((F + 8) * V)
+  int HR;       // halo rows per item ((F + KTAP - 1) * V)
   int abytes;   // bytes per LDS halo buffer
+  int T_tile;   // frames the tiles walk (output frames; fold 2: dY frames)
+  int fold;     // stride-2 folding: 0 none, 1 input parity (forward), 2 output parity (data grad)
+  int cpar;     // fold 1: 64-channel items per input parity; fold 2: output channels per parity
+  int wc32, wk16;  // fragment image dims: (output channels / 32, input channels / 16)
   long long* dbg;  // DBG & 4: per-block phase cycles [block][16]
 };
 
@@ -72,13 +74,13 @@ struct TileInfo {
   int n, f0, fe, ct;
 };
 
-DEV TileInfo tile_info(int tile, const WGeom& g, int T_out) {
+DEV TileInfo tile_info(int tile, const WGeom& g) {
   TileInfo ti;
   ti.ct = tile % g.ncol;
   const int rt = tile / g.ncol;
   ti.n = rt / g.tiles_n;
   ti.f0 = (rt - ti.n * g.tiles_n) * g.F;
-  ti.fe = min(g.F, T_out - ti.f0);
+  ti.fe = min(g.F, g.T_tile - ti.f0);
   return ti;
 }
 
@@ -93,8 +95,9 @@ DEV TileInfo tile_info(int tile, const WGeom& g, int T_out) {
 // helpers drain that image during item k+1 before they overwrite buf b with item k+2's halo.
 // DBG (diagnostic instantiations, STGCN_WIDE_DBG=<bits>): bit1 no helper work (results wrong), bit2 phase
 // timers (s_memtime of MMA wave 0 / helper wave 4 into g.dbg)
-template <int BN, int NBUF, int PRO, int DBG = 0>
+template <int BN, int KTAP, int NBUF, int PRO, int DBG = 0>
 __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_desc a, const WGeom g) {
+  constexpr int SPI = KTAP * KS;  // k-steps per item
   constexpr int TN = BN / 64;
   constexpr int LEAD = NBUF - 1;
   constexpr int PAIR = 2 * SPI;  // k-steps per item pair
@@ -147,17 +150,32 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
     auto issue_A = [&](int w) {  // item w's halo units -> registers
       int gi;
       const int tile = item_tile(w, gi);
-      const TileInfo ti = tile_info(tile, g, a.T_out);
-      const int fi0 = ti.f0 - (KT - 1) / 2;
-      a_lo = max(0, -fi0) * V;
-      a_hi = min(g.HR, (a.T_in - fi0) * V);
-      const bf16* base = in + ((long)ti.n * a.T_in + fi0) * V * a.in_ld + gi * KG + ucol * 8;
-      static_for<NA>([&]<int i>() {
-        const int row = min(max(row0u + 32 * i, a_lo), a_hi - 1);
-        ra[i] = *reinterpret_cast<const uint4*>(base + row * a.in_ld);
-      });
+      const TileInfo ti = tile_info(tile, g);
+      const int fi0 = ti.f0 - (KTAP - 1) / 2;
+      int cg = gi;  // 64-channel group of the source tensor
+      if (g.fold == 1) {
+        // halo frame z = fi0 + fl is the pair (x[2z], x[2z+1]); this item reads parity gi / cpar
+        const int par = gi / g.cpar;
+        cg = gi - par * g.cpar;
+        a_lo = max(0, -fi0) * V;
+        a_hi = min(g.HR, ((a.T_in - par + 1) / 2 - fi0) * V);
+        const bf16* base = in + (long)ti.n * a.T_in * V * a.in_ld + cg * KG + ucol * 8;
+        static_for<NA>([&]<int i>() {
+          const int row = min(max(row0u + 32 * i, a_lo), a_hi - 1);
+          const int fl = row / V, v = row - fl * V;
+          ra[i] = *reinterpret_cast<const uint4*>(base + ((2 * (fi0 + fl) + par) * V + v) * (long)a.in_ld);
+        });
+      } else {
+        a_lo = max(0, -fi0) * V;
+        a_hi = min(g.HR, (a.T_in - fi0) * V);
+        const bf16* base = in + ((long)ti.n * a.T_in + fi0) * V * a.in_ld + gi * KG + ucol * 8;
+        static_for<NA>([&]<int i>() {
+          const int row = min(max(row0u + 32 * i, a_lo), a_hi - 1);
+          ra[i] = *reinterpret_cast<const uint4*>(base + row * a.in_ld);
+        });
+      }
       if (PRO == 1) {
-        const int c = gi * KG + ucol * 8;
+        const int c = cg * KG + ucol * 8;
         const float4 s0 = *reinterpret_cast<const float4*>(a.pro_a + c);
         const float4 s1 = *reinterpret_cast<const float4*>(a.pro_a + c + 4);
         const float4 h0 = *reinterpret_cast<const float4*>(a.pro_b + c);
@@ -191,7 +209,7 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
     auto drain = [&](int w, const char* img) {
       int gi;
       const int tile = item_tile(w, gi);
-      const TileInfo ti = tile_info(tile, g, a.T_out);
+      const TileInfo ti = tile_info(tile, g);
       const int rows_valid = ti.fe * V;
       const int n0 = ti.ct * BN;
       if (a.stats) {
@@ -205,13 +223,17 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
       }
       // lane = row quad (4 rows), helper wave h = 8-channel units 4h..4h+3: per unit, 8 conflict-free
       // ds_read_b64 (4 rows of one column each) are transposed in registers into 4 row units of 16 B
-      bf16* __restrict__ outb = reinterpret_cast<bf16*>(a.out) + ((long)ti.n * a.T_out + ti.f0) * V * (long)a.out_ld;
+      // fold 2: column tile n0 of the folded [dx_even | dx_odd] space -> parity par, channel base cb
+      const int par = g.fold == 2 ? n0 / g.cpar : 0;
+      const int cb = n0 - par * (g.fold == 2 ? g.cpar : 0);
+      bf16* __restrict__ outs = reinterpret_cast<bf16*>(a.out) + (long)ti.n * a.T_out * V * a.out_ld;
+      bf16* __restrict__ outb = outs + (long)ti.f0 * V * a.out_ld;
       const int rq = htid & 63, hw = htid >> 6;
       if (4 * rq >= rows_valid) return;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int cu = hw * 4 + k;
-        if (n0 + cu * 8 >= a.Cout) continue;
+        if (cb + cu * 8 >= a.Cout) continue;
         uint2 col[8];
 #pragma unroll
         for (int c = 0; c < 8; ++c) col[c] = *reinterpret_cast<const uint2*>(img + (cu * 8 + c) * CSO + rq * 8);
@@ -226,7 +248,12 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
           u.y = __builtin_amdgcn_perm((e >> 1) ? col[3].y : col[3].x, (e >> 1) ? col[2].y : col[2].x, sel);
           u.z = __builtin_amdgcn_perm((e >> 1) ? col[5].y : col[5].x, (e >> 1) ? col[4].y : col[4].x, sel);
           u.w = __builtin_amdgcn_perm((e >> 1) ? col[7].y : col[7].x, (e >> 1) ? col[6].y : col[6].x, sel);
-          bf16* p = outb + (long)rl * a.out_ld + n0 + cu * 8;
+          bf16* p = outb + (long)rl * a.out_ld + cb + cu * 8;
+          if (g.fold == 2) {  // tile frame u -> output frame 2u + par
+            const int fl = rl / V, v = rl - fl * V, fr = 2 * (ti.f0 + fl) + par;
+            if (fr >= a.T_out) continue;
+            p = outs + ((long)fr * V + v) * a.out_ld + cb + cu * 8;
+          }
           if (a.accumulate) {
             float f[8], o[8];
             unpack16(u, f, (bf16*)nullptr);
@@ -273,7 +300,7 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
   const int lr = lane & 31, lh = lane >> 5;
   // B fragment j at k-step (t, ks) of item (ct, gi): the contiguous 1-KiB block
   // [t][c32 = ct*BN/32 + wn*TN + j][k16 = gi*4 + ks] of the fragment image (stgcn_pack_weight_frag)
-  const int c32n = a.Cout_pad / 32, k16n = a.Cin_pad / 16;
+  const int c32n = g.wc32, k16n = g.wk16;
   const int kcc = c32n * k16n * 512;  // elements per tap
   const int wnu = __builtin_amdgcn_readfirstlane(wn);
   const int wlane = lane * 8;
@@ -325,7 +352,7 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
   auto dump = [&](int w, char* img) {
     int gi;
     const int tile = item_tile(w, gi);
-    const TileInfo ti = tile_info(tile, g, a.T_out);
+    const TileInfo ti = tile_info(tile, g);
     const int rows_valid = ti.fe * V;
     const int n0 = ti.ct * BN;
 #pragma unroll
@@ -394,8 +421,9 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
   }
   lds_barrier();  // P
 
-  const int qsign = a.trans ? -1 : 1;
-  const int qbase = a.trans ? KT - 1 : 0;
+  const bool rev = a.trans && g.fold == 0;  // stride-1 data grad: taps reversed
+  const int qsign = rev ? -1 : 1;
+  const int qbase = rev ? KTAP - 1 : 0;
   for (int w = 0; w < nitems; w += 2) {
     const int woff0 = item_woff(w), woff1 = item_woff(w + 1), woff2 = item_woff(w + 2);
     // per-lane/uniform address bases re-materialised each pair (opaque to LICM: otherwise the
@@ -461,7 +489,46 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
   if (wave == 0) tflush(0);
 }
 
+// Parity-folded fragment image of a stride-2 Kt = 9 weight [9][Co][Ci] (fp32, any strides): the 5-tap
+// conv the wide kernel runs instead (see conv_wide_launch) —
+//   forward   W'[t][co][par*Ci + ci] = W[2t + par][co][ci]
+//   data grad W'[t][par*Co + co][ci] = W[8 - 2t + par][co][ci]      (taps outside 0..8 are zero)
+// laid out like stgcn_pack_weight_frag (1-KiB blocks [t][co'/32][ci'/16]).
+__global__ void pack_s2frag_kernel(const float* __restrict__ src, long s0, long s1, long s2, int Co, int Ci, int trans,
+                                   int co_f, int ci_f, bf16* __restrict__ dst) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = 5L * co_f * ci_f;
+  if (idx >= total) return;
+  const int cip = (int)(idx % ci_f);
+  const int cop = (int)((idx / ci_f) % co_f);
+  const int t = (int)(idx / ((long)co_f * ci_f));
+  int co = cop, ci = cip, dt;
+  if (trans) {
+    const int par = cop >= Co;
+    co = cop - par * Co;
+    dt = 8 - 2 * t + par;
+  } else {
+    const int par = cip >= Ci;
+    ci = cip - par * Ci;
+    dt = 2 * t + par;
+  }
+  const float v = (dt >= 0 && dt <= 8) ? src[dt * s0 + co * s1 + ci * s2] : 0.f;
+  const long blk = ((long)t * (co_f / 32) + cop / 32) * (ci_f / 16) + cip / 16;
+  const int l = ((cip & 15) >> 3) * 32 + (cop & 31);
+  dst[blk * 512 + l * 8 + (cip & 7)] = (bf16)v;
+}
+
 }  // namespace
+
+int pack_s2frag_launch(const float* src, long s0, long s1, long s2, int Co, int Ci, void* dst, int trans,
+                       hipStream_t s) {
+  const int co_f = trans ? 2 * Co : Co, ci_f = trans ? Ci : 2 * Ci;
+  if (co_f % 32 || ci_f % 16) return STGCN_EBADSHAPE;
+  const long total = 5L * co_f * ci_f;
+  hipLaunchKernelGGL(pack_s2frag_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, src, s0, s1, s2, Co,
+                     Ci, trans, co_f, ci_f, (bf16*)dst);
+  return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
+}
 
 long long* wide_dbg_ptr = nullptr;
 int wide_debug_read(long long* host, long n) {
@@ -475,21 +542,53 @@ long conv_rows_num_row_blocks(long M, int cout);
 int conv_wide_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
   static const bool off = getenv("STGCN_NO_WIDE") != nullptr;  // A/B switch
   if (off || dtype != 1 || !a.w_frag) return -1;
-  if (a.Kt != KT || a.pad != (KT - 1) / 2 || a.stride != 1 || a.T_in != a.T_out) return -1;
+  if (a.Kt != 9 || a.pad != 4) return -1;
   if (a.pro != 0 && a.pro != 1) return -1;
   if (a.bias_mode != 0 && a.bias_mode != 1) return -1;
-  if (a.Cin != a.Cin_pad || a.Cin_pad % (2 * KG) || a.in_ld % 8 || a.V > 32) return -1;
-  if (a.Cout % 8 || a.out_ld % 8) return -1;  // 16-B row stores of the epilogue
-  const int BN = 128;  // BN = 256 (acc 256 + B ring) does not fit the register file without spills
-  if (a.Cout_pad % BN) return -1;
+  if (a.in_ld % 8 || a.V > 32 || a.Cin % 8 || a.Cout % 8 || a.out_ld % 8) return -1;
   WGeom g;
   g.dbg = nullptr;
+  int ktap, cin_f, cout_f;  // folded conv: taps, input / output channels
+  if (a.stride == 1) {
+    if (a.T_in != a.T_out) return -1;
+    g.fold = 0;
+    ktap = 9;
+    cin_f = a.Cin;
+    cout_f = a.Cout;
+    g.T_tile = a.T_out;
+  } else if (a.stride == 2 && !a.trans) {
+    // y[f] = sum_{j=-2..2} [W(2j+4) | W(2j+5)] (x[2(f+j)], x[2(f+j)+1]): a 5-tap conv over frame pairs
+    if (a.T_out != (a.T_in - 1) / 2 + 1) return -1;
+    g.fold = 1;
+    ktap = 5;
+    cin_f = 2 * a.Cin;
+    cout_f = a.Cout;
+    g.T_tile = a.T_out;
+    g.cpar = a.Cin / KG;
+    if (a.Cin % KG) return -1;
+  } else if (a.stride == 2 && a.trans) {
+    // [dx(2u) | dx(2u+1)] = sum_{j=-2..2} [Wd(4-2j) ; Wd(5-2j)] dy(u+j): a 5-tap conv with 2*Cout outputs
+    if (a.T_in != (a.T_out - 1) / 2 + 1 || a.bias_mode != 0 || a.stats || a.pro != 0) return -1;
+    g.fold = 2;
+    ktap = 5;
+    cin_f = a.Cin;
+    cout_f = 2 * a.Cout;
+    g.T_tile = a.T_in;
+    g.cpar = a.Cout;
+    if (a.Cout % 128) return -1;
+  } else {
+    return -1;
+  }
+  if (cin_f % (2 * KG) || cout_f % 128) return -1;  // unpadded folded channels: the image is exact
+  const int BN = 128;  // BN = 256 (acc 256 + B ring) does not fit the register file without spills
+  g.wc32 = cout_f / 32;
+  g.wk16 = cin_f / 16;
   g.F = 256 / a.V;
-  g.HR = (g.F + KT - 1) * a.V;
+  g.HR = (g.F + ktap - 1) * a.V;
   if (g.HR > HR_CAP || g.F < 1) return -1;
-  g.G = a.Cin_pad / KG;
-  g.tiles_n = (a.T_out + g.F - 1) / g.F;
-  g.ncol = a.Cout_pad / BN;
+  g.G = cin_f / KG;
+  g.tiles_n = (g.T_tile + g.F - 1) / g.F;
+  g.ncol = cout_f / BN;
   const long nt = (long)a.N * g.tiles_n * g.ncol;
   if (nt <= 0 || nt > 0x7fffffffL) return -1;
   g.ntiles = (int)nt;
@@ -506,25 +605,26 @@ int conv_wide_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
   }
   const int tpb = (g.ntiles + ncu - 1) / ncu;
   const int grid = (g.ntiles + tpb - 1) / tpb;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_wide_kernel<128, 6, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-    (void)hipFuncSetAttribute((const void*)conv_wide_kernel<128, 6, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-    attr = true;
-  }
-  const dim3 gd((unsigned)grid), bd(2 * NT), bd2(2 * NT);
+  const dim3 gd((unsigned)grid), bd(2 * NT);
   static const int dbg = getenv("STGCN_WIDE_DBG") ? atoi(getenv("STGCN_WIDE_DBG")) : 0;
-  if (dbg) {
-    static long long* dbuf = nullptr;
-    if (!dbuf) (void)hipMalloc(&dbuf, 16 * 4096 * sizeof(long long));
-    wide_dbg_ptr = dbuf;
-    g.dbg = dbuf;
-    auto* k = dbg == 2 ? conv_wide_kernel<128, 6, 1, 2> : conv_wide_kernel<128, 6, 1, 4>;
+  auto kern = [&]() -> void (*)(const stgcn_conv_desc, const WGeom) {
+    if (dbg && ktap == 9) {
+      static long long* dbuf = nullptr;
+      if (!dbuf) (void)hipMalloc(&dbuf, 16 * 4096 * sizeof(long long));
+      wide_dbg_ptr = dbuf;
+      g.dbg = dbuf;
+      return dbg == 2 ? conv_wide_kernel<128, 9, 6, 1, 2> : conv_wide_kernel<128, 9, 6, 1, 4>;
+    }
+    if (ktap == 9) return a.pro ? conv_wide_kernel<128, 9, 6, 1> : conv_wide_kernel<128, 9, 6, 0>;
+    return a.pro ? conv_wide_kernel<128, 5, 5, 1> : conv_wide_kernel<128, 5, 5, 0>;
+  };
+  auto* k = kern();
+  static bool attr[4] = {false, false, false, false};
+  const int ai = (ktap == 9 ? 0 : 2) + (a.pro ? 1 : 0);
+  if (!attr[ai] || dbg) {
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-    hipLaunchKernelGGL(k, gd, bd2, lds, s, a, g);
-    return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
+    attr[ai] = true;
   }
-  if (a.pro) hipLaunchKernelGGL((conv_wide_kernel<128, 6, 1>), gd, bd, lds, s, a, g);
-  else hipLaunchKernelGGL((conv_wide_kernel<128, 6, 0>), gd, bd, lds, s, a, g);
+  hipLaunchKernelGGL(k, gd, bd, lds, s, a, g);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }

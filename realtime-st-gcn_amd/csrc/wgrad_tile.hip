@@ -375,6 +375,14 @@ int launch_w(const stgcn_wgrad_desc& a, const Plan& p, hipStream_t s) {
 
 }  // namespace
 
+// level 1 of slab_reduce alone: part[RS][E] = fixed-order sums of the R slabs; returns RS (< 0 on error)
+int slab_reduce1_launch(const float* slab, int R, long E, float* part, hipStream_t s) {
+  const int RS = R < RS_MAX ? R : RS_MAX;
+  const unsigned blocks = (unsigned)((E / 4 + 255) / 256);
+  hipLaunchKernelGGL(slab_reduce1_kernel, dim3(blocks, RS), dim3(256), 0, s, slab, R, RS, E, part);
+  return hipGetLastError() == hipSuccess ? RS : -STGCN_EHIP;
+}
+
 // deterministic two-level sum of R fp32 slabs [R][E] into dw (+=); part holds RS_MAX * E floats
 int slab_reduce_launch(const float* slab, int R, long E, float* part, float* dw, hipStream_t s) {
   const int RS = R < RS_MAX ? R : RS_MAX;

@@ -29,7 +29,6 @@
 
 namespace {
 
-constexpr int KT = 9, PADT = 4;
 constexpr int NT = 512;              // 8 waves
 constexpr int KM = 128;              // K rows per tile (F*V <= 128, rest zero rows)
 constexpr int PR = 64;               // bytes per panel row (32 bf16 channels)
@@ -71,11 +70,14 @@ struct WWGeom {
   int tiles_n;   // tiles per sample
   int tpb;       // tiles per block (contiguous range of the sample-major tile sequence)
   int R;         // row-range blocks per output block (slab count)
-  float* slab;   // [R][KT][Cout][Cin]
+  int fold;      // 1: stride-2 conv folded into 5 taps over frame pairs (input channels 2*Cin, parity-major)
+  int cin_f;     // input channels of the (folded) GEMM
+  float* slab;   // [R][KTAP][Cout][cin_f]
 };
 
-template <int PRO>
+template <int PRO, int KTAP>
 __global__ __launch_bounds__(NT, 1) void wgrad_wide_kernel(const stgcn_wgrad_desc a, const WWGeom g) {
+  constexpr int KT = KTAP, PADT = (KTAP - 1) / 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int V = a.V, F = g.F;
   const int XP = g.MS * V * PR;                 // bytes per input panel (ring + mirror)
@@ -84,7 +86,11 @@ __global__ __launch_bounds__(NT, 1) void wgrad_wide_kernel(const stgcn_wgrad_des
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wc = wave >> 1, wi = wave & 1;      // co tile (32), ci tile (32)
   const int ob = blockIdx.x % (g.nco * g.nci), rg = blockIdx.x / (g.nco * g.nci);
-  const int co0 = (ob % g.nco) * COB, ci0 = (ob / g.nco) * CIB;
+  const int co0 = (ob % g.nco) * COB, cf0 = (ob / g.nco) * CIB;  // cf0: folded input channel
+  // fold: ring frame z holds input frame 2z + par of the source channels ci0 .. ci0+63
+  const int par = g.fold ? cf0 / a.Cin : 0;
+  const int ci0 = cf0 - par * a.Cin;
+  const int fmul = g.fold ? 2 : 1;
   const int tiles_n = g.tiles_n;
   const int k_begin = rg * g.tpb, k_end = min(a.N * tiles_n, k_begin + g.tpb);
 
@@ -128,8 +134,9 @@ __global__ __launch_bounds__(NT, 1) void wgrad_wide_kernel(const stgcn_wgrad_des
       rx[i] = make_uint4(0, 0, 0, 0);
       if (r < nf * V) {
         const int fl = r / V, v = r - fl * V, f = fa + fl;
-        if (cok && f >= 0 && f < a.T_in)
-          rx[i] = *reinterpret_cast<const uint4*>(xin + (((long)n * a.T_in + f) * V + v) * a.in_ld + ci0 + xcu * 8);
+        const int fs = fmul * f + par;  // source frame
+        if (cok && f >= 0 && fs < a.T_in)
+          rx[i] = *reinterpret_cast<const uint4*>(xin + (((long)n * a.T_in + fs) * V + v) * a.in_ld + ci0 + xcu * 8);
       }
     });
   };
@@ -139,7 +146,7 @@ __global__ __launch_bounds__(NT, 1) void wgrad_wide_kernel(const stgcn_wgrad_des
       if (r < nf * V) {
         const int fl = r / V, v = r - fl * V, f = fa + fl;
         uint4 u = rx[i];
-        if (PRO == 1 && f >= 0 && f < a.T_in) {
+        if (PRO == 1 && f >= 0 && fmul * f + par < a.T_in) {
           float e[8];
           unpack16(u, e, (bf16*)nullptr);
 #pragma unroll
@@ -223,41 +230,78 @@ __global__ __launch_bounds__(NT, 1) void wgrad_wide_kernel(const stgcn_wgrad_des
   }
 
   // ---- block partial -> slab [rg][t][co][ci]: lane holds ci = ci0 + 32 wi + (lane&31), co rows acc_row
-  float* __restrict__ out = g.slab + (long)rg * KT * a.Cout * a.Cin;
-  const int ci = ci0 + 32 * wi + (lane & 31);
+  float* __restrict__ out = g.slab + (long)rg * KT * a.Cout * g.cin_f;
+  const int ci = cf0 + 32 * wi + (lane & 31);
 #pragma unroll
   for (int t = 0; t < KT; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int co = co0 + 32 * wc + acc_row(r, lane);
-      if (co < a.Cout && ci < a.Cin) out[((long)t * a.Cout + co) * a.Cin + ci] = acc[t][r];
+      if (co < a.Cout && ci < g.cin_f) out[((long)t * a.Cout + co) * g.cin_f + ci] = acc[t][r];
     }
 }
 
 struct WPlan {
   bool ok;
   WWGeom g;
+  int ktap;
   size_t lds;
   long slab_elems;
 };
 
 constexpr int RS_PART = 16;  // level-1 partials of slab_reduce
 
+// level 2 of the folded reduction: dW[2t + par][co][ci] += sum_r part[r][t][co][par*Cin + ci]
+__global__ void unfold_reduce2_kernel(const float* __restrict__ part, int RS, int Cout, int Cin, float* __restrict__ dw) {
+  const long E4 = 5L * Cout * 2 * Cin / 4;
+  const long e4 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e4 >= E4) return;
+  const long e = e4 * 4;
+  const int cf = (int)(e % (2 * Cin));
+  const long tc = e / (2 * Cin);
+  const int co = (int)(tc % Cout), t = (int)(tc / Cout);
+  const int par = cf / Cin, ci = cf - par * Cin, dt = 2 * t + par;
+  if (dt > 8) return;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int r = 0; r < RS; ++r) {
+    const float4 v = *reinterpret_cast<const float4*>(part + (long)r * 4 * E4 + e);
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  float4* d = reinterpret_cast<float4*>(dw + ((long)dt * Cout + co) * Cin + ci);
+  float4 o = *d;
+  o.x += acc.x; o.y += acc.y; o.z += acc.z; o.w += acc.w;
+  *d = o;
+}
+
 WPlan wplan(const stgcn_wgrad_desc& a) {
   WPlan p{};
   p.ok = false;
   static const bool off = getenv("STGCN_NO_WGRAD_WIDE") != nullptr;  // A/B switch
   if (off) return p;
-  if (a.Kt != KT || a.pad != PADT || a.stride != 1 || a.T_in != a.T_out) return p;
+  if (a.Kt != 9 || a.pad != 4) return p;
+  WWGeom& g = p.g;
+  if (a.stride == 1 && a.T_in == a.T_out) {
+    g.fold = 0;
+    p.ktap = 9;
+    g.cin_f = a.Cin;
+  } else if (a.stride == 2 && a.T_out == (a.T_in - 1) / 2 + 1 && a.Cin % CIB == 0) {
+    // dW[2t + par][co][ci] = sum_f dY[f][co] x[2(f + t - 2) + par][ci]: a 5-tap weight gradient over
+    // frame pairs (input channels parity-major, 2*Cin), unfolded by the final reduction
+    g.fold = 1;
+    p.ktap = 5;
+    g.cin_f = 2 * a.Cin;
+  } else {
+    return p;
+  }
   if (a.pro != 0 && a.pro != 1) return p;
   if (a.Cout < COB || a.Cin < CIB || a.Cout % 8 || a.Cin % 8 || a.in_ld % 8 || a.dy_ld % 8 || a.V > 32) return p;
-  WWGeom& g = p.g;
+  const int padt = (p.ktap - 1) / 2;
   g.F = KM / a.V;
-  g.RS = 2 * g.F + 2 * PADT;
-  g.MS = g.RS + g.F + 2 * PADT - 1;  // a window starting at slot RS-1 ends at slot MS-1
+  g.RS = 2 * g.F + 2 * padt;
+  g.MS = g.RS + g.F + 2 * padt - 1;  // a window starting at slot RS-1 ends at slot MS-1
   if (g.F < 1 || g.F * a.V > KM || g.F * a.V > 64 * X_U) return p;
   g.nco = (a.Cout + COB - 1) / COB;
-  g.nci = (a.Cin + CIB - 1) / CIB;
+  g.nci = (g.cin_f + CIB - 1) / CIB;
   const int nob = g.nco * g.nci;
   g.tiles_n = (a.T_out + g.F - 1) / g.F;
   const long total = (long)a.N * g.tiles_n;
@@ -272,7 +316,7 @@ WPlan wplan(const stgcn_wgrad_desc& a) {
   // the allocation (they land in the dY buffers; finite, multiplied by zero dY rows)
   p.lds = 2 * (size_t)g.MS * a.V * PR + 2 * (size_t)DY_BYTES;
   if (p.lds > LDS_MAX || (size_t)(KM - g.F * a.V) * PR > 2 * (size_t)DY_BYTES) return p;
-  p.slab_elems = (long)(g.R + RS_PART) * KT * a.Cout * a.Cin;
+  p.slab_elems = (long)(g.R + RS_PART) * p.ktap * a.Cout * g.cin_f;
   p.ok = true;
   return p;
 }
@@ -280,6 +324,7 @@ WPlan wplan(const stgcn_wgrad_desc& a) {
 }  // namespace
 
 int slab_reduce_launch(const float* slab, int R, long E, float* part, float* dw, hipStream_t s);
+int slab_reduce1_launch(const float* slab, int R, long E, float* part, hipStream_t s);
 
 long wgrad_wide_workspace(const stgcn_wgrad_desc& a, int dtype) {
   if (dtype != 1) return 0;
@@ -293,18 +338,23 @@ int wgrad_wide_launch(const stgcn_wgrad_desc& a, int dtype, hipStream_t s) {
   WPlan p = wplan(a);
   if (!p.ok || a.work_bytes < p.slab_elems * (long)sizeof(float)) return -1;
   p.g.slab = reinterpret_cast<float*>(a.work);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)wgrad_wide_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)wgrad_wide_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
+  auto* k = p.ktap == 9 ? (a.pro == 1 ? wgrad_wide_kernel<1, 9> : wgrad_wide_kernel<0, 9>)
+                        : (a.pro == 1 ? wgrad_wide_kernel<1, 5> : wgrad_wide_kernel<0, 5>);
+  static bool attr[4] = {false, false, false, false};
+  const int ai = (p.ktap == 9 ? 0 : 2) + (a.pro == 1 ? 1 : 0);
+  if (!attr[ai]) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+    attr[ai] = true;
   }
   const unsigned grid = (unsigned)(p.g.nco * p.g.nci * p.g.R);
-  if (a.pro == 1)
-    hipLaunchKernelGGL(wgrad_wide_kernel<1>, dim3(grid), dim3(NT), p.lds, s, a, p.g);
-  else
-    hipLaunchKernelGGL(wgrad_wide_kernel<0>, dim3(grid), dim3(NT), p.lds, s, a, p.g);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(NT), p.lds, s, a, p.g);
   if (hipGetLastError() != hipSuccess) return STGCN_EHIP;
-  const long E = (long)KT * a.Cout * a.Cin;
-  return slab_reduce_launch(p.g.slab, p.g.R, E, p.g.slab + (long)p.g.R * E, a.dw, s);
+  const long E = (long)p.ktap * a.Cout * p.g.cin_f;
+  float* part = p.g.slab + (long)p.g.R * E;
+  if (!p.g.fold) return slab_reduce_launch(p.g.slab, p.g.R, E, part, a.dw, s);
+  const int RS = slab_reduce1_launch(p.g.slab, p.g.R, E, part, s);
+  if (RS < 0) return -RS;
+  hipLaunchKernelGGL(unfold_reduce2_kernel, dim3((unsigned)((E / 4 + 255) / 256)), dim3(256), 0, s, (const float*)part,
+                     RS, a.Cout, a.Cin, a.dw);
+  return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }

@@ -134,7 +134,7 @@ class StgcnLayerFunction(torch.autograd.Function):
 
         # ---- temporal conv on relu(norm1(g)) (norm applied in the prologue)
         wt3 = wt.detach().float().squeeze(-1).permute(2, 0, 1)  # [Kt][Cout][Cin]
-        wtp, cpt, kpt = K.pack_weight(wt3, dtype)
+        wtp, cpt, kpt = K.pack_weight(wt3, dtype, stride=stride)
         u = K.conv_rows(g, wtp, Cout, Cout, cpt, kpt, T, T_out, Kt=kt, stride=stride, pad=pad,
                         bias=bt.detach().float().contiguous(), stats=st2 if norm == BN else None,
                         tag=f"tcn_fwd_c{Cout}" if stride == 1 else None, **pro1)
@@ -265,7 +265,7 @@ class StgcnLayerFunction(torch.autograd.Function):
 
         # ---- temporal conv: dh = conv^T(du), dWt, dbt
         wtT = wt.detach().float().squeeze(-1).permute(2, 1, 0)  # [Kt][Cin=Cout][Cout]: W[co][ci][dt] -> [dt][ci][co]
-        wtTp, cq, kq = K.pack_weight(wtT, dtype)
+        wtTp, cq, kq = K.pack_weight(wtT, dtype, stride=stride, trans=True)
         dh = K.conv_rows(du, wtTp, Cout, Cout, cq, kq, T_out, T, Kt=kt, stride=stride, pad=pad, trans=True)
         if norm == BN:
             pro1 = dict(pro=1, pro_a=sc1, pro_b=sh1)

@@ -56,12 +56,14 @@ def row_blocks(M: int, cout: int) -> int:
     return L.lib().stgcn_conv_rows_row_blocks(M, cout)
 
 
-def pack_weight(w3: torch.Tensor, dtype) -> tuple:
+def pack_weight(w3: torch.Tensor, dtype, stride: int = 1, trans: bool = False) -> tuple:
     """[Kt][Cout][Cin] float weight -> padded contiguous [Kt][Cout_pad][Cin_pad] of ``dtype``.
 
     bf16 Kt=9 weights with >= 128 (padded) channels on both sides also get the MFMA-fragment image the
     wide-channel conv kernel reads (stgcn_pack_weight_frag), in the same allocation; ``out.frag_ptr``
-    is its address (conv_rows passes it as ``w_frag``)."""
+    is its address and ``out.frag_stride`` the conv stride it is for (conv_rows passes it as ``w_frag``
+    to calls of that stride).  For ``stride=2`` the image is the parity-folded 5-tap form
+    (stgcn_pack_weight_s2frag, ``trans`` selecting the data-gradient fold)."""
     Kt, Co, Ci = w3.shape
     cp = -(-Co // col_tile(Co)) * col_tile(Co)
     kp = -(-Ci // 32) * 32
@@ -69,13 +71,23 @@ def pack_weight(w3: torch.Tensor, dtype) -> tuple:
         w3 = w3.float()
     s0, s1, s2 = w3.stride()
     n = Kt * cp * kp
-    if dtype == torch.bfloat16 and Kt == 9 and cp % 128 == 0 and kp % 128 == 0:
+    if dtype == torch.bfloat16 and Kt == 9 and stride == 2 and Co % 64 == 0 and Ci % 64 == 0:
+        nf = 5 * 2 * Co * Ci
+        buf = torch.empty(n + nf, dtype=dtype, device=w3.device)
+        out = buf[:n].view(Kt, cp, kp)
+        L.check(L.lib().stgcn_pack_weight(w3.data_ptr(), s0, s1, s2, Kt, Co, Ci, out.data_ptr(), cp, kp,
+                                          L.dtype_code(dtype), L.stream()), "pack_weight")
+        L.check(L.lib().stgcn_pack_weight_s2frag(w3.data_ptr(), s0, s1, s2, Co, Ci, buf[n:].data_ptr(), int(trans),
+                                                 L.dtype_code(dtype), L.stream()), "pack_weight_s2frag")
+        out.frag_ptr, out.frag_stride = buf[n:].data_ptr(), 2
+        return out, cp, kp
+    if dtype == torch.bfloat16 and Kt == 9 and stride == 1 and cp % 128 == 0 and kp % 128 == 0:
         buf = torch.empty(2 * n, dtype=dtype, device=w3.device)
         out = buf[:n].view(Kt, cp, kp)
         L.check(L.lib().stgcn_pack_weight_frag(w3.data_ptr(), s0, s1, s2, Kt, Co, Ci, out.data_ptr(),
                                                buf[n:].data_ptr(), cp, kp, L.dtype_code(dtype), L.stream()),
                 "pack_weight_frag")
-        out.frag_ptr = buf[n:].data_ptr()
+        out.frag_ptr, out.frag_stride = buf[n:].data_ptr(), 1
         return out, cp, kp
     out = torch.empty((Kt, cp, kp), dtype=dtype, device=w3.device)
     L.check(L.lib().stgcn_pack_weight(w3.data_ptr(), s0, s1, s2, Kt, Co, Ci, out.data_ptr(), cp, kp,
@@ -94,7 +106,7 @@ def conv_rows(x, w3p, Cin, Cout, cp, kp, T_in, T_out, Kt=1, stride=1, pad=0, tra
         out = cl_empty(N, Cout, T_out, V, x.dtype, x.device)
     d = L.ConvDesc()
     d.in_, d.out, d.w = x.data_ptr(), out.data_ptr(), w3p.data_ptr()
-    d.w_frag = getattr(w3p, "frag_ptr", None)
+    d.w_frag = getattr(w3p, "frag_ptr", None) if getattr(w3p, "frag_stride", 0) == stride else None
     d.bias = L.ptr(bias)
     d.pro_a, d.pro_b, d.pro_stats = L.ptr(pro_a), L.ptr(pro_b), L.ptr(pro_stats)
     d.stats = L.ptr(stats)

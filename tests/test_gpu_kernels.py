@@ -26,7 +26,8 @@ def cl(x, dtype=torch.float32):
                                                   (128, 256, 9, 1, 12), (8, 64, 1, 1, 5), (64, 52, 1, 1, 1),
                                                   (24, 48, 9, 2, 11), (768, 256, 1, 1, 9), (256, 768, 1, 1, 9),
                                                   (256, 256, 9, 1, 10), (4, 8, 9, 2, 9), (64, 128, 1, 2, 21),
-                                                  (128, 128, 9, 2, 31), (128, 256, 1, 2, 8)])
+                                                  (128, 128, 9, 2, 31), (128, 256, 1, 2, 8), (256, 256, 9, 2, 20),
+                                                  (128, 256, 9, 2, 30), (256, 128, 9, 2, 151)])
 def test_conv_rows_fwd_and_trans(K, dtype, tol, cin, cout, kt, stride, T):
     torch.manual_seed(0)
     N, V = 3, 25
@@ -36,7 +37,7 @@ def test_conv_rows_fwd_and_trans(K, dtype, tol, cin, cout, kt, stride, T):
     b = torch.randn(cout)
     ref = F.conv2d(x, w, b, stride=(stride, 1), padding=(pad, 0))
     T_out = ref.shape[2]
-    wp, cp, kp = K.pack_weight(w.squeeze(-1).permute(2, 0, 1).to(DEV), dtype)
+    wp, cp, kp = K.pack_weight(w.squeeze(-1).permute(2, 0, 1).to(DEV), dtype, stride=stride)
     y = K.conv_rows(cl(x, dtype), wp, cin, cout, cp, kp, T, T_out, Kt=kt, stride=stride, pad=pad,
                     bias=b.to(DEV))
     assert_close(y.float(), ref, tol, "conv fwd")
@@ -44,7 +45,7 @@ def test_conv_rows_fwd_and_trans(K, dtype, tol, cin, cout, kt, stride, T):
     dy = torch.randn(ref.shape)
     xr = x.clone().requires_grad_(True)
     F.conv2d(xr, w, b, stride=(stride, 1), padding=(pad, 0)).backward(dy)
-    wtp, cq, kq = K.pack_weight(w.squeeze(-1).permute(2, 1, 0).to(DEV), dtype)
+    wtp, cq, kq = K.pack_weight(w.squeeze(-1).permute(2, 1, 0).to(DEV), dtype, stride=stride, trans=True)
     dx = K.conv_rows(cl(dy, dtype), wtp, cout, cin, cq, kq, T_out, T, Kt=kt, stride=stride, pad=pad, trans=True)
     assert_close(dx.float(), xr.grad, tol, "conv trans")
 
@@ -292,19 +293,51 @@ def test_conv_wide_prologue_stats(K, cin, cout, T, N):
     assert_close(dx.float(), xr.grad, 2e-2, "wide conv trans")
 
 
-@pytest.mark.parametrize("cin,cout,T,N", [(128, 128, 37, 3), (256, 256, 23, 2), (64, 256, 16, 3), (256, 128, 150, 2)])
-def test_wgrad_wide_prologue(K, cin, cout, T, N):
-    """>= 128-output-channel Kt=9 stride-1 weight gradient (wgrad_wide.hip, frame ring, bf16) with the
-    BN1+ReLU prologue, against torch fp32."""
+@pytest.mark.parametrize("cin,cout,T,N,stride", [(128, 128, 37, 3, 1), (256, 256, 23, 2, 1), (64, 256, 16, 3, 1),
+                                                 (256, 128, 150, 2, 1), (128, 128, 300, 2, 2), (256, 256, 41, 2, 2),
+                                                 (64, 128, 30, 3, 2)])
+def test_wgrad_wide_prologue(K, cin, cout, T, N, stride):
+    """>= 128-output-channel Kt=9 weight gradient (wgrad_wide.hip, frame ring, bf16; stride 2 folded into
+    5 taps over frame pairs) with the BN1+ReLU prologue, against torch fp32."""
     torch.manual_seed(7)
     V = 25
     x = torch.randn(N, cin, T, V) * 1.5 + 0.3
     pa, pb = torch.rand(cin) + 0.5, torch.randn(cin)
     h = torch.relu(x * pa.view(1, -1, 1, 1) + pb.view(1, -1, 1, 1))
     w = (torch.randn(cout, cin, 9, 1) / (9 * cin) ** 0.5).requires_grad_(True)
-    y = F.conv2d(h, w, None, padding=(4, 0))
+    y = F.conv2d(h, w, None, stride=(stride, 1), padding=(4, 0))
     dy = torch.randn(y.shape)
     y.backward(dy)
-    dw = K.conv_wgrad(cl(x, torch.bfloat16), cl(dy, torch.bfloat16), cin, cout, T, T, Kt=9, pad=4, pro=1,
-                      pro_a=pa.to(DEV), pro_b=pb.to(DEV))
+    dw = K.conv_wgrad(cl(x, torch.bfloat16), cl(dy, torch.bfloat16), cin, cout, T, y.shape[2], Kt=9, stride=stride,
+                      pad=4, pro=1, pro_a=pa.to(DEV), pro_b=pb.to(DEV))
     assert_close(dw.cpu().permute(1, 2, 0).unsqueeze(-1), w.grad, 2e-2, "wide wgrad+prologue")
+
+
+@pytest.mark.parametrize("cin,cout,T,N", [(128, 128, 300, 2), (256, 256, 150, 2), (128, 256, 33, 3)])
+def test_conv_wide_stride2_prologue_stats(K, cin, cout, T, N):
+    """Stride-2 Kt=9 conv folded into a 5-tap conv over frame pairs (conv_wide.hip fold 1/2): BN1+ReLU
+    prologue, bias, BN2 partials, and the data gradient, against torch fp32."""
+    torch.manual_seed(4)
+    V = 25
+    x = torch.randn(N, cin, T, V) * 1.5 + 0.5
+    sc, sh = torch.rand(cin) + 0.5, torch.randn(cin)
+    w = torch.randn(cout, cin, 9, 1) / (cin * 9) ** 0.5
+    b = torch.randn(cout)
+    h = torch.relu(x * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1))
+    ref = F.conv2d(h, w, b, stride=(2, 1), padding=(4, 0))
+    T_out = ref.shape[2]
+    wp, cp, kp = K.pack_weight(w.squeeze(-1).permute(2, 0, 1).to(DEV), torch.bfloat16, stride=2)
+    st = torch.zeros((K.row_blocks(N * T_out * V, cout), cp, 4), device=DEV)
+    y = K.conv_rows(cl(x, torch.bfloat16), wp, cin, cout, cp, kp, T, T_out, Kt=9, stride=2, pad=4, bias=b.to(DEV),
+                    pro=1, pro_a=sc.to(DEV), pro_b=sh.to(DEV), stats=st)
+    assert_close(y.float(), ref, 2e-2, "s2 conv+prologue")
+    mr, _, _ = K.bn_finalize(st, st.shape[0], cp, cout, None, None)
+    yr = y.float().cpu()
+    assert_close(mr[:, 0].cpu(), yr.mean(dim=(0, 2, 3)), 2e-3, "bn mean")
+    assert_close(mr[:, 1].cpu(), 1 / torch.sqrt(yr.var(dim=(0, 2, 3), unbiased=False) + 1e-5), 2e-3, "bn rstd")
+    dy = torch.randn(ref.shape)
+    xr = x.clone().requires_grad_(True)
+    F.conv2d(xr, w, None, stride=(2, 1), padding=(4, 0)).backward(dy)
+    wtp, cq, kq = K.pack_weight(w.squeeze(-1).permute(2, 1, 0).to(DEV), torch.bfloat16, stride=2, trans=True)
+    dx = K.conv_rows(cl(dy, torch.bfloat16), wtp, cout, cin, cq, kq, T_out, T, Kt=9, stride=2, pad=4, trans=True)
+    assert_close(dx.float(), xr.grad, 2e-2, "s2 conv trans")

@@ -50,14 +50,14 @@ for name, N, T, V, Cin, Cout, Kt, s, trans, pro in cases:
     Ti, To = (T_out, T) if trans else (T, T_out)
     x = torch.randn(N, Cin, Ti, V, device=dev).to(dt).contiguous(memory_format=torch.channels_last)
     w = torch.randn(Kt, Cout, Cin, device=dev) * 0.05
-    wp, cp, kp = K.pack_weight(w, dt)
+    wp, cp, kp = K.pack_weight(w, dt, stride=s, trans=trans)
     sc = torch.rand(Cin, device=dev) + 0.5
     sh = torch.randn(Cin, device=dev)
     b = torch.randn(Cout, device=dev)
     kw = dict(pro=1, pro_a=sc, pro_b=sh) if pro else {}
     if not trans:  # forward convs feed a BatchNorm: epilogue partial statistics
         kw["stats"] = torch.zeros((K.row_blocks(N * To * V, Cout), cp, 4), device=dev)
-    f = lambda: K.conv_rows(x, wp, Cin, Cout, cp, kp, Ti, To, Kt=Kt, stride=s, pad=pad, trans=trans, bias=b, **kw)
+    f = lambda: K.conv_rows(x, wp, Cin, Cout, cp, kp, Ti, To, Kt=Kt, stride=s, pad=pad, trans=trans, bias=None if trans else b, **kw)
     ms = timeit(f)
     flops = 2.0 * N * To * V * Cin * Cout * Kt
     byts = (N * Ti * V * Cin + N * To * V * Cout) * 2
