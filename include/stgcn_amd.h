@@ -137,6 +137,30 @@ typedef struct {
 } stgcn_gconv_desc;
 
 int stgcn_gconv(const stgcn_gconv_desc* d, int dtype, void* stream);
+
+/* Fused frame-tiled graph convolution (bf16; gcn_tile.hip), A applied on the fly to whole-frame tiles:
+ *   trans_a 0 (forward, tgcn.py:71-79):  out[(i,w)][co] (+)= sum_{p,ci} W'[co][p*Cin+ci] sum_v A[p][v][w] in[(i,v)][ci]
+ *                                          (+ bias[w][co])
+ *   trans_a 1 (data grad):               out[(i,v)][c]  (+)= sum_{p,k} W'[c][p*Cin+k]  sum_w A[p][v][w] in[(i,w)][k]
+ * W' = the Kt = 1 MFMA-fragment image of stgcn_pack_weight_frag ([Cout_pad][Kw_pad], Kw_pad >= P*Cin):
+ * forward W'[co][p*Cin+ci] = W[p*Cout+co][ci]; data grad (in = dg, Cin = conv Cout, Cout = conv Cin)
+ * W'[ci][p*Cout+co] = W[p*Cout+co][ci].  A: [P][V][V] fp32 (A * edge importance).  dmax[p] >= the
+ * largest number of nonzeros of a column (trans_a 0) / row (trans_a 1) of A[p].  Optional BN partial
+ * statistics [stgcn_gcn_tile_row_blocks][Cout_pad] as stgcn_conv_rows.
+ * Replaces: conv1x1 + einsum of ConvTemporalGraphical.forward (tgcn.py:71-79) and its input grad. */
+typedef struct {
+  const void* in;
+  void* out;
+  const void* w_frag;
+  const float* A;
+  const float* bias; /* [V][Cout] or NULL */
+  float* stats;
+  int NT, V, P, Cin, Cout, Cout_pad, Kw_pad, in_ld, out_ld, trans_a, accumulate;
+  int dmax[4];
+} stgcn_gcn_tile_desc;
+
+int stgcn_gcn_tile(const stgcn_gcn_tile_desc* d, int dtype, void* stream);
+long stgcn_gcn_tile_row_blocks(int NT, int V);
 long stgcn_gconv_row_blocks(int NT, int V);
 int stgcn_gconv_weights(const float* A, const float* W, const int* nbr, const int* deg, int P, int V, int J, int Cout,
                         int Cin, int trans, void* out, int rows_pad, int cols_pad, int dtype, void* stream);

@@ -29,6 +29,13 @@ class ConvDesc(ctypes.Structure):
                [("w_frag", c_void_p)]
 
 
+class GcnTileDesc(ctypes.Structure):
+    _fields_ = [("in_", c_void_p), ("out", c_void_p), ("w_frag", c_void_p), ("A", c_void_p), ("bias", c_void_p),
+                ("stats", c_void_p)] + \
+               [(n, c_int) for n in ("NT", "V", "P", "Cin", "Cout", "Cout_pad", "Kw_pad", "in_ld", "out_ld",
+                                     "trans_a", "accumulate")] + [("dmax", c_int * 4)]
+
+
 class WgradDesc(ctypes.Structure):
     _fields_ = [("in_", c_void_p), ("dy", c_void_p), ("dw", c_void_p), ("pro_a", c_void_p), ("pro_b", c_void_p),
                 ("pro_stats", c_void_p)] + \
@@ -86,6 +93,8 @@ _SIGS = {
     "stgcn_gcn_bias_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "stgcn_pack_weight": (c_int, [c_void_p, ctypes.c_long, ctypes.c_long, ctypes.c_long, c_int, c_int, c_int,
                                   c_void_p, c_int, c_int, c_int, c_void_p]),
+    "stgcn_gcn_tile": (c_int, [ctypes.POINTER(GcnTileDesc), c_int, c_void_p]),
+    "stgcn_gcn_tile_row_blocks": (ctypes.c_long, [c_int, c_int]),
     "stgcn_pack_weight_s2frag": (c_int, [c_void_p, ctypes.c_long, ctypes.c_long, ctypes.c_long, c_int, c_int,
                                          c_void_p, c_int, c_int, c_void_p]),
     "stgcn_pack_weight_frag": (c_int, [c_void_p, ctypes.c_long, ctypes.c_long, ctypes.c_long, c_int, c_int, c_int,

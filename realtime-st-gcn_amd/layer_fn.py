@@ -101,15 +101,25 @@ class StgcnLayerFunction(torch.autograd.Function):
         # ---- graph convolution: g = sum_p A_p-mix(x) W_p + bias2d
         sup = cfg[5] if len(cfg) > 5 else None
         gather = sup is not None and A32.dim() == 3 and not sup.dense(P)
+        tiled = gather and K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype)  # fused frame-tiled graph conv
         bias2d = K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
         if norm == BN:  # all BatchNorm partial-statistics buffers of the layer from one zero fill
             cpo = -(-Cout // K.col_tile(Cout)) * K.col_tile(Cout)
-            st_shapes = [(K.gconv_row_blocks(N * T, V) if gather else K.row_blocks(M1, Cout), cpo, 4),
+            rb1 = (K.gcn_tile_row_blocks(N * T, V) if tiled else K.gconv_row_blocks(N * T, V)) if gather \
+                else K.row_blocks(M1, Cout)
+            st_shapes = [(rb1, cpo, 4),
                          (K.row_blocks(M2, Cout), cpo, 4)] + ([(K.row_blocks(M2, Cout), cpo, 4)] if res_conv else [])
             st_all = K.zeros_arena(dev, *st_shapes)
             st1, st2 = st_all[0], st_all[1]
             str_ = st_all[2] if res_conv else None
-        if gather:  # joint-gathered GEMM over per-joint effective weights (gconv.hip), no XA in HBM
+        if tiled:  # A-mix on the fly into the MFMA operand of whole-frame tiles (gcn_tile.hip)
+            wgf = wg.detach().float().view(P, Cout, Cin).permute(1, 0, 2).reshape(Cout, P * Cin)  # W'[co][p*Cin+ci]
+            wimg, cpg, kwg = K.pack_frag1(wgf, dtype)
+            if norm == BN:
+                assert cpg == cpo
+            g = K.gcn_tile(x, A32, wimg, kwg, Cin, Cout, cpg, sup, bias=bias2d, stats=st1 if norm == BN else None)
+            XA = None
+        elif gather:  # joint-gathered GEMM over per-joint effective weights (gconv.hip), no XA in HBM
             wg2 = wg.detach().float().reshape(P * Cout, Cin).contiguous()
             wgp = K.gconv_weights(A32, wg2, sup, Cout, Cin, False, dtype)
             cpg, kpg = wgp.shape[2], wgp.shape[3]
@@ -299,8 +309,13 @@ class StgcnLayerFunction(torch.autograd.Function):
             # weight/adjacency grads from dWeff[w][j] = sum_i dg[(i,w)] x[(i,S(w)_j)]^T
             sup = ctx.sup
             wg2 = wg.detach().float().reshape(P * Cout, Cin).contiguous()
-            wgT = K.gconv_weights(A32, wg2, sup, Cout, Cin, True, dtype)
-            K.gconv(dg, wgT, sup, Cout, Cin, trans=True, out=dx, accumulate=dx_written)
+            if K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype):  # dx = sum_p A_p-mix(dg) W_p^T, fused (gcn_tile.hip)
+                wdf = wg.detach().float().view(P, Cout, Cin).permute(2, 0, 1).reshape(Cin, P * Cout)
+                wimgT, cq, kwT = K.pack_frag1(wdf, dtype)
+                K.gcn_tile(dg, A32, wimgT, kwT, Cout, Cin, cq, sup, trans_a=True, out=dx, accumulate=dx_written)
+            else:
+                wgT = K.gconv_weights(A32, wg2, sup, Cout, Cin, True, dtype)
+                K.gconv(dg, wgT, sup, Cout, Cin, trans=True, out=dx, accumulate=dx_written)
             dweff = K.gconv_wgrad(x, dg, sup, Cin, Cout)
             dwg2, dA = K.gconv_finish(dweff, A32, wg2, sup, Cout, Cin, dW=z_dwg, dA=z_dA)
             grads["wg"] = dwg2.view(P * Cout, Cin, 1, 1)

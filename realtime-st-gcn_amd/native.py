@@ -7,6 +7,8 @@ HIP stream; all arithmetic happens in the HIP kernels.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib as L
@@ -250,6 +252,10 @@ class GraphSupport:
 
         self.nbr, self.deg = pack(S)
         self.rnbr, self.rdeg = pack(R)
+        # per-partition max degree of a column (forward mix) / row (data-grad mix) of A[p] (gcn_tile)
+        ap = (A.detach() != 0).cpu().numpy()  # [P][v][w]
+        self.dmax_fwd = [int(ap[p].sum(0).max()) for p in range(ap.shape[0])]
+        self.dmax_bwd = [int(ap[p].sum(1).max()) for p in range(ap.shape[0])]
 
     def dense(self, P):
         """A-first (amix) is cheaper when the support is denser than P entries per output joint."""
@@ -272,6 +278,54 @@ def gconv_weights(A, W, sup, Cout, Cin, trans, dtype):
 
 def gconv_row_blocks(NT: int, V: int) -> int:
     return L.lib().stgcn_gconv_row_blocks(NT, V)
+
+
+def pack_frag1(w2: torch.Tensor, dtype) -> tuple:
+    """[Cout][K] fp32 1x1 weight -> its MFMA-fragment image (stgcn_pack_weight_frag, Kt = 1):
+    (image, Cout_pad, K_pad)."""
+    Co, Ci = w2.shape
+    cp = -(-Co // col_tile(Co)) * col_tile(Co)
+    kp = -(-Ci // 32) * 32
+    if w2.dtype != torch.float32:
+        w2 = w2.float()
+    buf = torch.empty(2 * cp * kp, dtype=dtype, device=w2.device)
+    s1, s2 = w2.stride()
+    L.check(L.lib().stgcn_pack_weight_frag(w2.data_ptr(), 0, s1, s2, 1, Co, Ci, buf.data_ptr(), buf[cp * kp:].data_ptr(),
+                                           cp, kp, L.dtype_code(dtype), L.stream()), "pack_weight_frag")
+    return buf[cp * kp:], cp, kp
+
+
+_GCN_TILE = os.environ.get("STGCN_GCN_TILE", "0") == "1"
+
+
+def gcn_tile_ok(sup, P, Cin, Cout, V, dtype) -> bool:
+    """Shapes the fused frame-tiled graph conv (gcn_tile.hip) takes, forward and data grad.  Opt-in
+    (STGCN_GCN_TILE=1): measured slower than the joint-gathered gconv.hip on the config-2 shapes
+    (DESIGN.md section 4), kept as the A-first fused path under test."""
+    return (_GCN_TILE and dtype == torch.bfloat16 and sup is not None and P <= 3 and V <= 32 and Cin % 32 == 0 and Cout % 32 == 0
+            and max(sup.dmax_fwd + sup.dmax_bwd) <= 8 and Cin % 64 == 0 and Cout % 64 == 0)
+
+
+def gcn_tile_row_blocks(NT: int, V: int) -> int:
+    return L.lib().stgcn_gcn_tile_row_blocks(NT, V)
+
+
+def gcn_tile(x, A, wimg, kw_pad, Cin, Cout, cp, sup, trans_a=False, bias=None, stats=None, out=None,
+             accumulate=False):
+    """Fused graph conv (stgcn_gcn_tile): out rows (N, Cout, T, V) (+)= W' . A-mix(x) (+ bias[w][co])."""
+    N, _, T, V = x.shape
+    if out is None:
+        out = cl_empty(N, Cout, T, V, x.dtype, x.device)
+    d = L.GcnTileDesc()
+    d.in_, d.out, d.w_frag, d.A = x.data_ptr(), out.data_ptr(), wimg.data_ptr(), A.data_ptr()
+    d.bias, d.stats = L.ptr(bias), L.ptr(stats)
+    d.NT, d.V, d.P, d.Cin, d.Cout, d.Cout_pad, d.Kw_pad = N * T, V, A.shape[0], Cin, Cout, cp, kw_pad
+    d.in_ld, d.out_ld, d.trans_a, d.accumulate = rows_ld(x), rows_ld(out), int(trans_a), int(accumulate)
+    dm = sup.dmax_bwd if trans_a else sup.dmax_fwd
+    for i, v in enumerate(dm[:4]):
+        d.dmax[i] = v
+    L.check(L.lib().stgcn_gcn_tile(d, L.dtype_code(x.dtype), L.stream()), "gcn_tile")
+    return out
 
 
 def gconv(x, wpk, sup, Cin, Cout, trans=False, bias=None, stats=None, out=None, accumulate=False, tag=None):

@@ -114,3 +114,23 @@ for name, N, T, Cin, Cout in gcases:
         print(f"{name + tag:22s} {ms*1e3:9.1f} us  {flops/ms/1e9:8.1f} TFLOP/s  {byts/ms/1e6:8.1f} GB/s", flush=True)
     ms = timeit(lambda: K.gconv_wgrad(x, dg, sup, Cin, Cout))
     print(f"{name.replace('fwd', 'wgrad'):22s} {ms*1e3:9.1f} us  {flops/ms/1e9:8.1f} TFLOP/s", flush=True)
+
+# fused frame-tiled graph conv (gcn_tile.hip): same shapes, forward (+bias, stats) and data grad
+for name, N, T, Cin, Cout in gcases:
+    if only and not name.startswith(only.replace("gconv", "gcn_tile")) and not name.startswith(only):
+        continue
+    Pp, V = A0.shape[0], A0.shape[-1]
+    W = torch.randn(Pp * Cout, Cin, device=dev) / Cin ** 0.5
+    x = torch.randn(N, Cin, T, V, device=dev).to(dt).contiguous(memory_format=torch.channels_last)
+    dg = torch.randn(N, Cout, T, V, device=dev).to(dt).contiguous(memory_format=torch.channels_last)
+    wimg, cp, kw = K.pack_frag1(W.view(Pp, Cout, Cin).permute(1, 0, 2).reshape(Cout, Pp * Cin), dt)
+    wT, cq, kwT = K.pack_frag1(W.view(Pp, Cout, Cin).permute(2, 0, 1).reshape(Cin, Pp * Cout), dt)
+    b2 = K.gcn_bias(A0, torch.randn(Pp * Cout, device=dev), N, Cout)
+    st = torch.zeros((K.gcn_tile_row_blocks(N * T, V), cp, 4), device=dev)
+    flops = 2.0 * N * T * V * Pp * Cin * Cout
+    byts = (N * T * V * (Cin + Cout)) * 2
+    for tag, f in (("", lambda: K.gcn_tile(x, A0, wimg, kw, Cin, Cout, cp, sup, bias=b2, stats=st)),
+                   ("_dgrad", lambda: K.gcn_tile(dg, A0, wT, kwT, Cout, Cin, cq, sup, trans_a=True))):
+        ms = timeit(f)
+        print(f"{name.replace('gconv', 'gcn_tile') + tag:22s} {ms*1e3:9.1f} us  {flops/ms/1e9:8.1f} TFLOP/s  "
+              f"{byts/ms/1e6:8.1f} GB/s", flush=True)
