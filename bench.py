@@ -245,7 +245,7 @@ def main():
                                    "bwd + Adam", "global_batch": N_BATCH * world, "seq_len": T_LEN, "joints": V_J,
                        "parallelism": f"dp{world}" if world > 1 else "single",
                        "launch": "eager" if not args.graph else "hip-graph replay (fwd+bwd | allreduce | Adam)"},
-            "roofline": {"kernel": "conv_tile_kernel (frame-tiled temporal conv fwd, C=64, Kt=9, stride 1)",
+            "roofline": {"kernel": "conv_wide_kernel<64,9,12,*,0,32> (persistent warp-specialised temporal conv fwd, C=64, Kt=9, stride 1)",
                          "bound": "mfma", "achieved": round(achieved, 2) if achieved else None,
                          "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4) if achieved else None,

@@ -138,15 +138,17 @@ typedef struct {
 
 int stgcn_gconv(const stgcn_gconv_desc* d, int dtype, void* stream);
 
-/* Fused frame-tiled graph convolution (bf16; gcn_tile.hip), A applied on the fly to whole-frame tiles:
+/* Fused graph convolution (bf16; gcn_tile.hip): per frame, the joint mix and the 1x1 conv as two chained
+ * MFMA products (the mix's accumulators feed the conv directly):
  *   trans_a 0 (forward, tgcn.py:71-79):  out[(i,w)][co] (+)= sum_{p,ci} W'[co][p*Cin+ci] sum_v A[p][v][w] in[(i,v)][ci]
  *                                          (+ bias[w][co])
  *   trans_a 1 (data grad):               out[(i,v)][c]  (+)= sum_{p,k} W'[c][p*Cin+k]  sum_w A[p][v][w] in[(i,w)][k]
- * W' = the Kt = 1 MFMA-fragment image of stgcn_pack_weight_frag ([Cout_pad][Kw_pad], Kw_pad >= P*Cin):
- * forward W'[co][p*Cin+ci] = W[p*Cout+co][ci]; data grad (in = dg, Cin = conv Cout, Cout = conv Cin)
- * W'[ci][p*Cout+co] = W[p*Cout+co][ci].  A: [P][V][V] fp32 (A * edge importance).  dmax[p] >= the
- * largest number of nonzeros of a column (trans_a 0) / row (trans_a 1) of A[p].  Optional BN partial
- * statistics [stgcn_gcn_tile_row_blocks][Cout_pad] as stgcn_conv_rows.
+ * w_frag = the Kt = 1 MFMA-fragment image (stgcn_pack_weight_frag, [Cout_pad][Kw_pad], Kw_pad >= P*Cin)
+ * of W'' with the columns of every 16-wide group permuted: W''[c][16m + 8h + j] = W'[c][16m + 8(j/4) + 4h + j%4]
+ * (h < 2, j < 8); forward W'[co][p*Cin+ci] = W[p*Cout+co][ci]; data grad (in = dg, Cin = conv Cout,
+ * Cout = conv Cin) W'[ci][p*Cout+co] = W[p*Cout+co][ci].  A: [P][V][V] fp32 (A * edge importance),
+ * P <= 3, 16 < V <= 32; Cin % 32 == 0, Cout % 64 == 0.  dmax is unused (kept for ABI stability).
+ * Optional BN partial statistics [stgcn_gcn_tile_row_blocks(NT, V, Cout)][Cout_pad] as stgcn_conv_rows.
  * Replaces: conv1x1 + einsum of ConvTemporalGraphical.forward (tgcn.py:71-79) and its input grad. */
 typedef struct {
   const void* in;
@@ -160,7 +162,7 @@ typedef struct {
 } stgcn_gcn_tile_desc;
 
 int stgcn_gcn_tile(const stgcn_gcn_tile_desc* d, int dtype, void* stream);
-long stgcn_gcn_tile_row_blocks(int NT, int V);
+long stgcn_gcn_tile_row_blocks(int NT, int V, int Cout);
 long stgcn_gconv_row_blocks(int NT, int V);
 int stgcn_gconv_weights(const float* A, const float* W, const int* nbr, const int* deg, int P, int V, int J, int Cout,
                         int Cin, int trans, void* out, int rows_pad, int cols_pad, int dtype, void* stream);

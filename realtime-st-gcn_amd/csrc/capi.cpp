@@ -22,7 +22,7 @@ int conv_wgrad_launch(WgradArgs a, int dtype, hipStream_t s);
 int pack_s2frag_launch(const float* src, long s0, long s1, long s2, int Co, int Ci, void* dst, int trans,
                        hipStream_t s);
 int gcn_tile_launch(const stgcn_gcn_tile_desc& a, hipStream_t s);
-long gcn_tile_row_blocks(int NT, int V);
+long gcn_tile_row_blocks(int NT, int V, int Cout);
 long wgrad_tile_workspace(const WgradArgs& a, int dtype);
 long wgrad_wide_workspace(const WgradArgs& a, int dtype);
 int wgrad_wide_launch(const WgradArgs& a, int dtype, hipStream_t s);
@@ -111,7 +111,7 @@ int stgcn_gcn_tile(const stgcn_gcn_tile_desc* d, int dtype, void* stream) {
   if (d->in_ld < d->Cin || d->out_ld < d->Cout) return STGCN_EBADSHAPE;
   return gcn_tile_launch(*d, STREAM(stream));
 }
-long stgcn_gcn_tile_row_blocks(int NT, int V) { return gcn_tile_row_blocks(NT, V); }
+long stgcn_gcn_tile_row_blocks(int NT, int V, int Cout) { return gcn_tile_row_blocks(NT, V, Cout); }
 int stgcn_pack_weight(const float* src, long s0, long s1, long s2, int Kt, int Co, int Ci, void* dst, int Cout_pad,
                       int Cin_pad, int dtype, void* stream) {
   CHECK_DTYPE(dtype);

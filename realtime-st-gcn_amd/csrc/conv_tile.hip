@@ -675,6 +675,12 @@ int conv_wide_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s);
 
 int conv_tile_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
   static const bool no_persist = getenv("STGCN_NO_PERSIST") != nullptr;  // A/B switch
+  // 64-channel stride-1 forward: the wide kernel's 32-channel items beat the weight-resident kernel
+  // (70 vs 74 us on the config-2 shape); the transposed (data-grad) pass stays on conv_persist (61 vs 64 us)
+  if (a.stride == 1 && !a.trans && a.Cin == 64) {
+    const int r = conv_wide_launch(a, dtype, s);
+    if (r >= 0) return r;
+  }
   if (!no_persist) {  // weight-resident persistent kernel for the 64-channel Kt=9 convs
     const int r = conv_persist_launch(a, dtype, s);
     if (r >= 0) return r;

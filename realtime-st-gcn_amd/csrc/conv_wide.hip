@@ -40,6 +40,11 @@ constexpr int HR_CAP = 456;          // max halo rows per item (V = 25: 18 frame
 constexpr int NA = (HR_CAP * 8 + NT - 1) / NT;  // 16-B halo units per thread (15)
 constexpr int CSO = 256 * 2 + 8;                  // column bytes of the column-major output tile image (256 rows)
 constexpr int ABYTES_MIN = (128 * CSO > NA * 32 * RSA ? 128 * CSO : NA * 32 * RSA);  // halo buffer / tile image
+// halo buffer bytes for item width kg (>= every staged unit row of a helper thread, and the tile image)
+constexpr int abytes_for(int kg) {
+  const int upr = kg / 8, rstep = 256 / upr, na = (HR_CAP * upr + 255) / 256, halo = na * rstep * (2 * kg + 16);
+  return halo > 128 * CSO ? halo : 128 * CSO;
+}
 constexpr int LDS_MAX = 160 * 1024;
 
 // compile-time loop: f.template operator()<I>() for I = 0..N-1 (guaranteed unrolled; register arrays
@@ -95,8 +100,12 @@ DEV TileInfo tile_info(int tile, const WGeom& g) {
 // helpers drain that image during item k+1 before they overwrite buf b with item k+2's halo.
 // DBG (diagnostic instantiations, STGCN_WIDE_DBG=<bits>): bit1 no helper work (results wrong), bit2 phase
 // timers (s_memtime of MMA wave 0 / helper wave 4 into g.dbg)
-template <int BN, int KTAP, int NBUF, int PRO, int DBG = 0>
+template <int BN, int KTAP, int NBUF, int PRO, int DBG = 0, int KGT = 64>
 __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_desc a, const WGeom g) {
+  // item width: 64 input channels (>= 128-channel layers) or 32 (64-channel layers: two items per tile)
+  constexpr int KG = KGT, KS = KG / 16, RSA = 2 * KG + 16;
+  constexpr int UPR = KG / 8, RSTEP = NT / UPR;            // 16-B units per halo row, rows per staging pass
+  constexpr int NA = (HR_CAP * UPR + NT - 1) / NT;         // halo units per helper thread
   constexpr int SPI = KTAP * KS;  // k-steps per item
   constexpr int TN = BN / 64;
   constexpr int LEAD = NBUF - 1;
@@ -143,11 +152,14 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
   if (!mma) {
     // =============================== helper waves ===============================
     const int htid = tid - NT;
-    const int ucol = htid & 7, row0u = htid >> 3;
-    int a_lo = 0, a_hi = 0;
-    uint4 ra[NA];
-    float sc[8], sh[8];
-    auto issue_A = [&](int w) {  // item w's halo units -> registers
+    const int ucol = htid % UPR, row0u = htid / UPR;
+    // NSET register sets: item w + 1 + NSET's halo is requested in window w.  Two sets for the 32-channel
+    // items (short MMA time per item: the loads need two items of cover), one for 64-channel items
+    constexpr int NSET = KG == 32 ? 2 : 1;
+    int a_lo[NSET], a_hi[NSET];
+    uint4 ra[NSET][NA];
+    float sc[NSET][8], sh[NSET][8];
+    auto issue_A = [&]<int SET>(int w) {  // item w's halo units -> register set SET
       int gi;
       const int tile = item_tile(w, gi);
       const TileInfo ti = tile_info(tile, g);
@@ -157,21 +169,21 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
         // halo frame z = fi0 + fl is the pair (x[2z], x[2z+1]); this item reads parity gi / cpar
         const int par = gi / g.cpar;
         cg = gi - par * g.cpar;
-        a_lo = max(0, -fi0) * V;
-        a_hi = min(g.HR, ((a.T_in - par + 1) / 2 - fi0) * V);
+        a_lo[SET] = max(0, -fi0) * V;
+        a_hi[SET] = min(g.HR, ((a.T_in - par + 1) / 2 - fi0) * V);
         const bf16* base = in + (long)ti.n * a.T_in * V * a.in_ld + cg * KG + ucol * 8;
         static_for<NA>([&]<int i>() {
-          const int row = min(max(row0u + 32 * i, a_lo), a_hi - 1);
+          const int row = min(max(row0u + RSTEP * i, a_lo[SET]), a_hi[SET] - 1);
           const int fl = row / V, v = row - fl * V;
-          ra[i] = *reinterpret_cast<const uint4*>(base + ((2 * (fi0 + fl) + par) * V + v) * (long)a.in_ld);
+          ra[SET][i] = *reinterpret_cast<const uint4*>(base + ((2 * (fi0 + fl) + par) * V + v) * (long)a.in_ld);
         });
       } else {
-        a_lo = max(0, -fi0) * V;
-        a_hi = min(g.HR, (a.T_in - fi0) * V);
+        a_lo[SET] = max(0, -fi0) * V;
+        a_hi[SET] = min(g.HR, (a.T_in - fi0) * V);
         const bf16* base = in + ((long)ti.n * a.T_in + fi0) * V * a.in_ld + gi * KG + ucol * 8;
         static_for<NA>([&]<int i>() {
-          const int row = min(max(row0u + 32 * i, a_lo), a_hi - 1);
-          ra[i] = *reinterpret_cast<const uint4*>(base + row * a.in_ld);
+          const int row = min(max(row0u + RSTEP * i, a_lo[SET]), a_hi[SET] - 1);
+          ra[SET][i] = *reinterpret_cast<const uint4*>(base + row * a.in_ld);
         });
       }
       if (PRO == 1) {
@@ -180,24 +192,24 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
         const float4 s1 = *reinterpret_cast<const float4*>(a.pro_a + c + 4);
         const float4 h0 = *reinterpret_cast<const float4*>(a.pro_b + c);
         const float4 h1 = *reinterpret_cast<const float4*>(a.pro_b + c + 4);
-        sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
-        sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
-        sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w;
-        sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
+        sc[SET][0] = s0.x; sc[SET][1] = s0.y; sc[SET][2] = s0.z; sc[SET][3] = s0.w;
+        sc[SET][4] = s1.x; sc[SET][5] = s1.y; sc[SET][6] = s1.z; sc[SET][7] = s1.w;
+        sh[SET][0] = h0.x; sh[SET][1] = h0.y; sh[SET][2] = h0.z; sh[SET][3] = h0.w;
+        sh[SET][4] = h1.x; sh[SET][5] = h1.y; sh[SET][6] = h1.z; sh[SET][7] = h1.w;
       }
     };
-    auto store_A = [&](char* buf) {  // prologue (BN1 scale/shift + ReLU) + zero rows -> LDS halo buffer
+    auto store_A = [&]<int SET>(char* buf) {  // prologue (BN1 scale/shift + ReLU) + zero rows -> LDS halo buffer
       static_for<NA>([&]<int i>() {
-        const int row = row0u + 32 * i;
-        uint4 v = ra[i];
+        const int row = row0u + RSTEP * i;
+        uint4 v = ra[SET][i];
         if (PRO == 1) {
           float f[8];
           unpack16(v, f, (bf16*)nullptr);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], sc[j], sh[j]), 0.f);
+          for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], sc[SET][j], sh[SET][j]), 0.f);
           v = pack16(f, (bf16*)nullptr);
         }
-        const bool ok = row >= a_lo && row < a_hi;
+        const bool ok = row >= a_lo[SET] && row < a_hi[SET];
         v.x = ok ? v.x : 0u;
         v.y = ok ? v.y : 0u;
         v.z = ok ? v.z : 0u;
@@ -231,8 +243,8 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
       const int rq = htid & 63, hw = htid >> 6;
       if (4 * rq >= rows_valid) return;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int cu = hw * 4 + k;
+      for (int k = 0; k < BN / 32; ++k) {  // BN/8 units of 8 channels over the 4 helper waves
+        const int cu = hw * (BN / 32) + k;
         if (cb + cu * 8 >= a.Cout) continue;
         uint2 col[8];
 #pragma unroll
@@ -267,26 +279,39 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
       }
     };
 
-    // loads run one item ahead of the LDS writes: item w+2's halo is requested right after item w+1's
-    // is written (window w), so a whole item of MMA time covers its HBM latency
-    issue_A(0);
-    store_A(sA0);
-    if (nitems > 1) issue_A(1);
+    // item w lives in register set w % NSET and LDS buffer w & 1; nitems is even (G even)
+    issue_A.template operator()<0>(0);
+    store_A.template operator()<0>(sA0);
+    if (nitems > 1) issue_A.template operator()<1 % NSET>(1);
+    if (NSET == 2 && nitems > 2) issue_A.template operator()<0>(2);
     lds_barrier();  // P
     tmark(-1);
-    for (int w = 0; w < nitems; ++w) {
-      char* const nb = (w & 1) ? sA0 : sA1;  // buffer of item w + 1
+    for (int w = 0; w < nitems; w += 2) {
+      // window w: item w+1 -> sA1, request item w+1+NSET
       if ((DBG & 2) == 0) {
-        if (w > 0 && tile_end(w - 1)) drain(w - 1, nb);
+        if (w > 0 && tile_end(w - 1)) drain(w - 1, sA1);
         tmark(0);
-        if (w + 1 < nitems) store_A(nb);
+        if (w + 1 < nitems) store_A.template operator()<1 % NSET>(sA1);
         tmark(1);
-        if (w + 2 < nitems) issue_A(w + 2);
+        if (w + 1 + NSET < nitems) issue_A.template operator()<(1 + NSET) % NSET>(w + 1 + NSET);
         tmark(2);
       }
       lds_barrier();  // E_w
       tmark(3);
       if (tile_end(w)) lds_barrier();  // I_w
+      tmark(4);
+      // window w+1: item w+2 -> sA0, request item w+2+NSET
+      if ((DBG & 2) == 0) {
+        if (tile_end(w)) drain(w, sA0);
+        tmark(0);
+        if (w + 2 < nitems) store_A.template operator()<2 % NSET>(sA0);
+        tmark(1);
+        if (w + 2 + NSET < nitems) issue_A.template operator()<(2 + NSET) % NSET>(w + 2 + NSET);
+        tmark(2);
+      }
+      lds_barrier();  // E_{w+1}
+      tmark(3);
+      if (tile_end(w + 1)) lds_barrier();  // I_{w+1}
       tmark(4);
     }
     if ((DBG & 2) == 0) drain(nitems - 1, ((nitems - 1) & 1) ? sA1 : sA0);
@@ -579,21 +604,25 @@ int conv_wide_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
   } else {
     return -1;
   }
-  if (cin_f % (2 * KG) || cout_f % 128) return -1;  // unpadded folded channels: the image is exact
-  const int BN = 128;  // BN = 256 (acc 256 + B ring) does not fit the register file without spills
+  // item width: 64 input channels, or 32 for the 64-channel stride-1 convs (two items per tile)
+  const int kg = (g.fold == 0 && cin_f == 64) ? 32 : KG;
+  if (cin_f % (2 * kg) || cout_f % 64) return -1;  // unpadded folded channels: the image is exact
+  // BN = 256 (acc 256 + B ring) does not fit the register file without spills
+  const int BN = cout_f % 128 == 0 ? 128 : 64;
+  if (BN == 64 && kg != 32) return -1;
   g.wc32 = cout_f / 32;
   g.wk16 = cin_f / 16;
   g.F = 256 / a.V;
   g.HR = (g.F + ktap - 1) * a.V;
   if (g.HR > HR_CAP || g.F < 1) return -1;
-  g.G = cin_f / KG;
+  g.G = cin_f / kg;
   g.tiles_n = (g.T_tile + g.F - 1) / g.F;
   g.ncol = cout_f / BN;
   const long nt = (long)a.N * g.tiles_n * g.ncol;
   if (nt <= 0 || nt > 0x7fffffffL) return -1;
   g.ntiles = (int)nt;
   if (a.stats && (long)a.N * g.tiles_n > conv_rows_num_row_blocks((long)a.N * a.T_out * a.V, a.Cout)) return -1;
-  g.abytes = ABYTES_MIN;
+  g.abytes = abytes_for(kg);
   const size_t lds = 2 * (size_t)g.abytes + (size_t)WM * BN * 16;
   if (lds > (size_t)LDS_MAX) return -1;
   static int ncu = 0;
@@ -615,12 +644,14 @@ int conv_wide_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
       g.dbg = dbuf;
       return dbg == 2 ? conv_wide_kernel<128, 9, 6, 1, 2> : conv_wide_kernel<128, 9, 6, 1, 4>;
     }
+    if (kg == 32)
+      return a.pro ? conv_wide_kernel<64, 9, 12, 1, 0, 32> : conv_wide_kernel<64, 9, 12, 0, 0, 32>;
     if (ktap == 9) return a.pro ? conv_wide_kernel<128, 9, 6, 1> : conv_wide_kernel<128, 9, 6, 0>;
     return a.pro ? conv_wide_kernel<128, 5, 5, 1> : conv_wide_kernel<128, 5, 5, 0>;
   };
   auto* k = kern();
-  static bool attr[4] = {false, false, false, false};
-  const int ai = (ktap == 9 ? 0 : 2) + (a.pro ? 1 : 0);
+  static bool attr[6] = {false, false, false, false, false, false};
+  const int ai = (kg == 32 ? 4 : ktap == 9 ? 0 : 2) + (a.pro ? 1 : 0);
   if (!attr[ai] || dbg) {
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
     attr[ai] = true;

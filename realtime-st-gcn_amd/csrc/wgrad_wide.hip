@@ -85,6 +85,15 @@ __global__ __launch_bounds__(NT, 1) void wgrad_wide_kernel(const stgcn_wgrad_des
   char* const sY = smem + 2 * XP;               // dY buffers [2][4 panels][KM rows]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wc = wave >> 1, wi = wave & 1;      // co tile (32), ci tile (32)
+  {
+    // Zero the whole LDS image first: the K-padding rows of a tap window and ring slots of frames never
+    // staged are read as MFMA operands multiplied by zero dY rows, and LDS left by an earlier kernel
+    // may hold NaN bit patterns (0 * NaN = NaN).
+    uint4* z = reinterpret_cast<uint4*>(smem);
+    const int nz = (2 * XP + 2 * DY_BYTES) / 16;
+    for (int e = tid; e < nz; e += NT) z[e] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+  }
   const int ob = blockIdx.x % (g.nco * g.nci), rg = blockIdx.x / (g.nco * g.nci);
   const int co0 = (ob % g.nco) * COB, cf0 = (ob / g.nco) * CIB;  // cf0: folded input channel
   // fold: ring frame z holds input frame 2z + par of the source channels ci0 .. ci0+63

@@ -105,7 +105,7 @@ class StgcnLayerFunction(torch.autograd.Function):
         bias2d = K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
         if norm == BN:  # all BatchNorm partial-statistics buffers of the layer from one zero fill
             cpo = -(-Cout // K.col_tile(Cout)) * K.col_tile(Cout)
-            rb1 = (K.gcn_tile_row_blocks(N * T, V) if tiled else K.gconv_row_blocks(N * T, V)) if gather \
+            rb1 = (K.gcn_tile_row_blocks(N * T, V, Cout) if tiled else K.gconv_row_blocks(N * T, V)) if gather \
                 else K.row_blocks(M1, Cout)
             st_shapes = [(rb1, cpo, 4),
                          (K.row_blocks(M2, Cout), cpo, 4)] + ([(K.row_blocks(M2, Cout), cpo, 4)] if res_conv else [])
@@ -114,7 +114,8 @@ class StgcnLayerFunction(torch.autograd.Function):
             str_ = st_all[2] if res_conv else None
         if tiled:  # A-mix on the fly into the MFMA operand of whole-frame tiles (gcn_tile.hip)
             wgf = wg.detach().float().view(P, Cout, Cin).permute(1, 0, 2).reshape(Cout, P * Cin)  # W'[co][p*Cin+ci]
-            wimg, cpg, kwg = K.pack_frag1(wgf, dtype)
+            wimg, cpg, kwg = K.pack_gcn_weight(wgf, dtype)
+            kpg = kwg
             if norm == BN:
                 assert cpg == cpo
             g = K.gcn_tile(x, A32, wimg, kwg, Cin, Cout, cpg, sup, bias=bias2d, stats=st1 if norm == BN else None)
@@ -309,9 +310,9 @@ class StgcnLayerFunction(torch.autograd.Function):
             # weight/adjacency grads from dWeff[w][j] = sum_i dg[(i,w)] x[(i,S(w)_j)]^T
             sup = ctx.sup
             wg2 = wg.detach().float().reshape(P * Cout, Cin).contiguous()
-            if K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype):  # dx = sum_p A_p-mix(dg) W_p^T, fused (gcn_tile.hip)
+            if K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype, trans=True):  # dx = sum_p A_p-mix(dg) W_p^T, fused (gcn_tile.hip)
                 wdf = wg.detach().float().view(P, Cout, Cin).permute(2, 0, 1).reshape(Cin, P * Cout)
-                wimgT, cq, kwT = K.pack_frag1(wdf, dtype)
+                wimgT, cq, kwT = K.pack_gcn_weight(wdf, dtype)
                 K.gcn_tile(dg, A32, wimgT, kwT, Cout, Cin, cq, sup, trans_a=True, out=dx, accumulate=dx_written)
             else:
                 wgT = K.gconv_weights(A32, wg2, sup, Cout, Cin, True, dtype)

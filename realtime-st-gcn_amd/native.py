@@ -83,7 +83,7 @@ def pack_weight(w3: torch.Tensor, dtype, stride: int = 1, trans: bool = False) -
                                                  L.dtype_code(dtype), L.stream()), "pack_weight_s2frag")
         out.frag_ptr, out.frag_stride = buf[n:].data_ptr(), 2
         return out, cp, kp
-    if dtype == torch.bfloat16 and Kt == 9 and stride == 1 and cp % 128 == 0 and kp % 128 == 0:
+    if dtype == torch.bfloat16 and Kt == 9 and stride == 1 and cp % 64 == 0 and kp % 64 == 0:
         buf = torch.empty(2 * n, dtype=dtype, device=w3.device)
         out = buf[:n].view(Kt, cp, kp)
         L.check(L.lib().stgcn_pack_weight_frag(w3.data_ptr(), s0, s1, s2, Kt, Co, Ci, out.data_ptr(),
@@ -295,19 +295,45 @@ def pack_frag1(w2: torch.Tensor, dtype) -> tuple:
     return buf[cp * kp:], cp, kp
 
 
-_GCN_TILE = os.environ.get("STGCN_GCN_TILE", "0") == "1"
+_GCN_TILE = os.environ.get("STGCN_GCN_TILE", "0")  # "0" never (default), "1" every shape it takes, "auto"
 
 
-def gcn_tile_ok(sup, P, Cin, Cout, V, dtype) -> bool:
-    """Shapes the fused frame-tiled graph conv (gcn_tile.hip) takes, forward and data grad.  Opt-in
-    (STGCN_GCN_TILE=1): measured slower than the joint-gathered gconv.hip on the config-2 shapes
-    (DESIGN.md section 4), kept as the A-first fused path under test."""
-    return (_GCN_TILE and dtype == torch.bfloat16 and sup is not None and P <= 3 and V <= 32 and Cin % 32 == 0 and Cout % 32 == 0
-            and max(sup.dmax_fwd + sup.dmax_bwd) <= 8 and Cin % 64 == 0 and Cout % 64 == 0)
+def gcn_tile_ok(sup, P, Cin, Cout, V, dtype, trans=False) -> bool:
+    """Whether the graph conv of a layer (Cin -> Cout) runs on the fused kernel (gcn_tile.hip: joint mix
+    + 1x1 conv as two chained MFMA products) in the forward (trans False) or data-grad direction.
+    "auto" takes it where it measured faster than the joint-gathered gconv.hip in isolation (DESIGN.md
+    section 4): when the kernel writes 64 channels.  Beyond that the two-stage form executes ~2x the
+    MFMA work of the gathered one (stage-1 mix per 64-channel column tile, joints padded 25 -> 32) and
+    loses.  Default "0": inside the training step (cold HBM inputs) "auto" measured equal to gconv.hip
+    (0.46 ms/step either way), so the gathered path stays the default."""
+    if _GCN_TILE == "0" or dtype != torch.bfloat16 or sup is None or P > 3 or not 16 < V <= 32:
+        return False
+    if Cin not in (64, 128, 256) or Cout not in (64, 128, 256):
+        return False
+    return _GCN_TILE == "1" or (Cin if trans else Cout) == 64
 
 
-def gcn_tile_row_blocks(NT: int, V: int) -> int:
-    return L.lib().stgcn_gcn_tile_row_blocks(NT, V)
+def gcn_tile_row_blocks(NT: int, V: int, Cout: int) -> int:
+    return L.lib().stgcn_gcn_tile_row_blocks(NT, V, Cout)
+
+
+_PERM16 = {}
+
+
+def pack_gcn_weight(w2: torch.Tensor, dtype) -> tuple:
+    """[Cout][P*Cin] fp32 W' -> the stgcn_gcn_tile weight image: the Kt = 1 fragment image of W' with the
+    columns of every 16-wide group in the order of the mix accumulators' rows (include/stgcn_amd.h):
+    (image, Cout_pad, K_pad)."""
+    K = w2.shape[1]
+    key = (K, w2.device)
+    perm = _PERM16.get(key)
+    if perm is None:
+        h = torch.arange(16) // 8
+        j = torch.arange(16) % 8
+        within = 8 * (j // 4) + 4 * h + j % 4
+        perm = (torch.arange(K) // 16 * 16 + within.repeat(K // 16)).to(w2.device)
+        _PERM16[key] = perm
+    return pack_frag1(w2.float().index_select(1, perm), dtype)
 
 
 def gcn_tile(x, A, wimg, kw_pad, Cin, Cout, cp, sup, trans_a=False, bias=None, stats=None, out=None,

@@ -359,9 +359,9 @@ def test_gcn_tile(K, pkg, cin, cout, T, N):
     ref = torch.einsum("npctv,pvw->nctw", y, A)
     sup = K.GraphSupport(A.to(DEV))
     A32 = A.to(DEV).contiguous()
-    wimg, cp, kw = K.pack_frag1(W.view(P, cout, cin).permute(1, 0, 2).reshape(cout, P * cin).to(DEV), torch.bfloat16)
+    wimg, cp, kw = K.pack_gcn_weight(W.view(P, cout, cin).permute(1, 0, 2).reshape(cout, P * cin).to(DEV), torch.bfloat16)
     bias2d = K.gcn_bias(A32, b.to(DEV), N, cout)
-    st = torch.zeros((K.gcn_tile_row_blocks(N * T, V), cp, 4), device=DEV)
+    st = torch.zeros((K.gcn_tile_row_blocks(N * T, V, cout), cp, 4), device=DEV)
     g = K.gcn_tile(cl(x, torch.bfloat16), A32, wimg, kw, cin, cout, cp, sup, bias=bias2d, stats=st)
     assert_close(g.float(), ref, 2e-2, "gcn_tile fwd")
     mr, _, _ = K.bn_finalize(st, st.shape[0], cp, cout, None, None)
@@ -373,6 +373,6 @@ def test_gcn_tile(K, pkg, cin, cout, T, N):
     yr = torch.einsum("npctv,pvw->nctw", F.conv2d(xr, W.view(P * cout, cin, 1, 1), b).view(N, P, cout, T, V), A)
     dg = torch.randn(yr.shape)
     yr.backward(dg)
-    wT, cq, kwT = K.pack_frag1(W.view(P, cout, cin).permute(2, 0, 1).reshape(cin, P * cout).to(DEV), torch.bfloat16)
+    wT, cq, kwT = K.pack_gcn_weight(W.view(P, cout, cin).permute(2, 0, 1).reshape(cin, P * cout).to(DEV), torch.bfloat16)
     dx = K.gcn_tile(cl(dg, torch.bfloat16), A32, wT, kwT, cout, cin, cq, sup, trans_a=True)
     assert_close(dx.float(), xr.grad, 2e-2, "gcn_tile dgrad")

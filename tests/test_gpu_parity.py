@@ -145,6 +145,46 @@ def test_layer_vs_oracle_larger(P, norm, cin, cout, stride):
         assert_grad_close(named[k].grad, g, TOL, k, grad_floor(grads, k), reduction=True)
 
 
+@pytest.mark.parametrize("gcn_mode", ["0", "1"])
+@pytest.mark.parametrize("cin,cout,stride", [(64, 64, 1), (64, 128, 2), (128, 64, 1)])
+def test_layer_bf16_vs_oracle(P, cin, cout, stride, gcn_mode, monkeypatch):
+    """bf16 perf path of one BatchNorm layer at config-2 widths on the 25-joint graph (the shapes that
+    route the graph conv through the fused gcn_tile kernel in one or both directions) vs the fp32
+    oracle: forward and every gradient within bf16 tolerance, with the graph conv on the gathered
+    gconv.hip ("0") and on the fused gcn_tile.hip ("1")."""
+    monkeypatch.setattr(P.native, "_GCN_TILE", gcn_mode)
+    torch.manual_seed(5)
+    N, T = 3, 40
+    A = torch.tensor(P.Graph(**P.PKU_MMD).A, dtype=torch.float32)
+    layer = P.StgcnLayer(cin, cout, (9, 25), 3, 25, stride=stride, normalization="BatchNorm")
+    M = 1 + 0.1 * torch.randn(3, 25, 25)
+    x = torch.randn(N, cin, T, 25)
+    dy = torch.randn(N, cout, (T - 1) // stride + 1, 25)
+    sd = {k: v.clone().requires_grad_(True) for k, v in layer.state_dict().items()}
+    xr = x.clone().requires_grad_(True)
+    Ar = (A * M).requires_grad_(True)
+    ref = O.stgcn_layer(xr, Ar, sd, "", 9, stride, True, "BatchNorm")
+    ref.backward(dy)
+    layer = P.set_compute_dtype(layer.to(DEV), "bf16")
+    xg = x.to(DEV).requires_grad_(True)
+    Ag = (A * M).to(DEV).requires_grad_(True)
+    y = layer(xg, Ag)
+    y.backward(dy.to(DEV))
+    tol = 4e-2
+    assert_close(y.float(), ref, tol, "y")
+    assert_grad_close(xg.grad, xr.grad, tol, "dx")
+    assert_grad_close(Ag.grad, Ar.grad, tol, "dA", reduction=True)
+    named = dict(layer.named_parameters())
+    grads = {k: v.grad for k, v in sd.items() if v.grad is not None}
+    for k, g in grads.items():
+        if float(g.abs().max()) < 1e-3 * grad_floor(grads, k):
+            # a conv bias feeding a batch-statistics BatchNorm: its true gradient is 0 (the reference's
+            # is fp32 rounding noise, ours the sum of bf16-rounded BN input grads over all rows)
+            assert float(named[k].grad.abs().max()) < 0.3 * grad_floor(grads, k), k
+            continue
+        assert_grad_close(named[k].grad, g, tol, k, grad_floor(grads, k), reduction=True)
+
+
 def test_model_bf16_vs_oracle(P):
     """bf16 perf path, 9-layer as_is model (narrow widths), vs the fp32 oracle: 3e-2 relative."""
     d = load_golden("model_stgcn_bn_9layer_narrow")

@@ -123,10 +123,10 @@ for name, N, T, Cin, Cout in gcases:
     W = torch.randn(Pp * Cout, Cin, device=dev) / Cin ** 0.5
     x = torch.randn(N, Cin, T, V, device=dev).to(dt).contiguous(memory_format=torch.channels_last)
     dg = torch.randn(N, Cout, T, V, device=dev).to(dt).contiguous(memory_format=torch.channels_last)
-    wimg, cp, kw = K.pack_frag1(W.view(Pp, Cout, Cin).permute(1, 0, 2).reshape(Cout, Pp * Cin), dt)
-    wT, cq, kwT = K.pack_frag1(W.view(Pp, Cout, Cin).permute(2, 0, 1).reshape(Cin, Pp * Cout), dt)
+    wimg, cp, kw = K.pack_gcn_weight(W.view(Pp, Cout, Cin).permute(1, 0, 2).reshape(Cout, Pp * Cin), dt)
+    wT, cq, kwT = K.pack_gcn_weight(W.view(Pp, Cout, Cin).permute(2, 0, 1).reshape(Cin, Pp * Cout), dt)
     b2 = K.gcn_bias(A0, torch.randn(Pp * Cout, device=dev), N, Cout)
-    st = torch.zeros((K.gcn_tile_row_blocks(N * T, V), cp, 4), device=dev)
+    st = torch.zeros((K.gcn_tile_row_blocks(N * T, V, Cout), cp, 4), device=dev)
     flops = 2.0 * N * T * V * Pp * Cin * Cout
     byts = (N * T * V * (Cin + Cout)) * 2
     for tag, f in (("", lambda: K.gcn_tile(x, A0, wimg, kw, Cin, Cout, cp, sup, bias=b2, stats=st)),
