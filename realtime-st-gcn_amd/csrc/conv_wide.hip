@@ -73,6 +73,7 @@ struct WGeom {
   int cpar;     // fold 1: 64-channel items per input parity; fold 2: output channels per parity
   int wc32, wk16;  // fragment image dims: (output channels / 32, input channels / 16)
   long long* dbg;  // DBG & 4: per-block phase cycles [block][16]
+  int strided;     // 1: block b takes tiles b, b + grid, ... (A/B switch STGCN_WIDE_STRIDED); 0: a contiguous run
 };
 
 struct TileInfo {
@@ -117,7 +118,10 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
   const bool mma = wave < 4;
   const int V = a.V;
   const int grid = gridDim.x;
-  const int ntile_b = (g.ntiles - (int)blockIdx.x + grid - 1) / grid;
+  const int tpb = (g.ntiles + grid - 1) / grid;  // contiguous tile runs: neighbour halos stay in L2
+  const int tile0 = g.strided ? (int)blockIdx.x : (int)blockIdx.x * tpb;
+  const int tstep = g.strided ? grid : 1;
+  const int ntile_b = g.strided ? (g.ntiles - (int)blockIdx.x + grid - 1) / grid : min(tpb, g.ntiles - tile0);
   if (ntile_b <= 0) return;
   const int nitems = ntile_b * g.G;
 
@@ -131,7 +135,7 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
     w = min(w, nitems - 1);
     const int tl = w / g.G;
     gi = w - tl * g.G;
-    return (int)blockIdx.x + tl * grid;
+    return tile0 + tl * tstep;
   };
   auto tile_end = [&](int w) { return w < nitems && (w % g.G) == g.G - 1; };
   long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
@@ -573,6 +577,10 @@ int conv_wide_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
   if (a.in_ld % 8 || a.V > 32 || a.Cin % 8 || a.Cout % 8 || a.out_ld % 8) return -1;
   WGeom g;
   g.dbg = nullptr;
+  {
+    static const int st = getenv("STGCN_WIDE_STRIDED") ? atoi(getenv("STGCN_WIDE_STRIDED")) : 0;
+    g.strided = st;
+  }
   int ktap, cin_f, cout_f;  // folded conv: taps, input / output channels
   if (a.stride == 1) {
     if (a.T_in != a.T_out) return -1;

@@ -97,15 +97,24 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float4* part, in
   __shared__ double sn[256], sm[256], sq[256];
   const int c = blockIdx.x;
   double n = 0, mean = 0, m2 = 0;
-  for (int b = threadIdx.x; b < nb; b += 256) {
-    const float4 g = part[(long)b * ldp + c];
-    const double nb_ = g.x;
-    if (nb_ == 0) continue;
-    const double tot = n + nb_;
-    const double d = g.y - mean;
-    mean += d * nb_ / tot;
-    m2 += g.z + d * d * n * nb_ / tot;
-    n = tot;
+  // chunks of 8 partials per thread: all 8 loads in flight before the (divide-carrying) merges
+  for (int b0 = 0; b0 < nb; b0 += 256 * 8) {
+    float4 gv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int b = b0 + threadIdx.x + 256 * u;
+      gv[u] = b < nb ? part[(long)b * ldp + c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const double nb_ = gv[u].x;
+      if (nb_ == 0) continue;
+      const double tot = n + nb_;
+      const double d = gv[u].y - mean;
+      mean += d * nb_ / tot;
+      m2 += gv[u].z + d * d * n * nb_ / tot;
+      n = tot;
+    }
   }
   sn[threadIdx.x] = n;
   sm[threadIdx.x] = mean;
