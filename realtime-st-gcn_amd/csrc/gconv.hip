@@ -23,6 +23,7 @@
 // tile); A rows staged through registers into padded LDS rows, B (packed Weff) by LDS-DMA with the
 // XOR swizzle on the source, fragment double-buffering, BN partial statistics in the epilogue.
 #include "common.h"
+#include <stdlib.h>
 #include "../../include/stgcn_amd.h"
 
 namespace {
@@ -573,6 +574,123 @@ __global__ __launch_bounds__(256, 2) void gconv_wgrad_kernel(const stgcn_gconv_w
   }
 }
 
+// Joint-grouped variant: block = (output joint w, COB output channels, 64 input channels, row range).
+// Every pair (w, j < deg[w]) shares the dy[:, w] panel, so a 64-row tile stages dy once plus deg x
+// panels (one per neighbour) instead of deg (dy, x) pairs: (1 + deg) / (2 deg) of the L2 -> LDS traffic
+// at COB = 64 and (COB/64 + deg) / (2 deg COB/64) at COB = 128.  Waves = (32-co quarter, 32-ci half);
+// each keeps one 32x32 accumulator per neighbour (J2 <= 5) and per k-step reads one dy fragment and
+// deg x fragments (ds_read_b64_tr_b16) for deg MFMAs.  Partials go to the same slab as above.
+constexpr int W2M = 64;   // rows per tile
+constexpr int J2 = 5;     // max neighbours per joint
+template <int COB>
+__global__ __launch_bounds__(COB / 16 * 64, 1) void gconv_wgrad2_kernel(const stgcn_gconv_wgrad_desc a, const WGG g) {
+  constexpr int NW = COB / 16, NT = NW * 64;
+  constexpr int PANEL = W2M * WPR;           // 32 channels x 64 rows
+  constexpr int DYP = COB / 32;              // dy panels
+  constexpr int STAGE = (DYP + 2 * J2) * PANEL;
+  constexpr int DYU = COB * W2M / 8 / NT;    // dy 16-B units per thread (2)
+  constexpr int XU = 64 * W2M / 8 / NT;      // x units per thread per neighbour (2 at COB 64, 1 at 128)
+  static_assert(DYU >= 1 && XU >= 1, "units");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cq = wave % DYP, ch = wave / DYP;  // co quarter (32), ci half (32)
+  const int V = a.V;
+  const int ngrp = g.nco * g.nci;
+  const int w = blockIdx.x / (ngrp * g.R);
+  const int rem = blockIdx.x % (ngrp * g.R);
+  const int rr = rem / ngrp, grp = rem % ngrp;
+  const int deg = a.deg[w];
+  const int co0 = (grp % g.nco) * COB, ci0 = (grp / g.nco) * 64;
+  const int t0 = rr * g.tpb, t1 = min(g.ntile, t0 + g.tpb);
+  int src[J2];
+#pragma unroll
+  for (int j = 0; j < J2; ++j) src[j] = j < deg ? a.nbr[w * a.J + j] : 0;
+
+  const bf16* __restrict__ dy = reinterpret_cast<const bf16*>(a.dy);
+  const bf16* __restrict__ x = reinterpret_cast<const bf16*>(a.x);
+  uint4 ry[DYU], rx[J2][XU];
+  // dy unit e = tid + NT*u: row e / (COB/8), 8 channels at (e % (COB/8)) * 8; x unit: row e / 8, ch (e % 8) * 8
+  auto load = [&](int t) {
+#pragma unroll
+    for (int u = 0; u < DYU; ++u) {
+      const int e = tid + NT * u, row = e / (COB / 8), cu = e % (COB / 8);
+      const int i = t * W2M + row;
+      ry[u] = make_uint4(0, 0, 0, 0);
+      if (i < a.NT && co0 + cu * 8 < a.Cout) ry[u] = *reinterpret_cast<const uint4*>(dy + ((long)i * V + w) * a.dy_ld + co0 + cu * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < J2; ++j)
+#pragma unroll
+      for (int u = 0; u < XU; ++u) {
+        const int e = tid + NT * u, row = e >> 3, cu = e & 7;
+        const int i = t * W2M + row;
+        rx[j][u] = make_uint4(0, 0, 0, 0);
+        if (j < deg && i < a.NT && ci0 + cu * 8 < a.Cin)
+          rx[j][u] = *reinterpret_cast<const uint4*>(x + ((long)i * V + src[j]) * a.x_ld + ci0 + cu * 8);
+      }
+  };
+  auto store = [&](int buf) {
+    char* base = smem + buf * STAGE;
+#pragma unroll
+    for (int u = 0; u < DYU; ++u) {
+      const int e = tid + NT * u, row = e / (COB / 8), cu = e % (COB / 8);
+      *reinterpret_cast<uint4*>(base + (cu >> 2) * PANEL + row * WPR + (cu & 3) * 16) = ry[u];
+    }
+#pragma unroll
+    for (int j = 0; j < J2; ++j)
+#pragma unroll
+      for (int u = 0; u < XU; ++u) {
+        const int e = tid + NT * u, row = e >> 3, cu = e & 7;
+        if (j < deg)
+          *reinterpret_cast<uint4*>(base + (DYP + 2 * j + (cu >> 2)) * PANEL + row * WPR + (cu & 3) * 16) = rx[j][u];
+      }
+  };
+
+  f32x16 acc[J2];
+#pragma unroll
+  for (int j = 0; j < J2; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+
+  int cur = 0;
+  if (t0 < t1) {
+    load(t0);
+    store(0);
+  }
+  __syncthreads();
+  for (int t = t0; t < t1; ++t) {
+    const bool more = t + 1 < t1;
+    if (more) load(t + 1);
+    const char* base = smem + cur * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < W2M / 16; ++ks) {
+      const bf16x8 fa = trfrag(base + cq * PANEL, ks * 16, lane);
+#pragma unroll
+      for (int j = 0; j < J2; ++j)
+        if (j < deg) {
+          const bf16x8 fb = trfrag(base + (DYP + 2 * j + ch) * PANEL, ks * 16, lane);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, acc[j], 0, 0, 0);
+        }
+    }
+    if (more) store(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // block partial of each pair (w, j) -> slab[rr][w*J + j][co][ci]
+  const int cc = ci0 + ch * 32 + (lane & 31);
+#pragma unroll
+  for (int j = 0; j < J2; ++j) {
+    if (j >= deg) continue;
+    float* slab = g.slab + ((long)rr * V * a.J + w * a.J + j) * a.Cout * a.Cin;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int oc = co0 + cq * 32 + acc_row(r, lane);
+      if (oc < a.Cout && cc < a.Cin) slab[(long)oc * a.Cin + cc] = acc[j][r];
+    }
+  }
+}
+
 // fp32 parity path of the gather wgrad: one thread per (pair, co, ci), loop over rows (small sizes)
 __global__ void gconv_wgrad_f32_kernel(const stgcn_gconv_wgrad_desc a) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -715,6 +833,29 @@ __global__ void gconv_dA_reduce_kernel(const float* __restrict__ part, const int
   dA[((long)p * V + nbr[w * J + j]) * V + w] += s;
 }
 
+// joint-grouped plan (gconv_wgrad2_kernel): COB = 128 when Cout % 128 == 0; 0 = not taken
+int w2_cob(const stgcn_gconv_wgrad_desc& a) {
+  static const bool off = getenv("STGCN_GCONV_WGRAD1") != nullptr;  // A/B switch: the per-pair kernel
+  if (off || a.J > J2 || a.Cin % 64 || a.Cout % 128) return 0;
+  // COB = 64 measured slower than the per-pair kernel at Cout = 64 (82 vs 69 us: one 4-wave block per
+  // CU against two); kept instantiable for narrower graphs
+  return 128;
+}
+
+WGG wplan2(const stgcn_gconv_wgrad_desc& a, int cob) {
+  WGG g{};
+  g.ntile = (a.NT + W2M - 1) / W2M;
+  g.nco = a.Cout / cob;
+  g.nci = a.Cin / 64;
+  const long groups = (long)a.V * g.nco * g.nci;
+  long R = (256 + groups - 1) / groups;
+  if (R > g.ntile) R = g.ntile;
+  if (R < 1) R = 1;
+  g.tpb = (int)((g.ntile + R - 1) / R);
+  g.R = (g.ntile + g.tpb - 1) / g.tpb;
+  return g;
+}
+
 WGG wplan(const stgcn_gconv_wgrad_desc& a) {
   WGG g{};
   g.ntile = (a.NT + WKM - 1) / WKM;
@@ -759,7 +900,8 @@ int gconv_weights_launch(const float* A, const float* W, const int* nbr, const i
 
 long gconv_wgrad_workspace(const stgcn_gconv_wgrad_desc& a, int dtype) {
   if (dtype != 1) return 0;
-  const WGG g = wplan(a);
+  const int cob = w2_cob(a);
+  const WGG g = cob ? wplan2(a, cob) : wplan(a);
   return (long)g.R * a.V * a.J * a.Cout * a.Cin * (long)sizeof(float);
 }
 
@@ -770,6 +912,24 @@ int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s
     return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
   }
   if (a.Cin % 8 || a.Cout % 8 || a.x_ld % 8 || a.dy_ld % 8) return STGCN_EBADSHAPE;
+  const int cob = w2_cob(a);
+  if (cob) {
+    WGG g = wplan2(a, cob);
+    if (!a.work || a.work_bytes < (long)g.R * E * (long)sizeof(float)) return STGCN_EBADSHAPE;
+    g.slab = reinterpret_cast<float*>(a.work);
+    const size_t lds = 2 * (size_t)(cob / 32 + 2 * J2) * W2M * WPR;
+    auto* k = cob == 128 ? gconv_wgrad2_kernel<128> : gconv_wgrad2_kernel<64>;
+    static bool attr2[2] = {false, false};
+    if (!attr2[cob == 128]) {
+      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr2[cob == 128] = true;
+    }
+    const long blocks = (long)a.V * g.nco * g.nci * g.R;
+    hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(cob / 16 * 64), lds, s, a, g);
+    hipLaunchKernelGGL(gslab_reduce_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, (const float*)g.slab,
+                       g.R, E, (long)a.Cout * a.Cin, a.deg, a.J, a.dweff);
+    return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
+  }
   WGG g = wplan(a);
   if (!a.work || a.work_bytes < (long)g.R * E * (long)sizeof(float)) return STGCN_EBADSHAPE;
   g.slab = reinterpret_cast<float*>(a.work);

@@ -481,30 +481,81 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, i
 }
 
 // ------------------------------------------------------------------ head: global average pool
-// out[n][c] = mean_{r < R} x[(n*R + r)][c]
+// out[n][c] = mean_{r < R} x[(n*R + r)][c].  Block = (sample n, 64 channels); 256 threads = 8 units of
+// 8 channels x 32 row groups, 16-B loads (bf16) four rows in flight per thread, fixed-order LDS combine.
 template <typename T>
 __global__ __launch_bounds__(256) void pool_rows_kernel(const T* __restrict__ x, int ld, int R, int C,
                                                         T* __restrict__ out, int ldo) {
-  __shared__ float red[256];
+  constexpr int VEC = 16 / (int)sizeof(T);  // channels per 16-B unit
+  constexpr int UPB = 64 / VEC;             // units per 64-channel block
+  constexpr int RG = 256 / UPB;             // row groups
+  __shared__ float red[RG][64];
   const int n = blockIdx.y;
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int rs = threadIdx.x >> 6;
-  float s = 0.f;
-  if (c < C)
-    for (int r = rs; r < R; r += 4) s += Tr<T>::to_f(x[((long)n * R + r) * ld + c]);
-  red[threadIdx.x] = s;
+  const int u = threadIdx.x % UPB, rg = threadIdx.x / UPB;
+  const int c0 = blockIdx.x * 64 + u * VEC;
+  const bool vec = (ld % VEC) == 0 && c0 + VEC <= C;
+  float s[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) s[e] = 0.f;
+  const T* base = x + (long)n * R * ld + c0;
+  if (vec) {
+    int r = rg;
+    for (; r + 3 * RG < R; r += 4 * RG) {
+      uint4 q[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) q[k] = *reinterpret_cast<const uint4*>(base + (long)(r + k * RG) * ld);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float f[VEC];
+        unpack16(q[k], f, (T*)nullptr);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) s[e] += f[e];
+      }
+    }
+    for (; r < R; r += RG) {
+      float f[VEC];
+      unpack16(*reinterpret_cast<const uint4*>(base + (long)r * ld), f, (T*)nullptr);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) s[e] += f[e];
+    }
+  } else {
+    for (int r = rg; r < R; r += RG)
+#pragma unroll
+      for (int e = 0; e < VEC; ++e)
+        if (c0 + e < C) s[e] += Tr<T>::to_f(base[(long)r * ld + e]);
+  }
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) red[rg][u * VEC + e] = s[e];
   __syncthreads();
-  if (rs == 0 && c < C) {
-    const float t = red[threadIdx.x] + red[threadIdx.x + 64] + red[threadIdx.x + 128] + red[threadIdx.x + 192];
-    out[(long)n * ldo + c] = Tr<T>::from_f(t / (float)R);
+  if (threadIdx.x < 64) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    float t = 0.f;
+    for (int k = 0; k < RG; ++k) t += red[k][threadIdx.x];
+    if (c < C) out[(long)n * ldo + c] = Tr<T>::from_f(t / (float)R);
   }
 }
 
+// dx[m][c] = dp[m / R][c] / R; one thread per 16-B unit of a row when aligned
 template <typename T>
 __global__ __launch_bounds__(256) void unpool_rows_kernel(const T* __restrict__ dp, int ldp, int R, int C, long M,
                                                           T* __restrict__ dx, int ldx) {
-  const long total = M * C;
+  constexpr int VEC = 16 / (int)sizeof(T);
   const float inv = 1.f / (float)R;
+  if ((C % VEC) == 0 && (ldp % VEC) == 0 && (ldx % VEC) == 0) {
+    const int CU = C / VEC;
+    const long total = M * CU;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+      const long m = i / CU;
+      const int c = (int)(i - m * CU) * VEC;
+      float f[VEC];
+      unpack16(*reinterpret_cast<const uint4*>(dp + (m / R) * ldp + c), f, (T*)nullptr);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) f[e] *= inv;
+      *reinterpret_cast<uint4*>(dx + m * ldx + c) = pack16(f, (T*)nullptr);
+    }
+    return;
+  }
+  const long total = M * C;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     const long m = i / C;
     const int c = (int)(i % C);
@@ -677,7 +728,7 @@ int pool_rows_launch(const void* x, int ld, int N, int R, int C, void* out, int 
 }
 
 int unpool_rows_launch(const void* dp, int ldp, int R, int C, long M, void* dx, int ldx, int dtype, hipStream_t s) {
-  DISPATCH_T(dtype, hipLaunchKernelGGL(unpool_rows_kernel<T>, dim3(grid_for(M * C)), dim3(256), 0, s, (const T*)dp,
+  DISPATCH_T(dtype, hipLaunchKernelGGL(unpool_rows_kernel<T>, dim3(grid_for(M * C / 8 + 1)), dim3(256), 0, s, (const T*)dp,
                                        ldp, R, C, M, (T*)dx, ldx));
   RET_HIP;
 }
