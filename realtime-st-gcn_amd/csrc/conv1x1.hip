@@ -1,0 +1,223 @@
+// 1x1 convolutions of the layer (residual.0 stgcn.py:165-170 at stride 1 or 2, and their input grads)
+// as a row GEMM: out[m][co] (+)= sum_ci W[co][ci] in[row(m)][ci] (+ bias[co]), with optional BatchNorm
+// partial statistics of the output.
+//   forward, stride S:  row(m) = input row of frame S*t for output frame t (the temporal subsampling of
+//                       a 1x1 conv with stride (S, 1));
+//   trans (input grad): output frame t takes input frame t/S when S divides t, else it is zero (the
+//                       transposed strided 1x1 conv scatters into every S-th frame only).
+// A tile is 128 output rows x BN output channels; the block stages its 128 input rows whole (all Cin
+// channels, rows padded by 16 B: conflict-free ds_read_b128) and streams the Kt = 1 MFMA-fragment
+// image of W (stgcn_pack_weight_frag) from L2 straight into registers; 4 waves = 2 row halves x 2
+// column halves, 32x32x16 bf16 MFMA.  The epilogue adds the bias, computes per-channel Welford
+// partials on the fp32 sums and writes 16-B rows through an LDS transpose of the tile.
+// The frame-tiled conv_tile kernel staged (F-1)*S + 1 input frames per F output frames with the
+// generic Kt halo logic: at stride 2 half of every halo was discarded; this kernel reads each needed
+// input row once.
+#include "common.h"
+#include "../../include/stgcn_amd.h"
+#include <stdlib.h>
+
+namespace {
+
+constexpr int BM = 128;  // output rows per tile
+constexpr int NT = 256;
+
+struct XGeom {
+  long M;     // output rows
+  int ncol;   // column tiles
+  int nrow;   // row tiles
+  int k16n;   // K blocks per column of the fragment image (Cin_pad / 16)
+};
+
+template <int KS, int BN>
+__global__ __launch_bounds__(NT, 2) void conv1x1_kernel(const stgcn_conv_desc a, const XGeom g) {
+  constexpr int CIN = KS * 16;
+  constexpr int RS = CIN * 2 + 16;           // padded LDS row (bytes)
+  constexpr int TM = 2, TN = BN / 64;        // wave tile: 64 rows x BN/2 columns
+  constexpr int UPR = CIN / 8;               // 16-B units per input row
+  constexpr int AU = BM * UPR / NT;          // units per thread
+  static_assert(BM * UPR % NT == 0, "A units");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int ct = blockIdx.x % g.ncol, rt = blockIdx.x / g.ncol;
+  const long m0 = (long)rt * BM;
+  const int n0 = ct * BN;
+  const int V = a.V, S = a.stride;
+
+  // ---- stage the tile's input rows (zero rows: past M, or frames the transposed conv does not feed)
+  const bf16* __restrict__ in = reinterpret_cast<const bf16*>(a.in);
+  {
+    uint4 ra[AU];
+#pragma unroll
+    for (int u = 0; u < AU; ++u) {
+      const int e = tid + u * NT, row = e / UPR, cu = e % UPR;
+      const long m = m0 + row;
+      ra[u] = make_uint4(0, 0, 0, 0);
+      if (m < g.M) {
+        const long fr = m / V;
+        const int v = (int)(m - fr * V);
+        const int t = (int)(fr % a.T_out);
+        const long n = fr / a.T_out;
+        int ti = -1;
+        if (!a.trans) ti = t * S;
+        else if (t % S == 0) ti = t / S;
+        if (ti >= 0) ra[u] = *reinterpret_cast<const uint4*>(in + ((n * a.T_in + ti) * V + v) * a.in_ld + cu * 8);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < AU; ++u) {
+      const int e = tid + u * NT, row = e / UPR, cu = e % UPR;
+      *reinterpret_cast<uint4*>(smem + row * RS + cu * 16) = ra[u];
+    }
+  }
+  __syncthreads();
+
+  // ---- K loop: A fragments from LDS, B fragments (fragment image blocks [c32][k16]) from L2
+  const bf16* __restrict__ wf = reinterpret_cast<const bf16*>(a.w_frag);
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const char* arow[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) arow[i] = smem + ((wm * TM + i) * 32 + lr) * RS + lh * 16;
+  const bf16* bcol[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) bcol[j] = wf + (long)((n0 >> 5) + wn * TN + j) * g.k16n * 512 + lane * 8;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    bf16x8 fb[TN], fa[TM];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) fb[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(bcol[j] + ks * 512));
+#pragma unroll
+    for (int i = 0; i < TM; ++i) fa[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(arow[i] + ks * 32));
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+  }
+
+  // ---- epilogue: bias, BN partials (fp32 values of the valid rows), bf16 tile -> LDS -> 16-B rows
+  const int rows_valid = (int)((g.M - m0) < BM ? (g.M - m0) : BM);
+  __syncthreads();  // every wave is done reading the staged rows
+  constexpr int OS = BN * 2 + 16;  // padded output row in LDS
+  float4* red = reinterpret_cast<float4*>(smem + BM * OS);  // [2 row halves][BN]
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int cl = (wn * TN + j) * 32 + lr;  // column within the tile
+    const int col = n0 + cl;
+    const float b = (a.bias && a.bias_mode == 1) ? a.bias[col] : 0.f;
+    float s = 0.f, cnt = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (wm * TM + i) * 32 + acc_row(r, lane);
+        const float v = acc[i][j][r] + b;
+        acc[i][j][r] = v;
+        *reinterpret_cast<bf16*>(smem + row * OS + cl * 2) = (bf16)v;
+        if (row < rows_valid) {
+          s += v;
+          cnt += 1.f;
+        }
+      }
+    if (a.stats) {
+      Welford w;
+      w.n = cnt;
+      w.mean = cnt > 0.f ? s / cnt : 0.f;
+      float m2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = (wm * TM + i) * 32 + acc_row(r, lane);
+          const float d = acc[i][j][r] - w.mean;
+          if (row < rows_valid) m2 += d * d;
+        }
+      w.m2 = m2;
+      Welford o;
+      o.n = __shfl_xor(w.n, 32);
+      o.mean = __shfl_xor(w.mean, 32);
+      o.m2 = __shfl_xor(w.m2, 32);
+      const Welford t = welford_merge(w, o);
+      if (lh == 0) red[wm * BN + cl] = make_float4(t.n, t.mean, t.m2, 0.f);
+    }
+  }
+  __syncthreads();
+  if (a.stats && tid < BN) {
+    const float4 p = red[tid], q = red[BN + tid];
+    const Welford t = welford_merge(Welford{p.x, p.y, p.z}, Welford{q.x, q.y, q.z});
+    reinterpret_cast<float4*>(a.stats)[(long)rt * a.Cout_pad + n0 + tid] = make_float4(t.n, t.mean, t.m2, 0.f);
+  }
+  bf16* __restrict__ out = reinterpret_cast<bf16*>(a.out);
+  constexpr int OU = BN / 8;  // 16-B units per output row
+#pragma unroll
+  for (int u = 0; u < BM * OU / NT; ++u) {
+    const int e = tid + u * NT, row = e / OU, cu = e % OU;
+    if (row < rows_valid) {
+      uint4 v = *reinterpret_cast<const uint4*>(smem + row * OS + cu * 16);
+      uint4* p = reinterpret_cast<uint4*>(out + (m0 + row) * a.out_ld + n0 + cu * 8);
+      if (a.accumulate) {
+        float f[8], o[8];
+        unpack16(v, f, (bf16*)nullptr);
+        unpack16(*p, o, (bf16*)nullptr);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) f[k] += o[k];
+        v = pack16(f, (bf16*)nullptr);
+      }
+      *p = v;
+    }
+  }
+}
+
+template <int KS, int BN>
+int launch1(const stgcn_conv_desc& a, const XGeom& g, hipStream_t s) {
+  constexpr int RS = KS * 16 * 2 + 16, OS = BN * 2 + 16;
+  size_t lds = (size_t)BM * RS;
+  const size_t lout = (size_t)BM * OS + 2 * BN * 16;
+  if (lout > lds) lds = lout;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv1x1_kernel<KS, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL((conv1x1_kernel<KS, BN>), dim3((unsigned)((long)g.nrow * g.ncol)), dim3(NT), lds, s, a, g);
+  return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
+}
+
+}  // namespace
+
+long conv_rows_num_row_blocks(long M, int cout);
+
+// returns -1 when the shape is not handled here
+int conv1x1_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
+  static const bool off = getenv("STGCN_NO_CONV1X1") != nullptr;  // A/B switch
+  if (off || dtype != 1 || !a.w_frag || a.Kt != 1 || a.pad != 0 || a.pro != 0) return -1;
+  if (a.stride < 1 || a.bias_mode < 0 || a.bias_mode > 1) return -1;
+  if (a.trans ? a.T_in != (a.T_out - 1) / a.stride + 1 : a.T_out != (a.T_in - 1) / a.stride + 1) return -1;
+  if (a.in_ld % 8 || a.out_ld % 8 || a.Cout % 64 || a.Cin_pad != a.Cin || a.Cout_pad < a.Cout) return -1;
+  if (a.Cin != 64 && a.Cin != 128 && a.Cin != 256) return -1;
+  XGeom g;
+  g.M = (long)a.N * a.T_out * a.V;
+  const int BN = a.Cout % 128 == 0 ? 128 : 64;
+  g.ncol = a.Cout / BN;
+  const long nrow = (g.M + BM - 1) / BM;
+  if (nrow * g.ncol > 0x7fffffffL) return -1;
+  g.nrow = (int)nrow;
+  g.k16n = a.Cin_pad / 16;
+  if (a.stats && nrow > conv_rows_num_row_blocks(g.M, a.Cout)) return -1;
+  if (BN == 128) {
+    if (a.Cin == 64) return launch1<4, 128>(a, g, s);
+    if (a.Cin == 128) return launch1<8, 128>(a, g, s);
+    return launch1<16, 128>(a, g, s);
+  }
+  if (a.Cin == 64) return launch1<4, 64>(a, g, s);
+  if (a.Cin == 128) return launch1<8, 64>(a, g, s);
+  return launch1<16, 64>(a, g, s);
+}

@@ -673,8 +673,14 @@ int conv_persist_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s);
 
 int conv_wide_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s);
 
+int conv1x1_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s);
+
 int conv_tile_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
   static const bool no_persist = getenv("STGCN_NO_PERSIST") != nullptr;  // A/B switch
+  if (a.Kt == 1) {  // 1x1 convs (residual, stride 1 or 2, and their input grads): row GEMM (conv1x1.hip)
+    const int r = conv1x1_launch(a, dtype, s);
+    if (r >= 0) return r;
+  }
   // 64-channel stride-1 forward: the wide kernel's 32-channel items beat the weight-resident kernel
   // (70 vs 74 us on the config-2 shape); the transposed (data-grad) pass stays on conv_persist (61 vs 64 us)
   if (a.stride == 1 && !a.trans && a.Cin == 64) {

@@ -91,6 +91,15 @@ def pack_weight(w3: torch.Tensor, dtype, stride: int = 1, trans: bool = False) -
                 "pack_weight_frag")
         out.frag_ptr, out.frag_stride = buf[n:].data_ptr(), 1
         return out, cp, kp
+    if dtype == torch.bfloat16 and Kt == 1 and kp == Ci and Ci in (64, 128, 256) and Co % 64 == 0:
+        # 1x1 weights: fragment image for the row-GEMM kernel (conv1x1.hip), valid at any stride
+        buf = torch.empty(2 * n, dtype=dtype, device=w3.device)
+        out = buf[:n].view(Kt, cp, kp)
+        L.check(L.lib().stgcn_pack_weight_frag(w3.data_ptr(), s0, s1, s2, Kt, Co, Ci, out.data_ptr(),
+                                               buf[n:].data_ptr(), cp, kp, L.dtype_code(dtype), L.stream()),
+                "pack_weight_frag")
+        out.frag_ptr, out.frag_stride = buf[n:].data_ptr(), 0
+        return out, cp, kp
     out = torch.empty((Kt, cp, kp), dtype=dtype, device=w3.device)
     L.check(L.lib().stgcn_pack_weight(w3.data_ptr(), s0, s1, s2, Kt, Co, Ci, out.data_ptr(), cp, kp,
                                       L.dtype_code(dtype), L.stream()), "pack_weight")
@@ -108,7 +117,8 @@ def conv_rows(x, w3p, Cin, Cout, cp, kp, T_in, T_out, Kt=1, stride=1, pad=0, tra
         out = cl_empty(N, Cout, T_out, V, x.dtype, x.device)
     d = L.ConvDesc()
     d.in_, d.out, d.w = x.data_ptr(), out.data_ptr(), w3p.data_ptr()
-    d.w_frag = getattr(w3p, "frag_ptr", None) if getattr(w3p, "frag_stride", 0) == stride else None
+    fs = getattr(w3p, "frag_stride", None)
+    d.w_frag = getattr(w3p, "frag_ptr", None) if fs is not None and fs in (stride, 0) else None
     d.bias = L.ptr(bias)
     d.pro_a, d.pro_b, d.pro_stats = L.ptr(pro_a), L.ptr(pro_b), L.ptr(pro_stats)
     d.stats = L.ptr(stats)
