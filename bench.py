@@ -46,9 +46,11 @@ def loss_fn(logits, labels, weight):
     return ce + mse
 
 
-def tcn_flops_c64():
-    # temporal conv of a C=64, stride-1 layer: 2*N*T*V*C*C*Kt
-    return 2.0 * N_BATCH * T_LEN * V_J * 64 * 64 * 9
+# The roofline kernel: conv_wide_kernel<128,9,6,1,0,64>, the Kt=9 stride-1 temporal-conv forward of the
+# C=128 (T=150) and C=256 (T=75) layers — the dominant kernel template of the step (with its data-grad
+# twin <128,9,6,0>), 4 launches per step.  Algorithmic work per launch = 2*N*T*V*C*C*Kt.
+ROOF_TAGS = {"tcn_fwd_c128": 2.0 * N_BATCH * (T_LEN // 2) * V_J * 128 * 128 * 9,
+             "tcn_fwd_c256": 2.0 * N_BATCH * (T_LEN // 4) * V_J * 256 * 256 * 9}
 
 
 def cpu_baseline(pkg, model_cpu_sd):
@@ -150,18 +152,18 @@ def main():
             torch.distributed.all_reduce(flat)
         opt_step()
 
-    # live timing of the dominant kernel (temporal-conv forward of the C=64 layers): HIP events on
+    # live timing of the roofline kernel (ROOF_TAGS: temporal-conv forward of the C=128/256 layers): HIP events on
     # the stream the kernel is launched on.  ROCm refuses timing events inside a captured graph, so in
     # graph mode the events bracket the launches of one eager step run right after the timed region.
     events = []
     timing = {"on": False}
 
     def hook(tag, phase):
-        if tag != "tcn_fwd_c64" or not timing["on"]:
+        if tag not in ROOF_TAGS or not timing["on"]:
             return
         ev = torch.cuda.Event(enable_timing=True)
         ev.record(torch.cuda.current_stream())
-        events.append(ev)
+        events.append((tag, ev))
 
     K.EVENT_HOOK = hook
     for _ in range(max(args.warmup, 2)):
@@ -220,18 +222,25 @@ def main():
         elapsed = t.item()
 
     # eager mode: every launch of the timed region; graph mode: the 6 launches of the step after it
-    kt = [events[i].elapsed_time(events[i + 1]) for i in range(0, len(events) - 1, 2)]
-    k_ms = sum(kt) / len(kt) if kt else float("nan")
-    achieved = tcn_flops_c64() / (k_ms * 1e-3) / 1e12 if kt else None
+    # (start, end) event pairs of the roofline launches: achieved = their algorithmic flops / their time
+    kt = [(events[i][0], events[i][1].elapsed_time(events[i + 1][1])) for i in range(0, len(events) - 1, 2)]
+    k_ms = sum(t for _, t in kt) / len(kt) if kt else float("nan")
+    achieved = sum(ROOF_TAGS[g] for g, _ in kt) / (sum(t for _, t in kt) * 1e-3) / 1e12 if kt else None
 
     frames = world * args.steps * N_BATCH * T_LEN
     value = frames / elapsed
     if rank == 0:
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_tcn_fwd_c64.json")
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+        # HBM bytes per launch from the PMC passes of each launch shape (tools/pmc_conv.sh), averaged over
+        # the timed launches like `achieved`
+        per = {}
+        for g in ROOF_TAGS:
+            pmc = os.path.join(ROOT, "profiles", f"pmc_{g}.json")
+            if os.path.exists(pmc):
+                with open(pmc) as f:
+                    per[g] = json.load(f).get("hbm_bytes_per_launch")
+        if kt and all(per.get(g) for g, _ in kt):
+            traffic = sum(per[g] for g, _ in kt) / len(kt)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(pkg, cpu_sd)
@@ -245,7 +254,8 @@ def main():
                                    "bwd + Adam", "global_batch": N_BATCH * world, "seq_len": T_LEN, "joints": V_J,
                        "parallelism": f"dp{world}" if world > 1 else "single",
                        "launch": "eager" if not args.graph else "hip-graph replay (fwd+bwd | allreduce | Adam)"},
-            "roofline": {"kernel": "conv_wide_kernel<64,9,12,*,0,32> (persistent warp-specialised temporal conv fwd, C=64, Kt=9, stride 1)",
+            "roofline": {"kernel": "conv_wide_kernel<128,9,6,1,0,64> (persistent warp-specialised Kt=9 stride-1 "
+                                   "temporal conv fwd of the C=128 and C=256 layers, 4 launches/step)",
                          "bound": "mfma", "achieved": round(achieved, 2) if achieved else None,
                          "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4) if achieved else None,
