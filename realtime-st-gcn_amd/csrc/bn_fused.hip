@@ -43,6 +43,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_fused_kernel(const stgcn_bn
   const T* dy = reinterpret_cast<const T*>(a.dy);
   const T* mref = reinterpret_cast<const T*>(a.mref);
   const T* x1 = reinterpret_cast<const T*>(a.x1);
+  // BN1 backward: the mask reference and the normalised input are the same tensor (g): load it once
+  const bool same_x = MASK == 2 && (const void*)x1 == (const void*)mref && a.ldx1 == a.ldm;
   const T* x2 = reinterpret_cast<const T*>(a.x2);
   float s0[VEC], s1[VEC], s2[VEC];
 #pragma unroll
@@ -68,7 +70,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_fused_kernel(const stgcn_bn
         const long mm = ok[u] ? m : mb;
         Udz[u] = *reinterpret_cast<const uint4*>(dy + mm * a.lddy + c0);
         Umr[u] = *reinterpret_cast<const uint4*>(mref + mm * a.ldm + c0);
-        Uxa[u] = *reinterpret_cast<const uint4*>(x1 + mm * a.ldx1 + c0);
+        if (!same_x) Uxa[u] = *reinterpret_cast<const uint4*>(x1 + mm * a.ldx1 + c0);
         if (X2) Uxb[u] = *reinterpret_cast<const uint4*>(x2 + mm * a.ldx2 + c0);
       }
 #pragma unroll
@@ -77,7 +79,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_fused_kernel(const stgcn_bn
         float dz[1][VEC], mr[1][VEC], xa[1][VEC], xb[1][VEC];
         unpack16(Udz[u], dz[0], (T*)nullptr);
         unpack16(Umr[u], mr[0], (T*)nullptr);
-        unpack16(Uxa[u], xa[0], (T*)nullptr);
+        unpack16(same_x ? Umr[u] : Uxa[u], xa[0], (T*)nullptr);
         if (X2) unpack16(Uxb[u], xb[0], (T*)nullptr);
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
@@ -145,6 +147,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(const stgcn_bn_
   const T* dy = reinterpret_cast<const T*>(a.dy);
   const T* mref = reinterpret_cast<const T*>(a.mref);
   const T* x1 = reinterpret_cast<const T*>(a.x1);
+  // BN1 backward: the mask reference and the normalised input are the same tensor (g): load it once
+  const bool same_x = MASK == 2 && (const void*)x1 == (const void*)mref && a.ldx1 == a.ldm;
   const T* x2 = reinterpret_cast<const T*>(a.x2);
   T* o1 = reinterpret_cast<T*>(a.out1);
   T* o2 = reinterpret_cast<T*>(a.out2);
@@ -188,7 +192,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(const stgcn_bn_
         const long mm = ok[u] ? m : mb;
         Udz[u] = *reinterpret_cast<const uint4*>(dy + mm * a.lddy + c0);
         Umr[u] = *reinterpret_cast<const uint4*>(mref + mm * a.ldm + c0);
-        Uxa[u] = *reinterpret_cast<const uint4*>(x1 + mm * a.ldx1 + c0);
+        if (!same_x) Uxa[u] = *reinterpret_cast<const uint4*>(x1 + mm * a.ldx1 + c0);
         if (O2 == 1) Uxb[u] = *reinterpret_cast<const uint4*>(x2 + mm * a.ldx2 + c0);
         if (O2 && a.acc2) Upa[u] = *reinterpret_cast<const uint4*>(o2 + mm * a.ldo2 + c0);
       }
@@ -199,7 +203,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(const stgcn_bn_
         float dz[VEC], mr[VEC], xa[VEC], xb[VEC], pa[VEC];
         unpack16(Udz[u], dz, (T*)nullptr);
         unpack16(Umr[u], mr, (T*)nullptr);
-        unpack16(Uxa[u], xa, (T*)nullptr);
+        unpack16(same_x ? Umr[u] : Uxa[u], xa, (T*)nullptr);
         if (O2 == 1) unpack16(Uxb[u], xb, (T*)nullptr);
         if (O2 && a.acc2) unpack16(Upa[u], pa, (T*)nullptr);
         float r1[VEC], r2[VEC];
