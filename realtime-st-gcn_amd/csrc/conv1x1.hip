@@ -175,6 +175,85 @@ __global__ __launch_bounds__(NT, 2) void conv1x1_kernel(const stgcn_conv_desc a,
   }
 }
 
+// Narrow 1x1 convs (fcn_in 3 -> 64, stgcn.py:49, and its input grad 64 -> 3) are pure streaming: VALU
+// dot products, weights ([Cout_pad][Cin_pad] packed image) staged once per block in LDS; blocks stride
+// over the rows.
+//   WIDE_OUT (Cin <= 16, Cout <= 64, Cout % 8 == 0): thread = (row, 8 output channels), the row's Cin
+//     inputs as scalars (any ld), coalesced 16-B stores, weights k-major in LDS (conflict-free)
+//   !WIDE_OUT (Cout <= 8, Cin % 8 == 0): thread = row, 16-B input loads, Cout scalar outputs (any ld),
+//     weights read as broadcasts
+template <bool WIDE_OUT>
+__global__ __launch_bounds__(NT) void conv1x1_narrow_kernel(const stgcn_conv_desc a, long M) {
+  __shared__ __attribute__((aligned(16))) float sw[4096];
+  const int KP = a.Cin_pad;
+  const bf16* __restrict__ w = reinterpret_cast<const bf16*>(a.w);
+  for (int e = threadIdx.x; e < a.Cout_pad * KP; e += NT) sw[e] = (float)w[e];
+  __syncthreads();
+  const bf16* __restrict__ in = reinterpret_cast<const bf16*>(a.in);
+  bf16* __restrict__ out = reinterpret_cast<bf16*>(a.out);
+  const bool bias = a.bias && a.bias_mode == 1;
+  if constexpr (WIDE_OUT) {
+    // weights transposed in LDS (k-major): the 8 units of a row sit in 8 distinct banks
+    const int CP = a.Cout_pad, CU = a.Cout / 8;
+    __syncthreads();
+    for (int e = threadIdx.x; e < CP * KP; e += NT) {
+      const int co = e / KP, k = e - co * KP;
+      sw[k * CP + co] = (float)w[e];
+    }
+    __syncthreads();
+    // 32-bit index math (the launcher guarantees M * Cout / 8 < 2^31): a 64-bit division per unit
+    // cost more than the unit's arithmetic
+    const unsigned n = (unsigned)(M * CU);
+    for (unsigned i = blockIdx.x * NT + threadIdx.x; i < n; i += gridDim.x * NT) {
+      const unsigned m = i / (unsigned)CU;
+      const int c0 = (int)(i - m * (unsigned)CU) * 8;
+      const bf16* xr = in + (long)m * a.in_ld;
+      float f[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = bias ? a.bias[c0 + e] : 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (k < a.Cin) {
+          const float xk = (float)xr[k];
+          const float4 w0 = *reinterpret_cast<const float4*>(&sw[k * CP + c0]);
+          const float4 w1 = *reinterpret_cast<const float4*>(&sw[k * CP + c0 + 4]);
+          f[0] = fmaf(w0.x, xk, f[0]); f[1] = fmaf(w0.y, xk, f[1]); f[2] = fmaf(w0.z, xk, f[2]); f[3] = fmaf(w0.w, xk, f[3]);
+          f[4] = fmaf(w1.x, xk, f[4]); f[5] = fmaf(w1.y, xk, f[5]); f[6] = fmaf(w1.z, xk, f[6]); f[7] = fmaf(w1.w, xk, f[7]);
+        }
+      uint4* p = reinterpret_cast<uint4*>(out + (long)m * a.out_ld + c0);
+      if (a.accumulate) {
+        float o[8];
+        unpack16(*p, o, (bf16*)nullptr);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] += o[e];
+      }
+      *p = pack16(f, (bf16*)nullptr);
+    }
+    return;
+  }
+  for (long m = (long)blockIdx.x * NT + threadIdx.x; m < M; m += (long)gridDim.x * NT) {
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = (bias && e < a.Cout) ? a.bias[e] : 0.f;
+    for (int k0 = 0; k0 < a.Cin; k0 += 8) {
+      float x[8];
+      unpack16(*reinterpret_cast<const uint4*>(in + m * a.in_ld + k0), x, (bf16*)nullptr);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (e < a.Cout) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[e] = fmaf(sw[e * KP + k0 + k], x[k], acc[e]);
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (e < a.Cout) {
+        bf16* p = out + m * a.out_ld + e;
+        *p = (bf16)(a.accumulate ? acc[e] + (float)*p : acc[e]);
+      }
+  }
+}
+
 template <int KS, int BN>
 int launch1(const stgcn_conv_desc& a, const XGeom& g, hipStream_t s) {
   constexpr int RS = KS * 16 * 2 + 16, OS = BN * 2 + 16;
@@ -198,7 +277,22 @@ long conv_rows_num_row_blocks(long M, int cout);
 // returns -1 when the shape is not handled here
 int conv1x1_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
   static const bool off = getenv("STGCN_NO_CONV1X1") != nullptr;  // A/B switch
-  if (off || dtype != 1 || !a.w_frag || a.Kt != 1 || a.pad != 0 || a.pro != 0) return -1;
+  if (off || dtype != 1 || a.Kt != 1 || a.pad != 0 || a.pro != 0) return -1;
+  if (a.stride == 1 && a.T_in == a.T_out && !a.stats && a.bias_mode >= 0 && a.bias_mode <= 1 &&
+      (long)a.Cout_pad * a.Cin_pad <= 4096) {
+    const long M = (long)a.N * a.T_out * a.V;
+    long nb = (M + NT - 1) / NT;
+    if (nb > 1024) nb = 1024;
+    if (a.Cin <= 16 && a.Cout <= 64 && a.Cout % 8 == 0 && a.out_ld % 8 == 0 && M * (a.Cout / 8) < 0x7fffffffL) {
+      hipLaunchKernelGGL(conv1x1_narrow_kernel<true>, dim3((unsigned)nb), dim3(NT), 0, s, a, M);
+      return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
+    }
+    if (a.Cout <= 8 && a.Cin % 8 == 0 && a.in_ld % 8 == 0) {
+      hipLaunchKernelGGL(conv1x1_narrow_kernel<false>, dim3((unsigned)nb), dim3(NT), 0, s, a, M);
+      return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
+    }
+  }
+  if (!a.w_frag) return -1;
   if (a.stride < 1 || a.bias_mode < 0 || a.bias_mode > 1) return -1;
   if (a.trans ? a.T_in != (a.T_out - 1) / a.stride + 1 : a.T_out != (a.T_in - 1) / a.stride + 1) return -1;
   if (a.in_ld % 8 || a.out_ld % 8 || a.Cout % 64 || a.Cin_pad != a.Cin || a.Cout_pad < a.Cout) return -1;
