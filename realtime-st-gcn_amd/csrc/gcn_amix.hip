@@ -257,13 +257,18 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
 __global__ __launch_bounds__(256) void gcn_bias_kernel(const float* A, const float* b, float* out, int P, int V, int C,
                                                        int per_sample) {
   // out[(n), w, c] = sum_p b[p*C + c] * colsum_p[w],  colsum_p[w] = sum_v A[(n), p, v, w] (staged in LDS)
+  // A is staged in LDS by coalesced loads first: a per-thread loop of V dependent global loads was the
+  // whole cost of this kernel
   __shared__ float cs[4 * VMAX];
+  __shared__ float sA[4 * VMAX * VMAX];
   const int n = blockIdx.y;
   const float* An = A + (per_sample ? (long)n * P * V * V : 0);
+  for (int i = threadIdx.x; i < P * V * V; i += blockDim.x) sA[i] = An[i];
+  __syncthreads();
   for (int i = threadIdx.x; i < P * V; i += blockDim.x) {
     const int p = i / V, w = i % V;
     float t = 0.f;
-    for (int v = 0; v < V; ++v) t += An[(p * V + v) * V + w];
+    for (int v = 0; v < V; ++v) t += sA[(p * V + v) * V + w];
     cs[i] = t;
   }
   __syncthreads();
@@ -295,10 +300,13 @@ __global__ __launch_bounds__(256) void gcn_bias_bwd_kernel(const float* A, const
     return;
   }
   __shared__ float cs[4 * VMAX];
+  __shared__ float sA[4 * VMAX * VMAX];
+  for (int i = threadIdx.x; i < P * V * V; i += 256) sA[i] = A[i];
+  __syncthreads();
   for (int i = threadIdx.x; i < P * V; i += 256) {
     const int p = i / V, w = i % V;
     float t = 0.f;
-    for (int v = 0; v < V; ++v) t += A[(p * V + v) * V + w];
+    for (int v = 0; v < V; ++v) t += sA[(p * V + v) * V + w];
     cs[i] = t;
   }
   __syncthreads();

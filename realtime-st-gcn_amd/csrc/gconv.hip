@@ -762,23 +762,39 @@ __global__ void gconv_dA_kernel(const float* __restrict__ dweff, const float* __
 
 constexpr int PMAX = 4;
 // dW[p][e] += sum_{pairs} A[p][v][w] dWeff[pair][e] for all p in one pass (dWeff read once).
-// Block = 64 e-columns x 4 groups over target joints w (w = g, g+4, ...); fixed-order LDS combine.
+// Block = 64 e-columns x 4 groups over the used (w, j) pairs (pair list and coefficients A[p][S(w)_j][w]
+// staged in LDS first: the per-pair deg -> nbr -> A chain of dependent global loads was this kernel's
+// cost); fixed-order LDS combine.
+constexpr int DW_PAIRS = 32 * 8;  // V * J upper bound for the LDS tables
 __global__ __launch_bounds__(256) void gconv_dw_all_kernel(const float* __restrict__ dweff, const float* __restrict__ A,
                                                            const int* nbr, const int* deg, int P, int V, int J, long E,
                                                            float* dW) {
+  __shared__ int spair[DW_PAIRS];
+  __shared__ float scoef[DW_PAIRS][PMAX];
+  __shared__ int snp;
+  if (threadIdx.x == 0) {  // compacted list of used pairs, in (w, j) order
+    int n = 0;
+    for (int w = 0; w < V; ++w)
+      for (int j = 0; j < deg[w]; ++j) spair[n++] = w * J + j;
+    snp = n;
+  }
+  __syncthreads();
+  const int np = snp;
+  for (int i = threadIdx.x; i < np * PMAX; i += 256) {
+    const int k = i / PMAX, p = i % PMAX;
+    const int pr = spair[k], w = pr / J;
+    scoef[k][p] = p < P ? A[((long)p * V + nbr[pr]) * V + w] : 0.f;
+  }
+  __syncthreads();
   const int g = threadIdx.x >> 6;
   const long e = (long)blockIdx.x * 64 + (threadIdx.x & 63);
   float acc[PMAX] = {0.f, 0.f, 0.f, 0.f};
   if (e < E) {
-    for (int w = g; w < V; w += 4) {
-      const int dg = deg[w];
-      for (int j = 0; j < dg; ++j) {
-        const int v = nbr[w * J + j];
-        const float d = dweff[(long)(w * J + j) * E + e];
+#pragma unroll 4
+    for (int k = g; k < np; k += 4) {
+      const float d = dweff[(long)spair[k] * E + e];
 #pragma unroll
-        for (int p = 0; p < PMAX; ++p)
-          if (p < P) acc[p] += A[((long)p * V + v) * V + w] * d;
-      }
+      for (int p = 0; p < PMAX; ++p) acc[p] += scoef[k][p] * d;
     }
   }
   __shared__ float part[4][PMAX][64];
@@ -955,7 +971,7 @@ long gconv_wgrad_finish_workspace(int P, int V, int J, int Cout, int Cin) {
 int gconv_wgrad_finish_launch(const float* dweff, const float* A, const float* W, const int* nbr, const int* deg,
                               int P, int V, int J, int Cout, int Cin, float* dW, float* dA, void* work, hipStream_t s) {
   const long E = (long)Cout * Cin;
-  if (P > PMAX || (dA && !work)) {  // generic per-partition path (dA via atomics-free per-(pair,p) blocks)
+  if (P > PMAX || (dA && !work) || V * J > DW_PAIRS) {  // generic per-partition path (dA via per-(pair,p) blocks)
     const long n = (long)P * E;
     if (dW)
       hipLaunchKernelGGL(gconv_dw_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dweff, A, nbr, deg, P,
