@@ -389,10 +389,21 @@ __global__ void gconv_weights_kernel(const float* __restrict__ A, const float* _
   const int C8 = C_pad / 8;
   const long total = (long)V * J * R_pad * C8;
   if (idx >= total) return;
-  const int c0 = (int)(idx % C8) * 8;
-  const long t1 = idx / C8;
-  const int r = (int)(t1 % R_pad);
-  const long aj = t1 / R_pad;
+  // forward: c (ci) fastest across lanes, so W rows are read as float4 runs; trans: r (ci) fastest, so
+  // the 8 scalar reads of W[co][r] per thread are coalesced across lanes
+  int c0, r;
+  long aj;
+  if (!trans) {
+    c0 = (int)(idx % C8) * 8;
+    const long t1 = idx / C8;
+    r = (int)(t1 % R_pad);
+    aj = t1 / R_pad;
+  } else {
+    r = (int)(idx % R_pad);
+    const long t1 = idx / R_pad;
+    c0 = (int)(t1 % C8) * 8;
+    aj = t1 / C8;
+  }
   const int j = (int)(aj % J), a = (int)(aj / J);
   if (j >= deg[a]) return;
   const int R = trans ? Cin : Cout, C = trans ? Cout : Cin;

@@ -94,10 +94,12 @@ __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const T* __restri
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const float4* part, int nb, int ldp, int C,
                                                           const float* gamma, const float* beta, float eps,
                                                           float2* mean_rstd, float* scale, float* shift) {
-  __shared__ double sn[256], sm[256], sq[256];
+  // fp64 power sums (n, sum n*mean, sum M2 + n*mean^2) instead of pairwise Chan merges: adds only (no
+  // division chain), a wave reduction and one LDS step; at fp64 the final var = S2/n - mean^2 loses
+  // ~1e-16 * mean^2/var, far below the fp32 result
+  __shared__ double sred[3][4];
   const int c = blockIdx.x;
-  double n = 0, mean = 0, m2 = 0;
-  // chunks of 8 partials per thread: all 8 loads in flight before the (divide-carrying) merges
+  double n = 0, s1 = 0, s2 = 0;
   for (int b0 = 0; b0 < nb; b0 += 256 * 8) {
     float4 gv[8];
 #pragma unroll
@@ -107,36 +109,33 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float4* part, in
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const double nb_ = gv[u].x;
-      if (nb_ == 0) continue;
-      const double tot = n + nb_;
-      const double d = gv[u].y - mean;
-      mean += d * nb_ / tot;
-      m2 += gv[u].z + d * d * n * nb_ / tot;
-      n = tot;
+      const double cnt = gv[u].x, mu = gv[u].y;
+      n += cnt;
+      s1 += cnt * mu;
+      s2 += (double)gv[u].z + cnt * mu * mu;
     }
   }
-  sn[threadIdx.x] = n;
-  sm[threadIdx.x] = mean;
-  sq[threadIdx.x] = m2;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    n += __shfl_xor(n, o);
+    s1 += __shfl_xor(s1, o);
+    s2 += __shfl_xor(s2, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    sred[0][threadIdx.x >> 6] = n;
+    sred[1][threadIdx.x >> 6] = s1;
+    sred[2][threadIdx.x >> 6] = s2;
+  }
   __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) {
-      const double na = sn[threadIdx.x], nb2 = sn[threadIdx.x + s];
-      const double tot = na + nb2;
-      if (tot > 0) {
-        const double d = sm[threadIdx.x + s] - sm[threadIdx.x];
-        sm[threadIdx.x] += d * nb2 / tot;
-        sq[threadIdx.x] += sq[threadIdx.x + s] + d * d * na * nb2 / tot;
-        sn[threadIdx.x] = tot;
-      }
-    }
-    __syncthreads();
-  }
   if (threadIdx.x == 0) {
-    const double var = sn[0] > 0 ? sq[0] / sn[0] : 0.0;  // biased (BatchNorm)
+    const double tn = ((sred[0][0] + sred[0][1]) + sred[0][2]) + sred[0][3];
+    const double t1 = ((sred[1][0] + sred[1][1]) + sred[1][2]) + sred[1][3];
+    const double t2 = ((sred[2][0] + sred[2][1]) + sred[2][2]) + sred[2][3];
+    const double m = tn > 0 ? t1 / tn : 0.0;
+    double var = tn > 0 ? t2 / tn - m * m : 0.0;  // biased (BatchNorm)
+    if (var < 0) var = 0;
     const float rstd = (float)(1.0 / sqrt(var + (double)eps));
-    const float mu = (float)sm[0];
+    const float mu = (float)m;
     mean_rstd[c] = make_float2(mu, rstd);
     if (scale) {
       const float g = gamma ? gamma[c] : 1.f;
