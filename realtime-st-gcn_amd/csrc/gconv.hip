@@ -591,12 +591,13 @@ __global__ __launch_bounds__(256, 2) void gconv_wgrad_kernel(const stgcn_gconv_w
 // at COB = 64 and (COB/64 + deg) / (2 deg COB/64) at COB = 128.  Waves = (32-co quarter, 32-ci half);
 // each keeps one 32x32 accumulator per neighbour (J2 <= 5) and per k-step reads one dy fragment and
 // deg x fragments (ds_read_b64_tr_b16) for deg MFMAs.  Partials go to the same slab as above.
-constexpr int W2M = 64;   // rows per tile
+constexpr int w2m(int cob) { return cob == 128 ? 64 : 32; }  // rows per tile (LDS: 112 / 48 KB double-buffered)
 constexpr int J2 = 5;     // max neighbours per joint
 template <int COB>
-__global__ __launch_bounds__(COB / 16 * 64, 1) void gconv_wgrad2_kernel(const stgcn_gconv_wgrad_desc a, const WGG g) {
+__global__ __launch_bounds__(COB / 16 * 64, COB == 64 ? 3 : 1) void gconv_wgrad2_kernel(const stgcn_gconv_wgrad_desc a, const WGG g) {
   constexpr int NW = COB / 16, NT = NW * 64;
-  constexpr int PANEL = W2M * WPR;           // 32 channels x 64 rows
+  constexpr int W2M = w2m(COB);
+  constexpr int PANEL = W2M * WPR;           // 32 channels x W2M rows
   constexpr int DYP = COB / 32;              // dy panels
   constexpr int STAGE = (DYP + 2 * J2) * PANEL;
   constexpr int DYU = COB * W2M / 8 / NT;    // dy 16-B units per thread (2)
@@ -860,22 +861,22 @@ __global__ void gconv_dA_reduce_kernel(const float* __restrict__ part, const int
   dA[((long)p * V + nbr[w * J + j]) * V + w] += s;
 }
 
-// joint-grouped plan (gconv_wgrad2_kernel): COB = 128 when Cout % 128 == 0; 0 = not taken
+// joint-grouped plan (gconv_wgrad2_kernel): COB = 128 when Cout % 128 == 0, else 64; 0 = not taken
 int w2_cob(const stgcn_gconv_wgrad_desc& a) {
   static const bool off = getenv("STGCN_GCONV_WGRAD1") != nullptr;  // A/B switch: the per-pair kernel
-  if (off || a.J > J2 || a.Cin % 64 || a.Cout % 128) return 0;
-  // COB = 64 measured slower than the per-pair kernel at Cout = 64 (82 vs 69 us: one 4-wave block per
-  // CU against two); kept instantiable for narrower graphs
-  return 128;
+  if (off || a.J > J2 || a.Cin % 64 || a.Cout % 64) return 0;
+  // Cout = 64: 32-row tiles, 48 KB of LDS, three 4-wave blocks per CU (72 -> 56 us at config-2 C = 64)
+  return a.Cout % 128 ? 64 : 128;
 }
 
 WGG wplan2(const stgcn_gconv_wgrad_desc& a, int cob) {
   WGG g{};
-  g.ntile = (a.NT + W2M - 1) / W2M;
+  g.ntile = (a.NT + w2m(cob) - 1) / w2m(cob);
   g.nco = a.Cout / cob;
   g.nci = a.Cin / 64;
   const long groups = (long)a.V * g.nco * g.nci;
-  long R = (256 + groups - 1) / groups;
+  const long target = cob == 64 ? 512 : 256;  // COB 64: 3 blocks fit a CU
+  long R = (target + groups - 1) / groups;
   if (R > g.ntile) R = g.ntile;
   if (R < 1) R = 1;
   g.tpb = (int)((g.ntile + R - 1) / R);
@@ -944,7 +945,7 @@ int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s
     WGG g = wplan2(a, cob);
     if (!a.work || a.work_bytes < (long)g.R * E * (long)sizeof(float)) return STGCN_EBADSHAPE;
     g.slab = reinterpret_cast<float*>(a.work);
-    const size_t lds = 2 * (size_t)(cob / 32 + 2 * J2) * W2M * WPR;
+    const size_t lds = 2 * (size_t)(cob / 32 + 2 * J2) * w2m(cob) * WPR;
     auto* k = cob == 128 ? gconv_wgrad2_kernel<128> : gconv_wgrad2_kernel<64>;
     static bool attr2[2] = {false, false};
     if (!attr2[cob == 128]) {
