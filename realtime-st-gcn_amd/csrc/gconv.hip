@@ -861,12 +861,15 @@ __global__ void gconv_dA_reduce_kernel(const float* __restrict__ part, const int
   dA[((long)p * V + nbr[w * J + j]) * V + w] += s;
 }
 
-// joint-grouped plan (gconv_wgrad2_kernel): COB = 128 when Cout % 128 == 0, else 64; 0 = not taken
+// joint-grouped plan (gconv_wgrad2_kernel): COB (output channels per block); 0 = not taken
 int w2_cob(const stgcn_gconv_wgrad_desc& a) {
   static const bool off = getenv("STGCN_GCONV_WGRAD1") != nullptr;  // A/B switch: the per-pair kernel
   if (off || a.J > J2 || a.Cin % 64 || a.Cout % 64) return 0;
-  // Cout = 64: 32-row tiles, 48 KB of LDS, three 4-wave blocks per CU (72 -> 56 us at config-2 C = 64)
-  return a.Cout % 128 ? 64 : 128;
+  // COB = 64: 32-row tiles, 48 KB of LDS, three 4-wave blocks per CU.  Measured against COB = 128 (64-row
+  // tiles, one 8-wave block per CU): C=128 78 vs 85 us, C=256 143 vs 153 us, equal at 64 -> 128; and
+  // 56 vs 72 us (per-pair kernel) at C = 64.  COB = 128 stays selectable (STGCN_GCONV_WGRAD2_COB128).
+  static const bool cob128 = getenv("STGCN_GCONV_WGRAD2_COB128") != nullptr;
+  return (cob128 && a.Cout % 128 == 0) ? 128 : 64;
 }
 
 WGG wplan2(const stgcn_gconv_wgrad_desc& a, int cob) {
