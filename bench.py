@@ -46,9 +46,9 @@ def loss_fn(logits, labels, weight):
     return ce + mse
 
 
-# The roofline kernel: conv_wide_kernel<128,9,6,1,0,64>, the Kt=9 stride-1 temporal-conv forward of the
+# The roofline kernel: conv_wide_kernel<128,9,8,1,0,64>, the Kt=9 stride-1 temporal-conv forward of the
 # C=128 (T=150) and C=256 (T=75) layers — the dominant kernel template of the step (with its data-grad
-# twin <128,9,6,0>), 4 launches per step.  Algorithmic work per launch = 2*N*T*V*C*C*Kt.
+# twin <128,9,8,0>), 4 launches per step.  Algorithmic work per launch = 2*N*T*V*C*C*Kt.
 ROOF_TAGS = {"tcn_fwd_c128": 2.0 * N_BATCH * (T_LEN // 2) * V_J * 128 * 128 * 9,
              "tcn_fwd_c256": 2.0 * N_BATCH * (T_LEN // 4) * V_J * 256 * 256 * 9}
 
@@ -254,7 +254,7 @@ def main():
                                    "bwd + Adam", "global_batch": N_BATCH * world, "seq_len": T_LEN, "joints": V_J,
                        "parallelism": f"dp{world}" if world > 1 else "single",
                        "launch": "eager" if not args.graph else "hip-graph replay (fwd+bwd | allreduce | Adam)"},
-            "roofline": {"kernel": "conv_wide_kernel<128,9,6,1,0,64> (persistent warp-specialised Kt=9 stride-1 "
+            "roofline": {"kernel": "conv_wide_kernel<128,9,8,1,0,64> (persistent warp-specialised Kt=9 stride-1 "
                                    "temporal conv fwd of the C=128 and C=256 layers, 4 launches/step)",
                          "bound": "mfma", "achieved": round(achieved, 2) if achieved else None,
                          "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
