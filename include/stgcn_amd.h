@@ -177,6 +177,7 @@ typedef struct {
   int NT, V, J, Cin, Cout, x_ld, dy_ld;
   void* work;
   long work_bytes;
+  float* rowsum; /* optional [V][Cout]: rowsum[w][co] = sum_i dy[(i,w)][co] (bias through A), or NULL */
 } stgcn_gconv_wgrad_desc;
 
 int stgcn_gconv_wgrad(const stgcn_gconv_wgrad_desc* d, int dtype, void* stream);

@@ -470,7 +470,8 @@ DEV bf16x8 trfrag(const char* panel, int row0, int lane) {
 
 struct WGG {
   int ntile, tpb, R, nco, nci;
-  float* slab;  // [R][V*J][Cout][Cin]
+  float* slab;     // [R][V*J][Cout][Cin]
+  float* rowpart;  // joint-grouped kernel: [R][V][Cout] partial row sums of dy per joint, or NULL
 };
 
 __global__ __launch_bounds__(256, 2) void gconv_wgrad_kernel(const stgcn_gconv_wgrad_desc a, const WGG g) {
@@ -663,10 +664,29 @@ __global__ __launch_bounds__(COB / 16 * 64, COB == 64 ? 3 : 1) void gconv_wgrad2
   for (int j = 0; j < J2; ++j)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  // per-joint row sums of dy (the bias-through-A gradient) ride along in the first ci-group's blocks
+  const bool rsum = g.rowpart != nullptr && grp / g.nco == 0;
+  float sacc[DYU][8];
+#pragma unroll
+  for (int u = 0; u < DYU; ++u)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sacc[u][e] = 0.f;
+  auto add_rows = [&]() {
+    if (rsum) {
+#pragma unroll
+      for (int u = 0; u < DYU; ++u) {
+        float f[8];
+        unpack16(ry[u], f, (bf16*)nullptr);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sacc[u][e] += f[e];
+      }
+    }
+  };
 
   int cur = 0;
   if (t0 < t1) {
     load(t0);
+    add_rows();
     store(0);
   }
   __syncthreads();
@@ -684,9 +704,27 @@ __global__ __launch_bounds__(COB / 16 * 64, COB == 64 ? 3 : 1) void gconv_wgrad2
           acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, acc[j], 0, 0, 0);
         }
     }
-    if (more) store(cur ^ 1);
+    if (more) {
+      add_rows();
+      store(cur ^ 1);
+    }
     __syncthreads();
     cur ^= 1;
+  }
+  if (rsum) {  // [row slot][COB] in LDS (the stages are free after the last barrier), fixed-order sum
+    float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int u = 0; u < DYU; ++u) {
+      const int e = tid + NT * u, row = e / (COB / 8), cu = e % (COB / 8);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[row * COB + cu * 8 + k] = sacc[u][k];
+    }
+    __syncthreads();
+    if (tid < COB && co0 + tid < a.Cout) {
+      float t = 0.f;
+      for (int r = 0; r < W2M; ++r) t += red[r * COB + tid];
+      g.rowpart[((long)rr * V + w) * a.Cout + co0 + tid] = t;
+    }
   }
 
   // block partial of each pair (w, j) -> slab[rr][w*J + j][co][ci]
@@ -723,6 +761,15 @@ __global__ void gconv_wgrad_f32_kernel(const stgcn_gconv_wgrad_desc a) {
   for (int i = 0; i < a.NT; ++i)
     s += dy[((long)i * a.V + w) * a.dy_ld + co] * x[((long)i * a.V + src) * a.x_ld + ci];
   a.dweff[idx] = s;
+}
+
+// out[e] = sum_r part[r][e] in fixed order (per-joint row-sum partials of the joint-grouped kernel)
+__global__ void rowpart_sum_kernel(const float* __restrict__ part, int R, long E, float* __restrict__ out) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  float s = 0.f;
+  for (int r = 0; r < R; ++r) s += part[(long)r * E + e];
+  out[e] = s;
 }
 
 // slab reduction (rows of the slab are whole [V*J][Cout][Cin] images): dweff[e] = sum_r slab[r][e]
@@ -936,6 +983,8 @@ long gconv_wgrad_workspace(const stgcn_gconv_wgrad_desc& a, int dtype) {
   if (dtype != 1) return 0;
   const int cob = w2_cob(a);
   const WGG g = cob ? wplan2(a, cob) : wplan(a);
+  if (cob && a.rowsum)
+    return ((long)g.R * a.V * a.J * a.Cout * a.Cin + (long)g.R * a.V * a.Cout) * (long)sizeof(float);
   return (long)g.R * a.V * a.J * a.Cout * a.Cin * (long)sizeof(float);
 }
 
@@ -949,8 +998,10 @@ int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s
   const int cob = w2_cob(a);
   if (cob) {
     WGG g = wplan2(a, cob);
-    if (!a.work || a.work_bytes < (long)g.R * E * (long)sizeof(float)) return STGCN_EBADSHAPE;
+    const long need = (long)g.R * E + (a.rowsum ? (long)g.R * a.V * a.Cout : 0);
+    if (!a.work || a.work_bytes < need * (long)sizeof(float)) return STGCN_EBADSHAPE;
     g.slab = reinterpret_cast<float*>(a.work);
+    g.rowpart = a.rowsum ? g.slab + (long)g.R * E : nullptr;
     const size_t lds = 2 * (size_t)(cob / 32 + 2 * J2) * w2m(cob) * WPR;
     auto* k = cob == 128 ? gconv_wgrad2_kernel<128> : gconv_wgrad2_kernel<64>;
     static bool attr2[2] = {false, false};
@@ -962,8 +1013,14 @@ int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s
     hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(cob / 16 * 64), lds, s, a, g);
     hipLaunchKernelGGL(gslab_reduce_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, (const float*)g.slab,
                        g.R, E, (long)a.Cout * a.Cin, a.deg, a.J, a.dweff);
+    if (a.rowsum) {
+      const long ER = (long)a.V * a.Cout;
+      hipLaunchKernelGGL(rowpart_sum_kernel, dim3((unsigned)((ER + 255) / 256)), dim3(256), 0, s,
+                         (const float*)g.rowpart, g.R, ER, a.rowsum);
+    }
     return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
   }
+  if (a.rowsum) return STGCN_EBADSHAPE;  // row sums ride only on the joint-grouped kernel
   WGG g = wplan(a);
   if (!a.work || a.work_bytes < (long)g.R * E * (long)sizeof(float)) return STGCN_EBADSHAPE;
   g.slab = reinterpret_cast<float*>(a.work);

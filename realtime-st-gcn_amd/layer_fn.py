@@ -317,7 +317,8 @@ class StgcnLayerFunction(torch.autograd.Function):
             else:
                 wgT = K.gconv_weights(A32, wg2, sup, Cout, Cin, True, dtype)
                 K.gconv(dg, wgT, sup, Cout, Cin, trans=True, out=dx, accumulate=dx_written)
-            dweff = K.gconv_wgrad(x, dg, sup, Cin, Cout)
+            fuse_s = A32.dim() == 3 and K.gconv_wgrad_rowsum_ok(sup, Cin, Cout, dtype)
+            dweff = K.gconv_wgrad(x, dg, sup, Cin, Cout, rowsum=z_S if fuse_s else None)
             dwg2, dA = K.gconv_finish(dweff, A32, wg2, sup, Cout, Cin, dW=z_dwg, dA=z_dA)
             grads["wg"] = dwg2.view(P * Cout, Cin, 1, 1)
             if ctx.cfg[6] and ctx.needs_input_grad[1]:
@@ -342,7 +343,8 @@ class StgcnLayerFunction(torch.autograd.Function):
             colsum = A32.sum(dim=2)                                         # [N][P][W]
             grads["bg"] = torch.einsum("npw,nwc->pc", colsum, Sn).reshape(-1)
         else:
-            S = K.rowgroup_sum(dg, M1, Cout, V, out=z_S)                      # [V(w)][Cout]
+            # [V(w)][Cout]; the joint-grouped weight-gradient kernel already produced it when it ran
+            S = z_S if (ctx.sup is not None and fuse_s) else K.rowgroup_sum(dg, M1, Cout, V, out=z_S)
             if not dA.is_contiguous():
                 dA = dA.contiguous()
             grads["bg"] = K.gcn_bias_bwd(A32, bg.detach().float().contiguous(), S, dA, Cout)

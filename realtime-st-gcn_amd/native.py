@@ -385,11 +385,19 @@ def gconv(x, wpk, sup, Cin, Cout, trans=False, bias=None, stats=None, out=None, 
     return out
 
 
-def gconv_wgrad(x, dy, sup, Cin, Cout):
-    """dWeff [V][J][Cout][Cin] fp32 = sum_i dy[(i,w)] x[(i, S(w)_j)]^T."""
+def gconv_wgrad_rowsum_ok(sup, Cin, Cout, dtype) -> bool:
+    """Whether gconv_wgrad can also return the per-joint row sums of dy (joint-grouped kernel only)."""
+    return (dtype == torch.bfloat16 and Cin % 64 == 0 and Cout % 64 == 0 and sup.J <= 5
+            and "STGCN_GCONV_WGRAD1" not in os.environ)
+
+
+def gconv_wgrad(x, dy, sup, Cin, Cout, rowsum=None):
+    """dWeff [V][J][Cout][Cin] fp32 = sum_i dy[(i,w)] x[(i, S(w)_j)]^T; with ``rowsum`` ([V][Cout] fp32,
+    overwritten) also the per-joint row sums of dy (gconv_wgrad_rowsum_ok shapes)."""
     N, _, T, V = x.shape
     dweff = torch.empty((V, sup.J, Cout, Cin), dtype=torch.float32, device=x.device)
     d = L.GconvWgradDesc()
+    d.rowsum = L.ptr(rowsum)
     d.x, d.dy, d.nbr, d.deg, d.dweff = x.data_ptr(), dy.data_ptr(), sup.nbr.data_ptr(), sup.deg.data_ptr(), \
         dweff.data_ptr()
     d.NT, d.V, d.J, d.Cin, d.Cout, d.x_ld, d.dy_ld = N * T, V, sup.J, Cin, Cout, rows_ld(x), rows_ld(dy)
