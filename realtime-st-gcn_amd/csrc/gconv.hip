@@ -24,6 +24,7 @@
 // XOR swizzle on the source, fragment double-buffering, BN partial statistics in the epilogue.
 #include "common.h"
 #include <stdlib.h>
+#include <utility>
 #include "../../include/stgcn_amd.h"
 
 namespace {
@@ -741,6 +742,167 @@ __global__ __launch_bounds__(COB / 16 * 64, COB == 64 ? 3 : 1) void gconv_wgrad2
   }
 }
 
+// DMA-ring variant of gconv_wgrad2_kernel<64> (the default): the same block = (joint w, 64 co, 64 ci,
+// row range) and wave split, but the 32-row tiles go global -> LDS with global_load_lds (no register
+// staging) into a ring of W3D(DEG) slots sized by the joint's degree, so D - 1 tiles are in flight
+// while one is consumed instead of one.  The register-staged kernel kept at most one tile (~16 KB)
+// per block in flight and sat at ~13 % of the MFMA peak, latency-bound on L2/MALL.  Body per degree
+// (DEG = deg[w], a block-uniform value) so the vmcnt counts are immediates.
+constexpr int W3_LDS = 80 * 1024;  // two blocks per CU
+constexpr int w3_stage(int deg) { return (2 + 2 * deg) * 32 * WPR; }
+constexpr int w3d(int deg) { return W3_LDS / w3_stage(deg) > 8 ? 8 : W3_LDS / w3_stage(deg); }
+
+template <int N, typename F>
+DEV void sfor(F&& f) {
+  [&]<int... I>(std::integer_sequence<int, I...>) { (f.template operator()<I>(), ...); }(
+      std::make_integer_sequence<int, N>{});
+}
+
+DEV unsigned lds_u32(const void* p) { return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p; }
+
+DEV void glds16m(const void* src, unsigned lds_off) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src),
+               "s"(__builtin_amdgcn_readfirstlane(lds_off)) : "memory", "m0");
+}
+
+template <int DEG>
+DEV void wgrad3_body(const stgcn_gconv_wgrad_desc& a, const WGG& g, char* smem, int w, int rr, int grp) {
+  constexpr int D = w3d(DEG), PANEL = 32 * WPR, STAGE = w3_stage(DEG), NU = 1 + DEG;
+  static_assert(D >= 3 && (D - 2) * NU <= 63, "ring");
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cq = wave & 1, ch = wave >> 1;  // co half (32), ci half (32)
+  const int V = a.V;
+  const int co0 = (grp % g.nco) * 64, ci0 = (grp / g.nco) * 64;
+  const int t0 = rr * g.tpb, t1 = min(g.ntile, t0 + g.tpb);
+  const bf16* __restrict__ dy = reinterpret_cast<const bf16*>(a.dy);
+  const bf16* __restrict__ x = reinterpret_cast<const bf16*>(a.x);
+  // this wave's DMA share of a tile: dy panel (wave >> 1) rows 16 (wave & 1) .. +15, and the same
+  // (panel, half) of every neighbour's x; lane -> (row lane / 4, 16-B unit lane % 4)
+  const int prow = 16 * (wave & 1) + (lane >> 2), pu = lane & 3, pp = wave >> 1;
+  const bf16* ysrc = dy + (long)w * a.dy_ld + co0 + pp * 32 + pu * 8;
+  const bf16* xsrc[DEG];
+#pragma unroll
+  for (int j = 0; j < DEG; ++j) xsrc[j] = x + (long)a.nbr[w * a.J + j] * a.x_ld + ci0 + pp * 32 + pu * 8;
+  const long ystep = (long)V * a.dy_ld, xstep = (long)V * a.x_ld;
+  const unsigned ring = lds_u32(smem);
+  const unsigned woff = (unsigned)(pp * PANEL + (wave & 1) * 1024);
+  auto issue = [&](int t) {
+    const int i = min(t * 32 + prow, a.NT - 1);  // rows past NT: clamped here, zeroed in LDS below
+    const unsigned slot = ring + (unsigned)(((t - t0) % D) * STAGE) + woff;
+    glds16m(ysrc + i * ystep, slot);
+#pragma unroll
+    for (int j = 0; j < DEG; ++j) glds16m(xsrc[j] + i * xstep, slot + (unsigned)((2 + 2 * j) * PANEL));
+  };
+#pragma unroll
+  for (int k = 0; k < D - 1; ++k)
+    if (t0 + k < t1) issue(t0 + k);
+
+  f32x16 acc[DEG];
+#pragma unroll
+  for (int j = 0; j < DEG; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  const bool rsum = g.rowpart != nullptr && grp / g.nco == 0;
+  float sacc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sacc[e] = 0.f;
+  // row-sum unit of this thread: row tid / 8, 8 channels at (tid % 8) * 8
+  const int srow = tid >> 3, scu = tid & 7;
+  const int soff = (scu >> 2) * PANEL + srow * WPR + (scu & 3) * 16;
+
+  for (int t = t0; t < t1; ++t) {
+    const int after = min(D - 2, t1 - 1 - t);  // tiles issued after t
+    sfor<D - 1>([&]<int m>() {
+      if (after == m) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(m * NU) : "memory");
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (t + D - 1 < t1) issue(t + D - 1);  // into the slot of tile t - 1, free after the barrier
+    char* base = smem + ((t - t0) % D) * STAGE;
+    if (t * 32 + 32 > a.NT) {  // last, partial tile: zero dy rows >= NT (block-uniform branch)
+      if (t * 32 + srow >= a.NT) *reinterpret_cast<uint4*>(base + soff) = make_uint4(0, 0, 0, 0);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    if (rsum) {
+      float f[8];
+      unpack16(*reinterpret_cast<const uint4*>(base + soff), f, (bf16*)nullptr);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sacc[e] += f[e];
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 fa = trfrag(base + cq * PANEL, ks * 16, lane);
+#pragma unroll
+      for (int j = 0; j < DEG; ++j) {
+        const bf16x8 fb = trfrag(base + (2 + 2 * j + ch) * PANEL, ks * 16, lane);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, acc[j], 0, 0, 0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if (rsum) {  // [row][64] in LDS, fixed-order column sums
+    float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[srow * 64 + scu * 8 + k] = sacc[k];
+    __syncthreads();
+    if (tid < 64) {
+      float s = 0.f;
+      for (int r = 0; r < 32; ++r) s += red[r * 64 + tid];
+      g.rowpart[((long)rr * V + w) * a.Cout + co0 + tid] = s;
+    }
+  }
+  const int cc = ci0 + ch * 32 + (lane & 31);
+#pragma unroll
+  for (int j = 0; j < DEG; ++j) {
+    float* slab = g.slab + ((long)rr * V * a.J + w * a.J + j) * a.Cout * a.Cin;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) slab[(long)(co0 + cq * 32 + acc_row(r, lane)) * a.Cin + cc] = acc[j][r];
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void gconv_wgrad3_kernel(const stgcn_gconv_wgrad_desc a, const WGG g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int ngrp = g.nco * g.nci;
+  const int w = blockIdx.x / (ngrp * g.R);
+  const int rem = blockIdx.x % (ngrp * g.R);
+  const int rr = rem / ngrp, grp = rem % ngrp;
+  // joints in decreasing-degree order (ties by index): the heaviest blocks are dispatched first and the
+  // light ones fill the tail.  Scratch in the ring's first bytes, before any DMA is issued.
+  int* sdeg = reinterpret_cast<int*>(smem);
+  int* order = sdeg + 64;
+  int wj = w;
+  if (a.V <= 64) {
+    const int tid = threadIdx.x;
+    if (tid < a.V) sdeg[tid] = a.deg[tid];
+    __syncthreads();
+    if (tid < a.V) {
+      const int d = sdeg[tid];
+      int r = 0;
+      for (int u = 0; u < a.V; ++u) r += (sdeg[u] > d) | ((sdeg[u] == d) & (u < tid));
+      order[r] = tid;
+    }
+    __syncthreads();
+    wj = order[w];
+    __syncthreads();
+  }
+  switch (a.deg[wj]) {
+    case 1: wgrad3_body<1>(a, g, smem, wj, rr, grp); break;
+    case 2: wgrad3_body<2>(a, g, smem, wj, rr, grp); break;
+    case 3: wgrad3_body<3>(a, g, smem, wj, rr, grp); break;
+    case 4: wgrad3_body<4>(a, g, smem, wj, rr, grp); break;
+    case 5: wgrad3_body<5>(a, g, smem, wj, rr, grp); break;
+    default:  // deg 0: no pairs (the reduction skips j >= deg); the row sums still come from here
+      if (g.rowpart != nullptr && grp / g.nco == 0 && threadIdx.x < 64) {
+        const int co = (grp % g.nco) * 64 + threadIdx.x;
+        const int i1 = min(a.NT, min(g.ntile, (rr + 1) * g.tpb) * 32);
+        const bf16* dy = reinterpret_cast<const bf16*>(a.dy);
+        float s = 0.f;
+        for (int i = rr * g.tpb * 32; i < i1; ++i) s += (float)dy[((long)i * a.V + wj) * a.dy_ld + co];
+        g.rowpart[((long)rr * a.V + wj) * a.Cout + co] = s;
+      }
+      break;
+  }
+}
+
 // fp32 parity path of the gather wgrad: one thread per (pair, co, ci), loop over rows (small sizes)
 __global__ void gconv_wgrad_f32_kernel(const stgcn_gconv_wgrad_desc a) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -919,14 +1081,25 @@ int w2_cob(const stgcn_gconv_wgrad_desc& a) {
   return (cob128 && a.Cout % 128 == 0) ? 128 : 64;
 }
 
+// the DMA-ring kernel (gconv_wgrad3) for COB = 64, except 64 -> 128 channels, where the register-staged
+// kernel measured 74 vs 82 us; STGCN_GCONV_WGRAD2_REG forces the register-staged one everywhere
+bool w3_ok(const stgcn_gconv_wgrad_desc& a) {
+  static const bool reg = getenv("STGCN_GCONV_WGRAD2_REG") != nullptr;
+  return !reg && !(a.Cin == 64 && a.Cout == 128);
+}
+
 WGG wplan2(const stgcn_gconv_wgrad_desc& a, int cob) {
   WGG g{};
   g.ntile = (a.NT + w2m(cob) - 1) / w2m(cob);
   g.nco = a.Cout / cob;
   g.nci = a.Cin / 64;
   const long groups = (long)a.V * g.nco * g.nci;
-  const long target = cob == 64 ? 512 : 256;  // COB 64: 3 blocks fit a CU
-  long R = (target + groups - 1) / groups;
+  const long target = cob == 64 ? 512 : 256;  // COB 64: 3 register-staged / 2 DMA-ring blocks fit a CU
+  // DMA ring: block target by the group count, measured per layer (targets 512 / 1024 / 2048): C = 64
+  // (25 groups) 49 / 40 / 56 us, C = 128 64 / 81 / 75 us, C = 256 108 / 113 / 130 us
+  static const long t3env = getenv("STGCN_W3_TARGET") ? atol(getenv("STGCN_W3_TARGET")) : 0;
+  const long t3 = t3env > 0 ? t3env : groups <= 32 ? 1024 : 512;
+  long R = (cob == 64 && w3_ok(a)) ? (t3 + groups - 1) / groups : (target + groups - 1) / groups;
   if (R > g.ntile) R = g.ntile;
   if (R < 1) R = 1;
   g.tpb = (int)((g.ntile + R - 1) / R);
@@ -1002,15 +1175,17 @@ int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s
     if (!a.work || a.work_bytes < need * (long)sizeof(float)) return STGCN_EBADSHAPE;
     g.slab = reinterpret_cast<float*>(a.work);
     g.rowpart = a.rowsum ? g.slab + (long)g.R * E : nullptr;
-    const size_t lds = 2 * (size_t)(cob / 32 + 2 * J2) * w2m(cob) * WPR;
-    auto* k = cob == 128 ? gconv_wgrad2_kernel<128> : gconv_wgrad2_kernel<64>;
-    static bool attr2[2] = {false, false};
-    if (!attr2[cob == 128]) {
+    const bool ring = cob == 64 && w3_ok(a);
+    const size_t lds = ring ? (size_t)W3_LDS : 2 * (size_t)(cob / 32 + 2 * J2) * w2m(cob) * WPR;
+    auto* k = ring ? gconv_wgrad3_kernel : cob == 128 ? gconv_wgrad2_kernel<128> : gconv_wgrad2_kernel<64>;
+    static bool attr2[3] = {false, false, false};
+    const int ka = ring ? 2 : cob == 128;
+    if (!attr2[ka]) {
       (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr2[cob == 128] = true;
+      attr2[ka] = true;
     }
     const long blocks = (long)a.V * g.nco * g.nci * g.R;
-    hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(cob / 16 * 64), lds, s, a, g);
+    hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(ring ? 256 : cob / 16 * 64), lds, s, a, g);
     hipLaunchKernelGGL(gslab_reduce_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, (const float*)g.slab,
                        g.R, E, (long)a.Cout * a.Cin, a.deg, a.J, a.dweff);
     if (a.rowsum) {

@@ -58,7 +58,11 @@ def test_gconv_fwd_bwd(K, pkg, dtype, tol, Cin, Cout, N, T):
     wT = K.gconv_weights(Ad, Wd, sup, Cout, Cin, True, dtype)
     dx = K.gconv(cl(dy, dtype), wT, sup, Cout, Cin, trans=True)
     assert_close(dx.float(), x.grad, tol, "gconv dgrad")
-    dweff = K.gconv_wgrad(cl(x.detach(), dtype), cl(dy, dtype), sup, Cin, Cout)
+    rs_ok = K.gconv_wgrad_rowsum_ok(sup, Cin, Cout, dtype)
+    rowsum = torch.empty((V, Cout), device=DEV) if rs_ok else None
+    dweff = K.gconv_wgrad(cl(x.detach(), dtype), cl(dy, dtype), sup, Cin, Cout, rowsum=rowsum)
+    if rs_ok:  # per-joint row sums of dy (the bias-through-A gradient), fused into the same kernel
+        assert_close(rowsum.cpu(), dy.to(dtype).float().sum(dim=(0, 2)).t(), 1e-4, "gconv rowsum")
     dW, dA = K.gconv_finish(dweff, Ad, Wd, sup, Cout, Cin)
     assert_close(dW, W.grad, tol, "gconv dW")
     # dA is produced on the graph's support (what A * edge_importance needs); off it, it is zero
