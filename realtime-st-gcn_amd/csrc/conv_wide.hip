@@ -656,6 +656,11 @@ int conv_wide_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
       return a.pro ? conv_wide_kernel<64, 9, 12, 1, 0, 32> : conv_wide_kernel<64, 9, 12, 0, 0, 32>;
     // B ring depth 8 (7 k-steps of L2 latency cover): measured 2-3 % faster than 4, 6 or 9 at C = 128/256
     if (ktap == 9) return a.pro ? conv_wide_kernel<128, 9, 8, 1> : conv_wide_kernel<128, 9, 8, 0>;
+    // stride-2 folded 5-tap form: ring depth must divide 40 k-steps per item pair.  Depth 8 measured equal
+    // to 5 in the full step (9.40 vs 9.39 ms, 3 interleaved runs); 10 spills (35 VGPRs).  A/B knob only.
+    static const int s2ring = getenv("STGCN_WIDE_S2_RING") ? atoi(getenv("STGCN_WIDE_S2_RING")) : 5;
+    if (s2ring == 8) return a.pro ? conv_wide_kernel<128, 5, 8, 1> : conv_wide_kernel<128, 5, 8, 0>;
+    if (s2ring == 10) return a.pro ? conv_wide_kernel<128, 5, 10, 1> : conv_wide_kernel<128, 5, 10, 0>;
     return a.pro ? conv_wide_kernel<128, 5, 5, 1> : conv_wide_kernel<128, 5, 5, 0>;
   };
   auto* k = kern();
