@@ -36,10 +36,13 @@ class AgcnLayer(nn.Module):
         self.compute_dtype = torch.float32
 
     def forward(self, x, A):
-        dt = self.compute_dtype
-        theta = LF.Conv1x1Function.apply(x, self.theta.weight, self.theta.bias, dt)
-        phi = LF.Conv1x1Function.apply(x, self.phi.weight, self.phi.bias, dt)
-        C = LF.AttentionFunction.apply(theta, phi, self.partitions, dt)          # (N, P, V, V)
+        # The attention logits theta^T phi contract over C'*T (4800 terms at config 5) and feed a softmax:
+        # with bf16-stored theta/phi their rounding moves the logits by O(0.1) and the softmax weights by
+        # O(10 %), so this branch runs in fp32 on every compute dtype (it is ~3 % of the layer's work).
+        att = torch.float32
+        theta = LF.Conv1x1Function.apply(x, self.theta.weight, self.theta.bias, att)
+        phi = LF.Conv1x1Function.apply(x, self.phi.weight, self.phi.bias, att)
+        C = LF.AttentionFunction.apply(theta, phi, self.partitions, att)         # (N, P, V, V)
         return self.st_gcn(x, A + self.B + C)                                    # aagcn.py:148
 
 

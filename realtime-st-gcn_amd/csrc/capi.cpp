@@ -328,10 +328,3 @@ int stgcn_attn_bwd(const void* th, const void* ph, int ld, int N, int T, int V, 
 
 }  // extern "C"
 
-// diagnostic (not part of include/stgcn_amd.h): phase timers of the persistent conv kernel
-int persist_debug_read(long long* host, long n);
-extern "C" int stgcn_debug_persist_timers(long long* host, long n) { return persist_debug_read(host, n); }
-int tile_debug_read(long long* host, long n);
-extern "C" int stgcn_debug_tile_timers(long long* host, long n) { return tile_debug_read(host, n); }
-int wide_debug_read(long long* host, long n);
-extern "C" int stgcn_debug_wide_timers(long long* host, long n) { return wide_debug_read(host, n); }

@@ -102,3 +102,8 @@ DEV float wave_sum(float v) {
 #define STGCN_EBADSHAPE 1
 #define STGCN_EDTYPE 2
 #define STGCN_EHIP 3
+
+// Per-device launcher state (runtime.cpp): the CU count of the stream's device, and a one-time (per kernel
+// and device) raise of a kernel's dynamic LDS limit.  Thread-safe; no other mutable state in the launchers.
+int stgcn_cu_count(hipStream_t s);
+int stgcn_lds_attr(const void* kernel, int bytes, hipStream_t s);

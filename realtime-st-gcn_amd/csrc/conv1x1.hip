@@ -260,12 +260,7 @@ int launch1(const stgcn_conv_desc& a, const XGeom& g, hipStream_t s) {
   size_t lds = (size_t)BM * RS;
   const size_t lout = (size_t)BM * OS + 2 * BN * 16;
   if (lout > lds) lds = lout;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv1x1_kernel<KS, BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    attr = true;
-  }
+  if (stgcn_lds_attr((const void*)conv1x1_kernel<KS, BN>, 160 * 1024, s)) return STGCN_EHIP;
   hipLaunchKernelGGL((conv1x1_kernel<KS, BN>), dim3((unsigned)((long)g.nrow * g.ncol)), dim3(NT), lds, s, a, g);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }

@@ -46,8 +46,6 @@ DEV void glds16(const void* src, char* lds_base) {
 }
 
 struct PGeom {
-  long long* dbg;  // diagnostic build only: per-block phase timers (s_memtime), else nullptr
-  int dmode;       // diagnostic: bit0 skip output stores, bit1 skip stats, bit2 skip scratch writes
   int F;        // frames per tile
   int RSL;      // ring slots (frames)
   int tiles_n;  // tiles per sample
@@ -251,7 +249,7 @@ __global__ __launch_bounds__(NT, 1) void conv_persist_kernel(const stgcn_conv_de
         const int ro = (r & 3) + 8 * (r >> 2);
         const float v = acc[i][r] + bias_c;
         acc[i][r] = v;
-        if (!(g.dmode & 4)) *reinterpret_cast<bf16*>(scratch + (i * 32 + 4 * lh + ro) * 64 + lr * 2) = (bf16)v;
+        *reinterpret_cast<bf16*>(scratch + (i * 32 + 4 * lh + ro) * 64 + lr * 2) = (bf16)v;
         if (full || (cok && lb + ro < rows_valid)) {
           s += v;
           cnt += 1.f;
@@ -261,7 +259,6 @@ __global__ __launch_bounds__(NT, 1) void conv_persist_kernel(const stgcn_conv_de
     // rows of this wave: wr*64 + lrow, 16 B units u = 0..3 of its 32 columns
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      if (g.dmode & 1) break;
       const int lrow = q * 16 + (lane >> 2), u = lane & 3;
       uint4 v = *reinterpret_cast<const uint4*>(scratch + lrow * 64 + u * 16);
       const int trow = wr * 64 + lrow;
@@ -278,7 +275,7 @@ __global__ __launch_bounds__(NT, 1) void conv_persist_kernel(const stgcn_conv_de
         if (wc * 32 + u * 8 < a.Cout) *reinterpret_cast<uint4*>(p) = v;
       }
     }
-    if (a.stats && cnt > 0.f && !(g.dmode & 2)) {
+    if (a.stats && cnt > 0.f) {
       const float mean = s / cnt;
       float m2 = 0.f;
 #pragma unroll
@@ -314,43 +311,21 @@ __global__ __launch_bounds__(NT, 1) void conv_persist_kernel(const stgcn_conv_de
 
   // ---- phases: group (p & 1) computes tile p; the other group finishes tile p-1, commits tile
   // p+1's frames (its own next tile) and prefetches tile p+3 (its tile after that)
-  long long tc = 0, te = 0, tcm = 0, tp = 0, t0 = g.dbg ? (long long)__builtin_amdgcn_s_memtime() : 0;
-  auto stamp = [&](long long& acc_t) {
-    if (g.dbg) {
-      const long long t1 = (long long)__builtin_amdgcn_s_memtime();
-      acc_t += t1 - t0;
-      t0 = t1;
-    }
-  };
-  long long tb = 0;
   for (int p = 0; p <= K; ++p) {
     if (grp == (p & 1)) {
       if (p < K) compute(p);
-      stamp(tc);
     } else {
       if (p >= 1) epilogue(p - 1);
-      stamp(te);
       if (p + 1 < K && !fresh(p + 1)) commit(p + 1);
-      stamp(tcm);
       if (p + 3 < K && !fresh(p + 3)) prefetch(p + 3);
-      stamp(tp);
     }
     bar();
-    stamp(tb);
     if (p + 1 < K && fresh(p + 1)) {  // a new sample: its halo overwrites slots of tile p
       stage_fresh(p + 1);
       bar();
     }
   }
 
-  if (g.dbg && lane == 0 && (wave == 0 || wave == 4)) {
-    long long* d = g.dbg + (long)blockIdx.x * 8 + (wave ? 4 : 0);
-    d[0] = tc;
-    d[1] = te;
-    d[2] = tcm;
-    d[3] = tp;
-    (void)tb;
-  }
   if (a.stats) {
     // merge lane halves (same column), then the 2 row groups x 2 wave groups per column via LDS
     Welford o;
@@ -376,14 +351,6 @@ __global__ __launch_bounds__(NT, 1) void conv_persist_kernel(const stgcn_conv_de
 }  // namespace
 
 long conv_rows_num_row_blocks(long M, int cout);
-long long* persist_dbg_ptr = nullptr;
-
-// copy the diagnostic timers (8 per block) of the last persistent launch to the host
-int persist_debug_read(long long* host, long n) {
-  if (!persist_dbg_ptr) return 1;
-  (void)hipDeviceSynchronize();
-  return hipMemcpy(host, persist_dbg_ptr, n * sizeof(long long), hipMemcpyDeviceToHost) == hipSuccess ? 0 : 3;
-}
 
 // -1: shape not handled (caller tries the next kernel)
 int conv_persist_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
@@ -391,16 +358,6 @@ int conv_persist_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
   if (a.Cin_pad != C || a.Cout_pad != C || a.Cin != C || a.in_ld % 8 || a.pro > 1) return -1;
   if (a.bias_mode > 1 || a.V > 32 || a.out_ld % 8 || a.Cout % 8) return -1;
   PGeom g;
-  g.dbg = nullptr;
-  static const int dmode = getenv("STGCN_PERSIST_MODE") ? atoi(getenv("STGCN_PERSIST_MODE")) : 0;
-  g.dmode = dmode;
-  static long long* dbg = nullptr;
-  static const bool want_dbg = getenv("STGCN_PERSIST_DBG") != nullptr;
-  if (want_dbg) {
-    if (!dbg) (void)hipMalloc(&dbg, 8 * 4096 * sizeof(long long));
-    g.dbg = dbg;
-    persist_dbg_ptr = dbg;
-  }
   g.F = ROWS / a.V;
   if (g.F < 1) return -1;
   g.RSL = 2 * g.F + KT - 1;
@@ -410,22 +367,11 @@ int conv_persist_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
   const long nt = (long)a.N * g.tiles_n;
   if (nt > 0x7fffffffL) return -1;
   g.ntiles = (int)nt;
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (ncu <= 0) ncu = 256;
-  }
+  const int ncu = stgcn_cu_count(s);
   g.tpb = (g.ntiles + ncu - 1) / ncu;
   const int grid = (g.ntiles + g.tpb - 1) / g.tpb;
   if (a.stats && grid > conv_rows_num_row_blocks((long)a.N * a.T_out * a.V, a.Cout)) return -1;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_persist_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LDS_MAX);
-    attr = true;
-  }
+  if (stgcn_lds_attr((const void*)conv_persist_kernel, LDS_MAX, s)) return STGCN_EHIP;
   hipLaunchKernelGGL(conv_persist_kernel, dim3(grid), dim3(NT), lds, s, a, g);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }

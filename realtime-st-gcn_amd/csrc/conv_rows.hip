@@ -305,12 +305,7 @@ int launch_conv(const ConvArgs& a, hipStream_t s) {
   const size_t lds = 2 * (BM + BN) * KC * sizeof(T);
   const size_t red = (a.stats ? (size_t)WM * BN * 16 : 0);
   const size_t bytes = lds > red ? lds : red;
-  static bool attr_set = false;  // benign race: idempotent attribute
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)conv_rows_kernel<T, WM, WN, TM, TN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        160 * 1024);
-    attr_set = true;
-  }
+  if (stgcn_lds_attr((const void*)conv_rows_kernel<T, WM, WN, TM, TN>, 160 * 1024, s)) return STGCN_EHIP;
   hipLaunchKernelGGL((conv_rows_kernel<T, WM, WN, TM, TN>), grid, dim3(256), bytes, s, a);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
@@ -358,17 +353,12 @@ int conv_rows_bn_tile(int cout) { return cout <= 64 ? 64 : 128; }
 // upper bound over both kernels (smallest row tile = 128); unused partial slots must be zeroed
 long conv_rows_num_row_blocks(long M, int cout) { (void)cout; return (M + 127) / 128; }
 
-int conv_halo_launch(const ConvArgs& a, int dtype, hipStream_t s);
 int conv_tile_launch(const ConvArgs& a, int dtype, hipStream_t s);
 
 int conv_rows_launch(const ConvArgs& a, int dtype, hipStream_t s) {
   static const bool v1_only = getenv("STGCN_CONV_V1") != nullptr;  // A/B switch for the microbench
   if (!v1_only) {  // frame-tiled kernel (conv_tile.hip) for the shapes it covers
     const int r = conv_tile_launch(a, dtype, s);
-    if (r >= 0) return r;
-  }
-  if (getenv("STGCN_HALO")) {  // experimental stride-1 halo kernel (opt-in until it beats this one)
-    const int r = conv_halo_launch(a, dtype, s);
     if (r >= 0) return r;
   }
   const int bn = conv_rows_bn_tile(a.Cout);

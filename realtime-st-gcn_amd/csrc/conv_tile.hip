@@ -70,7 +70,6 @@ struct TileGeom {
   int parity;      // 1: stride-2 transposed conv, tiles hold output frames of one parity
   int tiles_half;  // parity mode: tiles per (sample, parity)
   float inv_v;     // 1 / V
-  long long* dbg;  // diagnostic (STGCN_TILE_DBG): per-block phase cycles of wave 0, else nullptr
 };
 
 // s_waitcnt vmcnt(n) lgkmcnt(0) (gfx9 encoding: vmcnt[3:0] | expcnt[6:4]=7 | lgkmcnt[11:8] | vmcnt[5:4]<<14)
@@ -374,20 +373,6 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stg
     }
   };
 
-  long long tl = 0, tcp = 0, tst = 0, tbar = 0, tk0 = g.dbg ? (long long)__builtin_amdgcn_s_memtime() : 0;
-  long long q0 = 0, q1 = 0, q2 = 0, q3 = 0;
-  auto stamp = [&](long long& q) {
-    if (g.dbg) q = (long long)__builtin_amdgcn_s_memtime();
-  };
-  auto account = [&]() {
-    if (g.dbg) {
-      const long long q4 = (long long)__builtin_amdgcn_s_memtime();
-      tl += q1 - q0;
-      tcp += q2 - q1;
-      tst += q3 - q2;
-      tbar += q4 - q3;
-    }
-  };
 
   if constexpr (NBS == 2) {
     issue_A(0, ra[0]);
@@ -396,18 +381,13 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stg
     __syncthreads();
     for (int c = 0; c < nchunks; ++c) {
       const bool more = c + 1 < nchunks;
-      stamp(q0);
       if (more) {
         issue_A(c + 1, ra[0]);
         issue_B(c + 1, (c + 1) & 1);
       }
-      stamp(q1);
       compute(c & 1, c & 1);
-      stamp(q2);
       if (more) store(c + 1, (c + 1) & 1, ra[0]);
-      stamp(q3);
       __syncthreads();
-      account();
     }
   } else {
     // VMEM instructions a wave issues for one chunk (fast path: A_MAX loads + the whole B rounds)
@@ -425,46 +405,27 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stg
     for (int c = 0; c < nchunks; c += 2) {
       // even chunk c: A regs set 0 is free (chunk c was stored last step), B stage (c+2)%3 too
       const int b2 = b0 == 0 ? 2 : b0 - 1;  // (c+2) % 3
-      stamp(q0);
       if (c + 2 < nchunks) {
         issue_B(c + 2, b2);
         issue_A(c + 2, ra[0]);
       }
-      stamp(q1);
       compute(0, b0);
-      stamp(q2);
       if (c + 1 < nchunks) store(c + 1, 1, ra[1]);
-      stamp(q3);
       if (c + 2 < nchunks) wait_vm_lgkm0<VM_CHUNK>(); else wait_vm_lgkm0<0>();
       __builtin_amdgcn_s_barrier();
-      account();
       if (c + 1 >= nchunks) break;
       // odd chunk c+1
       const int b1 = b0 == 2 ? 0 : b0 + 1;  // (c+1) % 3
-      stamp(q0);
       if (c + 3 < nchunks) {
         issue_B(c + 3, b0);  // (c+3) % 3 == c % 3
         issue_A(c + 3, ra[1]);
       }
-      stamp(q1);
       compute(1, b1);
-      stamp(q2);
       if (c + 2 < nchunks) store(c + 2, 0, ra[0]);
-      stamp(q3);
       if (c + 3 < nchunks) wait_vm_lgkm0<VM_CHUNK>(); else wait_vm_lgkm0<0>();
       __builtin_amdgcn_s_barrier();
-      account();
       b0 = b2;  // (c+2) % 3
     }
-  }
-  if (g.dbg && tid == 0) {
-    long long* d = g.dbg + (long)blockIdx.x * 8;
-    d[0] = tl;
-    d[1] = tcp;
-    d[2] = tst;
-    d[3] = tbar;
-    d[4] = (long long)__builtin_amdgcn_s_memtime() - tk0;
-    d[5] = nchunks;
   }
 
   // ---------------------------------------------------------------- epilogue
@@ -553,13 +514,6 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stg
   }
 }
 
-long long* tile_dbg_ptr = nullptr;
-long long* tile_dbg_buffer() {
-  static const bool want = getenv("STGCN_TILE_DBG") != nullptr;
-  if (!want) return nullptr;
-  if (!tile_dbg_ptr) (void)hipMalloc(&tile_dbg_ptr, 8 * 65536 * sizeof(long long));
-  return tile_dbg_ptr;
-}
 
 template <typename T, int WM, int WN, int TM, int TN, int KC, int KT, int S, int MINW = 2>
 int launch_tile(const stgcn_conv_desc& a, long max_row_blocks, hipStream_t s) {
@@ -568,7 +522,6 @@ int launch_tile(const stgcn_conv_desc& a, long max_row_blocks, hipStream_t s) {
   constexpr int HR_MAX = S * BM + (KT - S > 0 ? (KT - S) * 32 : 0);
   if (a.Cout_pad % BN || a.Cin_pad % KC) return -1;
   TileGeom g;
-  g.dbg = tile_dbg_buffer();
   const bool flat = KT == 1 && S == 1;
   g.parity = (S == 2 && a.trans) ? 1 : 0;
   g.inv_v = 1.f / (float)a.V;
@@ -621,18 +574,12 @@ int launch_tile(const stgcn_conv_desc& a, long max_row_blocks, hipStream_t s) {
   size_t lds = 2 * ((size_t)A_BYTES + B_BYTES) + pro_bytes;
   if (red > lds) lds = red;
   if (!use3 && lds > 160 * 1024) return -1;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, false, 2>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (S == 2)
-      (void)hipFuncSetAttribute((const void*)conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, S == 2, 2>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (CAN3)
-      (void)hipFuncSetAttribute((const void*)conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, false, CAN3 ? 3 : 2>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
+  if (stgcn_lds_attr((const void*)conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, false, 2>, 160 * 1024, s) ||
+      (S == 2 &&
+       stgcn_lds_attr((const void*)conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, S == 2, 2>, 160 * 1024, s)) ||
+      (CAN3 && stgcn_lds_attr((const void*)conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, false, CAN3 ? 3 : 2>,
+                              160 * 1024, s)))
+    return STGCN_EHIP;
   if (g.parity)
     hipLaunchKernelGGL((conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, S == 2, 2>), dim3((unsigned)nblk),
                        dim3(WM * WN * 64), lds, s, a, g);
@@ -661,12 +608,6 @@ int tile_dispatch(const stgcn_conv_desc& a, long mrb, hipStream_t s) {
 }  // namespace
 
 long conv_rows_num_row_blocks(long M, int cout);
-
-int tile_debug_read(long long* host, long n) {
-  if (!tile_dbg_ptr) return 1;
-  (void)hipDeviceSynchronize();
-  return hipMemcpy(host, tile_dbg_ptr, n * sizeof(long long), hipMemcpyDeviceToHost) == hipSuccess ? 0 : 3;
-}
 
 // returns -1 when the shape is not handled here (caller falls back to conv_rows.hip)
 int conv_persist_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s);

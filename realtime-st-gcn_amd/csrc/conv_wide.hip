@@ -72,7 +72,6 @@ struct WGeom {
   int fold;     // stride-2 folding: 0 none, 1 input parity (forward), 2 output parity (data grad)
   int cpar;     // fold 1: 64-channel items per input parity; fold 2: output channels per parity
   int wc32, wk16;  // fragment image dims: (output channels / 32, input channels / 16)
-  long long* dbg;  // DBG & 4: per-block phase cycles [block][16]
   int strided;     // 1: block b takes tiles b, b + grid, ... (A/B switch STGCN_WIDE_STRIDED); 0: a contiguous run
 };
 
@@ -99,8 +98,7 @@ DEV TileInfo tile_info(int tile, const WGeom& g) {
 // item k+1; barrier E_k.  At a tile end the MMA waves dump acc (+ bias) as a column-major bf16 image
 // into buf b (8-B ds_write_b64 per 4 rows) and their Welford partials into sRed; barrier I_k; the
 // helpers drain that image during item k+1 before they overwrite buf b with item k+2's halo.
-// DBG (diagnostic instantiations, STGCN_WIDE_DBG=<bits>): bit1 no helper work (results wrong), bit2 phase
-// timers (s_memtime of MMA wave 0 / helper wave 4 into g.dbg)
+// DBG (compile-time A/B instantiations only): bit1 no helper work (results wrong)
 template <int BN, int KTAP, int NBUF, int PRO, int DBG = 0, int KGT = 64>
 __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_desc a, const WGeom g) {
   // item width: 64 input channels (>= 128-channel layers) or 32 (64-channel layers: two items per tile)
@@ -130,6 +128,9 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
   char* const sA0 = smem;
   char* const sA1 = smem + g.abytes;
   float4* const sRed = reinterpret_cast<float4*>(smem + 2 * g.abytes);  // [WM][BN]
+  // drain counter: each helper wave adds 1 when its reads of a tile image are done; the halo writes into
+  // that buffer wait until all four have (the image and the next halo share the buffer)
+  unsigned* const sCnt = reinterpret_cast<unsigned*>(smem + 2 * g.abytes + WM * BN * 16);
 
   auto item_tile = [&](int w, int& gi) {  // items past the block's last one are clamped to it
     w = min(w, nitems - 1);
@@ -138,20 +139,6 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
     return tile0 + tl * tstep;
   };
   auto tile_end = [&](int w) { return w < nitems && (w % g.G) == g.G - 1; };
-  long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
-  auto tmark = [&](int slot) {  // accumulate cycles since the previous mark into slot
-    if constexpr ((DBG & 4) != 0) {
-      const long long t = (long long)__builtin_amdgcn_s_memtime();
-      if (slot >= 0) tacc[slot] += t - tlast;
-      tlast = t;
-    }
-  };
-  auto tflush = [&](int base) {
-    if constexpr ((DBG & 4) != 0) {
-      if ((tid & 63) == 0)
-        for (int q = 0; q < 8; ++q) g.dbg[(long)blockIdx.x * 16 + base + q] = tacc[q];
-    }
-  };
 
   if (!mma) {
     // =============================== helper waves ===============================
@@ -283,44 +270,49 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
       }
     };
 
+    // Helper waves are not synchronised with each other inside a window, so a wave that finished its share
+    // of a drain must not overwrite the buffer with the next halo while another still reads the image:
+    // count finished drains per wave in LDS and wait for all four before the first halo write.
+    unsigned ndrain = 0;
+    auto drain_sync = [&]() {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(sCnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      ndrain += 4;
+      while (__hip_atomic_load(sCnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < ndrain)
+        __builtin_amdgcn_s_sleep(1);
+    };
+    if (htid == 0) *sCnt = 0u;  // visible to all helpers after barrier P
     // item w lives in register set w % NSET and LDS buffer w & 1; nitems is even (G even)
     issue_A.template operator()<0>(0);
     store_A.template operator()<0>(sA0);
     if (nitems > 1) issue_A.template operator()<1 % NSET>(1);
     if (NSET == 2 && nitems > 2) issue_A.template operator()<0>(2);
     lds_barrier();  // P
-    tmark(-1);
     for (int w = 0; w < nitems; w += 2) {
       // window w: item w+1 -> sA1, request item w+1+NSET
       if ((DBG & 2) == 0) {
-        if (w > 0 && tile_end(w - 1)) drain(w - 1, sA1);
-        tmark(0);
+        if (w > 0 && tile_end(w - 1)) {
+          drain(w - 1, sA1);
+          if (w + 1 < nitems) drain_sync();
+        }
         if (w + 1 < nitems) store_A.template operator()<1 % NSET>(sA1);
-        tmark(1);
         if (w + 1 + NSET < nitems) issue_A.template operator()<(1 + NSET) % NSET>(w + 1 + NSET);
-        tmark(2);
       }
       lds_barrier();  // E_w
-      tmark(3);
       if (tile_end(w)) lds_barrier();  // I_w
-      tmark(4);
       // window w+1: item w+2 -> sA0, request item w+2+NSET
       if ((DBG & 2) == 0) {
-        if (tile_end(w)) drain(w, sA0);
-        tmark(0);
+        if (tile_end(w)) {
+          drain(w, sA0);
+          if (w + 2 < nitems) drain_sync();
+        }
         if (w + 2 < nitems) store_A.template operator()<2 % NSET>(sA0);
-        tmark(1);
         if (w + 2 + NSET < nitems) issue_A.template operator()<(2 + NSET) % NSET>(w + 2 + NSET);
-        tmark(2);
       }
       lds_barrier();  // E_{w+1}
-      tmark(3);
       if (tile_end(w + 1)) lds_barrier();  // I_{w+1}
-      tmark(4);
     }
     if ((DBG & 2) == 0) drain(nitems - 1, ((nitems - 1) & 1) ? sA1 : sA0);
-    tmark(5);
-    if (wave == 4) tflush(8);
     return;
   }
 
@@ -499,23 +491,16 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[hs & 1][i], fb[hs % NBUF][j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (s == SPI - 1) {
-        tmark(3);
         lds_barrier();  // E_{w+h}
-        tmark(4);
       }
     };
     if (w % g.G == 0) load_bias(w);
-    tmark(-1);
     static_for<PAIR>(step);
-    tmark(0);
     if (tile_end(w + 1)) {
       dump(w + 1, sA1);
-      tmark(1);
       lds_barrier();  // I_{w+1}
-      tmark(2);
     }
   }
-  if (wave == 0) tflush(0);
 }
 
 // Parity-folded fragment image of a stride-2 Kt = 9 weight [9][Co][Ci] (fp32, any strides): the 5-tap
@@ -559,12 +544,6 @@ int pack_s2frag_launch(const float* src, long s0, long s1, long s2, int Co, int 
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
 
-long long* wide_dbg_ptr = nullptr;
-int wide_debug_read(long long* host, long n) {
-  if (!wide_dbg_ptr) return 1;
-  (void)hipDeviceSynchronize();
-  return hipMemcpy(host, wide_dbg_ptr, n * sizeof(long long), hipMemcpyDeviceToHost) == hipSuccess ? 0 : 3;
-}
 
 long conv_rows_num_row_blocks(long M, int cout);
 
@@ -576,7 +555,6 @@ int conv_wide_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
   if (a.bias_mode != 0 && a.bias_mode != 1) return -1;
   if (a.in_ld % 8 || a.V > 32 || a.Cin % 8 || a.Cout % 8 || a.out_ld % 8) return -1;
   WGeom g;
-  g.dbg = nullptr;
   {
     static const int st = getenv("STGCN_WIDE_STRIDED") ? atoi(getenv("STGCN_WIDE_STRIDED")) : 0;
     g.strided = st;
@@ -631,45 +609,23 @@ int conv_wide_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
   g.ntiles = (int)nt;
   if (a.stats && (long)a.N * g.tiles_n > conv_rows_num_row_blocks((long)a.N * a.T_out * a.V, a.Cout)) return -1;
   g.abytes = abytes_for(kg);
-  const size_t lds = 2 * (size_t)g.abytes + (size_t)WM * BN * 16;
+  const size_t lds = 2 * (size_t)g.abytes + (size_t)WM * BN * 16 + 16;
   if (lds > (size_t)LDS_MAX) return -1;
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (ncu <= 0) ncu = 256;
-  }
+  const int ncu = stgcn_cu_count(s);
   const int tpb = (g.ntiles + ncu - 1) / ncu;
   const int grid = (g.ntiles + tpb - 1) / tpb;
   const dim3 gd((unsigned)grid), bd(2 * NT);
-  static const int dbg = getenv("STGCN_WIDE_DBG") ? atoi(getenv("STGCN_WIDE_DBG")) : 0;
   auto kern = [&]() -> void (*)(const stgcn_conv_desc, const WGeom) {
-    if (dbg && ktap == 9) {
-      static long long* dbuf = nullptr;
-      if (!dbuf) (void)hipMalloc(&dbuf, 16 * 4096 * sizeof(long long));
-      wide_dbg_ptr = dbuf;
-      g.dbg = dbuf;
-      return dbg == 2 ? conv_wide_kernel<128, 9, 6, 1, 2> : conv_wide_kernel<128, 9, 6, 1, 4>;
-    }
     if (kg == 32)
       return a.pro ? conv_wide_kernel<64, 9, 12, 1, 0, 32> : conv_wide_kernel<64, 9, 12, 0, 0, 32>;
     // B ring depth 8 (7 k-steps of L2 latency cover): measured 2-3 % faster than 4, 6 or 9 at C = 128/256
     if (ktap == 9) return a.pro ? conv_wide_kernel<128, 9, 8, 1> : conv_wide_kernel<128, 9, 8, 0>;
     // stride-2 folded 5-tap form: ring depth must divide 40 k-steps per item pair.  Depth 8 measured equal
-    // to 5 in the full step (9.40 vs 9.39 ms, 3 interleaved runs); 10 spills (35 VGPRs).  A/B knob only.
-    static const int s2ring = getenv("STGCN_WIDE_S2_RING") ? atoi(getenv("STGCN_WIDE_S2_RING")) : 5;
-    if (s2ring == 8) return a.pro ? conv_wide_kernel<128, 5, 8, 1> : conv_wide_kernel<128, 5, 8, 0>;
-    if (s2ring == 10) return a.pro ? conv_wide_kernel<128, 5, 10, 1> : conv_wide_kernel<128, 5, 10, 0>;
+    // to 5 in the full step (9.40 vs 9.39 ms, 3 interleaved runs); 10 spills (35 VGPRs).
     return a.pro ? conv_wide_kernel<128, 5, 5, 1> : conv_wide_kernel<128, 5, 5, 0>;
   };
   auto* k = kern();
-  static bool attr[6] = {false, false, false, false, false, false};
-  const int ai = (kg == 32 ? 4 : ktap == 9 ? 0 : 2) + (a.pro ? 1 : 0);
-  if (!attr[ai] || dbg) {
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-    attr[ai] = true;
-  }
+  if (stgcn_lds_attr((const void*)k, LDS_MAX, s)) return STGCN_EHIP;
   hipLaunchKernelGGL(k, gd, bd, lds, s, a, g);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }

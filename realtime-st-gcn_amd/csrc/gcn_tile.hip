@@ -66,8 +66,12 @@ DEV bf16x8 trfrag(const char* panel, int row0, int lane) {
 // compiler would otherwise treat every later LDS read as aliasing the DMA and drain vmcnt to 0 before it,
 // which serialises the panel ring.  Ordering is kept by the "memory" clobbers here and on the explicit
 // vmcnt waits of the main loop.
+// m0 is reserved, so it is saved in an SGPR the asm owns and restored after the issue (not clobbered).
 DEV void glds16(const void* src, unsigned lds_off) {
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds_off) : "memory", "m0");
+  unsigned saved;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(saved) : "v"(src), "s"(lds_off) : "memory");
 }
 DEV unsigned lds_u32(const void* p) {
   return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
@@ -78,7 +82,6 @@ struct GMGeom {
   int R;     // row blocks
   int ncol;  // column tiles (Cout / 64)
   int k16n;  // K blocks per column of the weight image (Kw_pad / 16)
-  int dbg;   // STGCN_GT_DBG bits (A/B experiments): 1 no input DMA, 2 no output stores
 };
 
 template <int P, int G, int DBG = 0>
@@ -397,10 +400,6 @@ int gcn_tile_launch(const stgcn_gcn_tile_desc& a, hipStream_t s) {
   GMGeom g = plan(a.NT, a.Cout);
   const int G = a.Cin / 32;
   g.k16n = a.Kw_pad / 16;
-  {
-    const char* e = getenv("STGCN_GT_DBG");
-    g.dbg = e ? atoi(e) : 0;
-  }
   const size_t lds = (size_t)TN * a.P * G * 2 * 1024 + (size_t)NW * RING;
   if (lds > (size_t)LDS_MAX) return STGCN_EBADSHAPE;
   typedef void (*KFn)(const stgcn_gcn_tile_desc, const GMGeom);
@@ -410,13 +409,7 @@ int gcn_tile_launch(const stgcn_gcn_tile_desc& a, hipStream_t s) {
   const int gi = G == 2 ? 0 : G == 4 ? 1 : G == 8 ? 2 : -1;
   if (gi < 0) return STGCN_EBADSHAPE;
   KFn k = tab[a.P - 1][gi];
-  if (g.dbg && a.P == 3) {  // A/B experiments (STGCN_GT_DBG bits 1, 2), P = 3 only
-    static const KFn dt[3][3] = {{gcn_mfma_kernel<3, 2, 1>, gcn_mfma_kernel<3, 4, 1>, gcn_mfma_kernel<3, 8, 1>},
-                                 {gcn_mfma_kernel<3, 2, 2>, gcn_mfma_kernel<3, 4, 2>, gcn_mfma_kernel<3, 8, 2>},
-                                 {gcn_mfma_kernel<3, 2, 3>, gcn_mfma_kernel<3, 4, 3>, gcn_mfma_kernel<3, 8, 3>}};
-    k = dt[(g.dbg & 3) - 1][gi];
-  }
-  (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
+  if (stgcn_lds_attr((const void*)k, LDS_MAX, s)) return STGCN_EHIP;
   hipLaunchKernelGGL(k, dim3((unsigned)(g.R * g.ncol)), dim3(NW * 64), lds, s, a, g);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }

@@ -357,14 +357,9 @@ int launch_gconv(const stgcn_gconv_desc& a, hipStream_t s) {
   size_t lds = 2 * (size_t)STAGE;
   const size_t red = a.stats ? (size_t)WM * BN * 16 : 0;
   if (red > lds) lds = red;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gconv_kernel<T, WM, WN, TM, TN, KC, false>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)gconv_kernel<T, WM, WN, TM, TN, KC, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
+  if (stgcn_lds_attr((const void*)gconv_kernel<T, WM, WN, TM, TN, KC, false>, 160 * 1024, s) ||
+      stgcn_lds_attr((const void*)gconv_kernel<T, WM, WN, TM, TN, KC, true>, 160 * 1024, s))
+    return STGCN_EHIP;
   const bool accv = a.accumulate && (a.out_ld % VEC) == 0 && (a.Cout % VEC) == 0;
   if (accv)
     hipLaunchKernelGGL((gconv_kernel<T, WM, WN, TM, TN, KC, true>), dim3((unsigned)nblk), dim3(WM * WN * 64), lds, s,
@@ -760,9 +755,14 @@ DEV void sfor(F&& f) {
 
 DEV unsigned lds_u32(const void* p) { return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p; }
 
+// 16 B per lane, global -> LDS at M0 = lds_off (lane-linear).  m0 is a reserved register, so it is not
+// declared clobbered: the asm saves the compiler's m0 in an SGPR it owns and restores it after the
+// issue (the DMA samples M0 when it is issued).
 DEV void glds16m(const void* src, unsigned lds_off) {
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src),
-               "s"(__builtin_amdgcn_readfirstlane(lds_off)) : "memory", "m0");
+  unsigned saved;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(saved) : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_off)) : "memory");
 }
 
 template <int DEG>
@@ -1178,12 +1178,7 @@ int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s
     const bool ring = cob == 64 && w3_ok(a);
     const size_t lds = ring ? (size_t)W3_LDS : 2 * (size_t)(cob / 32 + 2 * J2) * w2m(cob) * WPR;
     auto* k = ring ? gconv_wgrad3_kernel : cob == 128 ? gconv_wgrad2_kernel<128> : gconv_wgrad2_kernel<64>;
-    static bool attr2[3] = {false, false, false};
-    const int ka = ring ? 2 : cob == 128;
-    if (!attr2[ka]) {
-      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr2[ka] = true;
-    }
+    if (stgcn_lds_attr((const void*)k, 160 * 1024, s)) return STGCN_EHIP;
     const long blocks = (long)a.V * g.nco * g.nci * g.R;
     hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(ring ? 256 : cob / 16 * 64), lds, s, a, g);
     hipLaunchKernelGGL(gslab_reduce_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, (const float*)g.slab,
@@ -1199,12 +1194,7 @@ int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s
   WGG g = wplan(a);
   if (!a.work || a.work_bytes < (long)g.R * E * (long)sizeof(float)) return STGCN_EBADSHAPE;
   g.slab = reinterpret_cast<float*>(a.work);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gconv_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    attr = true;
-  }
+  if (stgcn_lds_attr((const void*)gconv_wgrad_kernel, 160 * 1024, s)) return STGCN_EHIP;
   const long blocks = (long)a.V * a.J * g.nco * g.nci * g.R;
   const size_t lds = 2 * 4 * WKM * WPR;  // >= the 48 KB cross-wave reduction buffer
   hipLaunchKernelGGL(gconv_wgrad_kernel, dim3((unsigned)blocks), dim3(256), lds, s, a, g);

@@ -716,7 +716,7 @@ int ln_bwd_launch(const void* dy, int lddy, int mask, const void* mref, int ldm,
   const size_t lds = dgb ? (size_t)2 * V * C * 4 : 0;
   if (lds > 150 * 1024) return STGCN_EBADSHAPE;
   DISPATCH_T(dtype, {
-    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)ln_bwd_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (lds > 64 * 1024 && stgcn_lds_attr((const void*)ln_bwd_kernel<T>, (int)lds, s)) return STGCN_EHIP;
     hipLaunchKernelGGL(ln_bwd_kernel<T>, dim3((unsigned)((F + 3) / 4)), dim3(256), lds, s, (const T*)dy, lddy, mask,
                        (const T*)mref, ldm, (const T*)x, ldx, st, g, b, F, V, C, (T*)dx, lddx, accumulate, dgb);
   });

@@ -356,12 +356,7 @@ Plan plan(const stgcn_wgrad_desc& a) {
 
 template <int KT, int S, int NB, int TW, int NBW, bool LN>
 int launch_w1(const stgcn_wgrad_desc& a, const Plan& p, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)wgrad_tile_kernel<KT, S, NB, TW, NBW, LN>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
+  if (stgcn_lds_attr((const void*)wgrad_tile_kernel<KT, S, NB, TW, NBW, LN>, 160 * 1024, s)) return STGCN_EHIP;
   const unsigned grid = (unsigned)(p.g.R * p.g.nco * p.g.nci);
   hipLaunchKernelGGL((wgrad_tile_kernel<KT, S, NB, TW, NBW, LN>), dim3(grid), dim3(256), p.lds, s, a, p.g);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;

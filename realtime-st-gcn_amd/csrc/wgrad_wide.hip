@@ -349,12 +349,7 @@ int wgrad_wide_launch(const stgcn_wgrad_desc& a, int dtype, hipStream_t s) {
   p.g.slab = reinterpret_cast<float*>(a.work);
   auto* k = p.ktap == 9 ? (a.pro == 1 ? wgrad_wide_kernel<1, 9> : wgrad_wide_kernel<0, 9>)
                         : (a.pro == 1 ? wgrad_wide_kernel<1, 5> : wgrad_wide_kernel<0, 5>);
-  static bool attr[4] = {false, false, false, false};
-  const int ai = (p.ktap == 9 ? 0 : 2) + (a.pro == 1 ? 1 : 0);
-  if (!attr[ai]) {
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
-    attr[ai] = true;
-  }
+  if (stgcn_lds_attr((const void*)k, LDS_MAX, s)) return STGCN_EHIP;
   const unsigned grid = (unsigned)(p.g.nco * p.g.nci * p.g.R);
   hipLaunchKernelGGL(k, dim3(grid), dim3(NT), p.lds, s, a, p.g);
   if (hipGetLastError() != hipSuccess) return STGCN_EHIP;

@@ -34,6 +34,13 @@ def sub(d, prefix):
     return {k[len(prefix):]: v for k, v in d.items() if k.startswith(prefix)}
 
 
+def _report(name, rel_max, tol, l2=None):
+    """STGCN_TEST_REPORT=1: print every measured error (pytest -s) so tolerances stay evidence-based."""
+    if os.environ.get("STGCN_TEST_REPORT"):
+        extra = f" L2 {l2:.2e}" if l2 is not None else ""
+        print(f"[err] {name}: max/scale {rel_max:.2e}{extra} (tol {tol:g})", flush=True)
+
+
 def assert_close(got, ref, rel=1e-3, name="", scale_floor=0.0):
     """SURVEY §8(c) tolerance: max|got-ref| <= rel * max|ref| (plus a tiny absolute floor).
 
@@ -45,6 +52,7 @@ def assert_close(got, ref, rel=1e-3, name="", scale_floor=0.0):
     assert got.shape == ref.shape, f"{name}: shape {tuple(got.shape)} != {tuple(ref.shape)}"
     scale = max(ref.abs().max().item(), scale_floor)
     err = (got - ref).abs().max().item()
+    _report(name, err / max(scale, 1e-30), rel)
     assert err <= rel * scale + 1e-6, f"{name}: max err {err:.3e} > {rel:g} * {scale:.3e}"
 
 
@@ -68,6 +76,13 @@ def grad_floor(grads, key):
     return 0.0
 
 
+def bn_fed_bias(key):
+    """Conv biases that feed a batch-statistics BatchNorm (tcn.2 -> tcn.3, residual.0 -> residual.1 of a BN
+    StgcnLayer): their exact gradient is 0, so both the reference's and ours are rounding noise; they are
+    checked against an absolute bound relative to the paired weight gradient instead of elementwise."""
+    return key.endswith("tcn.2.bias") or key.endswith("residual.0.bias")
+
+
 def assert_grad_close(got, ref, rel=1e-3, name="", scale_floor=0.0, reduction=False):
     """Gradient parity.  Max-norm ``rel`` as in assert_close, except that gradients downstream of a
     ReLU whose input is within rounding of 0 can legitimately flip (the reference's own CPU and GPU
@@ -80,6 +95,8 @@ def assert_grad_close(got, ref, rel=1e-3, name="", scale_floor=0.0, reduction=Fa
     assert g.shape == r.shape, f"{name}: shape {tuple(g.shape)} != {tuple(r.shape)}"
     scale = max(r.abs().max().item(), scale_floor)
     err = (g - r).abs()
+    _report(name, err.max().item() / max(scale, 1e-30), rel,
+            ((g - r).norm() / max(r.norm().item(), 1e-30)).item())
     if err.max().item() <= rel * scale + 1e-6:
         return
     l2 = ((g - r).norm() / max(r.norm().item(), 1e-30)).item()
