@@ -8,8 +8,13 @@ WindowSegment.mask_segment) + backward + Adam step.  Inputs are resident in HBM 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 Kernels are launched eagerly from Python (the GPU stays busy: launch cost < kernel time); --graph
 captures the step into HIP graphs (torch.cuda.CUDAGraph) and replays them instead.
-N > 1: launched by torch.distributed.run, one process per GPU, DistributedDataParallel over RCCL
-(backend "nccl"); each rank processes its own 64-window batch (weak scaling).
+N > 1: one process per GPU, DistributedDataParallel over RCCL (backend "nccl").  Under
+torch.distributed.run (WORLD_SIZE set) the ranks are the launcher's; `python bench.py --gpus N` alone
+starts `torch.distributed.run --nproc-per-node N` as a child process (before anything touches the GPU)
+and exits with its status.  Each rank processes its own 64 consecutive windows of one synthetic trial
+of N*64 windows (weak scaling); the loss is the trial's (parallel.exchange_shard: the boundary MSE pair
+crosses ranks), so the gradient equals the single-process one up to per-replica BatchNorm statistics,
+as in the reference's DataParallel.
 Rank 0 prints ONE JSON line (metric/value/..., roofline, cpu_baseline).
 """
 from __future__ import annotations
@@ -38,12 +43,38 @@ HBM_PEAK_GBS = 8000.0
 
 
 def loss_fn(logits, labels, weight):
-    """utils/loss.py:25-41 with WindowSegment.mask_segment (N',C',1) -> (1,C',N') (segment_generator.py:151)."""
+    """utils/loss.py:25-41 with WindowSegment.mask_segment (N',C',1) -> (1,C',N') (segment_generator.py:151);
+    CPU baseline only (the GPU step uses the HIP loss kernel, loss.Loss)."""
     pred = logits.permute(2, 1, 0)                      # (1, classes, windows)
     ce = torch.nn.functional.cross_entropy(pred, labels, weight=weight)
     ls = torch.log_softmax(pred, dim=1)
     mse = 0.15 * torch.clamp((ls[:, :, 1:] - ls.detach()[:, :, :-1]) ** 2, 0, 16).mean()
     return ce + mse
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def spawn_ranks(args):
+    """`bench.py --gpus N` without a launcher: run torch.distributed.run as a child (this process has not
+    touched the GPU) and return its exit status."""
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 # The roofline kernel: conv_wide_kernel<128,9,8,1,0,64>, the Kt=9 stride-1 temporal-conv forward of the
@@ -76,23 +107,40 @@ def cpu_baseline(pkg, model_cpu_sd):
     for _ in range(reps):
         step(n_sample)
     dt = time.perf_counter() - t0
-    return {"value": reps * n_sample * T_LEN / dt, "unit": "skeleton-frames/s", "cores": threads, "kind": "port",
-            "sample": f"oracle fwd+bwd (torch CPU fp32) of the same 9-layer model at N={n_sample} T={T_LEN} V=25, "
-                      f"{reps} steps, {dt:.1f} s"}
+    value = reps * n_sample * T_LEN / dt
+    out = {"value": value, "unit": "skeleton-frames/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
+           "sample": f"oracle fwd+bwd (torch CPU fp32) of the same 9-layer model at N={n_sample} T={T_LEN} V=25, "
+                     f"{reps} steps, {dt:.1f} s"}
+    # tools/calibrate_cpu.py (build container): oracle time / reference time on one host, same shapes/threads
+    cal = os.path.join(ROOT, "profiles", "cpu_calibration.json")
+    if os.path.exists(cal):
+        with open(cal) as f:
+            c = json.load(f)
+        r = c["ratio_oracle_over_reference"]
+        out["calibration"] = {"ratio_oracle_over_reference": r, "measured_on": c["host_cpu"],
+                              "threads": c["threads"], "reference_equivalent_value": round(value * r, 1)}
+    return out
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=250)  # >= 2 s timed, so utilisation sampling sees it
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", action="store_true",
                     help="capture the step into HIP graphs and replay them (measured slower than eager here)")
     args = ap.parse_args()
 
+    ndev = torch.cuda.device_count()  # does not initialise HIP (safe before spawning the ranks)
+    if ndev < args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} needs {args.gpus} HIP devices, {ndev} visible")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -122,8 +170,13 @@ def main():
 
     gen = torch.Generator(device=dev).manual_seed(rank)
     x = torch.randn(N_BATCH, 3, T_LEN, V_J, device=dev, generator=gen)
-    labels = torch.randint(0, CLASSES, (1, N_BATCH), device=dev, generator=gen)
-    weight = (1 - torch.rand(CLASSES, device=dev, generator=gen) / CLASSES)
+    # the trial's labels and class distribution are the same on every rank (seeded alike)
+    gen_t = torch.Generator(device=dev).manual_seed(12345)
+    labels_trial = torch.randint(0, CLASSES, (1, N_BATCH * world), device=dev, generator=gen_t)
+    class_dist = torch.rand(CLASSES, device=dev, generator=gen_t) + 0.5
+    crit = pkg.loss.Loss(dev, class_dist)
+    w0, w1 = rank * N_BATCH, (rank + 1) * N_BATCH
+    labels = labels_trial[:, w0:w1]
 
     # Gradient exchange (N > 1): eager mode uses DistributedDataParallel (RCCL all-reduce of 16 MB
     # buckets overlapped with backward); graph mode all-reduces one flat fp32 buffer between the
@@ -132,8 +185,11 @@ def main():
     flat = torch.zeros(sum(numels), device=dev) if world > 1 and args.graph else None
 
     def fwd_bwd():
-        y = train_model(x)
-        loss = loss_fn(y, labels, weight)
+        pred = train_model(x).permute(2, 1, 0)  # (1, classes, windows): WindowSegment.mask_segment
+        shard = pkg.parallel.exchange_shard(pred, labels_trial, crit.weight, w0, N_BATCH * world) \
+            if world > 1 else None
+        ce, mse = crit(0, pred, labels, shard=shard)
+        loss = (ce + mse) * world  # DDP averages over ranks; the shares sum to the trial's loss
         loss.backward()
         if flat is not None:
             torch.cat([p.grad.reshape(-1) for p in params], out=flat)
@@ -246,7 +302,8 @@ def main():
             cpu = cpu_baseline(pkg, cpu_sd)
         out = {
             "metric": "skeleton-frames/sec/GPU (fwd+bwd), 10-layer ST-GCN N=64 T=300 V=25",
-            "value": round(value, 1), "unit": "skeleton-frames/s", "n_gpus": world, "steps": args.steps,
+            "value": round(value, 1), "unit": "skeleton-frames/s", "per_gpu": round(value / world, 1),
+            "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (randn skeletons, random labels/class weights), random-init weights",

@@ -284,6 +284,27 @@ int stgcn_attn_bwd(const void* theta, const void* phi, int ld, int N, int T, int
 
 int stgcn_abi_version(void);
 
+/* Segmentation loss + statistics of a prediction series (replaces utils/loss.py:25-41 Loss.__call__ and
+ * utils/statistics.py:5-16 Statistics.__call__ on the (1, C, L) output of segment_generator.mask_segment).
+ *   p: fp32 [L][ldp] predictions (frame w, class c); labels: int64 [L - first]; wt: fp32 [C] class weights
+ *   (1 - class_dist / sum, loss.py:20); mode: 0 'logits', 1 'logsoftmax', 2 'softmax' output_type;
+ *   first: 1 drops frame 0 from the CE and statistics (subsegment i > 0).
+ *   Data-parallel shards: prev = predictions of the frame before this shard (its MSE pair) or NULL,
+ *   den = the global CE weight sum (device fp32 scalar; NULL: this call's own), pairs = the global MSE
+ *   pair count (<= 0: this call's own).
+ *   Outputs: out[0] ce, out[1] mse (this call's share of the trial's loss), out[2] top-1 hits,
+ *   out[3] top-5 hits, out[4] this call's CE weight sum (out: fp32 [8]); dce / dmse [L][C] the gradients
+ *   of ce and mse w.r.t. p (NULL: skipped); top5 int32 [L][5] class indices (NULL: skipped).
+ *   work: stgcn_seg_loss_workspace(L) bytes.  Deterministic (fixed-order sums). */
+long stgcn_seg_loss_workspace(int L);
+int stgcn_seg_loss(const float* p, int ldp, const long* labels, const float* wt, const float* prev, int L, int C,
+                   int first, int mode, const float* den, float pairs, float* dce, float* dmse, int* top5, float* work,
+                   float* out, void* stream);
+/* dp[i] = (*gce) * dce[i] + (*gmse) * dmse[i]  (gce/gmse: device fp32 scalars, NULL = 0) — the backward of
+ * the two loss terms given the upstream gradients, without a host round trip. */
+int stgcn_seg_loss_bwd(const float* dce, const float* dmse, const float* gce, const float* gmse, long n, float* dp,
+                       void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -377,13 +377,44 @@ def aagcn_model(x, sd, arch, A_raw_far):
 # --------------------------------------------------------------------------------------
 
 
-def loss(i, logits, labels, class_dist):
-    """Weighted CE + 0.15 * clamped temporal MSE of log-softmax (loss.py:21-41)."""
+def loss(i, logits, labels, class_dist, output_type="logits"):
+    """Weighted CE + 0.15 * clamped temporal MSE (loss.py:8-41); output_type picks foo/bar (loss.py:10-18)."""
     w = 1 - class_dist / class_dist.sum()
-    ce = F.cross_entropy(logits if i == 0 else logits[:, :, 1:], labels, weight=w)
-    ls = F.log_softmax(logits, dim=1)
-    mse = 0.15 * torch.clamp((ls[:, :, 1:] - ls.detach()[:, :, :-1]) ** 2, 0, 16).mean()
+    foo = {"logits": lambda x: x, "logsoftmax": lambda x: x, "softmax": torch.log}[output_type]
+    bar = {"logits": lambda x: F.log_softmax(x, dim=1), "logsoftmax": torch.exp, "softmax": lambda x: x}[output_type]
+    ce = F.cross_entropy(foo(logits if i == 0 else logits[:, :, 1:]), labels, weight=w)
+    q = bar(logits)
+    mse = 0.15 * torch.clamp((q[:, :, 1:] - q.detach()[:, :, :-1]) ** 2, 0, 16).mean()
     return ce, mse
+
+
+def loss_shard(i, pred, labels, class_dist, prev, den, pairs, rank_first, output_type="logits"):
+    """One data-parallel shard's share of loss.py:25-41 over the whole series: pred (1, C, n) this shard's
+    frames, labels its labels (frame 0 dropped if i > 0 and rank_first), prev (C,) the frame before the
+    shard or None, den = sum of class weights over the series' labels, pairs = series length - 1.  The
+    shares of all shards sum to loss(i, series, ...); the MSE's left operand is detached (loss.py:37)."""
+    w = 1 - class_dist / class_dist.sum()
+    foo = {"logits": lambda x: x, "logsoftmax": lambda x: x, "softmax": torch.log}[output_type]
+    bar = {"logits": lambda x: F.log_softmax(x, dim=1), "logsoftmax": torch.exp, "softmax": lambda x: x}[output_type]
+    z = foo(pred if (i == 0 or not rank_first) else pred[:, :, 1:])
+    ce = F.cross_entropy(z, labels, weight=w, reduction="sum") / den
+    q = bar(pred)
+    if prev is not None:
+        q_prev = bar(prev.reshape(1, -1, 1).to(pred.dtype)).detach()
+        qa = torch.cat([q_prev, q.detach()[:, :, :-1]], dim=2)
+        qb = q
+    else:
+        qa, qb = q.detach()[:, :, :-1], q[:, :, 1:]
+    mse = 0.15 * torch.clamp((qb - qa) ** 2, 0, 16).sum() / (pred.shape[1] * pairs)
+    return ce, mse
+
+
+def statistics(i, predictions, labels):
+    """Top-1 / top-5 hits (statistics.py:5-16)."""
+    p = predictions if i == 0 else predictions[:, :, 1:]
+    _, top5 = torch.topk(p, k=5, dim=1)
+    top1 = top5[:, 0, :]
+    return top1, top5, int(torch.sum(top1 == labels)), int(torch.sum(top5 == labels[:, None])), labels.numel()
 
 
 # --------------------------------------------------------------------------------------

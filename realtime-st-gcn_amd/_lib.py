@@ -132,6 +132,10 @@ _SIGS = {
                                   c_int, c_void_p]),
     "stgcn_attn_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "stgcn_seg_loss_workspace": (ctypes.c_long, [c_int]),
+    "stgcn_seg_loss": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                               c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "stgcn_seg_loss_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p]),
 }
 
 EXPORTS = tuple(_SIGS)

@@ -83,6 +83,12 @@ int attn_scores_launch(const void* th, const void* ph, int ld, int N, int T_, in
 long attn_scores_workspace(int N, int T_, int V, int P);
 int attn_bwd_launch(const void* th, const void* ph, int ld, int N, int T_, int V, int P, int ce, const float* C,
                     const float* dC, float* dS, void* dth, void* dph, int dtype, hipStream_t s);
+long seg_loss_workspace_launch(int L);
+int seg_loss_launch(const float* p, int ldp, const long* labels, const float* wt, const float* prev, int L, int C,
+                    int first, int mode, const float* den, float pairs, float* dce, float* dmse, int* top5, float* work,
+                    float* out, hipStream_t s);
+int seg_loss_bwd_launch(const float* dce, const float* dmse, const float* gce, const float* gmse, long n, float* dp,
+                        hipStream_t s);
 
 #define CHECK_DTYPE(dt) \
   if ((dt) != 0 && (dt) != 1) return STGCN_EDTYPE
@@ -324,6 +330,18 @@ int stgcn_attn_bwd(const void* th, const void* ph, int ld, int N, int T, int V, 
   CHECK_DTYPE(dtype);
   if (!th || !ph || !C || !dC || !dS || !dth || !dph || ld < P * ce) return STGCN_EBADSHAPE;
   return attn_bwd_launch(th, ph, ld, N, T, V, P, ce, C, dC, dS, dth, dph, dtype, STREAM(stream));
+}
+
+long stgcn_seg_loss_workspace(int L) { return seg_loss_workspace_launch(L); }
+int stgcn_seg_loss(const float* p, int ldp, const long* labels, const float* wt, const float* prev, int L, int C,
+                   int first, int mode, const float* den, float pairs, float* dce, float* dmse, int* top5, float* work,
+                   float* out, void* stream) {
+  return seg_loss_launch(p, ldp, labels, wt, prev, L, C, first, mode, den, pairs, dce, dmse, top5, work, out,
+                         STREAM(stream));
+}
+int stgcn_seg_loss_bwd(const float* dce, const float* dmse, const float* gce, const float* gmse, long n, float* dp,
+                       void* stream) {
+  return seg_loss_bwd_launch(dce, dmse, gce, gmse, n, dp, STREAM(stream));
 }
 
 }  // extern "C"

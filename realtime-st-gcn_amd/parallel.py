@@ -1,14 +1,24 @@
-"""Data-parallel plumbing: shard long trials across ranks, wrap the model for RCCL gradient all-reduce.
+"""Data-parallel plumbing: shard long trials across ranks, make the loss of a sharded trial exact, wrap
+the model for RCCL gradient all-reduce, accumulate gradients over micro-steps.
 
 The reference's multi-GPU path is single-process nn.DataParallel (processor.py:32-33): it scatters the
 batch dimension — sliding windows (WindowSegment, utils/segment_generator.py:109-154) or overlapping
-time chunks (BufferSegment, segment_generator.py:18-106) of ONE trial — over the GPUs and reduces the
-gradients onto cuda:0.  Here every GPU is its own process (torch.distributed, backend "nccl" = RCCL
-over xGMI); each rank takes a contiguous slice of the windows/chunks (no data-path collective), and
-DistributedDataParallel all-reduces the fp32 gradients in buckets overlapped with backward.
-BatchNorm statistics stay per replica, exactly like the reference's DataParallel replicas.
+time chunks (BufferSegment, segment_generator.py:18-106) of ONE trial — over the GPUs, gathers the
+predictions onto cuda:0 for the loss, and reduces the gradients there.  Here every GPU is its own
+process (torch.distributed, backend "nccl" = RCCL over xGMI); each rank takes a contiguous slice of the
+windows/chunks, computes its share of the trial's loss (``SegmentShard``: the one cross-shard term is
+the temporal MSE pair at the shard boundary, which needs the previous rank's last prediction row — an
+all-gather of C floats per rank), and DistributedDataParallel all-reduces the fp32 gradients in buckets
+overlapped with backward.  BatchNorm statistics stay per replica, exactly like the reference's
+DataParallel replicas.  Gradient accumulation over trials (processor.py:531-564: ``loss /= batch_size``,
+optimizer step every ``batch_size`` trials) skips the all-reduce on all but the last micro-step
+(``accumulate``).
 """
 from __future__ import annotations
+
+import contextlib
+from dataclasses import dataclass
+from typing import Optional
 
 import torch
 
@@ -20,14 +30,9 @@ def rank_slice(n_units: int, world: int, rank: int):
     return start, start + base + (1 if rank < extra else 0)
 
 
-def window_starts(L: int, W: int):
-    """WindowSegment: the trial is left-padded by W-1 zero frames (segment_generator.py:116-122) and
-    every output frame t is predicted from the window [t, t+W) of the padded trial (:143)."""
-    return torch.arange(L)
-
-
 def windows_for_rank(trial: torch.Tensor, W: int, world: int, rank: int) -> torch.Tensor:
-    """trial (1, C, L, V) on the device -> this rank's windows (n, C, W, V) (segment_generator.py:132-145)."""
+    """trial (1, C, L, V) -> this rank's windows (n, C, W, V) (segment_generator.py:116-122,132-145): the
+    trial is left-padded by W-1 zero frames and output frame t is predicted from padded frames [t, t+W)."""
     _, C, L, V = trial.shape
     s, e = rank_slice(L, world, rank)
     padded = torch.nn.functional.pad(trial, (0, 0, W - 1, 0))
@@ -55,8 +60,62 @@ def chunks_for_rank(L: int, chunk: int, overlap: int, world: int, rank: int):
     return b[s:e]
 
 
+@dataclass
+class SegmentShard:
+    """What one rank needs to compute its exact share of a trial's loss (loss.Loss(..., shard=)).
+
+    prev: (C,) predictions of the frame right before this shard (the detached left operand of the
+          boundary MSE pair, loss.py:36-39), None for the shard that starts the series;
+    den:  the trial's CE weight sum  sum_w wt[y_w]  (device scalar) — every rank holds the trial's labels;
+    pairs: the trial's number of MSE pairs (L - 1);
+    rank_first: this shard holds frame 0 (only it applies the subsegment's ``i > 0`` frame drop)."""
+    prev: Optional[torch.Tensor]
+    den: torch.Tensor
+    pairs: int
+    rank_first: bool
+
+    @staticmethod
+    def local(pred_full, labels_full, weight, start, end, L, rank):
+        """Shard [start, end) of a series whose predictions are all in this process (tests, single GPU)."""
+        prev = pred_full[0, :, start - 1].detach() if start > 0 else None
+        den = weight[labels_full.reshape(-1).to(weight.device)].sum()
+        return SegmentShard(prev, den, L - 1, start == 0)
+
+
+def exchange_shard(pred_local, labels_full, weight, start, L, group=None):
+    """Build this rank's SegmentShard in a process group: all-gather every rank's last prediction row
+    (C floats each) so rank r gets the row right before its first frame.
+    pred_local: (1, C, n) this rank's predictions (n may be 0); labels_full: the whole series' labels."""
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    C = pred_local.shape[1]
+    last = pred_local[0, :, -1].detach().float() if pred_local.shape[2] > 0 else \
+        torch.zeros((C,), device=pred_local.device)
+    rows = [torch.empty_like(last) for _ in range(world)]
+    dist.all_gather(rows, last.contiguous(), group=group)
+    # rank_slice gives shards that differ by at most one unit, so only trailing shards can be empty and
+    # the shard before a non-empty rank r > 0 is rank r - 1
+    prev = rows[rank - 1] if start > 0 else None
+    den = weight[labels_full.reshape(-1).to(weight.device)].sum()
+    return SegmentShard(prev, den, L - 1, start == 0)
+
+
 def ddp(model: torch.nn.Module, device: torch.device, bucket_cap_mb: int = 16):
     """DistributedDataParallel over the initialised process group (RCCL on the GPU box, gloo in tests)."""
     from torch.nn.parallel import DistributedDataParallel as DDP
     ids = [device.index] if device.type == "cuda" else None
     return DDP(model, device_ids=ids, bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True)
+
+
+@contextlib.contextmanager
+def accumulate(model, last: bool):
+    """Micro-step context for gradient accumulation (processor.py:531-564): under DDP the bucketed
+    all-reduce runs only on the ``last`` micro-step of an optimizer step (DDP.no_sync on the others);
+    a plain module accumulates locally either way."""
+    if not last and hasattr(model, "no_sync"):
+        with model.no_sync():
+            yield
+    else:
+        yield

@@ -119,7 +119,30 @@ class OnlineLayer(nn.Module):
 
     def eval_(self):
         self.aggregate.A *= self.edge_importance
+        self._packed = None
         return
+
+    def _weights(self, Cin):
+        """Per-frame constants (packed GCN weight, A-pushed conv bias, packed residual weight), built once and
+        reused while the parameters are unchanged (keyed by their in-place version counters): the per-frame
+        step then launches only data-dependent kernels."""
+        A = self.aggregate.A
+        rw = self.residual[0].weight if self.is_residual_conv else None
+        key = (A.data_ptr(), A._version, self.conv.weight._version, self.conv.bias._version,
+               None if rw is None else rw._version)
+        pk = getattr(self, "_packed", None)
+        if pk is not None and pk[0] == key:
+            return pk[1]
+        P = A.shape[0]
+        Cout = self.aggregate.out_channels
+        A32 = A.detach().float().contiguous()
+        wg3 = self.conv.weight.detach().float().view(P, Cout, Cin).permute(1, 0, 2).reshape(1, Cout, P * Cin)
+        wgp, cp, kp = K.pack_weight(wg3, torch.float32)
+        bias2d = K.gcn_bias(A32, self.conv.bias.detach().float().contiguous(), 1, Cout)
+        res = K.pack_weight(rw.detach().float().view(1, Cout, Cin), torch.float32) if rw is not None else None
+        packed = (A32, wgp, cp, kp, bias2d, res)
+        self._packed = (key, packed)
+        return packed
 
     @torch.no_grad()
     def forward(self, x, A):
@@ -130,12 +153,14 @@ class OnlineLayer(nn.Module):
         Cout = self.aggregate.out_channels
         P = self.aggregate.A.shape[0]
         Cin = x.shape[1]
-        _, z, _ = LF.gcn_forward(x, self.aggregate.A.contiguous(), self.conv.weight, self.conv.bias, torch.float32)
+        A32, wgp, cp, kp, bias2d, resp = self._weights(Cin)
+        XA = K.amix_fwd(x, A32)
+        z = K.conv_rows(XA, wgp, P * Cin, Cout, cp, kp, 1, 1, bias=bias2d, bias_mode=2)
         a = self.aggregate.step(z)
         n = self.bn_relu[0]
         relu_mode = 3 if self.is_residual else 2
         if self.is_residual_conv:
-            wrp, cq, kq = K.pack_weight(self.residual[0].weight.float().view(1, Cout, Cin), torch.float32)
+            wrp, cq, kq = resp
             r = K.conv_rows(x, wrp, Cin, Cout, cq, kq, 1, 1)
         res_mode = 2 if self.is_residual_conv else (1 if self.is_residual else 0)
         res = r if self.is_residual_conv else (x if self.is_residual else None)

@@ -1,6 +1,7 @@
 """CPU-side checks (no GPU): the C-ABI library loads and exports every symbol include/stgcn_amd.h
 declares, the host-side Graph matches the reference's, modules keep the reference's API and
 state_dict layout, and the product refuses to run without the HIP device (no CPU fallback)."""
+import os
 import re
 
 import numpy as np
@@ -74,3 +75,21 @@ def test_no_cpu_fallback(pkg):
     A = torch.tensor(pkg.Graph(**pkg.PKU_MMD).A, dtype=torch.float32)
     with pytest.raises(RuntimeError, match="HIP device only"):
         layer(torch.randn(1, 8, 4, 25), A)
+
+
+def test_bench_multi_gpu_launch_rejected_cleanly_without_devices():
+    """`bench.py --gpus N` starts its own ranks only when N HIP devices are visible; here (no GPU) it
+    must refuse with a message, not a traceback; a launcher's WORLD_SIZE must agree with --gpus."""
+    import subprocess
+    import sys
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("devices present")
+    bench = os.path.join(ROOT, "bench.py")
+    r = subprocess.run([sys.executable, bench, "--gpus", "2", "--steps", "1"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode != 0 and "needs 2 HIP devices" in r.stderr and "Traceback" not in r.stderr
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, bench, "--gpus", "0", "--steps", "1"], capture_output=True, text=True,
+                       timeout=300, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr and "Traceback" not in r.stderr

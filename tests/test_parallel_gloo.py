@@ -1,6 +1,11 @@
 """Multi-rank plumbing on the CPU (gloo, world_size 2): trial sharding covers every window / chunk
-exactly once, and the DDP wrapper's gradient all-reduce equals the single-process gradient of the
-union batch (the data-parallel semantics the RCCL path uses on the GPU box)."""
+exactly once, the DDP wrapper's gradient all-reduce equals the single-process gradient of the union
+batch, and the ST-GCN training step of a sharded trial — windows_for_rank -> model -> exchange_shard ->
+per-rank loss share -> DDP all-reduce, with no_sync accumulation over two trials — reproduces the
+single-process gradient of the reference loss over the whole trials (processor.py:531-564,
+utils/loss.py:25-41).  The network here is the oracle's ST-GCN (LayerNorm config, per-frame statistics,
+so sharding cannot change it) with the package Model's parameters: the HIP kernels need a GPU, and this
+test is about the data-parallel path around them (parity of the kernels is the -m gpu suite's)."""
 import os
 import socket
 
@@ -91,3 +96,99 @@ def test_ddp_allreduce_matches_single_process(pkg):
     model(x).pow(2).sum().backward()
     for g, p in zip(got, model.parameters()):
         assert torch.allclose(torch.tensor(g), p.grad, atol=1e-5)
+
+
+LN_ARCH = {"strategy": "spatial", "in_feat": 3, "normalization": "LayerNorm", "num_classes": 52,
+           "output_type": "logits",
+           "st-gcn": {"in_feat": 3, "layers": 2, "kernel": 9, "importance": True, "in_ch": [8, 8],
+                      "out_ch": [8, 16], "stride": [1, 2], "residual": [1, 1], "dropout": [0, 0]}}
+
+
+class _OracleNet(torch.nn.Module):
+    """The oracle ST-GCN as an nn.Module over the package Model's parameters (so DDP can wrap it)."""
+
+    def __init__(self, pkg, O):
+        super().__init__()
+        torch.manual_seed(3)
+        m = pkg.MODELS["st-gcn"](rank=None, **dict(LN_ARCH, graph=pkg.PKU_MMD))
+        sd = m.state_dict()
+        g = torch.Generator().manual_seed(4)
+        for k, v in sd.items():
+            if k.startswith("edge_importance"):
+                sd[k] = v + 0.1 * torch.randn(v.shape, generator=g)
+        self.names = list(sd)
+        self.A = sd.pop("A")
+        self.p = torch.nn.ParameterList([torch.nn.Parameter(sd[k].double()) for k in self.names if k != "A"])
+        self.O = O
+        self.arch = dict(LN_ARCH, graph=pkg.PKU_MMD)
+
+    def forward(self, x):
+        sd = dict(zip([k for k in self.names if k != "A"], self.p))
+        sd["A"] = self.A.double()
+        return self.O.stgcn_model(x, sd, self.arch)
+
+
+def _trials():
+    g = torch.Generator().manual_seed(9)
+    out = []
+    for L in (13, 10):  # unequal-length trials (README.md:139-145)
+        out.append((torch.randn(1, 3, L, 25, generator=g, dtype=torch.float64), torch.randint(0, 52, (1, L), generator=g)))
+    return out
+
+
+W_WIN = 12
+CLASS_DIST = torch.arange(1, 53, dtype=torch.float64)
+
+
+def _model_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as ge
+    from oracle import stgcn_oracle as O
+    pkg = ge.load_package()
+    par = pkg.parallel
+    net = _OracleNet(pkg, O)
+    m = par.ddp(net, torch.device("cpu"))
+    w = 1 - CLASS_DIST / CLASS_DIST.sum()
+    trials = _trials()
+    for k, (trial, labels) in enumerate(trials):
+        L = trial.shape[2]
+        s, e = par.rank_slice(L, world, rank)
+        with par.accumulate(m, last=k == len(trials) - 1):
+            x = par.windows_for_rank(trial, W_WIN, world, rank)
+            pred = m(x).permute(2, 1, 0)                       # (1, 52, n): WindowSegment.mask_segment
+            shard = par.exchange_shard(pred, labels, w, s, L)
+            ce, mse = O.loss_shard(0, pred, labels[:, s:e], CLASS_DIST, shard.prev, shard.den, shard.pairs,
+                                   shard.rank_first)
+            # DDP averages over ranks: scale the share by world; processor.py:538-541 divides by batch_size
+            ((ce + mse) * world / len(trials)).backward()
+    if rank == 0:
+        out.put([p.grad.tolist() for p in net.p])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_stgcn_step_matches_single_process(pkg):
+    from oracle import stgcn_oracle as O
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_model_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    net = _OracleNet(pkg, O)
+    trials = _trials()
+    for trial, labels in trials:
+        x = pkg.parallel.windows_for_rank(trial, W_WIN, 1, 0)
+        ce, mse = O.loss(0, net(x).permute(2, 1, 0), labels, CLASS_DIST)
+        ((ce + mse) / len(trials)).backward()
+    for g, p in zip(got, net.p):
+        g = torch.tensor(g, dtype=torch.float64)
+        assert torch.allclose(g, p.grad, rtol=1e-7, atol=1e-10), (g - p.grad).abs().max()  # fp64 sum order
