@@ -84,6 +84,74 @@ ROOF_TAGS = {"tcn_fwd_c128": 2.0 * N_BATCH * (T_LEN // 2) * V_J * 128 * 128 * 9,
              "tcn_fwd_c256": 2.0 * N_BATCH * (T_LEN // 4) * V_J * 256 * 256 * 9}
 
 
+# north_star layer: StgcnLayer 64 -> 64, stride 1, Kt=9, BN, identity residual at N=64 T=300 V=25.
+# Algorithmic forward work: 2NTV*Cin*P*Cout (gcn) + 2NP*Cout*T*V^2 (A-mix, dense as the
+# reference counts it) + 2NTV*Cout^2*Kt (tcn) = 51.79 GFLOP.
+LAYER_FWD_FLOP = (2.0 * N_BATCH * T_LEN * V_J * 64 * 3 * 64 + 2.0 * N_BATCH * 3 * 64 * T_LEN * V_J * V_J
+                  + 2.0 * N_BATCH * T_LEN * V_J * 64 * 64 * 9)
+
+
+def layer_roofline(pkg, dev, reps=20):
+    """Layer-level roofline of the north_star layer's forward: the fused path (inference: pass 1 graph-conv
+    statistics, the fused graph conv + BN1 + ReLU + temporal conv kernel, BN2 + residual + ReLU) against the
+    unfused training-path forward of the same layer, both timed with HIP events around every launch of the
+    layer on the launch stream; plus the fused kernel's own launch time (events around that launch)."""
+    K = pkg.native
+    torch.manual_seed(0)
+    A = torch.tensor(pkg.Graph(**pkg.PKU_MMD).A, dtype=torch.float32, device=dev)
+    layer = pkg.StgcnLayer(64, 64, (9, V_J), A.shape[0], V_J, stride=1, normalization="BatchNorm").to(dev)
+    pkg.set_compute_dtype(layer, "bf16")
+    x = torch.randn(N_BATCH, 64, T_LEN, V_J, device=dev).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    kev = []
+
+    def hook(tag, phase):
+        if tag == "layer_fused":
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(torch.cuda.current_stream())
+            kev.append(ev)
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(torch.cuda.current_stream())
+        for _ in range(reps):
+            fn()
+        e1.record(torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    orig = K.layer_fused
+
+    def tagged(*a, **k):
+        k["tag"] = "layer_fused"
+        return orig(*a, **k)
+
+    K.layer_fused = tagged
+    prev_hook = K.EVENT_HOOK
+    K.EVENT_HOOK = hook
+    try:
+        with torch.no_grad():
+            fused_ms = timed(lambda: layer(x, A))
+    finally:
+        K.layer_fused = orig
+        K.EVENT_HOOK = prev_hook
+    xg = x.detach().requires_grad_(True)  # a differentiable input: the training path's forward (unfused)
+    unfused_ms = timed(lambda: layer(xg, A))
+    pairs = [(kev[i], kev[i + 1]) for i in range(6, len(kev) - 1, 2)]  # skip the warm-up launches
+    k_ms = sum(a.elapsed_time(b) for a, b in pairs) / len(pairs) if pairs else None
+    achieved = LAYER_FWD_FLOP / (fused_ms * 1e-3) / 1e12
+    return {"layer": "StgcnLayer(64, 64, (9, 25), 3, 25, BatchNorm) forward, N=64 T=300 V=25, bf16 (north_star)",
+            "bound": "mfma", "algorithmic_gflop": round(LAYER_FWD_FLOP / 1e9, 2),
+            "fused_fwd_ms": round(fused_ms, 4), "unfused_fwd_ms": round(unfused_ms, 4),
+            "fused_kernel_ms": round(k_ms, 4) if k_ms else None,
+            "achieved": round(achieved, 2), "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4),
+            "unfused_frac": round(LAYER_FWD_FLOP / (unfused_ms * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS, 4)}
+
+
 def cpu_baseline(pkg, model_cpu_sd):
     """Oracle (CPU restatement, oracle/stgcn_oracle.py) fwd+bwd on a bounded sample of the workload."""
     from oracle import stgcn_oracle as O
@@ -297,6 +365,7 @@ def main():
                     per[g] = json.load(f).get("hbm_bytes_per_launch")
         if kt and all(per.get(g) for g, _ in kt):
             traffic = sum(per[g] for g, _ in kt) / len(kt)
+        lroof = layer_roofline(pkg, dev) if world == 1 else None
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(pkg, cpu_sd)
@@ -317,6 +386,7 @@ def main():
                          "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4) if achieved else None,
                          "traffic": traffic, "avg_launch_ms": round(k_ms, 4), "launches_timed": len(kt)},
+            "layer_roofline": lroof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

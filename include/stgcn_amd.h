@@ -149,6 +149,7 @@ int stgcn_gconv(const stgcn_gconv_desc* d, int dtype, void* stream);
  * Cout = conv Cin) W'[ci][p*Cout+co] = W[p*Cout+co][ci].  A: [P][V][V] fp32 (A * edge importance),
  * P <= 3, 16 < V <= 32; Cin % 32 == 0, Cout % 64 == 0.  dmax is unused (kept for ABI stability).
  * Optional BN partial statistics [stgcn_gcn_tile_row_blocks(NT, V, Cout)][Cout_pad] as stgcn_conv_rows.
+ * out = NULL: statistics only (pass 1 of stgcn_layer_fused_fwd; no output stores).
  * Replaces: conv1x1 + einsum of ConvTemporalGraphical.forward (tgcn.py:71-79) and its input grad. */
 typedef struct {
   const void* in;
@@ -304,6 +305,35 @@ int stgcn_seg_loss(const float* p, int ldp, const long* labels, const float* wt,
  * the two loss terms given the upstream gradients, without a host round trip. */
 int stgcn_seg_loss_bwd(const float* dce, const float* dmse, const float* gce, const float* gmse, long n, float* dp,
                        void* stream);
+
+/* The fused ST-GCN layer forward (layer_fused.hip; BASELINE north_star): per tile of 16 frames, the
+ * graph conv (as stgcn_gcn_tile forward) of the tile and its 4-frame temporal halo is recomputed on the
+ * matrix cores into LDS, normalised h = relu(g * n1_scale + n1_shift) (BN1 folded; the conv bias pushed
+ * through A, gbias [V][64], is added first), and the Kt = 9 temporal conv (+ tbias) runs on h from LDS:
+ *   z[(n,t,w)][co] = tbias[co] + sum_{dt<9, ci} W[dt][co][ci] h[(n, t+dt-4, w)][ci]   (h = 0 outside [0,T))
+ * g never reaches HBM.  BatchNorm statistics of g come from pass 1 (stgcn_gcn_tile with out = NULL +
+ * stgcn_bn_finalize); z's partials (count, mean, M2) go to stats [stgcn_layer_fused_row_blocks][64]
+ * (or NULL) for bn_finalize.  bf16; Cin = Cout = 64; stride 1; P <= 3; 16 < V <= 25.
+ * wg_frag: the stgcn_gcn_tile weight image of W'[co][p*64+ci] = W[p*64+co][ci] (Kw_pad = P*64);
+ * wt_frag: the stgcn_pack_weight_frag image of the temporal weight [9][64][64].
+ * Replaces: StgcnLayer.forward's gcn + tcn[0:3] (models/stgcn/stgcn.py:151-159,181-193) with
+ * ConvTemporalGraphical.forward (models/utils/tgcn.py:58-79). */
+typedef struct {
+  const void* x;         /* bf16 rows [N][T][V][x_ld], 64 channels */
+  void* z;               /* bf16 rows [N][T][V][z_ld] */
+  const void* wg_frag;
+  const float* A;        /* [P][V][V] fp32 (A * edge importance) */
+  const float* gbias;    /* [V][64] or NULL */
+  const float* n1_scale; /* [64] */
+  const float* n1_shift; /* [64] */
+  const void* wt_frag;
+  const float* tbias;    /* [64] or NULL */
+  float* stats;          /* float4 [stgcn_layer_fused_row_blocks(N, T)][64] or NULL */
+  int N, T, V, P, x_ld, z_ld;
+} stgcn_layer_fused_desc;
+
+int stgcn_layer_fused_fwd(const stgcn_layer_fused_desc* d, void* stream);
+long stgcn_layer_fused_row_blocks(int N, int T);
 
 #ifdef __cplusplus
 }

@@ -62,6 +62,11 @@ class GconvWgradDesc(ctypes.Structure):
                [("work", c_void_p), ("work_bytes", c_long), ("rowsum", c_void_p)]
 
 
+class LayerFusedDesc(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in ("x", "z", "wg_frag", "A", "gbias", "n1_scale", "n1_shift", "wt_frag", "tbias",
+                                        "stats")] + [(n, c_int) for n in ("N", "T", "V", "P", "x_ld", "z_ld")]
+
+
 class BnBwdDesc(ctypes.Structure):
     _fields_ = [(n, c_void_p) for n in ("dy", "mref", "x1", "x2", "msc", "msh", "mean_rstd1", "mean_rstd2",
                                         "gamma1", "gamma2", "sums", "out1", "out2", "osum", "work")] + \
@@ -132,6 +137,8 @@ _SIGS = {
                                   c_int, c_void_p]),
     "stgcn_attn_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "stgcn_layer_fused_fwd": (c_int, [ctypes.POINTER(LayerFusedDesc), c_void_p]),
+    "stgcn_layer_fused_row_blocks": (ctypes.c_long, [c_int, c_int]),
     "stgcn_seg_loss_workspace": (ctypes.c_long, [c_int]),
     "stgcn_seg_loss": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                                c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

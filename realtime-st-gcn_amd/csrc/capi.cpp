@@ -83,6 +83,8 @@ int attn_scores_launch(const void* th, const void* ph, int ld, int N, int T_, in
 long attn_scores_workspace(int N, int T_, int V, int P);
 int attn_bwd_launch(const void* th, const void* ph, int ld, int N, int T_, int V, int P, int ce, const float* C,
                     const float* dC, float* dS, void* dth, void* dph, int dtype, hipStream_t s);
+int layer_fused_launch(const stgcn_layer_fused_desc& a, hipStream_t s);
+long layer_fused_row_blocks(int N, int T);
 long seg_loss_workspace_launch(int L);
 int seg_loss_launch(const float* p, int ldp, const long* labels, const float* wt, const float* prev, int L, int C,
                     int first, int mode, const float* den, float pairs, float* dce, float* dmse, int* top5, float* work,
@@ -113,7 +115,8 @@ int stgcn_conv_rows(const stgcn_conv_desc* d, int dtype, void* stream) {
 int stgcn_conv_rows_col_tile(int cout) { return conv_rows_bn_tile(cout); }
 int stgcn_gcn_tile(const stgcn_gcn_tile_desc* d, int dtype, void* stream) {
   if (dtype != 1) return STGCN_EDTYPE;
-  if (!d || !d->in || !d->out || !d->w_frag || !d->A) return STGCN_EBADSHAPE;
+  if (!d || !d->in || !d->w_frag || !d->A) return STGCN_EBADSHAPE;
+  if (!d->out && (!d->stats || d->accumulate)) return STGCN_EBADSHAPE;  /* out = NULL: statistics only */
   if (d->in_ld < d->Cin || d->out_ld < d->Cout) return STGCN_EBADSHAPE;
   return gcn_tile_launch(*d, STREAM(stream));
 }
@@ -331,6 +334,12 @@ int stgcn_attn_bwd(const void* th, const void* ph, int ld, int N, int T, int V, 
   if (!th || !ph || !C || !dC || !dS || !dth || !dph || ld < P * ce) return STGCN_EBADSHAPE;
   return attn_bwd_launch(th, ph, ld, N, T, V, P, ce, C, dC, dS, dth, dph, dtype, STREAM(stream));
 }
+
+int stgcn_layer_fused_fwd(const stgcn_layer_fused_desc* d, void* stream) {
+  if (!d) return STGCN_EBADSHAPE;
+  return layer_fused_launch(*d, STREAM(stream));
+}
+long stgcn_layer_fused_row_blocks(int N, int T) { return layer_fused_row_blocks(N, T); }
 
 long stgcn_seg_loss_workspace(int L) { return seg_loss_workspace_launch(L); }
 int stgcn_seg_loss(const float* p, int ldp, const long* labels, const float* wt, const float* prev, int L, int C,

@@ -203,6 +203,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gcn_mfma_kernel(const stgcn_gcn_ti
 #pragma unroll
   for (int t = 0; t < TN; ++t) acc[t] = zero;
   bf16* __restrict__ out = reinterpret_cast<bf16*>(a.out);
+  const bool has_out = out != nullptr;
   const bool stats = a.stats != nullptr, accum = a.accumulate != 0;
   const char* const wl = sW + lane * 16;
   float sink = 0.f;
@@ -268,7 +269,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gcn_mfma_kernel(const stgcn_gcn_ti
         static_assert(2 * (D - 2) + ST * CNT <= 63, "vmcnt range");
         if (pi + D < NP) {
           issue(pi + D);
-          if (k >= CNT)
+          if (k >= CNT && has_out)  // stats-only launches issue no stores: the DMA-only count below
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (D - 2) + ST * CNT) : "memory");
           else
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (D - 2)) : "memory");
@@ -298,8 +299,8 @@ __global__ __launch_bounds__(NW * 64, 1) void gcn_mfma_kernel(const stgcn_gcn_ti
       });
       if constexpr (cb == G - 1) {
         // ---- frame cf done: out[(cf, joint lr)][n0 + 32t + 8q + 4lh + e]
-        if (jok) {
-          bf16* orow = out + ((long)cf * V + lr) * a.out_ld + n0 + 4 * lh;
+        if (jok) {  // out == NULL: statistics only (pass 1 of the fused layer, layer_fused.hip)
+          bf16* orow = out ? out + ((long)cf * V + lr) * a.out_ld + n0 + 4 * lh : nullptr;
 #pragma unroll
           for (int t = 0; t < TN; ++t)
 #pragma unroll
@@ -308,7 +309,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gcn_mfma_kernel(const stgcn_gcn_ti
 #pragma unroll
               for (int e = 0; e < 4; ++e) v[e] = acc[t][4 * q + e] + breg[t][4 * q + e];
               uint2* po = reinterpret_cast<uint2*>(orow + 32 * t + 8 * q);
-              if (accum) {
+              if (accum && orow) {
                 const bf16x4 o = __builtin_bit_cast(bf16x4, *po);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) v[e] += (float)o[e];
@@ -318,7 +319,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gcn_mfma_kernel(const stgcn_gcn_ti
               for (int e = 0; e < 4; ++e) st[e] = (bf16)v[e];
               if constexpr (DBG & 2) {
                 sink += (float)st[0] + (float)st[1] + (float)st[2] + (float)st[3];
-              } else {
+              } else if (orow) {
                 *po = __builtin_bit_cast(uint2, st);
               }
               if (stats) {

@@ -144,8 +144,12 @@ class StgcnLayer(nn.Module):
             wr, br, nrw, nrb = rc.weight, rc.bias, rn.weight, rn.bias
         else:
             wr = br = nrw = nrb = None
+        # inference (no autograd graph will be built): the layer may run the fused forward kernel, which
+        # keeps nothing for a backward
+        infer = not torch.is_grad_enabled() or not (
+            x.requires_grad or A.requires_grad or any(p.requires_grad for p in self.parameters()))
         cfg = (self.kernel_size[0], self.stride, self.is_residual, self.normalization, self.compute_dtype,
-               self.graph_support(A), not self._graph_bound)
+               self.graph_support(A), not self._graph_bound, infer)
         return F_.StgcnLayerFunction.apply(x, A, self.gcn.conv.weight, self.gcn.conv.bias, n1.weight, n1.bias,
                                            conv.weight, conv.bias, n2.weight, n2.bias, wr, br, nrw, nrb, cfg)
 

@@ -18,6 +18,12 @@ from . import _lib as L
 EVENT_HOOK = None
 
 
+def _dense(A: torch.Tensor) -> torch.Tensor:
+    """Adjacency as the C-ABI reads it: dense row-major fp32 (graph.py's A is a transposed numpy view, and
+    torch.tensor keeps those strides)."""
+    return A if (A.dtype == torch.float32 and A.is_contiguous()) else A.float().contiguous()
+
+
 def rows_ld(t: torch.Tensor) -> int:
     """Row stride (elements) of a logical (N,C,T,V) activation stored channels-last."""
     if t.dim() != 4 or (t.stride(1) != 1 and t.shape[1] > 1):
@@ -158,7 +164,9 @@ def conv_wgrad(x, dy, Cin, Cout, T_in, T_out, Kt=1, stride=1, pad=0, pro=0, pro_
 
 
 def _amix_desc(x, out, A, N, T, V, P, Cin, accumulate=False, x_ld=None, out_ld=None):
+    A = _dense(A)
     d = L.AmixDesc()
+    d._keep = A  # a dense copy must outlive the descriptor's launch
     d.x, d.out, d.A = x.data_ptr(), L.ptr(out), A.data_ptr()
     d.N, d.T, d.V, d.P, d.Cin = N, T, V, P, Cin
     d.per_sample = int(A.dim() == 4)
@@ -219,6 +227,7 @@ def amix_dA(x, dw, A):
 
 def gcn_bias_bwd(A, b, S, dA, C):
     """Shared A: dA += bias-through-A term (in place), returns db [P*C] (stgcn_gcn_bias_bwd)."""
+    A = _dense(A)
     P, V = A.shape[0], A.shape[-1]
     db = torch.empty(P * C, dtype=torch.float32, device=A.device)
     L.check(L.lib().stgcn_gcn_bias_bwd(A.data_ptr(), b.data_ptr(), S.data_ptr(), P, V, C, dA.data_ptr(),
@@ -228,6 +237,7 @@ def gcn_bias_bwd(A, b, S, dA, C):
 
 def gcn_bias(A, b, N, C):
     """bias2d [V, C] (shared A) or [N, V, C] (per-sample A) = sum_p b_p * colsum(A_p)."""
+    A = _dense(A)
     P, V = A.shape[-3], A.shape[-1]
     per = A.dim() == 4
     out = torch.empty(((N,) if per else ()) + (V, C), dtype=torch.float32, device=A.device)
@@ -274,6 +284,7 @@ class GraphSupport:
 
 def gconv_weights(A, W, sup, Cout, Cin, trans, dtype):
     """Effective weights [V][J][R_pad][C_pad]: trans 0 -> (Cout, Cin) from S lists, 1 -> (Cin, Cout) from R lists."""
+    A = _dense(A)
     P, V = A.shape[0], A.shape[-1]
     R, C = (Cin, Cout) if trans else (Cout, Cin)
     rp = -(-R // col_tile(R)) * col_tile(R)
@@ -347,21 +358,62 @@ def pack_gcn_weight(w2: torch.Tensor, dtype) -> tuple:
 
 
 def gcn_tile(x, A, wimg, kw_pad, Cin, Cout, cp, sup, trans_a=False, bias=None, stats=None, out=None,
-             accumulate=False):
-    """Fused graph conv (stgcn_gcn_tile): out rows (N, Cout, T, V) (+)= W' . A-mix(x) (+ bias[w][co])."""
+             accumulate=False, stats_only=False):
+    """Fused graph conv (stgcn_gcn_tile): out rows (N, Cout, T, V) (+)= W' . A-mix(x) (+ bias[w][co]).
+    stats_only: no output, BN partial statistics only (pass 1 of the fused layer); returns None."""
     N, _, T, V = x.shape
-    if out is None:
+    if out is None and not stats_only:
         out = cl_empty(N, Cout, T, V, x.dtype, x.device)
+    A = _dense(A)
     d = L.GcnTileDesc()
-    d.in_, d.out, d.w_frag, d.A = x.data_ptr(), out.data_ptr(), wimg.data_ptr(), A.data_ptr()
+    d.in_, d.out, d.w_frag, d.A = x.data_ptr(), L.ptr(out), wimg.data_ptr(), A.data_ptr()
     d.bias, d.stats = L.ptr(bias), L.ptr(stats)
     d.NT, d.V, d.P, d.Cin, d.Cout, d.Cout_pad, d.Kw_pad = N * T, V, A.shape[0], Cin, Cout, cp, kw_pad
-    d.in_ld, d.out_ld, d.trans_a, d.accumulate = rows_ld(x), rows_ld(out), int(trans_a), int(accumulate)
+    d.in_ld, d.out_ld = rows_ld(x), (rows_ld(out) if out is not None else Cout)
+    d.trans_a, d.accumulate = int(trans_a), int(accumulate)
     dm = sup.dmax_bwd if trans_a else sup.dmax_fwd
     for i, v in enumerate(dm[:4]):
         d.dmax[i] = v
+    if d.out is None and not (out is None and stats_only and stats is not None):
+        raise RuntimeError("stgcn_amd: gcn_tile needs an output or stats_only with a stats buffer")
     L.check(L.lib().stgcn_gcn_tile(d, L.dtype_code(x.dtype), L.stream()), "gcn_tile")
     return out
+
+
+_FUSED = os.environ.get("STGCN_FUSED", "1")
+
+
+def layer_fused_ok(sup, P, Cin, Cout, V, kt, stride, dtype) -> bool:
+    """Whether a layer's forward can run as the fused graph conv + BN1 + ReLU + temporal conv kernel
+    (layer_fused.hip): bf16, 64 -> 64 channels, stride 1, Kt = 9, a batch-shared graph, 16 < V <= 25.
+    STGCN_FUSED=0 disables it (A/B)."""
+    return (_FUSED != "0" and dtype == torch.bfloat16 and sup is not None and P <= 3 and 16 < V <= 25
+            and Cin == 64 and Cout == 64 and kt == 9 and stride == 1)
+
+
+def layer_fused_row_blocks(N: int, T: int) -> int:
+    return L.lib().stgcn_layer_fused_row_blocks(N, T)
+
+
+def layer_fused(x, A, wimg, gbias, n1_scale, n1_shift, wt_packed, tbias, stats=None, tag=None):
+    """stgcn_layer_fused_fwd: z rows (N, 64, T, V) = tcn(relu(BN1(gcn(x)))) + tbias, g kept on chip."""
+    N, C, T, V = x.shape
+    if getattr(wt_packed, "frag_stride", None) != 1:
+        raise RuntimeError("stgcn_amd: layer_fused needs the stride-1 fragment image of the temporal weight")
+    z = cl_empty(N, C, T, V, x.dtype, x.device)
+    A = _dense(A)
+    d = L.LayerFusedDesc()
+    d.x, d.z, d.wg_frag, d.A = x.data_ptr(), z.data_ptr(), wimg.data_ptr(), A.data_ptr()
+    d.gbias, d.n1_scale, d.n1_shift = L.ptr(gbias), n1_scale.data_ptr(), n1_shift.data_ptr()
+    d.wt_frag, d.tbias, d.stats = wt_packed.frag_ptr, L.ptr(tbias), L.ptr(stats)
+    d.N, d.T, d.V, d.P, d.x_ld, d.z_ld = N, T, V, A.shape[0], rows_ld(x), rows_ld(z)
+    hook = EVENT_HOOK if tag is not None else None
+    if hook:
+        hook(tag, "start")
+    L.check(L.lib().stgcn_layer_fused_fwd(d, L.stream()), "layer_fused")
+    if hook:
+        hook(tag, "end")
+    return z
 
 
 def gconv(x, wpk, sup, Cin, Cout, trans=False, bias=None, stats=None, out=None, accumulate=False, tag=None):
@@ -412,6 +464,7 @@ def gconv_wgrad(x, dy, sup, Cin, Cout, rowsum=None):
 
 def gconv_finish(dweff, A, W, sup, Cout, Cin, dW=None, dA=None):
     """(dW [P*Cout][Cin], dA [P][V][V]) fp32 (+)= from dWeff (stgcn_gconv_wgrad_finish); zeroed if not given."""
+    A = _dense(A)
     P, V = A.shape[0], A.shape[-1]
     if dW is None:
         dW = torch.zeros((P * Cout, Cin), dtype=torch.float32, device=A.device)

@@ -1,0 +1,145 @@
+"""The fused ST-GCN layer forward (layer_fused.hip, the BASELINE north_star kernel: graph conv + BN1 + ReLU
++ temporal conv with g kept on chip, two-pass BatchNorm per SURVEY §7).
+
+* kernel level: stgcn_layer_fused_fwd through the C-ABI against torch fp32 on the same bf16-rounded
+  operands (oracle.tgcn = tgcn.py:58-79, F.conv2d = stgcn.py:154-159): z and its BN2 partial statistics,
+  at a short trial (a partial last tile, padding frames at both ends) and at the bench shape
+  (N=64 T=300: 1200 tiles, several per persistent block);
+* pass 1 (gcn_tile statistics only) against the statistics of the materialised graph conv;
+* layer / model level: StgcnLayer and the config-2 Model in inference (no autograd) — the path that
+  routes through the fused kernel — against the fp32 oracle (stgcn.py:80-97,181-193), bf16 tolerance.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import assert_close
+from oracle import stgcn_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+BF = torch.bfloat16
+
+
+@pytest.fixture(scope="module")
+def P(pkg):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return pkg
+
+
+def cl(x, dtype=torch.float32):
+    return x.to(DEV, dtype).contiguous(memory_format=torch.channels_last)
+
+
+def rb(t):
+    return t.to(BF).float()
+
+
+def _graph(P):
+    A = torch.tensor(P.Graph(**P.PKU_MMD).A, dtype=torch.float32)
+    g = torch.Generator().manual_seed(7)
+    return A * (1 + 0.1 * torch.randn(A.shape, generator=g))  # edge importance applied
+
+
+@pytest.mark.parametrize("N,T", [(2, 37), (64, 300)])
+def test_layer_fused_kernel(P, N, T):
+    K = P.native
+    torch.manual_seed(N + T)
+    V, C = 25, 64
+    A = _graph(P)
+    Pp = A.shape[0]
+    x = rb(torch.randn(N, C, T, V))
+    wg = rb(torch.randn(Pp * C, C, 1, 1) / C ** 0.5)
+    bg = torch.randn(Pp * C) * 0.1
+    wt = rb(torch.randn(C, C, 9, 1) / (9 * C) ** 0.5)
+    bt = torch.randn(C) * 0.1
+    sc, sh = torch.rand(C) + 0.5, torch.randn(C) * 0.5
+    g = O.tgcn(x, wg, bg, A)
+    h = torch.relu(g * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1))
+    ref = F.conv2d(rb(h), wt, bt, padding=(4, 0))
+
+    A_d = A.to(DEV)
+    sup = K.GraphSupport(A_d)
+    bias2d = K.gcn_bias(A_d, bg.to(DEV), N, C)
+    wgf = wg.view(Pp, C, C).permute(1, 0, 2).reshape(C, Pp * C).to(DEV)
+    wimg, cpg, kwg = K.pack_gcn_weight(wgf, BF)
+    wtp, _, _ = K.pack_weight(wt.squeeze(-1).permute(2, 0, 1).to(DEV), BF, stride=1)
+    st = torch.zeros((K.layer_fused_row_blocks(N, T), C, 4), device=DEV)
+    z = K.layer_fused(cl(x, BF), A_d, wimg, bias2d, sc.to(DEV), sh.to(DEV), wtp, bt.to(DEV), stats=st)
+    assert_close(z.float(), ref, 2e-2, "fused z")
+    mr, _, _ = K.bn_finalize(st, st.shape[0], C, C, None, None)
+    zf = z.float().cpu()  # statistics are of the fp32 values before the bf16 store
+    assert_close(mr[:, 0].cpu(), ref.mean(dim=(0, 2, 3)), 2e-2, "bn2 mean")
+    assert_close(mr[:, 1].cpu(), 1 / torch.sqrt(ref.var(dim=(0, 2, 3), unbiased=False) + 1e-5), 1e-2, "bn2 rstd")
+    del zf
+
+    # pass 1: statistics of g without storing it
+    rb1 = K.gcn_tile_row_blocks(N * T, V, C)
+    st1 = torch.zeros((rb1, cpg, 4), device=DEV)
+    assert K.gcn_tile(cl(x, BF), A_d, wimg, kwg, C, C, cpg, sup, bias=bias2d, stats=st1, stats_only=True) is None
+    m1, _, _ = K.bn_finalize(st1, rb1, cpg, C, None, None)
+    assert_close(m1[:, 0].cpu(), g.mean(dim=(0, 2, 3)), 2e-2, "bn1 mean")
+    assert_close(m1[:, 1].cpu(), 1 / torch.sqrt(g.var(dim=(0, 2, 3), unbiased=False) + 1e-5), 1e-2, "bn1 rstd")
+
+
+def _count_fused(P, monkeypatch):
+    calls = []
+    orig = P.native.layer_fused
+
+    def spy(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+
+    monkeypatch.setattr(P.native, "layer_fused", spy)
+    return calls
+
+
+@pytest.mark.parametrize("residual", [True, False])
+def test_stgcn_layer_inference_fused(P, monkeypatch, residual):
+    """StgcnLayer (BN, 64 -> 64, stride 1) under no_grad takes the fused kernel; vs the fp32 oracle."""
+    calls = _count_fused(P, monkeypatch)
+    torch.manual_seed(3)
+    N, T, V = 8, 100, 25
+    A = _graph(P)
+    layer = P.StgcnLayer(64, 64, (9, V), 3, V, stride=1, residual=residual, normalization="BatchNorm")
+    sd = {k: v.clone() for k, v in layer.state_dict().items()}
+    g = torch.Generator().manual_seed(5)
+    for k in sd:  # non-trivial affines
+        if k.endswith("weight") and sd[k].dim() == 1:
+            sd[k] = 1 + 0.2 * torch.randn(sd[k].shape, generator=g)
+        elif k.endswith("bias"):
+            sd[k] = 0.1 * torch.randn(sd[k].shape, generator=g)
+    layer.load_state_dict(sd)
+    x = torch.randn(N, 64, T, V)
+    ref = O.stgcn_layer(x, A, sd, "", 9, 1, residual, "BatchNorm")
+    layer = layer.to(DEV)
+    P.set_compute_dtype(layer, "bf16")
+    with torch.no_grad():
+        y = layer(x.to(DEV), A.to(DEV))
+    torch.cuda.synchronize()
+    assert len(calls) == 1, "the inference forward did not take the fused kernel"
+    assert_close(y.float().cpu(), ref, 3e-2, "fused layer")
+
+
+def test_model_inference_fused_config2(P, monkeypatch):
+    """The config-2 model (9 layers, N=16 T=300) in inference: layers 0-2 run fused; logits vs the oracle."""
+    calls = _count_fused(P, monkeypatch)
+    arch = {"strategy": "spatial", "in_feat": 3, "normalization": "BatchNorm", "num_classes": 52,
+            "output_type": "logits",
+            "st-gcn": {"in_feat": 3, "layers": 9, "kernel": 9, "importance": True,
+                       "in_ch": [64, 64, 64, 64, 128, 128, 128, 256, 256],
+                       "out_ch": [64, 64, 64, 128, 128, 128, 256, 256, 256],
+                       "stride": [1, 1, 1, 2, 1, 1, 2, 1, 1], "residual": [1] * 9, "dropout": [0] * 9},
+            "graph": P.PKU_MMD}
+    torch.manual_seed(1538574472)
+    m = P.MODELS["st-gcn"](rank=None, **arch)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    x = torch.randn(16, 3, 300, 25)
+    ref = O.stgcn_model(x, sd, arch)
+    m = m.to(DEV).set_compute_dtype("bf16")
+    with torch.no_grad():
+        y = m(x.to(DEV))
+    torch.cuda.synchronize()
+    assert len(calls) == 3
+    assert_close(y.float().cpu(), ref, 3e-2, "model logits (fused inference)")
