@@ -335,6 +335,16 @@ typedef struct {
 int stgcn_layer_fused_fwd(const stgcn_layer_fused_desc* d, void* stream);
 long stgcn_layer_fused_row_blocks(int N, int T);
 
+/* Segment metrics of one trial (evaluation): labels / pred int64 [L] framewise classes (device).
+ * out fp32 [K + 1]: F1@overlap[k] (utils/metrics/f1.py:14-52; NaN when the trial has no hit, as the
+ * reference) and the segmental edit score out[K] (utils/metrics/edit.py:10-33); confusion (int64 [C][C],
+ * [predicted][label], or NULL) += the framewise counts (utils/metrics/confusion.py:10-29).  overlap: fp32
+ * [K] device, K <= 8; work: stgcn_segment_metrics_workspace(L) bytes; status (device int): 0 ok, 1 more than
+ * 8192 segments in both sequences (edit score not computed).  One wave; bit-identical to the reference. */
+long stgcn_segment_metrics_workspace(int L);
+int stgcn_segment_metrics(const long* labels, const long* pred, int L, int C, const float* overlap, int K, void* work,
+                          long long* confusion, float* out, int* status, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

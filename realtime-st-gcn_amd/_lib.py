@@ -139,6 +139,9 @@ _SIGS = {
                                c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "stgcn_layer_fused_fwd": (c_int, [ctypes.POINTER(LayerFusedDesc), c_void_p]),
     "stgcn_layer_fused_row_blocks": (ctypes.c_long, [c_int, c_int]),
+    "stgcn_segment_metrics_workspace": (ctypes.c_long, [c_int]),
+    "stgcn_segment_metrics": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_void_p]),
     "stgcn_seg_loss_workspace": (ctypes.c_long, [c_int]),
     "stgcn_seg_loss": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                                c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -85,6 +85,9 @@ int attn_bwd_launch(const void* th, const void* ph, int ld, int N, int T_, int V
                     const float* dC, float* dS, void* dth, void* dph, int dtype, hipStream_t s);
 int layer_fused_launch(const stgcn_layer_fused_desc& a, hipStream_t s);
 long layer_fused_row_blocks(int N, int T);
+long seg_metrics_workspace_launch(int L);
+int seg_metrics_launch(const long* lab, const long* pred, int L, int C, const float* ov, int K, int* ws,
+                       unsigned long long* cm, float* out, int* status, hipStream_t s);
 long seg_loss_workspace_launch(int L);
 int seg_loss_launch(const float* p, int ldp, const long* labels, const float* wt, const float* prev, int L, int C,
                     int first, int mode, const float* den, float pairs, float* dce, float* dmse, int* top5, float* work,
@@ -340,6 +343,13 @@ int stgcn_layer_fused_fwd(const stgcn_layer_fused_desc* d, void* stream) {
   return layer_fused_launch(*d, STREAM(stream));
 }
 long stgcn_layer_fused_row_blocks(int N, int T) { return layer_fused_row_blocks(N, T); }
+
+long stgcn_segment_metrics_workspace(int L) { return seg_metrics_workspace_launch(L); }
+int stgcn_segment_metrics(const long* labels, const long* pred, int L, int C, const float* overlap, int K, void* work,
+                          long long* confusion, float* out, int* status, void* stream) {
+  return seg_metrics_launch(labels, pred, L, C, overlap, K, (int*)work, (unsigned long long*)confusion, out, status,
+                            STREAM(stream));
+}
 
 long stgcn_seg_loss_workspace(int L) { return seg_loss_workspace_launch(L); }
 int stgcn_seg_loss(const float* p, int ldp, const long* labels, const float* wt, const float* prev, int L, int C,

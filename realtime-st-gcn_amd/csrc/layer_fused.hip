@@ -1,49 +1,56 @@
 // The fused ST-GCN layer forward (BASELINE north_star): ConvTemporalGraphical (tgcn.py:58-79) -> BN1 ->
 // ReLU -> temporal Conv2d (Kt = 9) + bias (stgcn.py:151-159) in ONE kernel, with the graph-conv output
 // g and its normalised form h = relu(BN1(g)) living only in LDS.  The second BatchNorm's batch
-// statistics are emitted as per-tile partials (the consumer folds BN2 + residual + ReLU, stgcn.py:160,193).
+// statistics are emitted as per-block partials (the consumer folds BN2 + residual + ReLU, stgcn.py:160,193).
 //
 // BatchNorm needs global statistics of g before the temporal conv can consume h, so the layer is the
 // two-pass form of SURVEY §7: pass 1 = the fused graph conv with statistics only (gcn_tile.hip, no output
 // stores), bn_finalize -> BN1 scale/shift; pass 2 = this kernel, which RECOMPUTES the graph conv of its
-// tile (plus the temporal halo) on the matrix cores instead of reading g back from HBM.
+// frames on the matrix cores instead of reading g back from HBM.
 //
 // Shapes: bf16, Cin = Cout = 64, stride 1, Kt = 9 (pad 4), P <= 3 partitions, 16 < V <= 25 — the
 // north_star layer (N = 64, C = 64, T = 300, V = 25) and config 2's layers 0-2.
 //
-// Block = 4 waves, persistent over contiguous runs of tiles; tile = CF = 16 output frames of one sample.
-//   phase 1 (graph conv, per frame; gcn_tile.hip's two chained MFMA products): the HF = 24 frames
-//     [f0 - 4, f0 + 20) are split over the waves (6 each).  A frame's x rows arrive as two 32-channel
-//     panels [32 joint rows][32 ch] by global->LDS DMA into a per-wave ring (DP panels in flight); stage 1
+// Block = 8 waves, one contiguous run of output frames of one sample (a quarter of a sample at N = 64:
+// 256 blocks), walked in steps of CF = 8 frames.  Two roles run concurrently, one wave of each per SIMD,
+// so one role's MFMAs fill the other's latency gaps:
+//   GCN waves 4-7 (producers): per step, the 8 h frames the NEXT step needs.  A frame's x rows arrive as
+//     two 32-channel panels [32 joint rows][32 ch] by global->LDS DMA (issued one step ahead); stage 1
 //     mixes the joints (X^T A_p on MFMA, X^T by transposing LDS reads, A_p in registers), stage 2 runs the
-//     1x1 conv from the stage-1 accumulators (W' in LDS).  Epilogue: h = relu(g * s1 + (bias2d * s1 + b1))
-//     (BN1 folded; s1/b1 from pass 1) -> bf16 -> LDS rows [frame][joint][64 ch] (144-B rows).  Frames
-//     outside [0, T) are written as zeros: the temporal conv's zero padding applies to h.
-//   phase 2 (temporal conv): out^T[co][row] = sum_{dt,ci} W[dt][co][ci] h[row + dt*V][ci] over the tile's
-//     CF*V rows (flattened (frame, joint) rows: tap dt is a row offset of dt*V), 32x32x16 MFMAs with the
-//     weight fragments streamed from L2 (conv_wide.hip's fragment image) through a register ring and the
-//     h fragments read from LDS.  Wave = (32-channel half, row half: 7 row tiles of 32).  Epilogue: + bias,
-//     8-B stores of 4 consecutive channels per lane, BN2 (count, mean, M2) partials per (tile, channel).
+//     1x1 conv from the stage-1 accumulators (W' in LDS) — gcn_tile.hip's two chained products.  Epilogue:
+//     h = relu(g * s1 + (bias2d * s1 + b1)) (BN1 folded) -> bf16 -> the h ring.  Frames outside [0, T) are
+//     written as zeros (the temporal conv's zero padding applies to h).
+//   TCN waves 0-3 (consumers): out^T[co][row] = sum_{dt,ci} W[dt][co][ci] h[frame + dt - 4][row's joint][ci]
+//     over the step's 8*V rows, 32x32x16 MFMAs with the weight fragments streamed from L2 (conv_wide.hip's
+//     fragment image) through a register ring and the h fragments read from LDS.  Wave = (32 output
+//     channels, 4 row tiles of 32).  Epilogue: + bias, 8-B stores of 4 consecutive channels per lane; BN2
+//     (sum, sum of squares) kept in registers over the run and written once as (count, mean, M2) partials.
+// The h ring holds RF = 24 frames (a frame at slot a % RF): 16 being read for step s (frames 8s-4 ..
+// 8s+11 of the run) and 8 being written for step s+1; one block barrier per step hands them over.
 #include "common.h"
 #include "../../include/stgcn_amd.h"
+#include <stdlib.h>
 #include <utility>
 
 namespace {
 
-constexpr int NW = 4;
+constexpr int NWT = 4, NWG = 4, NW = NWT + NWG;
 constexpr int C = 64, G = C / 32;      // channels (in = out), 32-channel blocks
 constexpr int HALO = 4, KT = 9;
-constexpr int CF = 16, HF = CF + 2 * HALO;
-constexpr int KF = HF / NW;            // h frames per wave in phase 1
+constexpr int CF = 8;                  // output frames per step
+constexpr int RF = 24;                 // h ring frames (16 read + 8 written per step)
+constexpr int FPW = CF / NWG;          // h frames per GCN wave per step (2)
+constexpr int PRO = 2 * HALO + CF;     // h frames before the first step (16)
 constexpr int RSH = 2 * C + 16;        // h row bytes (144: conflict-free ds_read_b128 for any row offset)
 constexpr int PANEL = 32 * 64;         // [32 joint rows][32 ch] bf16
-constexpr int DP = 4;                  // panels in flight per wave
-constexpr int RT_MAX = 7;              // 32-row output tiles per wave (two row halves: 13 tiles at V = 25)
-constexpr int NB = 6;                  // temporal-conv weight fragment ring depth
+constexpr int SLOTS = FPW * G;         // panel slots per GCN wave (one step's panels)
+constexpr int RT = 4;                  // 32-row output tiles per TCN wave (8 frames x 25 joints = 7 tiles)
+constexpr int NB = 12;                 // temporal-conv weight fragment ring depth
 constexpr int KSTEPS = KT * C / 16;    // 36 k-steps of the temporal conv
 constexpr int VMAX = 25;
+constexpr int TARGET_BLOCKS = 256;     // MI355X CUs: runs per sample = 256 / N (fixed: the host sizes stats by it)
 constexpr int LDS_MAX = 160 * 1024;
-static_assert(HF % NW == 0, "frames per wave");
+static_assert(CF * VMAX <= 2 * RT * 32, "row tiles");
 
 template <int N, typename F>
 DEV void static_for(F&& f) {
@@ -76,25 +83,17 @@ DEV void glds16(const void* src, unsigned lds_off) {
                "s_mov_b32 m0, %0"
                : "=&s"(saved) : "v"(src), "s"(lds_off) : "memory");
 }
+// Block barrier for the LDS hand-offs only: waits for this wave's LDS ops, NOT its outstanding global
+// loads, DMA and stores (__syncthreads() would drain vmcnt: the weight-fragment ring, the next batch's
+// x DMA and the z stores would all be waited for at every step).
+DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 DEV unsigned lds_u32(const void* p) { return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p; }
 
-// wait until at most n of this wave's vector-memory ops are outstanding (n wave-uniform; rounded down)
-DEV void vm_wait(int n) {
-  if (n >= 6)
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if (n >= 4)
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if (n >= 2)
-    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
 struct FGeom {
-  int tiles_n;  // tiles per sample
-  int ntiles;   // N * tiles_n
-  int tpb;      // contiguous tiles per block
-  int nrt;      // 32-row output tiles per tile (ceil(CF * V / 32))
+  int dbg;     // A/B timing switch (STGCN_FUSED_DBG): bit 0 skip the GCN math, bit 1 skip the TCN math (results wrong)
+  int runs_n;  // runs per sample
+  int run;     // frames per run (multiple of CF)
   int off_tab, off_ring, off_h, off_red;  // LDS offsets
 };
 
@@ -106,18 +105,21 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lr = lane & 31, lh = lane >> 5;
   const int V = a.V, T = a.T;
-  const int t_first = blockIdx.x * g.tpb;
-  const int t_last = min(g.ntiles, t_first + g.tpb);
-  if (t_first >= t_last) return;  // block-uniform, before any barrier
+  const int n = blockIdx.x / g.runs_n;
+  const int R0 = (blockIdx.x - n * g.runs_n) * g.run;
+  if (n >= a.N || R0 >= T) return;  // block-uniform, before any barrier
+  const int R1 = min(T, R0 + g.run);
+  const int nsteps = (R1 - R0 + CF - 1) / CF;
+  const int nfr = (R1 - R0) + 2 * HALO;  // h frames the run needs: a in [0, nfr) <-> frame R0 - 4 + a
 
-  char* const sW = smem;                                        // [2][K16] 1-KiB W' fragment blocks
+  char* const sW = smem;                                          // [2][K16] 1-KiB W' fragment blocks
   float* const sSc = reinterpret_cast<float*>(smem + g.off_tab);  // [64] BN1 scale
-  float* const sBp = sSc + C;                                   // [V][64] bias2d * scale + shift
-  char* const sRing = smem + g.off_ring + wave * DP * PANEL;
-  char* const sH = smem + g.off_h;                              // [HF * V][RSH]
+  float* const sBp = sSc + C;                                     // [V][64] bias2d * scale + shift
+  char* const sH = smem + g.off_h;                                // [RF * V][RSH]
   float2* const sRed = reinterpret_cast<float2*>(smem + g.off_red);  // [2][64] (sum, sum of squares)
+  const int vrs = V * RSH;  // bytes per h frame
 
-  // ---- per block: W' slice, BN1 tables, zeroed panel rings (rows V..31 stay zero), stage-1 A operands
+  // ---- per block: W' slice, BN1 tables, zeroed panel rings (rows V..31 stay zero)
   {
     const uint4* wsrc = reinterpret_cast<const uint4*>(a.wg_frag);
     uint4* wdst = reinterpret_cast<uint4*>(sW);
@@ -129,265 +131,351 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
       sBp[e] = fmaf(b, a.n1_scale[c], a.n1_shift[c]);
     }
     uint4* z = reinterpret_cast<uint4*>(smem + g.off_ring);
-    for (int e = tid; e < NW * DP * PANEL / 16; e += NW * 64) z[e] = make_uint4(0, 0, 0, 0);
-  }
-  // B[k = input joint u][n = output joint o] = A[p][u][o]
-  bf16x8 ac[P][2];
-  {
-    const int o = min(lr, V - 1);
-    float av[P][2][8];
-#pragma unroll
-    for (int p = 0; p < P; ++p)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int u = min(16 * ks + 8 * lh + j, V - 1);
-          av[p][ks][j] = a.A[(long)p * V * V + (long)u * V + o];
-        }
-#pragma unroll
-    for (int p = 0; p < P; ++p)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int u = 16 * ks + 8 * lh + j;
-          ac[p][ks][j] = (bf16)((u < V && lr < V) ? av[p][ks][j] : 0.f);
-        }
+    for (int e = tid; e < NWG * SLOTS * PANEL / 16; e += NW * 64) z[e] = make_uint4(0, 0, 0, 0);
   }
   __syncthreads();
 
-  const bf16* __restrict__ xg = reinterpret_cast<const bf16*>(a.x);
+  if (wave >= NWT) {
+    // =============================== GCN waves: h frames ===============================
+    const int gw = wave - NWT;
+    bf16x8 ac[P][2];  // stage-1 B operands: B[k = input joint u][n = output joint o] = A[p][u][o]
+    {
+      const int o = min(lr, V - 1);
+      float av[P][2][8];
+#pragma unroll
+      for (int p = 0; p < P; ++p)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int u = min(16 * ks + 8 * lh + j, V - 1);
+            av[p][ks][j] = a.A[(long)p * V * V + (long)u * V + o];
+          }
+#pragma unroll
+      for (int p = 0; p < P; ++p)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int u = 16 * ks + 8 * lh + j;
+            ac[p][ks][j] = (bf16)((u < V && lr < V) ? av[p][ks][j] : 0.f);
+          }
+    }
+    const bf16* __restrict__ xg = reinterpret_cast<const bf16*>(a.x);
+    const int lrow = lane >> 2, lunit = lane & 3;
+    const bool row2 = lrow + 16 < V;
+    const unsigned ring0 = lds_u32(smem + g.off_ring + gw * SLOTS * PANEL);
+    const char* const ringp = smem + g.off_ring + gw * SLOTS * PANEL;
+    const char* const wl = sW + lane * 16;
+    const bf16* xs = xg + (long)n * T * V * a.x_ld + (long)lrow * a.x_ld + lunit * 8;
+    const f32x16 zero = {};
+
+    // the h frames of a "batch" b (b = 0: the prologue's first half, ...): frame a = base + gw + NWG*i
+    auto frame_ok = [&](int fa) { return fa < nfr && R0 - HALO + fa >= 0 && R0 - HALO + fa < T; };
+    auto issue = [&](int fa0) {  // DMA the panels of this wave's FPW frames fa0 + NWG*i (valid ones)
+#pragma unroll
+      for (int i = 0; i < FPW; ++i) {
+        const int fa = fa0 + NWG * i;
+        if (!frame_ok(fa)) continue;
+        const bf16* src = xs + (long)(R0 - HALO + fa) * V * a.x_ld;
+#pragma unroll
+        for (int cb = 0; cb < G; ++cb) {
+          const unsigned dst = ring0 + (unsigned)((i * G + cb) * PANEL);
+          glds16(src + cb * 32, dst);
+          if (row2) glds16(src + cb * 32 + 16L * a.x_ld, dst + 1024);
+        }
+      }
+    };
+    // compute the FPW frames whose panels sit in the ring; `next` >= 0: DMA that batch once the panels are read
+    auto compute = [&](int fa0, int next) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bf16x8 fx[FPW][G][2];
+#pragma unroll
+      for (int i = 0; i < FPW; ++i)
+#pragma unroll
+        for (int cb = 0; cb < G; ++cb) {
+          const char* pan = ringp + (i * G + cb) * PANEL;
+          fx[i][cb][0] = trfrag(pan, 0, lane);
+          fx[i][cb][1] = trfrag(pan, 16, lane);
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ring read: refill it with the next batch
+      if (next >= 0) issue(next);
+#pragma unroll
+      for (int i = 0; i < FPW; ++i) {
+        const int fa = fa0 + NWG * i;
+        if (fa >= nfr) continue;
+        char* hrow = sH + (fa % RF) * vrs;
+        if (!frame_ok(fa)) {  // padding frame: h = 0
+          for (int e = lane; e < V * 8; e += 64)
+            *reinterpret_cast<uint4*>(hrow + (e >> 3) * RSH + (e & 7) * 16) = make_uint4(0, 0, 0, 0);
+          continue;
+        }
+        f32x16 acc[2];
+        acc[0] = zero;
+        acc[1] = zero;
+        // per (channel block, partition): mix (stage 1) -> bf16 -> 1x1 conv (stage 2); one mix accumulator
+        // live at a time (register budget of two waves per SIMD; the TCN wave fills the dependency gaps)
+#pragma unroll
+        for (int cb = 0; cb < G; ++cb)
+#pragma unroll
+          for (int p = 0; p < P; ++p) {
+            f32x16 c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fx[i][cb][0], ac[p][0], zero, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fx[i][cb][1], ac[p][1], c1, 0, 0, 0);
+            bf16x8 wf[2][2];
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+              for (int t = 0; t < 2; ++t)
+                wf[s][t] = __builtin_bit_cast(
+                    bf16x8, *reinterpret_cast<const uint4*>(wl + (t * K16 + (p * G + cb) * 2 + s) * 1024));
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+              bf16x8 xb;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) xb[j] = (bf16)c1[8 * s + j];
+#pragma unroll
+              for (int t = 0; t < 2; ++t)
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[s][t], xb, acc[t], 0, 0, 0);
+            }
+          }
+        // epilogue: lane = joint lr, acc[t][r] = g^T[co = 32t + 8(r>>2) + 4lh + (r&3)][lr]
+        if (lr < V) {
+          char* hr = hrow + lr * RSH;
+          const float* bp = sBp + lr * C;
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+              const int co = 32 * t + 8 * q4 + 4 * lh;
+              const float4 s4 = *reinterpret_cast<const float4*>(sSc + co);
+              const float4 b4 = *reinterpret_cast<const float4*>(bp + co);
+              bf16x4 hv;
+              hv[0] = (bf16)fmaxf(fmaf(acc[t][4 * q4 + 0], s4.x, b4.x), 0.f);
+              hv[1] = (bf16)fmaxf(fmaf(acc[t][4 * q4 + 1], s4.y, b4.y), 0.f);
+              hv[2] = (bf16)fmaxf(fmaf(acc[t][4 * q4 + 2], s4.z, b4.z), 0.f);
+              hv[3] = (bf16)fmaxf(fmaf(acc[t][4 * q4 + 3], s4.w, b4.w), 0.f);
+              *reinterpret_cast<bf16x4*>(hr + co * 2) = hv;
+            }
+        }
+      }
+    };
+    // prologue: frames 0..15 in two batches of 8 (base 0 and 8); then step s produces base 8s + 8
+    issue(gw);
+    compute(gw, CF + gw);
+    compute(CF + gw, nsteps > 1 ? 2 * CF + gw : -1);
+    lds_barrier();  // S_0: frames 0..15 ready
+    for (int s = 1; s <= nsteps; ++s) {
+      // step s: the TCN waves read frames [8s-8, 8s+8); this wave writes frames base = 8s + 8 ..
+      if (s < nsteps && !(g.dbg & 1)) compute(CF * (s + 1) + gw, s + 1 < nsteps ? CF * (s + 2) + gw : -1);
+      lds_barrier();  // S_s
+    }
+    if (a.stats) lds_barrier();  // R: the TCN waves' statistics hand-off
+    return;
+  }
+
+  // =============================== TCN waves: temporal conv ===============================
   const bf16* __restrict__ wt = reinterpret_cast<const bf16*>(a.wt_frag);
   bf16* __restrict__ zg = reinterpret_cast<bf16*>(a.z);
-  const int lrow = lane >> 2, lunit = lane & 3;
-  const bool row2 = lrow + 16 < V;
-  const unsigned ring0 = lds_u32(sRing);
+  const int ct = wave & 1, rh = wave >> 1;
+  // this lane's output rows (step-relative frame fo, joint w) per row tile; rows past CF*V clamp to row 0
+  int fo_[RT], hw_[RT];
+  bool rok[RT];
+#pragma unroll
+  for (int i = 0; i < RT; ++i) {
+    const int r = (rh * RT + i) * 32 + lr;
+    rok[i] = r < CF * V;
+    const int rr = rok[i] ? r : 0;
+    fo_[i] = rr / V;
+    hw_[i] = (rr - fo_[i] * V) * RSH + lh * 16;
+  }
+  const bf16* wlane = wt + ct * 4 * 512 + lane * 8;  // 1-KiB block [dt][ct][ks] of the [9][2][4] image
+  const bf16* wcur = wlane;  // re-materialised per step (opaque): LICM would otherwise hoist all 36 weight
+                              // fragments of the step out of the step loop and spill them
+  auto load_w = [&](int s) {
+    const int dt = s >> 2, ks = s & 3;
+    return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(wcur + (dt * 8 + ks) * 512));
+  };
+  // row tiles of this wave: CF*V rows = nrt tiles of 32, the first RT to row half 0
+  const int nrt = (CF * V + 31) / 32;
+  const int rtn = rh == 0 ? min(RT, nrt) : nrt - RT;
+  static_assert(KSTEPS % NB == 0, "the weight ring runs on across steps");
+  bf16x8 fw[NB];  // k-step k's fragment in slot k % NB, the same every step
+#pragma unroll
+  for (int k = 0; k < NB - 1; ++k) fw[k] = load_w(k);
+  // BN2 (sum, sum of squares) of the run per channel, accumulated in LDS step by step (registers stay free
+  // for the k-loop); one writer per (row half, channel): deterministic
+  for (int c = lane; c < C; c += 64)
+    if (ct == 0) sRed[rh * C + c] = make_float2(0.f, 0.f);
   const f32x16 zero = {};
-  const char* const wl = sW + lane * 16;
-  const int vrs = V * RSH;  // bytes per h frame
-
-  for (int tile = t_first; tile < t_last; ++tile) {
-    const int n = tile / g.tiles_n;
-    const int f0 = (tile - n * g.tiles_n) * CF;
-    const int cfv = min(CF, T - f0);
-
-    // ================= phase 1: h = relu(BN1(graph conv)) for frames f0 - 4 .. f0 + 19 =================
-    // this wave's frames fl = wave + NW*k (k < KF); valid (inside [0, T)) for k in [k0, k1)
-    const int lo = max(0, HALO - f0), hi = min(HF, T - f0 + HALO);
-    const int k0 = lo > wave ? (lo - wave + NW - 1) / NW : 0;
-    const int k1 = min(KF, hi > wave ? (hi - wave + NW - 1) / NW : 0);
-    for (int k = 0; k < KF; ++k) {  // zero rows of the padding frames
-      if (k >= k0 && k < k1) continue;
-      char* fr = sH + (wave + NW * k) * vrs;
-      for (int e = lane; e < V * 8; e += 64)
-        *reinterpret_cast<uint4*>(fr + (e >> 3) * RSH + (e & 7) * 16) = make_uint4(0, 0, 0, 0);
-    }
-    const int npv = 2 * max(0, k1 - k0);
-    const bf16* src0 = xg + ((long)n * T + (f0 - HALO + wave + NW * k0)) * V * a.x_ld + (long)lrow * a.x_ld + lunit * 8;
-    const long fstep = (long)NW * V * a.x_ld;
-    auto issue = [&](int q) {  // panel q = (valid frame q/2, channel block q%2) -> ring slot q % DP
-      const bf16* src = src0 + (q >> 1) * fstep + (q & 1) * 32;
-      const unsigned dst = ring0 + (unsigned)((q % DP) * PANEL);
-      glds16(src, dst);
-      if (row2) glds16(src + 16L * a.x_ld, dst + 1024);
-    };
-    for (int q = 0; q < min(DP, npv); ++q) issue(q);
-    for (int vk = 0; vk < k1 - k0; ++vk) {
-      f32x16 acc[2];
-      acc[0] = zero;
-      acc[1] = zero;
-#pragma unroll
-      for (int cb = 0; cb < G; ++cb) {
-        const int q = 2 * vk + cb;
-        vm_wait(2 * min(DP - 1, npv - 1 - q));  // panel q landed (later panels may still be in flight)
-        const char* pan = sRing + (q % DP) * PANEL;
-        const bf16x8 fx0 = trfrag(pan, 0, lane);
-        const bf16x8 fx1 = trfrag(pan, 16, lane);
-        f32x16 c1[P];
-#pragma unroll
-        for (int p = 0; p < P; ++p) {
-          c1[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fx0, ac[p][0], zero, 0, 0, 0);
-          c1[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fx1, ac[p][1], c1[p], 0, 0, 0);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads retired: refill it
-        if (q + DP < npv) issue(q + DP);
-        bf16x8 wf[P][2][2];
-#pragma unroll
-        for (int p = 0; p < P; ++p)
-#pragma unroll
-          for (int s = 0; s < 2; ++s)
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-              wf[p][s][t] = __builtin_bit_cast(
-                  bf16x8, *reinterpret_cast<const uint4*>(wl + (t * K16 + (p * G + cb) * 2 + s) * 1024));
-#pragma unroll
-        for (int p = 0; p < P; ++p)
-#pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            bf16x8 xb;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) xb[j] = (bf16)c1[p][8 * s + j];
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-              acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[p][s][t], xb, acc[t], 0, 0, 0);
-          }
+  lds_barrier();  // S_0
+  // the step loop per row-tile count (compile-time: no per-k-step branches in the MFMA stream)
+  auto tcn_run = [&]<int RTN>() {
+    for (int s = 1; s <= nsteps; ++s) {
+      if (g.dbg & 2) {
+        lds_barrier();
+        continue;
       }
-      // epilogue: lane = joint lr, acc[t][r] = g^T[co = 32t + 8(r>>2) + 4lh + (r&3)][lr]
-      if (lr < V) {
-        const int fl = wave + NW * (k0 + vk);
-        char* hrow = sH + (fl * V + lr) * RSH;
-        const float* bp = sBp + lr * C;
+      wcur = wlane;
+      asm volatile("" : "+v"(wcur));
+      const int f0 = R0 + CF * (s - 1);           // first output frame of the step
+      const int base = (CF * (s - 1)) % RF;       // ring slot of run frame 8(s-1) (= output frame f0 - 4)
+      // byte offset of h row (frame f0 + fo + dt - 4, joint w) = slot(base + fo + dt) * vrs + w * RSH
+      int q_[RT];
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+      for (int i = 0; i < RT; ++i) q_[i] = base + fo_[i];
+      auto hoff = [&](int i, int dt) {
+        const int sl = q_[i] + dt;
+        return (sl >= RF ? sl - RF : sl) * vrs + hw_[i];
+      };
+      f32x16 acc[RT];
+#pragma unroll
+      for (int i = 0; i < RT; ++i) acc[i] = zero;
+      bf16x8 fb[3][RT];  // h fragments two k-steps ahead (LDS latency under eight waves' traffic)
+      int ad[RT];  // h byte offsets of the current tap (recomputed per tap, opaque to LICM: hoisting all 36
+                   // k-steps' addresses out of the unrolled loop would spill)
+#pragma unroll
+      for (int i = 0; i < RT; ++i) {
+        ad[i] = hoff(i, 0);
+        asm volatile("" : "+v"(ad[i]));
+        if (i < RTN) {
+          fb[0][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sH + ad[i]));
+          fb[1][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sH + ad[i] + 32));
+        }
+      }
+      static_for<KSTEPS>([&]<int k>() {
+        fw[(k + NB - 1) % NB] = load_w((k + NB - 1) % KSTEPS);  // runs into the next step's first k-steps
+        if constexpr (k + 2 < KSTEPS) {
+          constexpr int dt2 = (k + 2) >> 2, ks2 = (k + 2) & 3;
+          if constexpr (ks2 == 0) {
+#pragma unroll
+            for (int i = 0; i < RT; ++i) {
+              ad[i] = hoff(i, dt2);
+              asm volatile("" : "+v"(ad[i]));
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < RT; ++i)
+            if (i < RTN)
+              fb[(k + 2) % 3][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sH + ad[i] + ks2 * 32));
+        }
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+          if (i < RTN) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[k % NB], fb[k % 3][i], acc[i], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      // epilogue: acc[i][r] = out^T[co = 32ct + 8(r>>2) + 4lh + (r&3)][row (rh*RT + i)*32 + lr]
+      const int vrows = min(CF, R1 - f0) * V;
+      bf16* zt = zg + ((long)n * T + f0) * V * a.z_ld;
+      float tb[16], s1[16], s2[16];
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const int co = 32 * ct + 8 * q4 + 4 * lh;
+        const float4 b4 = a.tbias ? *reinterpret_cast<const float4*>(a.tbias + co) : make_float4(0.f, 0.f, 0.f, 0.f);
+        tb[4 * q4] = b4.x;
+        tb[4 * q4 + 1] = b4.y;
+        tb[4 * q4 + 2] = b4.z;
+        tb[4 * q4 + 3] = b4.w;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s1[r] = s2[r] = 0.f;
+#pragma unroll
+      for (int i = 0; i < RT; ++i) {
+        const int r = (rh * RT + i) * 32 + lr;
+        if (rok[i] && r < vrows) {
 #pragma unroll
           for (int q4 = 0; q4 < 4; ++q4) {
-            const int co = 32 * t + 8 * q4 + 4 * lh;
-            const float4 s4 = *reinterpret_cast<const float4*>(sSc + co);
-            const float4 b4 = *reinterpret_cast<const float4*>(bp + co);
-            bf16x4 hv;
-            hv[0] = (bf16)fmaxf(fmaf(acc[t][4 * q4 + 0], s4.x, b4.x), 0.f);
-            hv[1] = (bf16)fmaxf(fmaf(acc[t][4 * q4 + 1], s4.y, b4.y), 0.f);
-            hv[2] = (bf16)fmaxf(fmaf(acc[t][4 * q4 + 2], s4.z, b4.z), 0.f);
-            hv[3] = (bf16)fmaxf(fmaf(acc[t][4 * q4 + 3], s4.w, b4.w), 0.f);
-            *reinterpret_cast<bf16x4*>(hrow + co * 2) = hv;
+            bf16x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float v = acc[i][4 * q4 + e];
+              s1[4 * q4 + e] += v;
+              s2[4 * q4 + e] = fmaf(v, v, s2[4 * q4 + e]);
+              o[e] = (bf16)(v + tb[4 * q4 + e]);
+            }
+            *reinterpret_cast<bf16x4*>(zt + (long)r * a.z_ld + 32 * ct + 8 * q4 + 4 * lh) = o;
           }
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    // ================= phase 2: temporal conv over the tile's CF*V rows =================
-    const int ct = wave & 1, rh = wave >> 1;
-    const int rows = CF * V;  // rows of a full tile (a short last tile reads zero h frames, never stored)
-    int hoff[RT_MAX];
-#pragma unroll
-    for (int i = 0; i < RT_MAX; ++i) {
-      const int r = (rh * RT_MAX + i) * 32 + lr;
-      hoff[i] = (r < rows ? r : 0) * RSH + lh * 16;
-    }
-    f32x16 acc2[RT_MAX];
-#pragma unroll
-    for (int i = 0; i < RT_MAX; ++i) acc2[i] = zero;
-    // A fragment (weights) of k-step s = (dt, ks): 1-KiB block [dt][ct][ks] of the [9][2][4] image
-    const bf16* wlane = wt + ct * 4 * 512 + lane * 8;
-    bf16x8 fw[NB];
-    auto load_w = [&](int s) {
-      const int dt = s >> 2, ks = s & 3;
-      return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(wlane + (dt * 8 + ks) * 512));
-    };
-#pragma unroll
-    for (int s = 0; s < NB - 1; ++s) fw[s] = load_w(s);
-    bf16x8 fb[2][RT_MAX];
-#pragma unroll
-    for (int i = 0; i < RT_MAX; ++i) fb[0][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sH + hoff[i]));
-    static_for<KSTEPS>([&]<int s>() {
-      constexpr int dt = s >> 2, ks = s & 3;
-      if constexpr (s + NB - 1 < KSTEPS) fw[(s + NB - 1) % NB] = load_w(s + NB - 1);
-      if constexpr (s + 1 < KSTEPS) {
-        constexpr int dt1 = (s + 1) >> 2, ks1 = (s + 1) & 3;
-        const int off = dt1 * vrs + ks1 * 32;
-#pragma unroll
-        for (int i = 0; i < RT_MAX; ++i)
-          fb[(s + 1) & 1][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sH + hoff[i] + off));
-      }
-      (void)dt;
-      (void)ks;
-#pragma unroll
-      for (int i = 0; i < RT_MAX; ++i)
-        acc2[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[s % NB], fb[s & 1][i], acc2[i], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    });
-    // epilogue: acc2[i][r] = out^T[co = 32ct + 8(r>>2) + 4lh + (r&3)][row (rh*7 + i)*32 + lr]
-    float s1[16], s2[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) s1[r] = s2[r] = 0.f;
-    float tb[16];
-#pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) {
-      const int co = 32 * ct + 8 * q4 + 4 * lh;
-      const float4 b4 = a.tbias ? *reinterpret_cast<const float4*>(a.tbias + co) : make_float4(0.f, 0.f, 0.f, 0.f);
-      tb[4 * q4] = b4.x;
-      tb[4 * q4 + 1] = b4.y;
-      tb[4 * q4 + 2] = b4.z;
-      tb[4 * q4 + 3] = b4.w;
-    }
-    const int vrows = cfv * V;
-    bf16* zt = zg + ((long)n * T + f0) * V * a.z_ld;
-#pragma unroll
-    for (int i = 0; i < RT_MAX; ++i) {
-      const int r = (rh * RT_MAX + i) * 32 + lr;
-      if (r < vrows) {
-#pragma unroll
-        for (int q4 = 0; q4 < 4; ++q4) {
-          bf16x4 o;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float v = acc2[i][4 * q4 + e];
-            s1[4 * q4 + e] += v;
-            s2[4 * q4 + e] = fmaf(v, v, s2[4 * q4 + e]);
-            o[e] = (bf16)(v + tb[4 * q4 + e]);
-          }
-          *reinterpret_cast<bf16x4*>(zt + (long)r * a.z_ld + 32 * ct + 8 * q4 + 4 * lh) = o;
         }
       }
-    }
-    if (a.stats) {
+      if (a.stats) {  // the step's sums over this wave's rows (lanes) -> the run totals in LDS
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
+        for (int r = 0; r < 16; ++r) {
 #pragma unroll
-        for (int o = 1; o < 32; o <<= 1) {
-          s1[r] += __shfl_xor(s1[r], o);
-          s2[r] += __shfl_xor(s2[r], o);
+          for (int o = 1; o < 32; o <<= 1) {
+            s1[r] += __shfl_xor(s1[r], o);
+            s2[r] += __shfl_xor(s2[r], o);
+          }
+        }
+        if (lr == 0) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            float2* p = sRed + rh * C + 32 * ct + 8 * (r >> 2) + 4 * lh + (r & 3);
+            const float2 o = *p;
+            *p = make_float2(o.x + s1[r], o.y + s2[r]);
+          }
         }
       }
-      if (lr == 0) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sRed[rh * C + 32 * ct + 8 * (r >> 2) + 4 * lh + (r & 3)] = make_float2(s1[r], s2[r]);
-      }
-      __syncthreads();
-      if (tid < C) {
-        const float2 u0 = sRed[tid], u1 = sRed[C + tid];
-        const float t1 = u0.x + u1.x, t2 = u0.y + u1.y;
-        const float cnt = (float)vrows;
-        const float mu = t1 / cnt;
-        const float b = a.tbias ? a.tbias[tid] : 0.f;
-        reinterpret_cast<float4*>(a.stats)[(long)tile * C + tid] = make_float4(cnt, b + mu, fmaxf(t2 - t1 * mu, 0.f), 0.f);
-      }
+      lds_barrier();  // S_s: the GCN waves may overwrite the frames this step read
     }
-    __syncthreads();  // sH / sRed are rewritten by the next tile
+  };
+  if (rtn >= 4)
+    tcn_run.template operator()<4>();
+  else if (rtn == 3)
+    tcn_run.template operator()<3>();
+  else if (rtn == 2)
+    tcn_run.template operator()<2>();
+  else
+    tcn_run.template operator()<1>();
+  if (!a.stats) return;
+  lds_barrier();  // R (the GCN waves join it before they exit)
+  if (tid < C) {
+    const float2 u0 = sRed[tid], u1 = sRed[C + tid];
+    const float t1 = u0.x + u1.x, t2 = u0.y + u1.y;
+    const float cntr = (float)((R1 - R0) * V);
+    const float mu = t1 / cntr;
+    const float b = a.tbias ? a.tbias[tid] : 0.f;
+    reinterpret_cast<float4*>(a.stats)[(long)blockIdx.x * C + tid] = make_float4(cntr, b + mu, fmaxf(t2 - t1 * mu, 0.f), 0.f);
   }
+}
+
+FGeom plan(int N, int T) {
+  FGeom g{};
+  int per = TARGET_BLOCKS / (N > 0 ? N : 1);
+  if (per < 1) per = 1;
+  const int span = (T + per - 1) / per;
+  g.run = (span + CF - 1) / CF * CF;
+  g.runs_n = (T + g.run - 1) / g.run;
+  return g;
 }
 
 }  // namespace
 
-long layer_fused_row_blocks(int N, int T) { return (long)N * ((T + CF - 1) / CF); }
+long layer_fused_row_blocks(int N, int T) {
+  if (N < 1 || T < 1) return 1;
+  return (long)N * plan(N, T).runs_n;
+}
 
 int layer_fused_launch(const stgcn_layer_fused_desc& a, hipStream_t s) {
   if (!a.x || !a.z || !a.wg_frag || !a.A || !a.n1_scale || !a.n1_shift || !a.wt_frag) return STGCN_EBADSHAPE;
   if (a.N < 1 || a.T < 1 || a.V <= 16 || a.V > VMAX || a.P < 1 || a.P > 3) return STGCN_EBADSHAPE;
   if (a.x_ld < C || a.x_ld % 8 || a.z_ld < C || a.z_ld % 4) return STGCN_EBADSHAPE;
-  FGeom g{};
-  g.tiles_n = (a.T + CF - 1) / CF;
-  const long nt = (long)a.N * g.tiles_n;
-  if (nt > 0x7fffffffL) return STGCN_EBADSHAPE;
-  g.ntiles = (int)nt;
-  g.nrt = (CF * a.V + 31) / 32;
-  if (g.nrt > 2 * RT_MAX) return STGCN_EBADSHAPE;
+  FGeom g = plan(a.N, a.T);
+  {
+    const char* e = getenv("STGCN_FUSED_DBG");
+    g.dbg = e ? atoi(e) : 0;
+  }
+  const long nblk = (long)a.N * g.runs_n;
+  if (nblk > 0x7fffffffL) return STGCN_EBADSHAPE;
   const int K16 = a.P * G * 2;
   g.off_tab = 2 * K16 * 1024;
   g.off_ring = g.off_tab + ((C + a.V * C) * 4 + 255) / 256 * 256;
-  g.off_h = g.off_ring + NW * DP * PANEL;
-  g.off_red = g.off_h + (HF * a.V * RSH + 255) / 256 * 256;
+  g.off_h = g.off_ring + NWG * SLOTS * PANEL;
+  g.off_red = g.off_h + (RF * a.V * RSH + 255) / 256 * 256;
   const size_t lds = (size_t)g.off_red + 2 * C * 8;
   if (lds > (size_t)LDS_MAX) return STGCN_EBADSHAPE;
-  const int ncu = stgcn_cu_count(s);
-  g.tpb = (g.ntiles + ncu - 1) / ncu;
-  const int grid = (g.ntiles + g.tpb - 1) / g.tpb;
   typedef void (*KFn)(const stgcn_layer_fused_desc, const FGeom);
   static const KFn tab[3] = {layer_fused_kernel<1>, layer_fused_kernel<2>, layer_fused_kernel<3>};
   const KFn k = tab[a.P - 1];
   if (stgcn_lds_attr((const void*)k, LDS_MAX, s)) return STGCN_EHIP;
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(NW * 64), lds, s, a, g);
+  hipLaunchKernelGGL(k, dim3((unsigned)nblk), dim3(NW * 64), lds, s, a, g);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
