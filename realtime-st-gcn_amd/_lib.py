@@ -11,7 +11,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libstgcn_amd.so")
+LIB_PATH = os.environ.get("STGCN_LIB") or os.path.join(_HERE, "lib", "libstgcn_amd.so")  # STGCN_LIB: A/B builds
 
 _ERR = {1: "bad shape/arguments", 2: "unsupported dtype", 3: "HIP launch error"}
 

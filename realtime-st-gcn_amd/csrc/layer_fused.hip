@@ -88,6 +88,22 @@ DEV void glds16(const void* src, unsigned lds_off) {
 // x DMA and the z stores would all be waited for at every step).
 DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Sum over the 32 lanes of each wave half (lanes 0-31, 32-63) with DPP (VALU only, no LDS crossbar): the
+// totals land in lanes 31 and 63.
+template <int CTRL, int ROWS>
+DEV float dpp(float old, float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, v),
+                                                                 CTRL, ROWS, 0xf, false));
+}
+DEV float half_sum(float v) {
+  v += dpp<0xB1, 0xf>(0.f, v);   // quad_perm [1,0,3,2]
+  v += dpp<0x4E, 0xf>(0.f, v);   // quad_perm [2,3,0,1]
+  v += dpp<0x141, 0xf>(0.f, v);  // row_half_mirror: 8-lane sums
+  v += dpp<0x140, 0xf>(0.f, v);  // row_mirror: 16-lane (row) sums
+  v += dpp<0x142, 0xa>(0.f, v);  // row_bcast15 into rows 1 and 3: lanes 16-31 / 48-63 hold the half sums
+  return v;
+}
+
 DEV unsigned lds_u32(const void* p) { return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p; }
 
 struct FGeom {
@@ -399,13 +415,10 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
       if (a.stats) {  // the step's sums over this wave's rows (lanes) -> the run totals in LDS
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-#pragma unroll
-          for (int o = 1; o < 32; o <<= 1) {
-            s1[r] += __shfl_xor(s1[r], o);
-            s2[r] += __shfl_xor(s2[r], o);
-          }
+          s1[r] = half_sum(s1[r]);
+          s2[r] = half_sum(s2[r]);
         }
-        if (lr == 0) {
+        if (lr == 31) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             float2* p = sRed + rh * C + 32 * ct + 8 * (r >> 2) + 4 * lh + (r & 3);

@@ -113,6 +113,7 @@ class StgcnLayer(nn.Module):
         self.compute_dtype = torch.float32
         self._gsup = None
         self._graph_bound = False
+        self._fused_cache = {}  # packed weights of the fused inference forward (layer_fn._packs)
 
     def bind_graph(self, A, masked=True):
         """Cache the support lists of the static adjacency A (P, V, V) for the joint-gathered graph
@@ -149,7 +150,7 @@ class StgcnLayer(nn.Module):
         infer = not torch.is_grad_enabled() or not (
             x.requires_grad or A.requires_grad or any(p.requires_grad for p in self.parameters()))
         cfg = (self.kernel_size[0], self.stride, self.is_residual, self.normalization, self.compute_dtype,
-               self.graph_support(A), not self._graph_bound, infer)
+               self.graph_support(A), not self._graph_bound, infer, self._fused_cache)
         return F_.StgcnLayerFunction.apply(x, A, self.gcn.conv.weight, self.gcn.conv.bias, n1.weight, n1.bias,
                                            conv.weight, conv.bias, n2.weight, n2.bias, wr, br, nrw, nrb, cfg)
 
