@@ -345,6 +345,27 @@ long stgcn_segment_metrics_workspace(int L);
 int stgcn_segment_metrics(const long* labels, const long* pred, int L, int C, const float* overlap, int K, void* work,
                           long long* confusion, float* out, int* status, void* stream);
 
+/* RT-ST-GCN per-frame inference (config 3; rt_fused.hip), fp32, batch 1, rows [V][C] of one frame:
+ *   stgcn_rt_frame_in  : x (1,3,1,V) -> LayerNorm([3,1,V]) (ln_w/ln_b [3*V], element c*V+v) -> fcn_in
+ *                        (w [C0][3], b [C0]) -> out [V][C0]                        (rtstgcn.py:103,140-143)
+ *   stgcn_rt_frame_gcn : OnlineLayer's conv1x1 + A-mix (A [P][V][V] = graph * importance, w [P*Cout][Cin],
+ *                        bias2d [V][Cout] = the conv bias through A) and AggregateStgcn's FIFO step
+ *                        (fifo [S*(K-1)+1][V][Cout], acc [S][V][Cout], idx int[2] = (fifo, acc) indices,
+ *                        read only) -> a_out [V][Cout]; wr [Cout][Cin] (or NULL): the residual 1x1 conv
+ *                        (no bias) -> r_out                                    (rtstgcn.py:528-537,591-627)
+ *   stgcn_rt_frame_norm: y = relu(relu(LN(a)) + res) (res_mode 1: res = x, 2: res = LN_r(r)) or relu(LN(a))
+ *                        (res_mode 0); LN per frame over C*V, unbiased; advances idx   (rtstgcn.py:538-553)
+ *   stgcn_rt_frame_out : mean over V -> fcn_out (w [K][C], b [K]) -> out [K]          (rtstgcn.py:149-153) */
+int stgcn_rt_frame_in(const float* x, int V, const float* ln_w, const float* ln_b, const float* w, const float* b, int C0,
+                      float* out, void* stream);
+int stgcn_rt_frame_gcn(const float* x, int V, int Cin, int Cout, int P, const float* A, const float* w, const float* bias2d,
+                       float* fifo, float* acc, const int* idx, const float* wr, float* a_out, float* r_out,
+                       void* stream);
+int stgcn_rt_frame_norm(const float* a, const float* ln_w, const float* ln_b, int res_mode, const float* res,
+                        const float* lnr_w, const float* lnr_b, int V, int C, int* idx, int fifo_size, int S, float* y,
+                        void* stream);
+int stgcn_rt_frame_out(const float* x, int V, int C, const float* w, const float* b, int K, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

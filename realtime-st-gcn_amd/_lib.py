@@ -139,6 +139,11 @@ _SIGS = {
                                c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "stgcn_layer_fused_fwd": (c_int, [ctypes.POINTER(LayerFusedDesc), c_void_p]),
     "stgcn_layer_fused_row_blocks": (ctypes.c_long, [c_int, c_int]),
+    "stgcn_rt_frame_in": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "stgcn_rt_frame_gcn": (c_int, [c_void_p, c_int, c_int, c_int, c_int] + [c_void_p] * 10),
+    "stgcn_rt_frame_norm": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                    c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "stgcn_rt_frame_out": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "stgcn_segment_metrics_workspace": (ctypes.c_long, [c_int]),
     "stgcn_segment_metrics": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
                                       c_void_p, c_void_p, c_void_p]),

@@ -85,6 +85,14 @@ int attn_bwd_launch(const void* th, const void* ph, int ld, int N, int T_, int V
                     const float* dC, float* dS, void* dth, void* dph, int dtype, hipStream_t s);
 int layer_fused_launch(const stgcn_layer_fused_desc& a, hipStream_t s);
 long layer_fused_row_blocks(int N, int T);
+int rt_in_launch(const float* x, int V, const float* g, const float* b, const float* W, const float* bias, int C0,
+                 float* out, hipStream_t s);
+int rt_gcn_launch(const float* x, int V, int Cin, int Cout, int P, const float* A, const float* W, const float* bias2d,
+                  float* fifo, float* acc, const int* idx, const float* Wr, float* a_out, float* r_out,
+                  hipStream_t s);
+int rt_norm_launch(const float* a, const float* g, const float* b, int res_mode, const float* res, const float* gr,
+                   const float* br, int V, int C, int* idx, int fifo_size, int S, float* y, hipStream_t s);
+int rt_out_launch(const float* x, int V, int C, const float* W, const float* bias, int K, float* out, hipStream_t s);
 long seg_metrics_workspace_launch(int L);
 int seg_metrics_launch(const long* lab, const long* pred, int L, int C, const float* ov, int K, int* ws,
                        unsigned long long* cm, float* out, int* status, hipStream_t s);
@@ -343,6 +351,24 @@ int stgcn_layer_fused_fwd(const stgcn_layer_fused_desc* d, void* stream) {
   return layer_fused_launch(*d, STREAM(stream));
 }
 long stgcn_layer_fused_row_blocks(int N, int T) { return layer_fused_row_blocks(N, T); }
+
+int stgcn_rt_frame_in(const float* x, int V, const float* ln_w, const float* ln_b, const float* w, const float* b, int C0,
+                      float* out, void* stream) {
+  return rt_in_launch(x, V, ln_w, ln_b, w, b, C0, out, STREAM(stream));
+}
+int stgcn_rt_frame_gcn(const float* x, int V, int Cin, int Cout, int P, const float* A, const float* w, const float* bias2d,
+                       float* fifo, float* acc, const int* idx, const float* wr, float* a_out, float* r_out,
+                       void* stream) {
+  return rt_gcn_launch(x, V, Cin, Cout, P, A, w, bias2d, fifo, acc, idx, wr, a_out, r_out, STREAM(stream));
+}
+int stgcn_rt_frame_norm(const float* a, const float* ln_w, const float* ln_b, int res_mode, const float* res,
+                        const float* lnr_w, const float* lnr_b, int V, int C, int* idx, int fifo_size, int S, float* y,
+                        void* stream) {
+  return rt_norm_launch(a, ln_w, ln_b, res_mode, res, lnr_w, lnr_b, V, C, idx, fifo_size, S, y, STREAM(stream));
+}
+int stgcn_rt_frame_out(const float* x, int V, int C, const float* w, const float* b, int K, float* out, void* stream) {
+  return rt_out_launch(x, V, C, w, b, K, out, STREAM(stream));
+}
 
 long stgcn_segment_metrics_workspace(int L) { return seg_metrics_workspace_launch(L); }
 int stgcn_segment_metrics(const long* labels, const long* pred, int L, int C, const float* overlap, int K, void* work,

@@ -653,3 +653,57 @@ def attn_bwd(theta, phi, P, C, dC):
                                    C.data_ptr(), dC.data_ptr(), dS.data_ptr(), dth.data_ptr(), dph.data_ptr(),
                                    L.dtype_code(theta.dtype), L.stream()), "attn_bwd")
     return dth, dph
+
+
+# ------------------------------------------------------------------------------ RT per-frame inference (rt_fused.hip)
+def _f32c(t):
+    return t if (t.dtype == torch.float32 and t.is_contiguous()) else t.float().contiguous()
+
+
+def rt_frame_in(x, ln_w, ln_b, w, b):
+    """(1, 3, 1, V) frame -> LayerNorm([3,1,V]) -> fcn_in: rows (1, C0, 1, V) fp32."""
+    L.require_device(x)
+    x = _f32c(x)
+    V, C0 = x.shape[-1], w.shape[0]
+    out = cl_empty(1, C0, 1, V, torch.float32, x.device)
+    L.check(L.lib().stgcn_rt_frame_in(x.data_ptr(), V, _f32c(ln_w).data_ptr(), _f32c(ln_b).data_ptr(),
+                                      _f32c(w).data_ptr(), _f32c(b).data_ptr(), C0, out.data_ptr(), L.stream()),
+            "rt_frame_in")
+    return out
+
+
+def rt_frame_gcn(x, A, w, bias2d, fifo, acc, idx, wr=None):
+    """Online layer conv1x1 + A-mix + FIFO step (+ residual 1x1 conv): returns (a, r) rows (1, Cout, 1, V)."""
+    _, Cin, _, V = x.shape
+    P = A.shape[0]
+    Cout = w.shape[0] // P
+    if rows_ld(x) != Cin:
+        raise RuntimeError("stgcn_amd: rt_frame_gcn expects dense rows")
+    a = cl_empty(1, Cout, 1, V, torch.float32, x.device)
+    r = cl_empty(1, Cout, 1, V, torch.float32, x.device) if wr is not None else None
+    wr_ = _f32c(wr) if wr is not None else None
+    L.check(L.lib().stgcn_rt_frame_gcn(x.data_ptr(), V, Cin, Cout, P, _dense(A).data_ptr(), _f32c(w).data_ptr(),
+                                       L.ptr(bias2d), fifo.data_ptr(), acc.data_ptr(), idx.data_ptr(), L.ptr(wr_),
+                                       a.data_ptr(), L.ptr(r), L.stream()), "rt_frame_gcn")
+    return a, r
+
+
+def rt_frame_norm(a, ln_w, ln_b, res_mode, res, lnr_w, lnr_b, idx, fifo_size, S):
+    """y = relu(relu(LN(a)) + res) | relu(LN(a)); advances the FIFO indices."""
+    _, C, _, V = a.shape
+    y = cl_empty(1, C, 1, V, torch.float32, a.device)
+    L.check(L.lib().stgcn_rt_frame_norm(a.data_ptr(), _f32c(ln_w).data_ptr(), _f32c(ln_b).data_ptr(), int(res_mode),
+                                        L.ptr(res), L.ptr(None if lnr_w is None else _f32c(lnr_w)),
+                                        L.ptr(None if lnr_b is None else _f32c(lnr_b)), V, C, idx.data_ptr(),
+                                        int(fifo_size), int(S), y.data_ptr(), L.stream()), "rt_frame_norm")
+    return y
+
+
+def rt_frame_out(x, w, b):
+    """rows (1, C, 1, V) -> mean over V -> fcn_out: (1, K, 1)."""
+    _, C, _, V = x.shape
+    K = w.shape[0]
+    out = torch.empty((1, K, 1), dtype=torch.float32, device=x.device)
+    L.check(L.lib().stgcn_rt_frame_out(x.data_ptr(), V, C, _f32c(w).data_ptr(), L.ptr(None if b is None else _f32c(b)),
+                                       K, out.data_ptr(), L.stream()), "rt_frame_out")
+    return out

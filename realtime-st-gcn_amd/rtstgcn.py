@@ -154,6 +154,19 @@ class OnlineLayer(nn.Module):
         P = self.aggregate.A.shape[0]
         Cin = x.shape[1]
         A32, wgp, cp, kp, bias2d, resp = self._weights(Cin)
+        ag = self.aggregate
+        if self.normalization == "LayerNorm" and x.shape[1] % 4 == 0 and V <= 32 and P <= 3 and Cin <= 256:
+            # one frame in 2 launches (rt_fused.hip): conv1x1 + A-mix + FIFO (+ residual conv), then the norms
+            wr = self.residual[0].weight if self.is_residual_conv else None
+            a, r = K.rt_frame_gcn(x, A32, self.conv.weight.detach(), bias2d, ag.fifo, ag.accumulator, ag.idx,
+                                  None if wr is None else wr.detach())
+            n = self.bn_relu[0]
+            res_mode = 2 if self.is_residual_conv else (1 if self.is_residual else 0)
+            rn = self.residual[1] if self.is_residual_conv else None
+            return K.rt_frame_norm(a, LF._flat_ln(n.weight), LF._flat_ln(n.bias), res_mode,
+                                   r if self.is_residual_conv else (x if self.is_residual else None),
+                                   None if rn is None else LF._flat_ln(rn.weight),
+                                   None if rn is None else LF._flat_ln(rn.bias), ag.idx, ag.fifo_size, ag.stride)
         XA = K.amix_fwd(x, A32)
         z = K.conv_rows(XA, wgp, P * Cin, Cout, cp, kp, 1, 1, bias=bias2d, bias_mode=2)
         a = self.aggregate.step(z)
@@ -219,6 +232,16 @@ class Model(nn.Module):
         return self
 
     def forward(self, x):
+        if (self.online and self.normalization == "LayerNorm" and x.dim() == 4 and x.shape[0] == 1
+                and x.shape[2] == 1 and x.shape[1] == 3 and not torch.is_grad_enabled()):
+            # per-frame inference: fused input head, two launches per layer, fused output head (rt_fused.hip)
+            y = K.rt_frame_in(x, LF._flat_ln(self.norm_in.weight), LF._flat_ln(self.norm_in.bias),
+                              self.fcn_in.weight.detach().reshape(self.fcn_in.out_channels, -1),
+                              self.fcn_in.bias.detach())
+            for gcn in self.st_gcn:
+                y = gcn(y, self.A)
+            return K.rt_frame_out(y, self.fcn_out.weight.detach().reshape(self.fcn_out.out_channels, -1),
+                                  self.fcn_out.bias.detach())
         x = self.norm_in(x)
         C = x.shape[1]
         if C % IN_PAD:
