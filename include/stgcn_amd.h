@@ -366,6 +366,34 @@ int stgcn_rt_frame_norm(const float* a, const float* ln_w, const float* ln_b, in
                         void* stream);
 int stgcn_rt_frame_out(const float* x, int V, int C, const float* w, const float* b, int K, float* out, void* stream);
 
+/* Window staging (window.hip): the first activation of a batch of sliding windows
+ * (WindowSegment, utils/segment_generator.py:132-145) computed from the padded capture without forming the
+ * windows.  x: fp32 [Cin][Lp][V] (the reference's padded (1, Cin, Lp, V) capture, processor.py:372-374),
+ * Cin in {1,2,3,4,6,8}; windows n in [n0, n0+nw) hold frames [n, n+W) (n0 + nw + W - 1 <= Lp).
+ *   stgcn_window_stats : norm_in statistics of the windowed batch.  mode 0, BatchNorm1d(V*Cin) (batchnorm.py:
+ *       13-23): out = float4 (count, mean, M2, 0) partials [stgcn_window_stat_blocks(nw, W)][V*Cin], each
+ *       frame weighted by the number of windows holding it -> stgcn_bn_finalize(nb, ld = C = V*Cin);
+ *       mode 1, LayerNorm([Cin,1,V]) (layernorm.py:22-28): out = float2 (mean, rstd) per frame [nw+W-1],
+ *       unbiased variance.
+ *   stgcn_window_expand: out rows (n, t, v) [nw][W][V], ld ldo, dtype: fcn_in(norm_in(x[:, n+t, v]))
+ *       (stgcn.py:82-85) with w [Cout][Cin], bias [Cout] (or NULL).  mode 0: g/b = the folded affine
+ *       (scale, shift) [V*Cin] of stgcn_bn_finalize, fst NULL; mode 1: g/b = gamma/beta [Cin*V] (element
+ *       c*V+v), fst = the frame statistics.  Cout % (16 / element size) == 0.
+ *   stgcn_window_grad  : from dy rows (the gradient of expand's output, ld ldd): dw [Cout][Cin], db [Cout],
+ *       dgamma / dbeta (mode 0 [V*Cin] v*Cin+c with st = (mean, rstd) [V*Cin] of stgcn_bn_finalize; mode 1
+ *       [Cin*V] with st = the frame statistics); any output may be NULL.  One pass over dy (windows folded
+ *       onto frames); work: stgcn_window_grad_workspace bytes, no initialisation needed. */
+int stgcn_window_stat_blocks(int nw, int W);
+int stgcn_window_stats(const float* x, int Cin, int Lp, int V, int W, int n0, int nw, int mode, float eps, float* out,
+                       void* stream);
+int stgcn_window_expand(const float* x, int Cin, int Lp, int V, int W, int n0, int nw, int mode, const float* g,
+                        const float* b, const float* fst, const float* w, const float* bias, int Cout, void* out,
+                        int ldo, int dtype, void* stream);
+long stgcn_window_grad_workspace(int nw, int W, int V, int Cin, int Cout);
+int stgcn_window_grad(const void* dy, int ldd, int dtype, const float* x, int Cin, int Lp, int V, int W, int n0, int nw,
+                      int mode, const float* st, const float* gamma, const float* beta, const float* w, int Cout,
+                      void* work, float* dgamma, float* dbeta, float* dw, float* db, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

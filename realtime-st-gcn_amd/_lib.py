@@ -144,6 +144,13 @@ _SIGS = {
     "stgcn_rt_frame_norm": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int,
                                     c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "stgcn_rt_frame_out": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "stgcn_window_stat_blocks": (c_int, [c_int, c_int]),
+    "stgcn_window_stats": (c_int, [c_void_p] + [c_int] * 7 + [c_float, c_void_p, c_void_p]),
+    "stgcn_window_expand": (c_int, [c_void_p] + [c_int] * 7 + [c_void_p] * 5 + [c_int, c_void_p, c_int, c_int,
+                                                                                c_void_p]),
+    "stgcn_window_grad_workspace": (ctypes.c_long, [c_int] * 5),
+    "stgcn_window_grad": (c_int, [c_void_p, c_int, c_int, c_void_p] + [c_int] * 7 + [c_void_p] * 4 + [c_int] +
+                          [c_void_p] * 6),
     "stgcn_segment_metrics_workspace": (ctypes.c_long, [c_int]),
     "stgcn_segment_metrics": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
                                       c_void_p, c_void_p, c_void_p]),

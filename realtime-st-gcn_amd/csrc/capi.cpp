@@ -93,6 +93,16 @@ int rt_gcn_launch(const float* x, int V, int Cin, int Cout, int P, const float* 
 int rt_norm_launch(const float* a, const float* g, const float* b, int res_mode, const float* res, const float* gr,
                    const float* br, int V, int C, int* idx, int fifo_size, int S, float* y, hipStream_t s);
 int rt_out_launch(const float* x, int V, int C, const float* W, const float* bias, int K, float* out, hipStream_t s);
+int window_stat_blocks_launch(int nw, int W);
+int window_stats_launch(const float* x, int Cin, int Lp, int V, int W, int n0, int nw, int mode, float eps, float* out,
+                        hipStream_t s);
+int window_expand_launch(const float* x, int Cin, int Lp, int V, int W, int n0, int nw, int mode, const float* g,
+                         const float* b, const float* fst, const float* w, const float* bias, int Cout, void* out,
+                         int ldo, int dtype, hipStream_t s);
+long window_grad_workspace_launch(int nw, int W, int V, int Cin, int Cout);
+int window_grad_launch(const void* dy, int ldd, int dtype, const float* x, int Cin, int Lp, int V, int W, int n0, int nw,
+                       int mode, const float* st, const float* g, const float* b, const float* w, int Cout, float* work,
+                       float* dg, float* dbeta, float* dw, float* db, hipStream_t s);
 long seg_metrics_workspace_launch(int L);
 int seg_metrics_launch(const long* lab, const long* pred, int L, int C, const float* ov, int K, int* ws,
                        unsigned long long* cm, float* out, int* status, hipStream_t s);
@@ -368,6 +378,27 @@ int stgcn_rt_frame_norm(const float* a, const float* ln_w, const float* ln_b, in
 }
 int stgcn_rt_frame_out(const float* x, int V, int C, const float* w, const float* b, int K, float* out, void* stream) {
   return rt_out_launch(x, V, C, w, b, K, out, STREAM(stream));
+}
+
+int stgcn_window_stat_blocks(int nw, int W) { return window_stat_blocks_launch(nw, W); }
+int stgcn_window_stats(const float* x, int Cin, int Lp, int V, int W, int n0, int nw, int mode, float eps, float* out,
+                       void* stream) {
+  return window_stats_launch(x, Cin, Lp, V, W, n0, nw, mode, eps, out, STREAM(stream));
+}
+int stgcn_window_expand(const float* x, int Cin, int Lp, int V, int W, int n0, int nw, int mode, const float* g,
+                        const float* b, const float* fst, const float* w, const float* bias, int Cout, void* out,
+                        int ldo, int dtype, void* stream) {
+  return window_expand_launch(x, Cin, Lp, V, W, n0, nw, mode, g, b, fst, w, bias, Cout, out, ldo, dtype,
+                              STREAM(stream));
+}
+long stgcn_window_grad_workspace(int nw, int W, int V, int Cin, int Cout) {
+  return window_grad_workspace_launch(nw, W, V, Cin, Cout);
+}
+int stgcn_window_grad(const void* dy, int ldd, int dtype, const float* x, int Cin, int Lp, int V, int W, int n0, int nw,
+                      int mode, const float* st, const float* gamma, const float* beta, const float* w, int Cout,
+                      void* work, float* dgamma, float* dbeta, float* dw, float* db, void* stream) {
+  return window_grad_launch(dy, ldd, dtype, x, Cin, Lp, V, W, n0, nw, mode, st, gamma, beta, w, Cout, (float*)work,
+                            dgamma, dbeta, dw, db, STREAM(stream));
 }
 
 long stgcn_segment_metrics_workspace(int L) { return seg_metrics_workspace_launch(L); }

@@ -514,6 +514,44 @@ class InputBatchNormFunction(torch.autograd.Function):
         return dx, sums[:, 1].to(w.dtype), sums[:, 0].to(w.dtype), None
 
 
+class WindowStageFunction(torch.autograd.Function):
+    """norm_in + fcn_in of a batch of sliding windows (WindowSegment, segment_generator.py:132-145; stgcn.py:
+    82-85) straight from the padded capture (1, Cin, Lp, V): windows [n0, n0+nw) of W frames, never formed
+    (window.hip).  mode 0: BatchNorm1d(V*Cin) with the windowed batch's statistics (each frame weighted by
+    the windows holding it); mode 1: the per-frame LayerNorm([Cin,1,V]).  Returns the first activation
+    (nw, Cout, W, V) channels-last; backward gives the norm and fcn_in parameter gradients (the capture
+    takes none, as in the reference where it is data)."""
+
+    @staticmethod
+    def forward(ctx, capture, n0, nw, W, norm_w, norm_b, w, b, mode, dtype):
+        Cout = w.shape[0]
+        w2 = w.detach().float().reshape(Cout, -1)
+        bias = b.detach().float() if b is not None else None
+        g, be = norm_w.detach().float().reshape(-1), norm_b.detach().float().reshape(-1)
+        if mode == 0:
+            part, nb = K.window_stats(capture, W, n0, nw, 0)
+            VC = part.shape[1]
+            st, sc, sh = K.bn_finalize(part, nb, VC, VC, g, be)
+            y = K.window_expand(capture, W, n0, nw, 0, sc, sh, None, w2, bias, dtype)
+        else:
+            st, _ = K.window_stats(capture, W, n0, nw, 1)
+            y = K.window_expand(capture, W, n0, nw, 1, g, be, st, w2, bias, dtype)
+        ctx.save_for_backward(capture, norm_w, norm_b, w, b, st)
+        ctx.cfg = (n0, nw, W, mode)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        capture, norm_w, norm_b, w, b, st = ctx.saved_tensors
+        n0, nw, W, mode = ctx.cfg
+        dy = K.to_rows(dy, dy.dtype)
+        Cout = w.shape[0]
+        dg, dbe, dw, db = K.window_grad(dy, capture, W, n0, nw, mode, st, norm_w.detach().float().reshape(-1),
+                                        norm_b.detach().float().reshape(-1), w.detach().float().reshape(Cout, -1))
+        return (None, None, None, None, dg.view(norm_w.shape).to(norm_w.dtype), dbe.view(norm_b.shape).to(norm_b.dtype),
+                dw.view(w.shape).to(w.dtype), None if b is None else db.to(b.dtype), None, None)
+
+
 def _as_rows(t, F_, CV):
     # a (F_, 1, 1, CV) contiguous buffer viewed as logical (F_, CV, 1, 1) channels-last
     return t.permute(0, 2, 3, 1).contiguous().view(F_, 1, 1, CV).permute(0, 3, 1, 2)

@@ -707,3 +707,59 @@ def rt_frame_out(x, w, b):
     L.check(L.lib().stgcn_rt_frame_out(x.data_ptr(), V, C, _f32c(w).data_ptr(), L.ptr(None if b is None else _f32c(b)),
                                        K, out.data_ptr(), L.stream()), "rt_frame_out")
     return out
+
+
+# ------------------------------------------------------------------------------ window staging (window.hip)
+def _capture(x):
+    """(1, Cin, Lp, V) padded capture -> contiguous fp32 [Cin][Lp][V] on the device."""
+    L.require_device(x)
+    if x.dim() != 4 or x.shape[0] != 1:
+        raise RuntimeError(f"stgcn_amd: window staging takes one (1, C, L, V) capture, got {tuple(x.shape)}")
+    return _f32c(x)
+
+
+def window_stats(x, W, n0, nw, mode, eps=1e-5):
+    """BatchNorm1d partials (mode 0: (nb, V*Cin, 4) and nb) or LayerNorm frame statistics (mode 1: (F, 2))."""
+    x = _capture(x)
+    _, Cin, Lp, V = x.shape
+    if mode == 0:
+        nb = L.lib().stgcn_window_stat_blocks(nw, W)
+        out = torch.empty((nb, V * Cin, 4), dtype=torch.float32, device=x.device)
+    else:
+        nb = 0
+        out = torch.empty((nw + W - 1, 2), dtype=torch.float32, device=x.device)
+    L.check(L.lib().stgcn_window_stats(x.data_ptr(), Cin, Lp, V, W, n0, nw, mode, eps, out.data_ptr(), L.stream()),
+            "window_stats")
+    return out, nb
+
+
+def window_expand(x, W, n0, nw, mode, g, b, fst, w, bias, dtype):
+    """First activation of windows [n0, n0+nw): logical (nw, Cout, W, V) channels-last rows."""
+    x = _capture(x)
+    _, Cin, Lp, V = x.shape
+    Cout = w.shape[0]
+    out = cl_empty(nw, Cout, W, V, dtype, x.device)
+    L.check(L.lib().stgcn_window_expand(x.data_ptr(), Cin, Lp, V, W, n0, nw, mode, _f32c(g).data_ptr(),
+                                        _f32c(b).data_ptr(), L.ptr(fst), _f32c(w).data_ptr(),
+                                        L.ptr(None if bias is None else _f32c(bias)), Cout, out.data_ptr(), Cout,
+                                        L.dtype_code(dtype), L.stream()), "window_expand")
+    return out
+
+
+def window_grad(dy, x, W, n0, nw, mode, st, gamma, beta, w):
+    """(dgamma, dbeta, dw [Cout][Cin], db) of the staged first activation from its gradient rows."""
+    x = _capture(x)
+    _, Cin, Lp, V = x.shape
+    Cout = w.shape[0]
+    dev = x.device
+    work = _workspace(L.lib().stgcn_window_grad_workspace(nw, W, V, Cin, Cout), dev)
+    dg = torch.empty(V * Cin, dtype=torch.float32, device=dev)
+    dbeta = torch.empty(V * Cin, dtype=torch.float32, device=dev)
+    dw = torch.empty((Cout, Cin), dtype=torch.float32, device=dev)
+    db = torch.empty(Cout, dtype=torch.float32, device=dev)
+    L.check(L.lib().stgcn_window_grad(dy.data_ptr(), rows_ld(dy), L.dtype_code(dy.dtype), x.data_ptr(), Cin, Lp, V, W,
+                                      n0, nw, mode, _f32c(st).data_ptr(), _f32c(gamma).data_ptr(),
+                                      _f32c(beta).data_ptr(), _f32c(w).data_ptr(), Cout, work.data_ptr(),
+                                      dg.data_ptr(), dbeta.data_ptr(), dw.data_ptr(), db.data_ptr(), L.stream()),
+            "window_grad")
+    return dg, dbeta, dw, db

@@ -3,7 +3,9 @@
 ``Model(**arch)`` takes the reference's ``arch`` config dict (+ injected ``graph`` and
 ``num_classes``, processor.py:164-166); ``rank`` is accepted and ignored like in the reference.
 state_dict keys are identical (``A``, ``norm_in.*``, ``fcn_in.*``, ``gcn_networks.i.*``,
-``edge_importance.i``, ``fcn_out.*``).  forward(x (N, C, T, V)) -> (N, num_classes, 1).
+``edge_importance.i``, ``fcn_out.*``).  forward(x (N, C, T, V)) -> (N, num_classes, 1); x may also be a
+``segment.WindowBatch`` (WindowSegment's sliding windows over a padded capture), whose norm_in + fcn_in
+run from the capture without forming the windows (layer_fn.WindowStageFunction).
 """
 from __future__ import annotations
 
@@ -14,6 +16,7 @@ import torch.nn.functional as F
 from . import layer_fn as LF
 from .graph import Graph
 from .modules import BatchNorm1d, LayerNorm, StgcnLayer, resolve_dtype
+from .segment import WindowBatch
 
 IN_PAD = 8  # fcn_in input channels are zero-padded to one 16-byte unit (kernel vector width)
 
@@ -54,15 +57,25 @@ class Model(nn.Module):
                     m.compute_dtype = dt
         return self
 
+    def stage_windows(self, xb: WindowBatch):
+        """norm_in + fcn_in (stgcn.py:82-85) of sliding windows, from the padded capture."""
+        ln = self.normalization == "LayerNorm"
+        nw_, nb_ = (self.norm_in.weight, self.norm_in.bias) if ln else (self.norm_in.norm.weight, self.norm_in.norm.bias)
+        return LF.WindowStageFunction.apply(xb.capture, xb.n0, xb.nw, xb.W, nw_, nb_, self.fcn_in.weight,
+                                            self.fcn_in.bias, 1 if ln else 0, self.compute_dtype)
+
     def forward(self, x):
-        x = self.norm_in(x)                                          # stgcn.py:82 (fp32)
-        C = x.shape[1]
-        if C % IN_PAD:
-            x = F.pad(x.permute(0, 2, 3, 1), (0, IN_PAD - C % IN_PAD)).permute(0, 3, 1, 2)
-            w = F.pad(self.fcn_in.weight, (0, 0, 0, 0, 0, IN_PAD - C % IN_PAD))
+        if isinstance(x, WindowBatch):
+            x = self.stage_windows(x)
         else:
-            w = self.fcn_in.weight
-        x = LF.Conv1x1Function.apply(x, w, self.fcn_in.bias, self.compute_dtype)   # stgcn.py:85
+            x = self.norm_in(x)                                          # stgcn.py:82 (fp32)
+            C = x.shape[1]
+            if C % IN_PAD:
+                x = F.pad(x.permute(0, 2, 3, 1), (0, IN_PAD - C % IN_PAD)).permute(0, 3, 1, 2)
+                w = F.pad(self.fcn_in.weight, (0, 0, 0, 0, 0, IN_PAD - C % IN_PAD))
+            else:
+                w = self.fcn_in.weight
+            x = LF.Conv1x1Function.apply(x, w, self.fcn_in.bias, self.compute_dtype)   # stgcn.py:85
         for gcn, importance in zip(self.gcn_networks, self.edge_importance):       # stgcn.py:88-89
             gcn.bind_graph(self.A)  # support of the static graph (cached; no sync after the first call)
             x = gcn(x, self.A * importance)

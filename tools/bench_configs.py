@@ -7,8 +7,12 @@ config 3: RT-ST-GCN online inference (config/pku-mmd/ln/rtstgcn_local.json: LN, 
           advance the stream correctly).  Parity of the two against each other is checked.
 config 5: AAGCN (config/pku-mmd/as_is/aagcn_local.json: 2 streams, BN, 9 layers) fwd+bwd, bf16,
           N=64 T=300 V=25: skeleton-frames/s.
+f1:       window staging (config/pku-mmd/ln/stgcn_local.json: receptive_field 50, segment 1000): norm_in +
+          fcn_in of one segment's 1000 windows from the padded capture (window.hip) vs the reference's
+          order (unfold the windows, then norm_in and fcn_in on the copies — our HIP kernels on both sides),
+          fwd and bwd, BatchNorm and LayerNorm, bf16.
 
-    python tools/bench_configs.py [--frames 2000] [--steps 10]
+    python tools/bench_configs.py [--frames 2000] [--steps 10] [--only 3|5|f1]
 Prints one JSON line per config.
 """
 import argparse
@@ -122,6 +126,55 @@ def config5(P, dev, steps, warmup):
             "ms_per_step": round(1e3 * dt / steps, 3), "steps": steps, "data": "synthetic"}
 
 
+def staging(P, dev, reps=50):
+    import torch.nn.functional as F
+    W, nw, L, C, V, Cout = 50, 1000, 1000, 3, 25, 64
+    gen = torch.Generator(device=dev).manual_seed(5)
+    padded = F.pad(torch.randn(1, C, L, V, device=dev, generator=gen), (0, 0, W - 1, 0))
+    w = torch.randn(Cout, C, 1, 1, device=dev, generator=gen).requires_grad_(True)
+    b = torch.zeros(Cout, device=dev).requires_grad_(True)
+    bf = torch.bfloat16
+    out = {"config": "f1: window staging, 1000 windows x W=50 (ln/stgcn_local.json segment), C=3 -> 64, bf16",
+           "out_bytes": nw * W * V * Cout * 2}
+    for norm, mode in (("BatchNorm", 0), ("LayerNorm", 1)):
+        if mode == 0:
+            mod = P.BatchNorm1d(C * V).to(dev)
+            gw, gb = mod.norm.weight, mod.norm.bias
+        else:
+            mod = P.LayerNorm([C, 1, V]).to(dev)
+            gw, gb = mod.weight, mod.bias
+        dy = torch.randn(nw, W, V, Cout, device=dev, generator=gen).to(bf).permute(0, 3, 1, 2)
+
+        def staged():
+            return P.layer_fn.WindowStageFunction.apply(padded, 0, nw, W, gw, gb, w, b, mode, bf)
+
+        def unfolded():
+            x = P.segment.WindowBatch(padded, 0, nw, W).materialize()
+            x = mod(x)
+            x = F.pad(x.permute(0, 2, 3, 1), (0, 8 - C)).permute(0, 3, 1, 2)
+            return P.layer_fn.Conv1x1Function.apply(x, F.pad(w, (0, 0, 0, 0, 0, 8 - C)), b, bf)
+
+        for name, fn in (("staged", staged), ("unfold_norm_conv", unfolded)):
+            for _ in range(3):
+                fn().backward(dy)
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            tf = tb = 0.0
+            for _ in range(reps):
+                ev[0].record()
+                y = fn()
+                ev[1].record()
+                y.backward(dy)
+                ev[2].record()
+                torch.cuda.synchronize()
+                tf += ev[0].elapsed_time(ev[1])
+                tb += ev[1].elapsed_time(ev[2])
+            out["%s_%s_fwd_us" % (norm, name)] = round(1e3 * tf / reps, 1)
+            out["%s_%s_bwd_us" % (norm, name)] = round(1e3 * tb / reps, 1)
+        out["%s_staged_fwd_GBps" % norm] = round(out["out_bytes"] / (out["%s_staged_fwd_us" % norm] * 1e3), 1)
+        out["%s_staged_bwd_GBps" % norm] = round(out["out_bytes"] / (out["%s_staged_bwd_us" % norm] * 1e3), 1)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=2000)
@@ -135,6 +188,8 @@ def main():
         print(json.dumps(config3(P, dev, args.frames)), flush=True)
     if args.only in (None, "5"):
         print(json.dumps(config5(P, dev, args.steps, args.warmup)), flush=True)
+    if args.only in (None, "f1"):
+        print(json.dumps(staging(P, dev)), flush=True)
 
 
 if __name__ == "__main__":
