@@ -16,6 +16,7 @@ import torch.nn.functional as F
 from . import layer_fn as LF
 from .graph import Graph
 from .modules import BatchNorm1d, LayerNorm, StgcnLayer, resolve_dtype
+from .segment import WindowBatch
 from .stgcn import IN_PAD
 
 
@@ -101,13 +102,16 @@ class Model(nn.Module):
         return x
 
     def _stream(self, s, x):
-        x = s["norm_in"](x)
-        C = x.shape[1]
-        w = s["fcn_in"].weight
-        if C % IN_PAD:
-            x = F.pad(x.permute(0, 2, 3, 1), (0, IN_PAD - C % IN_PAD)).permute(0, 3, 1, 2)
-            w = F.pad(w, (0, 0, 0, 0, 0, IN_PAD - C % IN_PAD))
-        x = LF.Conv1x1Function.apply(x, w, s["fcn_in"].bias, self.compute_dtype)
+        if isinstance(x, WindowBatch):  # sliding windows staged from the capture (window.hip)
+            x = LF.stage_window_batch(x, s["norm_in"], s["fcn_in"], self.compute_dtype)
+        else:
+            x = s["norm_in"](x)
+            C = x.shape[1]
+            w = s["fcn_in"].weight
+            if C % IN_PAD:
+                x = F.pad(x.permute(0, 2, 3, 1), (0, IN_PAD - C % IN_PAD)).permute(0, 3, 1, 2)
+                w = F.pad(w, (0, 0, 0, 0, 0, IN_PAD - C % IN_PAD))
+            x = LF.Conv1x1Function.apply(x, w, s["fcn_in"].bias, self.compute_dtype)
         for gcn in s["gcn_networks"]:
             x = gcn(x, self.A)
         x = LF.PoolFunction.apply(x, self.compute_dtype)
@@ -115,8 +119,14 @@ class Model(nn.Module):
         return x.squeeze(-1).float()
 
     def forward(self, x_joint):
-        # bones: x_bone[..., j] = x[..., j] - x[..., src(j)] for joints that are someone's far neighbour
-        x_bone = (x_joint - x_joint[:, :, :, self.bone_src]) * self.bone_mask
+        # bones: x_bone[..., j] = x[..., j] - x[..., src(j)] for joints that are someone's far neighbour;
+        # a per-frame map, so a WindowBatch's bone windows are the windows of the capture's bones
+        if isinstance(x_joint, WindowBatch):
+            cap = x_joint.capture
+            x_bone = WindowBatch((cap - cap[:, :, :, self.bone_src]) * self.bone_mask, x_joint.n0, x_joint.nw,
+                                 x_joint.W)
+        else:
+            x_bone = (x_joint - x_joint[:, :, :, self.bone_src]) * self.bone_mask
         y_joint = self._stream(self.streams[0], x_joint)
         y_bone = self._stream(self.streams[1], x_bone)
         return self.probability(y_bone) + self.probability(y_joint)            # aagcn.py:95

@@ -552,6 +552,14 @@ class WindowStageFunction(torch.autograd.Function):
                 dw.view(w.shape).to(w.dtype), None if b is None else db.to(b.dtype), None, None)
 
 
+def stage_window_batch(xb, norm_in, fcn_in, dtype):
+    """norm_in (modules.BatchNorm1d or LayerNorm) + fcn_in of a segment.WindowBatch, from its capture."""
+    ln = not hasattr(norm_in, "norm")  # modules.BatchNorm1d wraps nn.BatchNorm1d as .norm
+    g, b = (norm_in.weight, norm_in.bias) if ln else (norm_in.norm.weight, norm_in.norm.bias)
+    return WindowStageFunction.apply(xb.capture, xb.n0, xb.nw, xb.W, g, b, fcn_in.weight, fcn_in.bias,
+                                     1 if ln else 0, dtype)
+
+
 def _as_rows(t, F_, CV):
     # a (F_, 1, 1, CV) contiguous buffer viewed as logical (F_, CV, 1, 1) channels-last
     return t.permute(0, 2, 3, 1).contiguous().view(F_, 1, 1, CV).permute(0, 3, 1, 2)

@@ -59,10 +59,7 @@ class Model(nn.Module):
 
     def stage_windows(self, xb: WindowBatch):
         """norm_in + fcn_in (stgcn.py:82-85) of sliding windows, from the padded capture."""
-        ln = self.normalization == "LayerNorm"
-        nw_, nb_ = (self.norm_in.weight, self.norm_in.bias) if ln else (self.norm_in.norm.weight, self.norm_in.norm.bias)
-        return LF.WindowStageFunction.apply(xb.capture, xb.n0, xb.nw, xb.W, nw_, nb_, self.fcn_in.weight,
-                                            self.fcn_in.bias, 1 if ln else 0, self.compute_dtype)
+        return LF.stage_window_batch(xb, self.norm_in, self.fcn_in, self.compute_dtype)
 
     def forward(self, x):
         if isinstance(x, WindowBatch):

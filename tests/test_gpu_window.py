@@ -116,3 +116,29 @@ def test_model_on_window_batch(P, norm):
     m.zero_grad()
     y2 = m(xb.materialize())  # the same HIP model on the reference's materialised tensor
     assert_close(y, y2, 1e-4, "staged vs materialised")
+
+
+def test_aagcn_on_window_batch(P):
+    """aa-gcn (both streams; the bone stream's windows are the windows of the capture's bones): staged ==
+    the same HIP model on the materialised batch, logits and every parameter gradient (fp32)."""
+    arch = {"strategy": "spatial", "in_feat": 3, "num_classes": 7, "output_type": "logits",
+            "normalization": "BatchNorm", "graph": P.PKU_MMD,
+            "aa-gcn": {"in_feat": 3, "layers": 2, "kernel": 9, "importance": True, "in_ch": [64, 64],
+                       "out_ch": [64, 64], "stride": [1, 1], "residual": [1, 1], "dropout": [0, 0]}}
+    torch.manual_seed(5)
+    m = P.MODELS["aa-gcn"](rank=None, **arch).to(DEV)
+    g = torch.Generator().manual_seed(6)
+    padded = F.pad(torch.randn(1, 3, 60, 25, generator=g), (0, 0, 19, 0)).to(DEV)
+    xb = P.segment.WindowBatch(padded, 3, 30, 20)
+    G = torch.randn(30, 7, generator=g).to(DEV)
+    y = m(xb)
+    (y.reshape(30, 7) * G).sum().backward()
+    grads = {k: p.grad.clone() for k, p in m.named_parameters()}
+    m.zero_grad()
+    y2 = m(xb.materialize())
+    (y2.reshape(30, 7) * G).sum().backward()
+    assert_close(y, y2, 1e-4, "aagcn logits staged vs materialised")
+    for k, p in m.named_parameters():
+        if bn_fed_bias(k) or k.endswith("phi.bias"):
+            continue
+        assert_grad_close(grads[k], p.grad, 1e-3, k, reduction=True)
