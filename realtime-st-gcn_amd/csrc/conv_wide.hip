@@ -224,18 +224,24 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
             reinterpret_cast<float4*>(a.stats)[(long)rt * a.Cout_pad + n0 + c] = make_float4(wv.n, wv.mean, wv.m2, 0.f);
         }
       }
-      // lane = row quad (4 rows), helper wave h = 8-channel units 4h..4h+3: per unit, 8 conflict-free
-      // ds_read_b64 (4 rows of one column each) are transposed in registers into 4 row units of 16 B
+      // thread = (row quad rq, 8-channel unit cu): a lane reads its unit's 8 columns x 4 rows (ds_read_b64
+      // each) and transposes them in registers into 4 row units of 16 B; in every store instruction
+      // groups of 8 consecutive lanes write 8 consecutive units of one row, i.e. whole 128-B lines (16-B
+      // pieces of a line stored by different instructions measured ~1.9x the output bytes in HBM writes)
       // fold 2: column tile n0 of the folded [dx_even | dx_odd] space -> parity par, channel base cb
       const int par = g.fold == 2 ? n0 / g.cpar : 0;
       const int cb = n0 - par * (g.fold == 2 ? g.cpar : 0);
       bf16* __restrict__ outs = reinterpret_cast<bf16*>(a.out) + (long)ti.n * a.T_out * V * a.out_ld;
       bf16* __restrict__ outb = outs + (long)ti.f0 * V * a.out_ld;
-      const int rq = htid & 63, hw = htid >> 6;
-      if (4 * rq >= rows_valid) return;
-#pragma unroll
-      for (int k = 0; k < BN / 32; ++k) {  // BN/8 units of 8 channels over the 4 helper waves
-        const int cu = hw * (BN / 32) + k;
+      // 64 lanes = 8 row quads x 8 units (a 128-B line per row and store instruction); with the 520-B
+      // column stride the 8 units x 8 quads of one ds_read_b64 land on 32 distinct bank pairs (2-way)
+      constexpr int UG = BN / 64;  // groups of 8 units per row
+      const int nq = (rows_valid + 3) >> 2, nq8 = (nq + 7) >> 3;
+      for (int idx = htid; idx < UG * nq8 * 64; idx += NT) {
+        const int cl = idx & 7, ql = (idx >> 3) & 7, rest = idx >> 6;
+        const int ug = rest / nq8, qh = rest - ug * nq8;
+        const int rq = qh * 8 + ql, cu = ug * 8 + cl;
+        if (rq >= nq) continue;
         if (cb + cu * 8 >= a.Cout) continue;
         uint2 col[8];
 #pragma unroll
