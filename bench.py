@@ -91,15 +91,16 @@ LAYER_FWD_FLOP = (2.0 * N_BATCH * T_LEN * V_J * 64 * 3 * 64 + 2.0 * N_BATCH * 3 
                   + 2.0 * N_BATCH * T_LEN * V_J * 64 * 64 * 9)
 
 
-def layer_roofline(pkg, dev, reps=20):
-    """Layer-level roofline of the north_star layer's forward: the fused path (inference: pass 1 graph-conv
-    statistics, the fused graph conv + BN1 + ReLU + temporal conv kernel, BN2 + residual + ReLU) against the
-    unfused training-path forward of the same layer, both timed with HIP events around every launch of the
-    layer on the launch stream; plus the fused kernel's own launch time (events around that launch)."""
+def layer_roofline(pkg, dev, reps=20, norm="BatchNorm"):
+    """Layer-level roofline of the north_star layer's forward: the fused path (inference; BatchNorm: pass 1
+    graph-conv statistics, the fused graph conv + BN1 + ReLU + temporal conv kernel, BN2 + residual + ReLU;
+    LayerNorm: the whole layer as the one fused kernel) against the unfused training-path forward of the
+    same layer, both timed with HIP events around every launch of the layer on the launch stream; plus the
+    fused kernel's own launch time (events around that launch)."""
     K = pkg.native
     torch.manual_seed(0)
     A = torch.tensor(pkg.Graph(**pkg.PKU_MMD).A, dtype=torch.float32, device=dev)
-    layer = pkg.StgcnLayer(64, 64, (9, V_J), A.shape[0], V_J, stride=1, normalization="BatchNorm").to(dev)
+    layer = pkg.StgcnLayer(64, 64, (9, V_J), A.shape[0], V_J, stride=1, normalization=norm).to(dev)
     pkg.set_compute_dtype(layer, "bf16")
     x = torch.randn(N_BATCH, 64, T_LEN, V_J, device=dev).to(torch.bfloat16).contiguous(
         memory_format=torch.channels_last)
@@ -143,7 +144,7 @@ def layer_roofline(pkg, dev, reps=20):
     pairs = [(kev[i], kev[i + 1]) for i in range(6, len(kev) - 1, 2)]  # skip the warm-up launches
     k_ms = sum(a.elapsed_time(b) for a, b in pairs) / len(pairs) if pairs else None
     achieved = LAYER_FWD_FLOP / (fused_ms * 1e-3) / 1e12
-    return {"layer": "StgcnLayer(64, 64, (9, 25), 3, 25, BatchNorm) forward, N=64 T=300 V=25, bf16 (north_star)",
+    return {"layer": f"StgcnLayer(64, 64, (9, 25), 3, 25, {norm}) forward, N=64 T=300 V=25, bf16 (north_star)",
             "bound": "mfma", "algorithmic_gflop": round(LAYER_FWD_FLOP / 1e9, 2),
             "fused_fwd_ms": round(fused_ms, 4), "unfused_fwd_ms": round(unfused_ms, 4),
             "fused_kernel_ms": round(k_ms, 4) if k_ms else None,
@@ -366,6 +367,7 @@ def main():
         if kt and all(per.get(g) for g, _ in kt):
             traffic = sum(per[g] for g, _ in kt) / len(kt)
         lroof = layer_roofline(pkg, dev) if world == 1 else None
+        lroof_ln = layer_roofline(pkg, dev, norm="LayerNorm") if world == 1 else None
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(pkg, cpu_sd)
@@ -387,6 +389,7 @@ def main():
                          "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4) if achieved else None,
                          "traffic": traffic, "avg_launch_ms": round(k_ms, 4), "launches_timed": len(kt)},
             "layer_roofline": lroof,
+            "layer_roofline_ln": lroof_ln,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -330,6 +330,14 @@ typedef struct {
   const float* tbias;    /* [64] or NULL */
   float* stats;          /* float4 [stgcn_layer_fused_row_blocks(N, T)][64] or NULL */
   int N, T, V, P, x_ld, z_ld;
+  /* LayerNorm layer (ln = 1): the whole layer y = relu(LN2(z) + residual * x) (layernorm.py:22-28 twice,
+   * stgcn.py:181-193) is written to z; n1_scale / n1_shift / stats unused (NULL); ln*_g / ln*_b are the
+   * LayerNorm([64,1,V]) parameters TRANSPOSED to [V][64] fp32. */
+  const float* ln1_g;
+  const float* ln1_b;
+  const float* ln2_g;
+  const float* ln2_b;
+  int ln, residual;
 } stgcn_layer_fused_desc;
 
 int stgcn_layer_fused_fwd(const stgcn_layer_fused_desc* d, void* stream);

@@ -27,6 +27,16 @@
 //     (sum, sum of squares) kept in registers over the run and written once as (count, mean, M2) partials.
 // The h ring holds RF = 24 frames (a frame at slot a % RF): 16 being read for step s (frames 8s-4 ..
 // 8s+11 of the run) and 8 being written for step s+1; one block barrier per step hands them over.
+//
+// LayerNorm variant (LN = true; the ln/ configs): both norms are per frame over C x V (layernorm.py:22-28,
+// unbiased), so the WHOLE layer is this one kernel, no second pass and no statistics leave the chip:
+//   GCN waves: a frame's 64 x V graph-conv values are one wave's accumulators -> the frame's mean and
+//     variance by two DPP wave reductions -> h = relu(LN1(g)) into the ring;
+//   TCN waves: per step, per row tile and frame, the (sum, sum of squares) of the wave's 32 channels by DPP
+//     wave reductions -> LDS; after a TCN-wave-only hand-off (an LDS arrival counter: a block barrier
+//     would wait for the GCN waves too) each lane combines the (<= 4) partials of its
+//     row's frame in a fixed order (deterministic) and stores y = relu(LN2(z) + x) (identity residual of the
+//     64 -> 64 stride-1 layer, x rows re-read from L2; gamma2/beta2 staged in LDS) instead of z.
 #include "common.h"
 #include "../../include/stgcn_amd.h"
 #include <stdlib.h>
@@ -104,16 +114,24 @@ DEV float half_sum(float v) {
   return v;
 }
 
+// total over all 64 lanes (both halves)
+DEV float wave_total(float v) {
+  v = half_sum(v);
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 31)) +
+         __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+
 DEV unsigned lds_u32(const void* p) { return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p; }
 
 struct FGeom {
-  int dbg;     // A/B timing switch (STGCN_FUSED_DBG): bit 0 skip the GCN math, bit 1 skip the TCN math (results wrong)
+  int dbg;     // A/B timing switch (STGCN_FUSED_DBG; results wrong): bit 0 skip the GCN math, bit 1 the TCN math,
+               // bit 2 (LN) the residual loads, bit 3 (LN) the LN2 statistics reductions
   int runs_n;  // runs per sample
   int run;     // frames per run (multiple of CF)
   int off_tab, off_ring, off_h, off_red;  // LDS offsets
 };
 
-template <int P>
+template <int P, bool LN>
 __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_layer_fused_desc a, const FGeom g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int K16 = P * G * 2;  // 16-wide K steps of W' (P*64 / 16)
@@ -132,7 +150,10 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
   float* const sSc = reinterpret_cast<float*>(smem + g.off_tab);  // [64] BN1 scale
   float* const sBp = sSc + C;                                     // [V][64] bias2d * scale + shift
   char* const sH = smem + g.off_h;                                // [RF * V][RSH]
-  float2* const sRed = reinterpret_cast<float2*>(smem + g.off_red);  // [2][64] (sum, sum of squares)
+  float2* const sRed = reinterpret_cast<float2*>(smem + g.off_red);  // BN: [2][64] (sum, sum of squares);
+  // LN: [row tile][frame slot k < 3][channel half] (sum, sum of squares) of the step's output rows
+  float2* const sG2 = reinterpret_cast<float2*>(smem + g.off_tab);     // LN: [V][64] (gamma2, beta2)
+  unsigned* const sCnt = reinterpret_cast<unsigned*>(smem + g.off_red + 2 * RT * 3 * 2 * 8);  // LN arrivals
   const int vrs = V * RSH;  // bytes per h frame
 
   // ---- per block: W' slice, BN1 tables, zeroed panel rings (rows V..31 stay zero)
@@ -140,11 +161,16 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
     const uint4* wsrc = reinterpret_cast<const uint4*>(a.wg_frag);
     uint4* wdst = reinterpret_cast<uint4*>(sW);
     for (int e = tid; e < 2 * K16 * 64; e += NW * 64) wdst[e] = wsrc[e];
-    for (int c = tid; c < C; c += NW * 64) sSc[c] = a.n1_scale[c];
-    for (int e = tid; e < V * C; e += NW * 64) {
-      const int c = e % C;
-      const float b = a.gbias ? a.gbias[e] : 0.f;
-      sBp[e] = fmaf(b, a.n1_scale[c], a.n1_shift[c]);
+    if (LN) {
+      for (int e = tid; e < V * C; e += NW * 64) sG2[e] = make_float2(a.ln2_g[e], a.ln2_b[e]);
+      if (tid == 0) *sCnt = 0u;
+    } else {
+      for (int c = tid; c < C; c += NW * 64) sSc[c] = a.n1_scale[c];
+      for (int e = tid; e < V * C; e += NW * 64) {
+        const int c = e % C;
+        const float b = a.gbias ? a.gbias[e] : 0.f;
+        sBp[e] = fmaf(b, a.n1_scale[c], a.n1_shift[c]);
+      }
     }
     uint4* z = reinterpret_cast<uint4*>(smem + g.off_ring);
     for (int e = tid; e < NWG * SLOTS * PANEL / 16; e += NW * 64) z[e] = make_uint4(0, 0, 0, 0);
@@ -255,7 +281,55 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
             }
           }
         // epilogue: lane = joint lr, acc[t][r] = g^T[co = 32t + 8(r>>2) + 4lh + (r&3)][lr]
-        if (lr < V) {
+        if constexpr (LN) {
+          // g = acc + gbias; the frame's LayerNorm statistics over its 64 x V values (lanes lr < V)
+          const int lc = min(lr, V - 1);
+          const bool jv = lr < V;
+          float sum = 0.f;
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+              const int co = 32 * t + 8 * q4 + 4 * lh;
+              const float4 b4 = a.gbias ? *reinterpret_cast<const float4*>(a.gbias + lc * C + co)
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+              acc[t][4 * q4 + 0] += b4.x;
+              acc[t][4 * q4 + 1] += b4.y;
+              acc[t][4 * q4 + 2] += b4.z;
+              acc[t][4 * q4 + 3] += b4.w;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) sum += jv ? acc[t][4 * q4 + e] : 0.f;
+            }
+          const float cnt = (float)(V * C);
+          const float mean = wave_total(sum) / cnt;
+          float sq = 0.f;
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const float d = acc[t][r] - mean;
+              sq = fmaf(d, d, sq);
+            }
+          sq = jv ? sq : 0.f;
+          const float rstd = 1.f / sqrtf(wave_total(sq) / (cnt - 1.f) + 1e-5f);
+          if (jv) {
+            char* hr = hrow + lr * RSH;
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+              for (int q4 = 0; q4 < 4; ++q4) {
+                const int co = 32 * t + 8 * q4 + 4 * lh;
+                const float4 g4 = *reinterpret_cast<const float4*>(a.ln1_g + lr * C + co);
+                const float4 b4 = *reinterpret_cast<const float4*>(a.ln1_b + lr * C + co);
+                bf16x4 hv;
+                hv[0] = (bf16)fmaxf(fmaf((acc[t][4 * q4 + 0] - mean) * rstd, g4.x, b4.x), 0.f);
+                hv[1] = (bf16)fmaxf(fmaf((acc[t][4 * q4 + 1] - mean) * rstd, g4.y, b4.y), 0.f);
+                hv[2] = (bf16)fmaxf(fmaf((acc[t][4 * q4 + 2] - mean) * rstd, g4.z, b4.z), 0.f);
+                hv[3] = (bf16)fmaxf(fmaf((acc[t][4 * q4 + 3] - mean) * rstd, g4.w, b4.w), 0.f);
+                *reinterpret_cast<bf16x4*>(hr + co * 2) = hv;
+              }
+          }
+        } else if (lr < V) {
           char* hr = hrow + lr * RSH;
           const float* bp = sBp + lr * C;
 #pragma unroll
@@ -294,7 +368,7 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
   bf16* __restrict__ zg = reinterpret_cast<bf16*>(a.z);
   const int ct = wave & 1, rh = wave >> 1;
   // this lane's output rows (step-relative frame fo, joint w) per row tile; rows past CF*V clamp to row 0
-  int fo_[RT], hw_[RT];
+  int fo_[RT], hw_[RT], jw_[RT];
   bool rok[RT];
 #pragma unroll
   for (int i = 0; i < RT; ++i) {
@@ -302,7 +376,8 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
     rok[i] = r < CF * V;
     const int rr = rok[i] ? r : 0;
     fo_[i] = rr / V;
-    hw_[i] = (rr - fo_[i] * V) * RSH + lh * 16;
+    jw_[i] = rr - fo_[i] * V;
+    hw_[i] = jw_[i] * RSH + lh * 16;
   }
   const bf16* wlane = wt + ct * 4 * 512 + lane * 8;  // 1-KiB block [dt][ct][ks] of the [9][2][4] image
   const bf16* wcur = wlane;  // re-materialised per step (opaque): LICM would otherwise hoist all 36 weight
@@ -320,9 +395,11 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
   for (int k = 0; k < NB - 1; ++k) fw[k] = load_w(k);
   // BN2 (sum, sum of squares) of the run per channel, accumulated in LDS step by step (registers stay free
   // for the k-loop); one writer per (row half, channel): deterministic
-  for (int c = lane; c < C; c += 64)
-    if (ct == 0) sRed[rh * C + c] = make_float2(0.f, 0.f);
+  if (!LN)
+    for (int c = lane; c < C; c += 64)
+      if (ct == 0) sRed[rh * C + c] = make_float2(0.f, 0.f);
   const f32x16 zero = {};
+  unsigned arrivals = 0;  // LN: TCN-wave arrivals expected at the counter so far
   lds_barrier();  // S_0
   // the step loop per row-tile count (compile-time: no per-k-step branches in the MFMA stream)
   auto tcn_run = [&]<int RTN>() {
@@ -394,6 +471,89 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) s1[r] = s2[r] = 0.f;
+      if constexpr (LN) {
+        // the residual rows first: their L2 latency runs under the statistics phase
+        const bf16* xres = reinterpret_cast<const bf16*>(a.x) + ((long)n * T + f0) * V * a.x_ld;
+        bf16x4 rv_[RT][4];
+#pragma unroll
+        for (int i = 0; i < RT; ++i) {
+          const int r = (rh * RT + i) * 32 + lr;
+          const bool ok = i < RTN && rok[i] && r < vrows && a.residual && !(g.dbg & 4);
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4) {
+            const bf16x4 zr = {};
+            rv_[i][q4] = ok ? *reinterpret_cast<const bf16x4*>(xres + (long)r * a.x_ld + 32 * ct + 8 * q4 + 4 * lh) : zr;
+          }
+        }
+        // z = acc + bias; per row tile ti and each of the <= 3 frames its 32 rows touch (V > 16): the
+        // (sum, sum of squares) of this wave's 32 channels over the tile's rows of that frame -> LDS
+#pragma unroll
+        for (int i = 0; i < RT; ++i) {
+          if (i >= RTN) break;
+          const int r = (rh * RT + i) * 32 + lr;
+          const bool ok = rok[i] && r < vrows;
+          float su = 0.f, sq = 0.f;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            acc[i][q] += tb[q];
+            su += acc[i][q];
+            sq = fmaf(acc[i][q], acc[i][q], sq);
+          }
+          const int ti = rh * RT + i, flo = ti * 32 / V;
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            const bool m = ok && fo_[i] == flo + k;
+            float ts = 0.f, tq = 0.f;
+            if (!(g.dbg & 8)) {
+              ts = wave_total(m ? su : 0.f);
+              tq = wave_total(m ? sq : 0.f);
+            }
+            if (lane == 0) sRed[(ti * 3 + k) * 2 + ct] = make_float2(ts, tq);
+          }
+        }
+        // hand-off among the 4 TCN waves only (a block barrier would also wait for the GCN waves' next
+        // frames and serialise the two roles): an LDS arrival counter
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_fetch_add(sCnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        arrivals += NWT;
+        while (__hip_atomic_load(sCnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < arrivals)
+          __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int i = 0; i < RT; ++i) {
+          const int r = (rh * RT + i) * 32 + lr;
+          if (i >= RTN || !rok[i] || r >= vrows) continue;
+          // the row's frame statistics from the partials of the (<= 2) tiles holding the frame, fixed order
+          const int fo = fo_[i];
+          float su = 0.f, sq = 0.f;
+          for (int tj = fo * V / 32; tj <= (fo * V + V - 1) / 32; ++tj) {
+            const int k = fo - tj * 32 / V;
+            const float2 u0 = sRed[(tj * 3 + k) * 2], u1 = sRed[(tj * 3 + k) * 2 + 1];
+            su += u0.x + u1.x;
+            sq += u0.y + u1.y;
+          }
+          const float cnt = (float)(V * C), mean = su / cnt;
+          const float2 st = make_float2(mean, 1.f / sqrtf(fmaxf(sq - su * mean, 0.f) / (cnt - 1.f) + 1e-5f));
+          const int w = jw_[i];
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4) {
+            const int co = 32 * ct + 8 * q4 + 4 * lh;
+            const float4 gb0 = *reinterpret_cast<const float4*>(sG2 + w * C + co);
+            const float4 gb1 = *reinterpret_cast<const float4*>(sG2 + w * C + co + 2);
+            const float4 g4 = make_float4(gb0.x, gb0.z, gb1.x, gb1.z), b4 = make_float4(gb0.y, gb0.w, gb1.y, gb1.w);
+            float rv[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) rv[e] = (float)rv_[i][q4][e];
+            bf16x4 o;
+            o[0] = (bf16)fmaxf(fmaf((acc[i][4 * q4 + 0] - st.x) * st.y, g4.x, b4.x) + rv[0], 0.f);
+            o[1] = (bf16)fmaxf(fmaf((acc[i][4 * q4 + 1] - st.x) * st.y, g4.y, b4.y) + rv[1], 0.f);
+            o[2] = (bf16)fmaxf(fmaf((acc[i][4 * q4 + 2] - st.x) * st.y, g4.z, b4.z) + rv[2], 0.f);
+            o[3] = (bf16)fmaxf(fmaf((acc[i][4 * q4 + 3] - st.x) * st.y, g4.w, b4.w) + rv[3], 0.f);
+            *reinterpret_cast<bf16x4*>(zt + (long)r * a.z_ld + co) = o;
+          }
+        }
+        lds_barrier();  // S_s
+        continue;
+      }
 #pragma unroll
       for (int i = 0; i < RT; ++i) {
         const int r = (rh * RT + i) * 32 + lr;
@@ -468,7 +628,9 @@ long layer_fused_row_blocks(int N, int T) {
 }
 
 int layer_fused_launch(const stgcn_layer_fused_desc& a, hipStream_t s) {
-  if (!a.x || !a.z || !a.wg_frag || !a.A || !a.n1_scale || !a.n1_shift || !a.wt_frag) return STGCN_EBADSHAPE;
+  if (!a.x || !a.z || !a.wg_frag || !a.A || !a.wt_frag) return STGCN_EBADSHAPE;
+  if (a.ln ? (!a.ln1_g || !a.ln1_b || !a.ln2_g || !a.ln2_b || a.stats) : (!a.n1_scale || !a.n1_shift))
+    return STGCN_EBADSHAPE;
   if (a.N < 1 || a.T < 1 || a.V <= 16 || a.V > VMAX || a.P < 1 || a.P > 3) return STGCN_EBADSHAPE;
   if (a.x_ld < C || a.x_ld % 8 || a.z_ld < C || a.z_ld % 4) return STGCN_EBADSHAPE;
   FGeom g = plan(a.N, a.T);
@@ -480,14 +642,15 @@ int layer_fused_launch(const stgcn_layer_fused_desc& a, hipStream_t s) {
   if (nblk > 0x7fffffffL) return STGCN_EBADSHAPE;
   const int K16 = a.P * G * 2;
   g.off_tab = 2 * K16 * 1024;
-  g.off_ring = g.off_tab + ((C + a.V * C) * 4 + 255) / 256 * 256;
+  g.off_ring = g.off_tab + ((a.ln ? a.V * C * 8 : (C + a.V * C) * 4) + 255) / 256 * 256;
   g.off_h = g.off_ring + NWG * SLOTS * PANEL;
   g.off_red = g.off_h + (RF * a.V * RSH + 255) / 256 * 256;
-  const size_t lds = (size_t)g.off_red + 2 * C * 8;
+  const size_t lds = (size_t)g.off_red + (a.ln ? 2 * RT * 3 * 2 * 8 + 16 : 2 * C * 8);
   if (lds > (size_t)LDS_MAX) return STGCN_EBADSHAPE;
   typedef void (*KFn)(const stgcn_layer_fused_desc, const FGeom);
-  static const KFn tab[3] = {layer_fused_kernel<1>, layer_fused_kernel<2>, layer_fused_kernel<3>};
-  const KFn k = tab[a.P - 1];
+  static const KFn tab[2][3] = {{layer_fused_kernel<1, false>, layer_fused_kernel<2, false>, layer_fused_kernel<3, false>},
+                                {layer_fused_kernel<1, true>, layer_fused_kernel<2, true>, layer_fused_kernel<3, true>}};
+  const KFn k = tab[a.ln ? 1 : 0][a.P - 1];
   if (stgcn_lds_attr((const void*)k, LDS_MAX, s)) return STGCN_EHIP;
   hipLaunchKernelGGL(k, dim3((unsigned)nblk), dim3(NW * 64), lds, s, a, g);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;

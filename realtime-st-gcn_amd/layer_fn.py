@@ -97,17 +97,28 @@ def _packs(cache, wg, wt, P, Cin, Cout, dtype):
     return val
 
 
-def fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, sup, dtype, tag=None, cache=None):
-    """StgcnLayer.forward (stgcn.py:181-193) as the two-pass fused form (layer_fused.hip):
-    pass 1 = graph conv statistics only (gcn_tile, no g stores) -> BN1 scale/shift; pass 2 = graph conv
-    recomputed per tile + BN1 + ReLU + temporal conv in one kernel (z + BN2 partials); then
-    y = relu(BN2(z) + x).  x: channels-last bf16 (N, 64, T, V)."""
+def _ln_vc(p, V, C):
+    """LayerNorm([C,1,V]) parameter -> [V][C] fp32 (the fused kernel's per-joint rows)."""
+    return p.detach().float().reshape(C, V).t().contiguous()
+
+
+def fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, sup, dtype, tag=None, cache=None,
+                        norm=BN):
+    """StgcnLayer.forward (stgcn.py:181-193) through layer_fused.hip.  BatchNorm: the two-pass fused form
+    (SURVEY §7): pass 1 = graph conv statistics only (gcn_tile, no g stores) -> BN1 scale/shift; pass 2 =
+    graph conv recomputed per tile + BN1 + ReLU + temporal conv in one kernel (z + BN2 partials); then
+    y = relu(BN2(z) + x).  LayerNorm (per-frame norms): the whole layer is the one kernel.
+    x: channels-last bf16 (N, 64, T, V)."""
     N, Cin, T, V = x.shape
     P = A32.shape[0]
     Cout = wt.shape[0]
     dev = x.device
     bias2d = K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
     wimg, cpg, kwg, wtp = _packs(cache, wg, wt, P, Cin, Cout, dtype)
+    if norm == LN:
+        ln = (_ln_vc(n1w, V, Cout), _ln_vc(n1b, V, Cout), _ln_vc(n2w, V, Cout), _ln_vc(n2b, V, Cout))
+        return K.layer_fused(x, A32, wimg, bias2d, None, None, wtp, bt.detach().float().contiguous(), tag=tag,
+                             ln=ln, residual=residual)
     rb1, rb2 = K.gcn_tile_row_blocks(N * T, V, Cout), K.layer_fused_row_blocks(N, T)
     # both kernels write every row block of their statistics: no zero fill
     st1 = torch.empty((rb1, cpg, 4), dtype=torch.float32, device=dev)
@@ -139,11 +150,11 @@ class StgcnLayerFunction(torch.autograd.Function):
         # ---- graph convolution: g = sum_p A_p-mix(x) W_p + bias2d
         sup = cfg[5] if len(cfg) > 5 else None
         gather = sup is not None and A32.dim() == 3 and not sup.dense(P)
-        if (norm == BN and gather and len(cfg) > 7 and cfg[7]
+        if (gather and len(cfg) > 7 and cfg[7]
                 and K.layer_fused_ok(sup, P, Cin, Cout, V, kt, stride, dtype)):
             # inference: the fused layer kernel (g never leaves the chip; nothing saved for backward)
             return fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, sup, dtype,
-                                       cache=cfg[8] if len(cfg) > 8 else None)
+                                       cache=cfg[8] if len(cfg) > 8 else None, norm=norm)
         tiled = gather and K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype)  # fused frame-tiled graph conv
         bias2d = K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
         if norm == BN:  # all BatchNorm partial-statistics buffers of the layer from one zero fill

@@ -395,8 +395,11 @@ def layer_fused_row_blocks(N: int, T: int) -> int:
     return L.lib().stgcn_layer_fused_row_blocks(N, T)
 
 
-def layer_fused(x, A, wimg, gbias, n1_scale, n1_shift, wt_packed, tbias, stats=None, tag=None):
-    """stgcn_layer_fused_fwd: z rows (N, 64, T, V) = tcn(relu(BN1(gcn(x)))) + tbias, g kept on chip."""
+def layer_fused(x, A, wimg, gbias, n1_scale, n1_shift, wt_packed, tbias, stats=None, tag=None, ln=None,
+                residual=False):
+    """stgcn_layer_fused_fwd.  BatchNorm layer: z rows (N, 64, T, V) = tcn(relu(BN1(gcn(x)))) + tbias, g kept
+    on chip (+ BN2 partials).  ln = (g1, b1, g2, b2) LayerNorm parameters as [V][64] fp32: the whole layer
+    y = relu(LN2(tcn(relu(LN1(gcn(x))))) + residual * x) in this one kernel."""
     N, C, T, V = x.shape
     if getattr(wt_packed, "frag_stride", None) != 1:
         raise RuntimeError("stgcn_amd: layer_fused needs the stride-1 fragment image of the temporal weight")
@@ -404,9 +407,16 @@ def layer_fused(x, A, wimg, gbias, n1_scale, n1_shift, wt_packed, tbias, stats=N
     A = _dense(A)
     d = L.LayerFusedDesc()
     d.x, d.z, d.wg_frag, d.A = x.data_ptr(), z.data_ptr(), wimg.data_ptr(), A.data_ptr()
-    d.gbias, d.n1_scale, d.n1_shift = L.ptr(gbias), n1_scale.data_ptr(), n1_shift.data_ptr()
+    d.gbias, d.n1_scale, d.n1_shift = L.ptr(gbias), L.ptr(n1_scale), L.ptr(n1_shift)
     d.wt_frag, d.tbias, d.stats = wt_packed.frag_ptr, L.ptr(tbias), L.ptr(stats)
     d.N, d.T, d.V, d.P, d.x_ld, d.z_ld = N, T, V, A.shape[0], rows_ld(x), rows_ld(z)
+    if ln is not None:
+        ln = [_f32c(t) for t in ln]
+        if any(t.numel() != V * C for t in ln):
+            raise RuntimeError("stgcn_amd: layer_fused LayerNorm parameters must be [V][64]")
+        d.ln1_g, d.ln1_b, d.ln2_g, d.ln2_b = (t.data_ptr() for t in ln)
+        d.ln, d.residual = 1, int(bool(residual))
+        d._keep = ln
     hook = EVENT_HOOK if tag is not None else None
     if hook:
         hook(tag, "start")

@@ -95,14 +95,16 @@ def _count_fused(P, monkeypatch):
     return calls
 
 
+@pytest.mark.parametrize("norm", ["BatchNorm", "LayerNorm"])
 @pytest.mark.parametrize("residual", [True, False])
-def test_stgcn_layer_inference_fused(P, monkeypatch, residual):
-    """StgcnLayer (BN, 64 -> 64, stride 1) under no_grad takes the fused kernel; vs the fp32 oracle."""
+def test_stgcn_layer_inference_fused(P, monkeypatch, residual, norm):
+    """StgcnLayer (64 -> 64, stride 1) under no_grad takes the fused kernel (BatchNorm: two passes + BN2
+    apply; LayerNorm: the whole layer in the one kernel); vs the fp32 oracle."""
     calls = _count_fused(P, monkeypatch)
     torch.manual_seed(3)
     N, T, V = 8, 100, 25
     A = _graph(P)
-    layer = P.StgcnLayer(64, 64, (9, V), 3, V, stride=1, residual=residual, normalization="BatchNorm")
+    layer = P.StgcnLayer(64, 64, (9, V), 3, V, stride=1, residual=residual, normalization=norm)
     sd = {k: v.clone() for k, v in layer.state_dict().items()}
     g = torch.Generator().manual_seed(5)
     for k in sd:  # non-trivial affines
@@ -112,7 +114,7 @@ def test_stgcn_layer_inference_fused(P, monkeypatch, residual):
             sd[k] = 0.1 * torch.randn(sd[k].shape, generator=g)
     layer.load_state_dict(sd)
     x = torch.randn(N, 64, T, V)
-    ref = O.stgcn_layer(x, A, sd, "", 9, 1, residual, "BatchNorm")
+    ref = O.stgcn_layer(x, A, sd, "", 9, 1, residual, norm)
     layer = layer.to(DEV)
     P.set_compute_dtype(layer, "bf16")
     with torch.no_grad():
@@ -120,6 +122,35 @@ def test_stgcn_layer_inference_fused(P, monkeypatch, residual):
     torch.cuda.synchronize()
     assert len(calls) == 1, "the inference forward did not take the fused kernel"
     assert_close(y.float().cpu(), ref, 3e-2, "fused layer")
+
+
+@pytest.mark.parametrize("T", [300, 37])
+def test_layer_fused_ln_kernel(P, T):
+    """The LayerNorm whole-layer kernel through the C-ABI at the bench shape (N=64: several runs per sample)
+    and a short trial (partial last step): y vs the fp32 oracle on the same bf16-rounded operands."""
+    K = P.native
+    torch.manual_seed(T)
+    N, V, C = (64 if T == 300 else 3), 25, 64
+    A = _graph(P)
+    Pp = A.shape[0]
+    x = rb(torch.randn(N, C, T, V))
+    wg = rb(torch.randn(Pp * C, C, 1, 1) / C ** 0.5)
+    bg = torch.randn(Pp * C) * 0.1
+    wt = rb(torch.randn(C, C, 9, 1) / (9 * C) ** 0.5)
+    bt = torch.randn(C) * 0.1
+    g1, b1, g2, b2 = (1 + 0.2 * torch.randn(C, 1, V), 0.2 * torch.randn(C, 1, V), 1 + 0.2 * torch.randn(C, 1, V),
+                      0.2 * torch.randn(C, 1, V))
+    h = torch.relu(O.layernorm_cv(O.tgcn(x, wg, bg, A), g1, b1))
+    ref = torch.relu(O.layernorm_cv(F.conv2d(rb(h), wt, bt, padding=(4, 0)), g2, b2) + x)
+    A_d = A.to(DEV)
+    bias2d = K.gcn_bias(A_d, bg.to(DEV), N, C)
+    wgf = wg.view(Pp, C, C).permute(1, 0, 2).reshape(C, Pp * C).to(DEV)
+    wimg, _, _ = K.pack_gcn_weight(wgf, BF)
+    wtp, _, _ = K.pack_weight(wt.squeeze(-1).permute(2, 0, 1).to(DEV), BF, stride=1)
+    vc = lambda t: t.reshape(C, V).t().contiguous().to(DEV)  # noqa: E731
+    y = K.layer_fused(cl(x, BF), A_d, wimg, bias2d, None, None, wtp, bt.to(DEV),
+                      ln=(vc(g1), vc(b1), vc(g2), vc(b2)), residual=True)
+    assert_close(y.float(), ref, 3e-2, "fused LN layer")
 
 
 def test_model_inference_fused_config2(P, monkeypatch):

@@ -12,4 +12,6 @@ import bench  # noqa: E402
 if __name__ == "__main__":
     pkg = ge.load_package()
     dev = torch.device("cuda", 0)
-    print(json.dumps(bench.layer_roofline(pkg, dev, reps=int(sys.argv[1]) if len(sys.argv) > 1 else 20)))
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    norm = sys.argv[2] if len(sys.argv) > 2 else "BatchNorm"
+    print(json.dumps(bench.layer_roofline(pkg, dev, reps=reps, norm=norm)))
