@@ -170,12 +170,22 @@ int attn_scores_launch(const void* th, const void* ph, int ld, int N, int T_, in
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
 
+int jmix_launch(const void* in, int in_ld, void* out, int out_ld, const float* M, int N, int T, int V, int P, int C,
+                int mode, int bt, int per_sample, int accumulate, int dtype, hipStream_t s);
+
 int attn_bwd_launch(const void* th, const void* ph, int ld, int N, int T_, int V, int P, int ce, const float* C,
                     const float* dC, float* dS, void* dth, void* dph, int dtype, hipStream_t s) {
   if (V > VMAX || P > 4) return STGCN_EBADSHAPE;
   const long rows = (long)N * P * V;
   hipLaunchKernelGGL(attn_softmax_bwd_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, C, dC, dS, rows,
                      V);
+  // dth = dS-mix of phi, dph = dS^T-mix of theta, per (sample, partition) channel group: MFMA (jmix.hip)
+  const int r1 = jmix_launch(ph, ld, dth, ld, dS, N, T_, V, P, ce, 2, 1, 1, 0, dtype, s);
+  if (r1 > 0) return r1;
+  if (r1 == 0) {
+    const int r2 = jmix_launch(th, ld, dph, ld, dS, N, T_, V, P, ce, 2, 0, 1, 0, dtype, s);
+    if (r2 >= 0) return r2;
+  }
   int fpb = (4096 + V * P * ce - 1) / (V * P * ce);
   if (fpb < 1) fpb = 1;
   dim3 grid((T_ + fpb - 1) / fpb, N);

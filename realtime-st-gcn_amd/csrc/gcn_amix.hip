@@ -341,10 +341,17 @@ int frames_per_block(int items_per_frame) {
     }                                                                                               \
   } while (0)
 
+int jmix_launch(const void* in, int in_ld, void* out, int out_ld, const float* M, int N, int T, int V, int P, int C,
+                int mode, int bt, int per_sample, int accumulate, int dtype, hipStream_t s);
+
 int amix_fwd_launch(const AmixArgs& a0, int dtype, hipStream_t s) {
   if (a0.V > VMAX || a0.P > 4) return STGCN_EBADSHAPE;
   AmixArgs a = a0;
   a.out_ld = a.P * a.Cin;
+  // dense joint mixing on MFMA (jmix.hip) where the shape allows; the gather kernel otherwise
+  const int r = jmix_launch(a.x, a.x_ld, a.out, a.out_ld, a.A, a.N, a.T, a.V, a.P, a.Cin, 0, 0, a.per_sample, 0,
+                            dtype, s);
+  if (r >= 0) return r;
   AMIX_DISPATCH(amix_fwd_kernel, a, a.V * a.P, dtype, s);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
@@ -352,9 +359,10 @@ int amix_fwd_launch(const AmixArgs& a0, int dtype, hipStream_t s) {
 int amix_trans_launch(const AmixArgs& a0, int dtype, hipStream_t s) {
   if (a0.V > VMAX || a0.P > 4) return STGCN_EBADSHAPE;
   AmixArgs a = a0;
-  const int xld = a.x_ld;
   a.x_ld = a.P * a.Cin;  // DW rows
-  (void)xld;
+  const int r = jmix_launch(a.x, a.x_ld, a.out, a.out_ld, a.A, a.N, a.T, a.V, a.P, a.Cin, 1, 0, a.per_sample,
+                            a.accumulate, dtype, s);
+  if (r >= 0) return r;
   AMIX_DISPATCH(amix_trans_kernel, a, a.V, dtype, s);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
