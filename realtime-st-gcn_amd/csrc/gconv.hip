@@ -66,7 +66,7 @@ struct GGeom {
 };
 
 // ------------------------------------------------------------------ gather GEMM (fwd and data grad)
-// ACCV: accumulate (out +=) through the vectorised LDS-scratch epilogue; a separate instantiation so
+// ACCV: stores (and accumulate, out +=) through the vectorised LDS-scratch epilogue; a separate instantiation so
 // the plain-store kernel keeps its register budget (<= 128 VGPRs: 2 blocks per CU)
 template <typename T, int WM, int WN, int TM, int TN, int KC, bool ACCV>
 __global__ __launch_bounds__(WM * WN * 64, 2) void gconv_kernel(const stgcn_gconv_desc a, const GGeom g) {
@@ -232,9 +232,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gconv_kernel(const stgcn_gcon
   constexpr int SROW = 32 * (int)sizeof(T) + 16;  // padded scratch row (bytes)
   constexpr int UR = 32 * (int)sizeof(T) / 16;     // 16-B units per 32-column row
   char* scratch = smem + wave * 32 * SROW;
-  // measured: the scratch path pays off for the read-modify-write (accumulate) case only; plain stores
-  // stay scattered (fewer LDS round trips, lower register pressure)
-  constexpr bool vec_out = ACCV;  // launcher: ACCV only with accumulate and 16-B aligned rows
+  constexpr bool vec_out = ACCV;  // launcher: ACCV when rows are 16-B aligned
   Welford ws[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -287,11 +285,15 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gconv_kernel(const stgcn_gcon
           if (rb + row < rows_valid && c0 + u * VEC < a.Cout) {
             T* p = out + ((long)(i0 + rb + row) * V + jt) * a.out_ld + c0 + u * VEC;
             float f[VEC], o[VEC];
-            unpack16(*reinterpret_cast<const uint4*>(scratch + row * SROW + u * 16), f, (T*)nullptr);
-            unpack16(*reinterpret_cast<const uint4*>(p), o, (T*)nullptr);
+            if (a.accumulate) {
+              unpack16(*reinterpret_cast<const uint4*>(scratch + row * SROW + u * 16), f, (T*)nullptr);
+              unpack16(*reinterpret_cast<const uint4*>(p), o, (T*)nullptr);
 #pragma unroll
-            for (int e = 0; e < VEC; ++e) f[e] += o[e];
-            *reinterpret_cast<uint4*>(p) = pack16(f, (T*)nullptr);
+              for (int e = 0; e < VEC; ++e) f[e] += o[e];
+              *reinterpret_cast<uint4*>(p) = pack16(f, (T*)nullptr);
+            } else {
+              *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(scratch + row * SROW + u * 16);
+            }
           }
         }
       }
@@ -360,7 +362,11 @@ int launch_gconv(const stgcn_gconv_desc& a, hipStream_t s) {
   if (stgcn_lds_attr((const void*)gconv_kernel<T, WM, WN, TM, TN, KC, false>, 160 * 1024, s) ||
       stgcn_lds_attr((const void*)gconv_kernel<T, WM, WN, TM, TN, KC, true>, 160 * 1024, s))
     return STGCN_EHIP;
-  const bool accv = a.accumulate && (a.out_ld % VEC) == 0 && (a.Cout % VEC) == 0;
+  // 16-B row stores through the LDS scratch whenever rows are 16-B aligned (A/B: STGCN_GCONV_SCATTER=1 keeps
+  // the per-element stores for plain outputs)
+  const char* sce = getenv("STGCN_GCONV_SCATTER");
+  const bool scatter = sce && sce[0] == '1';
+  const bool accv = (a.accumulate || !scatter) && (a.out_ld % VEC) == 0 && (a.Cout % VEC) == 0;
   if (accv)
     hipLaunchKernelGGL((gconv_kernel<T, WM, WN, TM, TN, KC, true>), dim3((unsigned)nblk), dim3(WM * WN * 64), lds, s,
                        a, g);

@@ -153,10 +153,12 @@ def test_layer_fused_ln_kernel(P, T):
     assert_close(y.float(), ref, 3e-2, "fused LN layer")
 
 
-def test_model_inference_fused_config2(P, monkeypatch):
-    """The config-2 model (9 layers, N=16 T=300) in inference: layers 0-2 run fused; logits vs the oracle."""
+@pytest.mark.parametrize("norm", ["BatchNorm", "LayerNorm"])
+def test_model_inference_fused_config2(P, monkeypatch, norm):
+    """The config-2 model (9 layers, N=16 T=300; as_is BatchNorm and the ln/ LayerNorm variant) in
+    inference: layers 0-2 run fused; logits vs the oracle."""
     calls = _count_fused(P, monkeypatch)
-    arch = {"strategy": "spatial", "in_feat": 3, "normalization": "BatchNorm", "num_classes": 52,
+    arch = {"strategy": "spatial", "in_feat": 3, "normalization": norm, "num_classes": 52,
             "output_type": "logits",
             "st-gcn": {"in_feat": 3, "layers": 9, "kernel": 9, "importance": True,
                        "in_ch": [64, 64, 64, 64, 128, 128, 128, 256, 256],
