@@ -276,6 +276,12 @@ int stgcn_rt_online_step(const void* z_f32, float* fifo, float* acc, int* idx, i
 /* AAGCN attention adjacency (models/aagcn/aagcn.py:142-145): C[n,p] = softmax_w(theta_p^T phi_p) over
  * K = T*ce, theta/phi rows [N][T][V][ld] (channel p*ce+c).  C: fp32 [N][P][V][V].  Backward writes
  * dS (scratch, fp32 like C) and dtheta/dphi (rows like theta/phi). */
+/* AgcnLayer's theta / phi projections for a bf16 model (aagcn.py:139-141): out[r][o] = bias[o] +
+ * sum_c w[o][c] x[r][c], x bf16 rows [M][ldx] (Cin % 16 == 0, <= 256), w fp32 [Nout][Cin] (theta and phi
+ * stacked), out fp32 rows [M][ldo]: fp32-accurate outputs (w split into two bf16 parts on the matrix cores)
+ * without converting x; the attention logits need fp32 theta/phi. */
+int stgcn_attn_proj(const void* x, int ldx, long M, int Cin, const float* w, const float* bias, int Nout, float* out,
+                    int ldo, void* stream);
 /* work: stgcn_attn_scores_workspace() bytes (deterministic T-chunk reduction) or NULL (atomics). */
 long stgcn_attn_scores_workspace(int N, int T, int V, int P);
 int stgcn_attn_scores(const void* theta, const void* phi, int ld, int N, int T, int V, int P, int ce, float* C,

@@ -152,6 +152,7 @@ _SIGS = {
     "stgcn_window_grad_workspace": (ctypes.c_long, [c_int] * 5),
     "stgcn_window_grad": (c_int, [c_void_p, c_int, c_int, c_void_p] + [c_int] * 7 + [c_void_p] * 4 + [c_int] +
                           [c_void_p] * 6),
+    "stgcn_attn_proj": (c_int, [c_void_p, c_int, c_long, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),
     "stgcn_segment_metrics_workspace": (ctypes.c_long, [c_int]),
     "stgcn_segment_metrics": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
                                       c_void_p, c_void_p, c_void_p]),

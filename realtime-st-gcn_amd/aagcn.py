@@ -41,8 +41,14 @@ class AgcnLayer(nn.Module):
         # with bf16-stored theta/phi their rounding moves the logits by O(0.1) and the softmax weights by
         # O(10 %), so this branch runs in fp32 on every compute dtype (it is ~3 % of the layer's work).
         att = torch.float32
-        theta = LF.Conv1x1Function.apply(x, self.theta.weight, self.theta.bias, att)
-        phi = LF.Conv1x1Function.apply(x, self.phi.weight, self.phi.bias, att)
+        Cin = self.theta.weight.shape[1]
+        if LF.attn_proj_ok(x, Cin, self.theta.weight.shape[0], self.phi.weight.shape[0], self.compute_dtype):
+            # bf16 model: fp32 theta/phi straight from the bf16 activation (attn_proj, W split hi + lo)
+            theta, phi = LF.AttnProjFunction.apply(x, self.theta.weight, self.theta.bias, self.phi.weight,
+                                                   self.phi.bias)
+        else:
+            theta = LF.Conv1x1Function.apply(x, self.theta.weight, self.theta.bias, att)
+            phi = LF.Conv1x1Function.apply(x, self.phi.weight, self.phi.bias, att)
         C = LF.AttentionFunction.apply(theta, phi, self.partitions, att)         # (N, P, V, V)
         return self.st_gcn(x, A + self.B + C)                                    # aagcn.py:148
 

@@ -202,3 +202,105 @@ int attn_bwd_launch(const void* th, const void* ph, int ld, int N, int T_, int V
   }
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
+
+// ---------------------------------------------------------------- attention projections (bf16 path)
+// out[r][o] = bias[o] + sum_c W[o][c] x[r][c]  for theta and phi stacked (o < Nout): x bf16 rows (exact
+// values), W fp32 split as W_hi + W_lo (two bf16 MFMAs, ~2^-17 relative coefficient error) and fp32
+// outputs: the attention logits contract theta^T phi over C'*T terms and then a softmax, so theta/phi
+// must not be rounded to bf16 (aagcn.py:142-145), but they need no fp32 MFMA either.
+// D^T = W x^T on 32x32x16 MFMAs: A = W rows (m = output channel) from LDS (hi/lo staged once per block for
+// its group of <= 128 output channels), B = x rows (n = row) straight from global as 16-B fragments held
+// in registers for all channel tiles; D lane = row, 4 consecutive channels per float4 store.
+namespace {
+constexpr int PJ_CG = 128;  // output channels per block group
+template <int KSN>
+__global__ __launch_bounds__(256) void attn_proj_kernel(const bf16* __restrict__ x, int ldx, long M, int Cin,
+                                                        const float* __restrict__ W, const float* __restrict__ bias,
+                                                        int Nout, float* __restrict__ out, int ldo, int rt_per_block) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int RS = Cin * 2 + 16;  // padded LDS row bytes
+  char* const sHi = smem;
+  char* const sLo = smem + PJ_CG * RS;
+  const int g = blockIdx.y;
+  const int o0 = g * PJ_CG, og = min(PJ_CG, Nout - o0);
+  for (int e = threadIdx.x; e < PJ_CG * Cin; e += 256) {  // stage W_hi / W_lo (rows >= og: zeros)
+    const int o = e / Cin, c = e - o * Cin;
+    const float w = o < og ? W[(long)(o0 + o) * Cin + c] : 0.f;
+    const bf16 h = (bf16)w;
+    *reinterpret_cast<bf16*>(sHi + o * RS + c * 2) = h;
+    *reinterpret_cast<bf16*>(sLo + o * RS + c * 2) = (bf16)(w - (float)h);
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, lr = lane & 31, lh = lane >> 5;
+  const int ntile = (og + 31) / 32;
+  const long rt_total = (M + 31) / 32;
+  const long rt0 = (long)blockIdx.x * rt_per_block, rt1 = min(rt_total, rt0 + rt_per_block);
+  for (long rt = rt0 + wave; rt < rt1; rt += 4) {
+    const long row = rt * 32 + lr;
+    const bool rok = row < M;
+    bf16x8 xf[KSN];
+#pragma unroll
+    for (int ks = 0; ks < KSN; ++ks) {
+      const uint4 u = rok ? *reinterpret_cast<const uint4*>(x + row * ldx + 16 * ks + 8 * lh) : make_uint4(0, 0, 0, 0);
+      xf[ks] = __builtin_bit_cast(bf16x8, u);
+    }
+    for (int ct = 0; ct < ntile; ++ct) {
+      f32x16 acc = {};
+      const char* ah = sHi + (ct * 32 + lr) * RS + lh * 16;
+      const char* al = sLo + (ct * 32 + lr) * RS + lh * 16;
+#pragma unroll
+      for (int ks = 0; ks < KSN; ++ks) {
+        const bf16x8 wh = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(ah + ks * 32));
+        const bf16x8 wl = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(al + ks * 32));
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xf[ks], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, xf[ks], acc, 0, 0, 0);
+      }
+      if (rok) {
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+          const int o = ct * 32 + 8 * q4 + 4 * lh;  // within the group
+          if (o >= og) continue;
+          float4 v = make_float4(acc[4 * q4], acc[4 * q4 + 1], acc[4 * q4 + 2], acc[4 * q4 + 3]);
+          if (bias) {
+            const float4 b = *reinterpret_cast<const float4*>(bias + o0 + o);
+            v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+          }
+          *reinterpret_cast<float4*>(out + row * ldo + o0 + o) = v;
+        }
+      }
+    }
+  }
+}
+}  // namespace
+
+int attn_proj_launch(const void* x, int ldx, long M, int Cin, const float* W, const float* bias, int Nout, float* out,
+                     int ldo, hipStream_t s) {
+  if (!x || !W || !out || M < 1 || Nout < 1 || Nout % 4 || ldo < Nout || ldo % 4 || Cin % 16 || Cin < 16 ||
+      Cin > 256 || ldx < Cin || ldx % 8)
+    return STGCN_EBADSHAPE;
+  const int KSN = Cin / 16;
+  const long rt_total = (M + 31) / 32;
+  const int groups = (Nout + PJ_CG - 1) / PJ_CG;
+  const int ncu = stgcn_cu_count(s);
+  long blocks = (long)(ncu > 0 ? ncu : 256) * 4 / groups;
+  if (blocks < 1) blocks = 1;
+  long rpb = (rt_total + blocks - 1) / blocks;
+  if (rpb < 4) rpb = 4;
+  blocks = (rt_total + rpb - 1) / rpb;
+  const size_t lds = (size_t)2 * PJ_CG * (Cin * 2 + 16);
+  const dim3 grid((unsigned)blocks, (unsigned)groups);
+  switch (KSN) {
+#define PJ_CASE(K)                                                                                            \
+  case K:                                                                                                     \
+    if (stgcn_lds_attr((const void*)attn_proj_kernel<K>, (int)lds, s)) return STGCN_EHIP;                      \
+    hipLaunchKernelGGL(attn_proj_kernel<K>, grid, dim3(256), lds, s, (const bf16*)x, ldx, M, Cin, W, bias, Nout, \
+                       out, ldo, (int)rpb);                                                                   \
+    break;
+    PJ_CASE(1) PJ_CASE(2) PJ_CASE(3) PJ_CASE(4) PJ_CASE(5) PJ_CASE(6) PJ_CASE(7) PJ_CASE(8)
+    PJ_CASE(9) PJ_CASE(10) PJ_CASE(11) PJ_CASE(12) PJ_CASE(13) PJ_CASE(14) PJ_CASE(15) PJ_CASE(16)
+#undef PJ_CASE
+    default:
+      return STGCN_EBADSHAPE;
+  }
+  return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
+}

@@ -81,6 +81,8 @@ int rt_online_launch(const float* z, float* fifo, float* acc, int* idx, int C, i
 int attn_scores_launch(const void* th, const void* ph, int ld, int N, int T_, int V, int P, int ce, float* S,
                        void* work, int dtype, hipStream_t s);
 long attn_scores_workspace(int N, int T_, int V, int P);
+int attn_proj_launch(const void* x, int ldx, long M, int Cin, const float* W, const float* bias, int Nout, float* out,
+                     int ldo, hipStream_t s);
 int attn_bwd_launch(const void* th, const void* ph, int ld, int N, int T_, int V, int P, int ce, const float* C,
                     const float* dC, float* dS, void* dth, void* dph, int dtype, hipStream_t s);
 int layer_fused_launch(const stgcn_layer_fused_desc& a, hipStream_t s);
@@ -343,6 +345,10 @@ int stgcn_rt_online_step(const void* z, float* fifo, float* acc, int* idx, int C
 }
 
 long stgcn_attn_scores_workspace(int N, int T, int V, int P) { return attn_scores_workspace(N, T, V, P); }
+int stgcn_attn_proj(const void* x, int ldx, long M, int Cin, const float* w, const float* bias, int Nout, float* out,
+                    int ldo, void* stream) {
+  return attn_proj_launch(x, ldx, M, Cin, w, bias, Nout, out, ldo, STREAM(stream));
+}
 int stgcn_attn_scores(const void* th, const void* ph, int ld, int N, int T, int V, int P, int ce, float* C, void* work,
                       int dtype, void* stream) {
   CHECK_DTYPE(dtype);

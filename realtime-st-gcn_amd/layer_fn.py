@@ -658,6 +658,53 @@ class AttentionFunction(torch.autograd.Function):
         return dth, dph, None, None
 
 
+def attn_proj_ok(x, Cin, Nt, Np, dtype) -> bool:
+    return dtype == torch.bfloat16 and Cin % 16 == 0 and Cin <= 256 and Nt % 4 == 0 and Np % 4 == 0
+
+
+class AttnProjFunction(torch.autograd.Function):
+    """AgcnLayer's theta and phi 1x1 convs (aagcn.py:139-141) for a bf16 model: one fp32-output projection
+    of the bf16 activation (stgcn_attn_proj: no fp32 copy of x, no fp32 GEMM), theta and phi the two
+    channel halves of one row buffer.  Backward: the two gradients (one buffer from attn_bwd) rounded to
+    bf16 once, then the bf16 transposed 1x1 conv (dx) and weight-gradient kernels; the bias gradients are
+    column sums of the fp32 gradients."""
+
+    @staticmethod
+    def forward(ctx, x, wt, bt, wp, bp):
+        x = K.to_rows(x, torch.bfloat16)
+        Nt, Np = wt.shape[0], wp.shape[0]
+        Cin = x.shape[1]
+        W = torch.cat([wt.detach().float().reshape(Nt, Cin), wp.detach().float().reshape(Np, Cin)])
+        b = torch.cat([bt.detach().float(), bp.detach().float()])
+        out = K.attn_proj(x, W, b)
+        ctx.save_for_backward(x, W)
+        ctx.split = (Nt, Np)
+        ctx.shapes = (wt.shape, wp.shape, wt.dtype)
+        return out[:, :Nt], out[:, Nt:]
+
+    @staticmethod
+    def backward(ctx, dth, dph):
+        x, W = ctx.saved_tensors
+        Nt, Np = ctx.split
+        N, Cin, T, V = x.shape
+        Nout = Nt + Np
+        es = dth.element_size()
+        if (dth.dim() == 4 and K.rows_ld(dth) == Nout and K.rows_ld(dph) == Nout
+                and dph.data_ptr() - dth.data_ptr() == Nt * es):
+            D = torch.as_strided(dth, (N, Nout, T, V), dth.stride())  # the attn_bwd buffer, both halves
+        else:
+            D = torch.cat([dth, dph], 1).contiguous(memory_format=torch.channels_last)
+        D = D.float()
+        D16 = D.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        wT, cq, kq = K.pack_weight(W.t().reshape(1, Cin, Nout), torch.bfloat16)
+        dx = K.conv_rows(D16, wT, Nout, Cin, cq, kq, T, T, trans=True)
+        dW = K.conv_wgrad(x, D16, Cin, Nout, T, T).view(Nout, Cin)
+        db = K.bn_bwd_reduce(D, N * T * V, Nout)[:, 0]
+        wts, wps, wdt = ctx.shapes
+        return (dx, dW[:Nt].reshape(wts).to(wdt), db[:Nt].to(wdt), dW[Nt:].reshape(wps).to(wdt),
+                db[Nt:].to(wdt))
+
+
 class RtOfflineLayerFunction(torch.autograd.Function):
     """OfflineLayer.forward (models/rtstgcn/rtstgcn.py:343-389) with the Toeplitz matmul it intends
     (rtstgcn.py:366-379) evaluated as the causal K//S-tap box sum it is:

@@ -654,11 +654,33 @@ def attn_scores(theta, phi, P):
     return C
 
 
+def attn_proj(x, w, b):
+    """theta/phi projections of a bf16 activation, fp32 out: rows (N, Nout, T, V) = w x + b (stgcn_attn_proj)."""
+    N, Cin, T, V = x.shape
+    Nout = w.shape[0]
+    out = cl_empty(N, Nout, T, V, torch.float32, x.device)
+    w = _f32c(w.reshape(Nout, Cin))
+    b = None if b is None else _f32c(b)
+    L.check(L.lib().stgcn_attn_proj(x.data_ptr(), rows_ld(x), N * T * V, Cin, w.data_ptr(), L.ptr(b), Nout,
+                                    out.data_ptr(), Nout, L.stream()), "attn_proj")
+    return out
+
+
 def attn_bwd(theta, phi, P, C, dC):
+    """(dtheta, dphi) as rows with theta's row stride; when theta and phi are the two halves of one row
+    buffer (attn_proj's output), so are the gradients (one buffer, no concatenation downstream)."""
     N, CH, T, V = theta.shape
     dS = torch.empty_like(C)
-    dth = torch.empty_like(theta)
-    dph = torch.empty_like(phi)
+    ld = rows_ld(theta)
+    if rows_ld(phi) != ld:
+        raise RuntimeError("stgcn_amd: attn_bwd needs theta and phi with the same row stride")
+    es = theta.element_size()
+    if ld >= 2 * CH and phi.data_ptr() - theta.data_ptr() == CH * es:
+        buf = torch.empty((N, T, V, ld), dtype=theta.dtype, device=theta.device).permute(0, 3, 1, 2)
+        dth, dph = buf[:, :CH], buf[:, CH:2 * CH]
+    else:
+        dth = torch.empty((N, T, V, ld), dtype=theta.dtype, device=theta.device).permute(0, 3, 1, 2)[:, :CH]
+        dph = torch.empty((N, T, V, ld), dtype=phi.dtype, device=phi.device).permute(0, 3, 1, 2)[:, :CH]
     L.check(L.lib().stgcn_attn_bwd(theta.data_ptr(), phi.data_ptr(), rows_ld(theta), N, T, V, P, CH // P,
                                    C.data_ptr(), dC.data_ptr(), dS.data_ptr(), dth.data_ptr(), dph.data_ptr(),
                                    L.dtype_code(theta.dtype), L.stream()), "attn_bwd")

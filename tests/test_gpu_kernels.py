@@ -376,3 +376,17 @@ def test_gcn_tile(K, pkg, cin, cout, T, N):
     wT, cq, kwT = K.pack_gcn_weight(W.view(P, cout, cin).permute(2, 0, 1).reshape(cin, P * cout).to(DEV), torch.bfloat16)
     dx = K.gcn_tile(cl(dg, torch.bfloat16), A32, wT, kwT, cout, cin, cq, sup, trans_a=True)
     assert_close(dx.float(), xr.grad, 2e-2, "gcn_tile dgrad")
+
+
+@pytest.mark.parametrize("Cin,Nout", [(64, 96), (128, 192), (256, 384), (16, 8)])
+def test_attn_proj(K, Cin, Nout):
+    """stgcn_attn_proj: fp32 theta/phi from a bf16 activation with the weight split into two bf16 parts:
+    within fp32 rounding of the fp32 product on the same (bf16-valued) inputs."""
+    torch.manual_seed(Cin + Nout)
+    N, T, V = 3, 37, 25
+    x = torch.randn(N, Cin, T, V).to(torch.bfloat16)
+    w = torch.randn(Nout, Cin) / Cin ** 0.5
+    b = torch.randn(Nout) * 0.1
+    ref = torch.einsum("oc,nctv->notv", w.double(), x.double()) + b.double().view(1, -1, 1, 1)
+    got = K.attn_proj(cl(x.float(), torch.bfloat16), w.to(DEV), b.to(DEV))
+    assert_close(got.cpu(), ref, 1e-5, "attn_proj")
