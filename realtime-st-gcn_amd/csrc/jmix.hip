@@ -23,7 +23,7 @@
 namespace {
 
 constexpr int NWJ = 4;             // waves per block
-constexpr int PMAXJ = 4;
+constexpr int PMAXJ = 3;
 constexpr int ITEMS_PER_WAVE = 16;  // target work items per wave (sizes the grid)
 
 template <typename T> struct JT;
@@ -79,7 +79,7 @@ struct JmixArgs {
   int cin;      // input channels per row (mode 0: C, else P*C)
 };
 
-template <typename T>
+template <typename T, int NP>
 __global__ __launch_bounds__(NWJ * 64) void jmix_kernel(const JmixArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int PANEL = JT<T>::PANEL, KS = JT<T>::KS;
@@ -88,9 +88,10 @@ __global__ __launch_bounds__(NWJ * 64) void jmix_kernel(const JmixArgs a) {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lr = lane & 31, lh = lane >> 5;
   const int V = a.V;
-  char* const buf = smem + wave * 2 * PMAXJ * PANEL;  // [2][npan] panels
+  constexpr int NBUF = 3;  // items in flight: the current one and the next two
+  char* const buf = smem + wave * NBUF * NP * PANEL;  // [NBUF][NP] panels
   // rows V..31 stay zero (the DMA never writes them)
-  for (int e = lane; e < 2 * PMAXJ * PANEL / 16; e += 64) reinterpret_cast<uint4*>(buf)[e] = make_uint4(0, 0, 0, 0);
+  for (int e = lane; e < NBUF * NP * PANEL / 16; e += 64) reinterpret_cast<uint4*>(buf)[e] = make_uint4(0, 0, 0, 0);
   __builtin_amdgcn_s_waitcnt(0);
 
   const long gw = (long)blockIdx.x * NWJ + wave;
@@ -107,18 +108,24 @@ __global__ __launch_bounds__(NWJ * 64) void jmix_kernel(const JmixArgs a) {
   };
   const int lrow = lane / UPR, lunit = lane % UPR;
   constexpr int RPI = 64 / UPR;  // panel rows per DMA instruction
+  // Every lane issues every DMA instruction (a fixed count per item, DMA_OPS, for the counted waits below):
+  // lanes past the frame's V rows or past a partial last channel block (mode 2) copy the frame's first
+  // unit instead — finite data, multiplied by zero coefficients (rows >= V) or masked (channels).
+  constexpr int DMA_OPS = NP * (32 / RPI);
   auto issue = [&](long it, int slot) {
     const long i = it / a.nob;
     const int ob = (int)(it - i * a.nob);
     const T* src0 = in + i * V * (long)a.in_ld;
-    for (int k = 0; k < a.npan; ++k) {
-      const unsigned pan = lds_u32(buf + (slot * PMAXJ + k) * PANEL);
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const unsigned pan = lds_u32(buf + (slot * NP + k) * PANEL);
       const int cb = panel_col(ob, k);
-      const bool uok = cb + lunit * (16 / ELT) < a.cin;  // a partial last block (mode 2) reads no further
+      const bool uok = cb + lunit * (16 / ELT) < a.cin;
 #pragma unroll
       for (int rr = 0; rr < 32; rr += RPI) {
         const int row = rr + lrow;
-        if (row < V && uok) dma16(src0 + (long)row * a.in_ld + cb + lunit * (16 / ELT), pan + rr * 32 * ELT);
+        const bool ok = row < V && uok;
+        dma16(ok ? src0 + (long)row * a.in_ld + cb + lunit * (16 / ELT) : src0, pan + rr * 32 * ELT);
       }
     }
   };
@@ -156,22 +163,77 @@ __global__ __launch_bounds__(NWJ * 64) void jmix_kernel(const JmixArgs a) {
     }
   };
 
-  issue(it0, 0);
+  // Pipeline per item j: [wait: panels(j), the accumulate loads(j-1) and the stores(j-2) are all a whole
+  // item old] [stores(j-1)] [DMA panels(j+1)] [accumulate loads(j)] [mix(j) -> registers].  Every global
+  // access of an item is thus covered by the next item's MFMAs instead of a wait right behind it.
+  typedef std::conditional_t<sizeof(T) == 2, bf16x4, float4> OVec;
   const f32x16 zero = {};
+  f32x16 pend = zero;                     // the previous item's results
+  OVec pold[4];                           // its accumulate operands
+  long pend_i = -1;
+  int pend_ob = 0;
+  auto out_ptr = [&](long i, int ob, int q4) {
+    return out + (i * V + lr) * (long)a.out_ld + 32 * ob + 8 * q4 + 4 * lh;
+  };
+  auto ch_ok = [&](int ob, int q4) { return lr < V && 32 * ob + 8 * q4 + 4 * lh < a.cout; };
+  auto flush = [&]() {
+    if (pend_i < 0) return;
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      if (!ch_ok(pend_ob, q4)) continue;
+      float v[4] = {pend[4 * q4], pend[4 * q4 + 1], pend[4 * q4 + 2], pend[4 * q4 + 3]};
+      if constexpr (sizeof(T) == 2) {
+        if (a.accumulate) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += (float)pold[q4][e];
+        }
+        bf16x4 r;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) r[e] = (bf16)v[e];
+        *reinterpret_cast<bf16x4*>(out_ptr(pend_i, pend_ob, q4)) = r;
+      } else {
+        if (a.accumulate) {
+          v[0] += pold[q4].x; v[1] += pold[q4].y; v[2] += pold[q4].z; v[3] += pold[q4].w;
+        }
+        *reinterpret_cast<float4*>(out_ptr(pend_i, pend_ob, q4)) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  };
+
+  // Order per item j: [stores(j-1)] [accumulate loads(j)] [DMA(j+2)] [mix(j)] [wait].  The youngest ops at
+  // the wait are DMA(j+2)'s DMA_OPS; waiting until at most DMA_OPS are outstanding (in-order completion)
+  // retires DMA(j+1), the loads(j) and everything older, and leaves j+2's panels in flight.
+  issue(it0, 0);
+  if (it0 + 1 < it1) {
+    issue(it0 + 1, 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA_OPS) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   for (long it = it0; it < it1; ++it) {
-    const int slot = (int)((it - it0) & 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this item's panels (and the previous item's stores)
-    if (it + 1 < it1) issue(it + 1, slot ^ 1);        // the next item's panels fly under this one's MFMAs
+    const int slot = (int)((it - it0) % NBUF);
+    flush();
     const long i = it / a.nob;
     const int ob = (int)(it - i * a.nob);
+    if (a.accumulate) {
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4)
+        if (ch_ok(ob, q4)) pold[q4] = *reinterpret_cast<const OVec*>(out_ptr(i, ob, q4));
+    }
+    if (it + 2 < it1) {
+      int s2 = slot + 2;
+      s2 = s2 >= NBUF ? s2 - NBUF : s2;
+      issue(it + 2, s2);  // two items ahead: their panels fly under this item's and the next one's MFMAs
+    }
     const long n = i / a.T;
     if (n != cur_n) {
       load_coef(n);
       cur_n = n;
     }
     f32x16 acc = zero;
-    for (int k = 0; k < a.npan; ++k) {
-      const char* pan = buf + (slot * PMAXJ + k) * PANEL;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const char* pan = buf + (slot * NP + k) * PANEL;
       // partitions feeding this (block, panel) and the channel rows each one owns (mode 2: groups of C)
       int p0, p1;
       if (a.mode == 0) p0 = p1 = (32 * ob) / a.C;
@@ -207,36 +269,16 @@ __global__ __launch_bounds__(NWJ * 64) void jmix_kernel(const JmixArgs a) {
         }
       }
     }
-    // D: lane = output joint lr, acc[r] = channel 32*ob + 8*(r>>2) + 4*lh + (r&3)
-    if (lr < V) {
-      T* orow = out + (i * V + lr) * (long)a.out_ld;
-#pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4) {
-        const int ch = 32 * ob + 8 * q4 + 4 * lh;
-        if (ch >= a.cout) continue;
-        float v[4] = {acc[4 * q4], acc[4 * q4 + 1], acc[4 * q4 + 2], acc[4 * q4 + 3]};
-        if constexpr (sizeof(T) == 2) {
-          bf16x4* po = reinterpret_cast<bf16x4*>(orow + ch);
-          if (a.accumulate) {
-            const bf16x4 o = *po;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += (float)o[e];
-          }
-          bf16x4 r;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) r[e] = (bf16)v[e];
-          *po = r;
-        } else {
-          float4* po = reinterpret_cast<float4*>(orow + ch);
-          if (a.accumulate) {
-            const float4 o = *po;
-            v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
-          }
-          *po = make_float4(v[0], v[1], v[2], v[3]);
-        }
-      }
-    }
+    // D: lane = output joint lr, acc[r] = channel 32*ob + 8*(r>>2) + 4*lh + (r&3); stored next item
+    pend = acc;
+    pend_i = i;
+    pend_ob = ob;
+    // next item's panels (DMA(j+1)) and this item's accumulate loads: all but the youngest DMA_OPS ops
+    if (it + 2 < it1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA_OPS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  flush();
 }
 
 }  // namespace
@@ -249,6 +291,7 @@ int jmix_launch(const void* in, int in_ld, void* out, int out_ld, const float* M
   const int cin = mode == 1 ? P * C : (mode == 0 ? C : P * C);
   const int cout = mode == 1 ? C : P * C;
   if (V < 1 || V > 32 || P < 1 || P > PMAXJ) return -1;
+  if (mode == 1 && P > 3) return -1;
   if ((mode == 0 || mode == 1) && C % 32) return -1;
   if (mode == 2 && (C % 4 || cout % 4)) return -1;
   if ((in_ld * elt) % 16 || (out_ld * elt) % 16 || in_ld < cin || out_ld < cout) return -1;
@@ -271,13 +314,21 @@ int jmix_launch(const void* in, int in_ld, void* out, int out_ld, const float* M
   a.ipw = (a.items + waves - 1) / waves;
   const long blocks = (a.items + a.ipw * NWJ - 1) / (a.ipw * NWJ);
   const int panel = dtype ? JT<bf16>::PANEL : JT<float>::PANEL;
-  const size_t lds = (size_t)NWJ * 2 * PMAXJ * panel;
+  const size_t lds = (size_t)NWJ * 3 * a.npan * panel;
+#define JM_LAUNCH(TT, NPV)                                                                                   \
+  do {                                                                                                       \
+    if (stgcn_lds_attr((const void*)jmix_kernel<TT, NPV>, (int)lds, s)) return STGCN_EHIP;                    \
+    hipLaunchKernelGGL((jmix_kernel<TT, NPV>), dim3((unsigned)blocks), dim3(NWJ * 64), lds, s, a);            \
+  } while (0)
   if (dtype) {
-    if (stgcn_lds_attr((const void*)jmix_kernel<bf16>, (int)lds, s)) return STGCN_EHIP;
-    hipLaunchKernelGGL(jmix_kernel<bf16>, dim3((unsigned)blocks), dim3(NWJ * 64), lds, s, a);
+    if (a.npan == 1) JM_LAUNCH(bf16, 1);
+    else if (a.npan == 2) JM_LAUNCH(bf16, 2);
+    else JM_LAUNCH(bf16, 3);
   } else {
-    if (stgcn_lds_attr((const void*)jmix_kernel<float>, (int)lds, s)) return STGCN_EHIP;
-    hipLaunchKernelGGL(jmix_kernel<float>, dim3((unsigned)blocks), dim3(NWJ * 64), lds, s, a);
+    if (a.npan == 1) JM_LAUNCH(float, 1);
+    else if (a.npan == 2) JM_LAUNCH(float, 2);
+    else JM_LAUNCH(float, 3);
   }
+#undef JM_LAUNCH
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }

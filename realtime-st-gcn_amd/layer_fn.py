@@ -638,13 +638,27 @@ class PoolFunction(torch.autograd.Function):
         return dx, None, None
 
 
+def _strided_rows_ok(t, dtype) -> bool:
+    """A (N, C, T, V) tensor the row kernels can read in place: the dtype, unit channel stride and evenly
+    strided rows (K.rows_ld)."""
+    if t.dtype != dtype or t.dim() != 4 or t.stride(1) != 1 or not t.is_cuda:
+        return False
+    try:
+        K.rows_ld(t)
+    except RuntimeError:
+        return False
+    return True
+
+
 class AttentionFunction(torch.autograd.Function):
     """C = softmax(theta^T phi) per (n, p) (models/aagcn/aagcn.py:142-145), theta/phi channels-last rows."""
 
     @staticmethod
     def forward(ctx, theta, phi, P, dtype):
-        theta = K.to_rows(theta, dtype)
-        phi = K.to_rows(phi, dtype)
+        # strided rows are fine (the kernels take a row stride): attn_proj's theta / phi are the two channel
+        # halves of one row buffer, and keeping them there lets attn_bwd return both gradients in one buffer
+        theta = theta if _strided_rows_ok(theta, dtype) else K.to_rows(theta, dtype)
+        phi = phi if _strided_rows_ok(phi, dtype) else K.to_rows(phi, dtype)
         C = K.attn_scores(theta, phi, P)
         ctx.save_for_backward(theta, phi, C)
         ctx.P = P
