@@ -112,13 +112,24 @@ __global__ __launch_bounds__(NT, 2) void conv1x1_kernel(const stgcn_conv_desc a,
     const int cl = (wn * TN + j) * 32 + lr;  // column within the tile
     const int col = n0 + cl;
     const float b = (a.bias && a.bias_mode == 1) ? a.bias[col] : 0.f;
+    // bias_mode 2 / 3: the graph-conv bias pushed through A, per joint [V][Cout] / per (sample, joint)
+    // [N][V][Cout] (tgcn.py:76 with the bias applied before the A-mix)
+    const bool rowbias = a.bias && (a.bias_mode == 2 || a.bias_mode == 3);
     float s = 0.f, cnt = 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = (wm * TM + i) * 32 + acc_row(r, lane);
-        const float v = acc[i][j][r] + b;
+        float bb = b;
+        if (rowbias) {
+          const long m = m0 + (row < rows_valid ? row : 0);
+          const long fr = m / V;
+          const int v = (int)(m - fr * V);
+          const long bi = a.bias_mode == 2 ? v : (fr / a.T_out) * V + v;
+          bb = a.bias[bi * a.Cout + col];
+        }
+        const float v = acc[i][j][r] + bb;
         acc[i][j][r] = v;
         *reinterpret_cast<bf16*>(smem + row * OS + cl * 2) = (bf16)v;
         if (row < rows_valid) {
@@ -288,10 +299,13 @@ int conv1x1_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
     }
   }
   if (!a.w_frag) return -1;
-  if (a.stride < 1 || a.bias_mode < 0 || a.bias_mode > 1) return -1;
+  if (a.stride < 1 || a.bias_mode < 0 || a.bias_mode > 3) return -1;
+  if (a.bias_mode >= 2 && (a.stride != 1 || a.trans)) return -1;
   if (a.trans ? a.T_in != (a.T_out - 1) / a.stride + 1 : a.T_out != (a.T_in - 1) / a.stride + 1) return -1;
   if (a.in_ld % 8 || a.out_ld % 8 || a.Cout % 64 || a.Cin_pad != a.Cin || a.Cout_pad < a.Cout) return -1;
-  if (a.Cin != 64 && a.Cin != 128 && a.Cin != 256) return -1;
+  // K = Cin: also the A-first graph conv's P * Cin = 192 at C = 64 (83 vs 125 us against conv_tile); at
+  // K = 384 the staged tile (100 KB of LDS, one block per CU) measured 2x slower than conv_tile
+  if (a.Cin != 64 && a.Cin != 128 && a.Cin != 192 && a.Cin != 256) return -1;
   XGeom g;
   g.M = (long)a.N * a.T_out * a.V;
   const int BN = a.Cout % 128 == 0 ? 128 : 64;
@@ -304,9 +318,11 @@ int conv1x1_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
   if (BN == 128) {
     if (a.Cin == 64) return launch1<4, 128>(a, g, s);
     if (a.Cin == 128) return launch1<8, 128>(a, g, s);
+    if (a.Cin == 192) return launch1<12, 128>(a, g, s);
     return launch1<16, 128>(a, g, s);
   }
   if (a.Cin == 64) return launch1<4, 64>(a, g, s);
   if (a.Cin == 128) return launch1<8, 64>(a, g, s);
+  if (a.Cin == 192) return launch1<12, 64>(a, g, s);
   return launch1<16, 64>(a, g, s);
 }

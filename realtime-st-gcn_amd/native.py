@@ -97,7 +97,7 @@ def pack_weight(w3: torch.Tensor, dtype, stride: int = 1, trans: bool = False) -
                 "pack_weight_frag")
         out.frag_ptr, out.frag_stride = buf[n:].data_ptr(), 1
         return out, cp, kp
-    if dtype == torch.bfloat16 and Kt == 1 and kp == Ci and Ci in (64, 128, 256) and Co % 64 == 0:
+    if dtype == torch.bfloat16 and Kt == 1 and kp == Ci and Ci in (64, 128, 192, 256) and Co % 64 == 0:
         # 1x1 weights: fragment image for the row-GEMM kernel (conv1x1.hip), valid at any stride
         buf = torch.empty(2 * n, dtype=dtype, device=w3.device)
         out = buf[:n].view(Kt, cp, kp)
