@@ -27,6 +27,8 @@ long wgrad_tile_workspace(const WgradArgs& a, int dtype);
 long wgrad_wide_workspace(const WgradArgs& a, int dtype);
 int wgrad_wide_launch(const WgradArgs& a, int dtype, hipStream_t s);
 int wgrad_tile_launch(const WgradArgs& a, int dtype, hipStream_t s);
+long wgrad1x1_workspace(const WgradArgs& a, int dtype);
+int wgrad1x1_launch(const WgradArgs& a, int dtype, hipStream_t s);
 int amix_fwd_launch(const AmixArgs& a, int dtype, hipStream_t s);
 long gconv_row_blocks(int NT, int V);
 long bn_bwd_fused_work_floats(long M, int C, int dtype);
@@ -167,7 +169,9 @@ long stgcn_conv_rows_row_blocks(long M, int cout) { return conv_rows_num_row_blo
 long stgcn_conv_wgrad_workspace(const stgcn_wgrad_desc* d, int dtype) {
   if (!d || (dtype != 0 && dtype != 1)) return 0;
   const long w = wgrad_wide_workspace(*d, dtype);  // >= 128-channel Kt=9 stride-1 path first
-  return w > 0 ? w : wgrad_tile_workspace(*d, dtype);
+  if (w > 0) return w;
+  const long w1 = wgrad1x1_workspace(*d, dtype);   // 1x1 split-K path
+  return w1 > 0 ? w1 : wgrad_tile_workspace(*d, dtype);
 }
 
 int stgcn_conv_wgrad(const stgcn_wgrad_desc* d, int dtype, void* stream) {
@@ -176,6 +180,8 @@ int stgcn_conv_wgrad(const stgcn_wgrad_desc* d, int dtype, void* stream) {
   if (d->pro && (!d->pro_a || !d->pro_b || (d->pro == 2 && !d->pro_stats))) return STGCN_EBADSHAPE;
   const int rw = wgrad_wide_launch(*d, dtype, STREAM(stream));  // bf16 >= 128-channel ring path (needs work)
   if (rw >= 0) return rw;
+  const int r1 = wgrad1x1_launch(*d, dtype, STREAM(stream));  // bf16 1x1 split-K row reduction (needs work)
+  if (r1 >= 0) return r1;
   const int r = wgrad_tile_launch(*d, dtype, STREAM(stream));  // bf16 frame-tiled path (needs work)
   if (r >= 0) return r;
   return conv_wgrad_launch(*d, dtype, STREAM(stream));

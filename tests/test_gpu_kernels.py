@@ -390,3 +390,17 @@ def test_attn_proj(K, Cin, Nout):
     ref = torch.einsum("oc,nctv->notv", w.double(), x.double()) + b.double().view(1, -1, 1, 1)
     got = K.attn_proj(cl(x.float(), torch.bfloat16), w.to(DEV), b.to(DEV))
     assert_close(got.cpu(), ref, 1e-5, "attn_proj")
+
+
+@pytest.mark.parametrize("Cin,Cout,N,T", [(192, 64, 2, 64), (64, 96, 2, 64), (768, 256, 1, 64), (64, 64, 3, 37)])
+def test_wgrad_1x1(K, Cin, Cout, N, T):
+    """Kt = 1 weight gradient (wgrad1x1.hip split-K path when M % 32 == 0, the frame-tiled kernel otherwise):
+    dW[co][ci] = sum over rows of dy[co] x[ci] on bf16 rows, fp32 accumulation; several chunks and groups."""
+    torch.manual_seed(Cin + Cout + T)
+    V = 25
+    x = torch.randn(N, Cin, T, V).to(torch.bfloat16)
+    dy = torch.randn(N, Cout, T, V).to(torch.bfloat16)
+    ref = torch.einsum("nctv,notv->oc", x.double(), dy.double())
+    dw = torch.zeros((1, Cout, Cin), device=DEV)
+    got = K.conv_wgrad(cl(x.float(), torch.bfloat16), cl(dy.float(), torch.bfloat16), Cin, Cout, T, T, dw=dw)
+    assert_close(got.reshape(Cout, Cin).cpu(), ref, 1e-4, "wgrad 1x1")
