@@ -101,5 +101,7 @@ def assert_grad_close(got, ref, rel=1e-3, name="", scale_floor=0.0, reduction=Fa
         return
     l2 = ((g - r).norm() / max(r.norm().item(), 1e-30)).item()
     frac = (err > rel * scale + 1e-6).double().mean().item()
+    if os.environ.get("STGCN_TEST_REPORT"):
+        print(f"[l2-path] {name}: L2 {l2:.2e} frac beyond {frac:.2e} reduction={reduction}", flush=True)
     assert l2 <= 3 * rel and (frac <= 5e-3 or reduction), \
         f"{name}: max err {err.max().item():.3e} > {rel:g}*{scale:.3e}; L2 rel {l2:.2e}, frac beyond {frac:.2e}"
