@@ -29,7 +29,7 @@ struct XGeom {
   int k16n;   // K blocks per column of the fragment image (Cin_pad / 16)
 };
 
-template <int KS, int BN>
+template <int KS, int BN, bool ROWB>
 __global__ __launch_bounds__(NT, 2) void conv1x1_kernel(const stgcn_conv_desc a, const XGeom g) {
   constexpr int CIN = KS * 16;
   constexpr int RS = CIN * 2 + 16;           // padded LDS row (bytes)
@@ -111,10 +111,10 @@ __global__ __launch_bounds__(NT, 2) void conv1x1_kernel(const stgcn_conv_desc a,
   for (int j = 0; j < TN; ++j) {
     const int cl = (wn * TN + j) * 32 + lr;  // column within the tile
     const int col = n0 + cl;
-    const float b = (a.bias && a.bias_mode == 1) ? a.bias[col] : 0.f;
-    // bias_mode 2 / 3: the graph-conv bias pushed through A, per joint [V][Cout] / per (sample, joint)
-    // [N][V][Cout] (tgcn.py:76 with the bias applied before the A-mix)
-    const bool rowbias = a.bias && (a.bias_mode == 2 || a.bias_mode == 3);
+    const float b = (!ROWB && a.bias && a.bias_mode == 1) ? a.bias[col] : 0.f;
+    // ROWB (bias_mode 2 / 3): the graph-conv bias pushed through A, per joint [V][Cout] / per (sample,
+    // joint) [N][V][Cout] (tgcn.py:76 with the bias applied before the A-mix).  A template flag: the
+    // per-row index math as a runtime branch cost the plain instantiations 2x (register pressure).
     float s = 0.f, cnt = 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -122,7 +122,7 @@ __global__ __launch_bounds__(NT, 2) void conv1x1_kernel(const stgcn_conv_desc a,
       for (int r = 0; r < 16; ++r) {
         const int row = (wm * TM + i) * 32 + acc_row(r, lane);
         float bb = b;
-        if (rowbias) {
+        if (ROWB) {
           const long m = m0 + (row < rows_valid ? row : 0);
           const long fr = m / V;
           const int v = (int)(m - fr * V);
@@ -265,14 +265,15 @@ __global__ __launch_bounds__(NT) void conv1x1_narrow_kernel(const stgcn_conv_des
   }
 }
 
-template <int KS, int BN>
+template <int KS, int BN, bool ROWB = false>
 int launch1(const stgcn_conv_desc& a, const XGeom& g, hipStream_t s) {
   constexpr int RS = KS * 16 * 2 + 16, OS = BN * 2 + 16;
   size_t lds = (size_t)BM * RS;
   const size_t lout = (size_t)BM * OS + 2 * BN * 16;
   if (lout > lds) lds = lout;
-  if (stgcn_lds_attr((const void*)conv1x1_kernel<KS, BN>, 160 * 1024, s)) return STGCN_EHIP;
-  hipLaunchKernelGGL((conv1x1_kernel<KS, BN>), dim3((unsigned)((long)g.nrow * g.ncol)), dim3(NT), lds, s, a, g);
+  constexpr bool RB = ROWB;
+  if (stgcn_lds_attr((const void*)conv1x1_kernel<KS, BN, RB>, 160 * 1024, s)) return STGCN_EHIP;
+  hipLaunchKernelGGL((conv1x1_kernel<KS, BN, RB>), dim3((unsigned)((long)g.nrow * g.ncol)), dim3(NT), lds, s, a, g);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
 
@@ -308,7 +309,9 @@ int conv1x1_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
   if (a.Cin != 64 && a.Cin != 128 && a.Cin != 192 && a.Cin != 256) return -1;
   XGeom g;
   g.M = (long)a.N * a.T_out * a.V;
-  const int BN = a.Cout % 128 == 0 ? 128 : 64;
+  // the per-row bias (bias_mode 2 / 3) only at 64-column tiles: at 128 its index math spills
+  const bool rowb = a.bias && a.bias_mode >= 2;
+  const int BN = a.Cout % 128 == 0 && !rowb ? 128 : 64;
   g.ncol = a.Cout / BN;
   const long nrow = (g.M + BM - 1) / BM;
   if (nrow * g.ncol > 0x7fffffffL) return -1;
@@ -320,6 +323,12 @@ int conv1x1_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
     if (a.Cin == 128) return launch1<8, 128>(a, g, s);
     if (a.Cin == 192) return launch1<12, 128>(a, g, s);
     return launch1<16, 128>(a, g, s);
+  }
+  if (rowb) {
+    if (a.Cin == 64) return launch1<4, 64, true>(a, g, s);
+    if (a.Cin == 128) return launch1<8, 64, true>(a, g, s);
+    if (a.Cin == 192) return launch1<12, 64, true>(a, g, s);
+    return launch1<16, 64, true>(a, g, s);
   }
   if (a.Cin == 64) return launch1<4, 64>(a, g, s);
   if (a.Cin == 128) return launch1<8, 64>(a, g, s);
