@@ -22,6 +22,8 @@
 //   * blocks are persistent (grid = CU count), each walking a contiguous run of tiles; items are
 //     processed in pairs (the channel-group count G = Cin / 64 is even), which makes the halo buffer
 //     and the B register set of every k-step compile-time;
+//   * C = 64 (two 32-channel items per tile): 8 helper waves and a separate tile-image buffer (the helpers
+//     bound that instantiation);
 //   * epilogue per tile: + bias, bf16 store, BatchNorm Welford partials per (tile, channel) (the
 //     float4 (count, mean, M2) layout bn_finalize merges; row-tile index = n * tiles_n + tile).
 #include "common.h"
@@ -34,7 +36,7 @@ namespace {
 constexpr int KG = 64;               // input channels per item
 constexpr int KS = KG / 16;          // MFMA k-steps per tap
 constexpr int NT = 256;              // 4 waves
-constexpr int WM = 2, WN = 2, TM = 4;
+constexpr int WM_MAX = 4;  // MMA wave rows (sRed is sized for the largest layout)
 constexpr int RSA = KG * 2 + 16;     // padded halo row bytes (144)
 constexpr int HR_CAP = 456;          // max halo rows per item (V = 25: 18 frames x 25 = 450)
 constexpr int NA = (HR_CAP * 8 + NT - 1) / NT;  // 16-B halo units per thread (15)
@@ -73,6 +75,7 @@ struct WGeom {
   int cpar;     // fold 1: 64-channel items per input parity; fold 2: output channels per parity
   int wc32, wk16;  // fragment image dims: (output channels / 32, input channels / 16)
   int strided;     // 1: block b takes tiles b, b + grid, ... (A/B switch STGCN_WIDE_STRIDED); 0: a contiguous run
+  int red_off;     // LDS byte offset of the Welford partials (after the halo buffers and, SEP, the tile image)
 };
 
 struct TileInfo {
@@ -98,15 +101,25 @@ DEV TileInfo tile_info(int tile, const WGeom& g) {
 // item k+1; barrier E_k.  At a tile end the MMA waves dump acc (+ bias) as a column-major bf16 image
 // into buf b (8-B ds_write_b64 per 4 rows) and their Welford partials into sRed; barrier I_k; the
 // helpers drain that image during item k+1 before they overwrite buf b with item k+2's halo.
-// DBG (compile-time A/B instantiations only): bit1 no helper work (results wrong)
-template <int BN, int KTAP, int NBUF, int PRO, int DBG = 0, int KGT = 64>
-__global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_desc a, const WGeom g) {
+// DBG (compile-time A/B instantiations only): bit1 no helper work, bit2 no MFMAs (timing; results wrong)
+// WMT: MMA-wave layout, WMT x (4 / WMT) waves over (256 rows x BN columns).  WMT = 4 at BN = 64: each wave
+// holds 64 rows x 64 columns, so every A fragment read from LDS feeds two MFMAs (the 2 x 2 layout reads
+// each A fragment in both column-half waves: LDS reads = MFMAs at C = 64)
+// NHW: helper waves (4, or 8 where staging + drain bound the kernel: C = 64)
+// SEPT (two-item tiles only, C = 64): the finished tile image gets its own LDS buffer, so the helpers drain it
+// in halves over both windows of the next tile instead of all of it before the next halo store
+template <int BN, int KTAP, int NBUF, int PRO, int DBG = 0, int KGT = 64, int WMT = 2, int APD = 1, int NHW = 4,
+          bool SEPT = false>
+__global__ __launch_bounds__((4 + NHW) * 64, 1) void conv_wide_kernel(const stgcn_conv_desc a, const WGeom g) {
+  constexpr int WM = WMT, WN = 4 / WMT, TM = 8 / WMT;
   // item width: 64 input channels (>= 128-channel layers) or 32 (64-channel layers: two items per tile)
   constexpr int KG = KGT, KS = KG / 16, RSA = 2 * KG + 16;
-  constexpr int UPR = KG / 8, RSTEP = NT / UPR;            // 16-B units per halo row, rows per staging pass
-  constexpr int NA = (HR_CAP * UPR + NT - 1) / NT;         // halo units per helper thread
+  constexpr int NTH = NHW * 64;                            // helper threads
+  constexpr int UPR = KG / 8, RSTEP = NTH / UPR;           // 16-B units per halo row, rows per staging pass
+  constexpr int NA = (HR_CAP * UPR + NTH - 1) / NTH;       // halo units per helper thread
   constexpr int SPI = KTAP * KS;  // k-steps per item
-  constexpr int TN = BN / 64;
+  constexpr int TN = BN / 32 / WN;
+  static_assert(TN >= 1 && WM * WN == 4, "wave layout");
   constexpr int LEAD = NBUF - 1;
   constexpr int PAIR = 2 * SPI;  // k-steps per item pair
   static_assert(PAIR % NBUF == 0, "B register ring must divide the pair");
@@ -127,10 +140,12 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
   const bf16* __restrict__ wp = reinterpret_cast<const bf16*>(a.w_frag);
   char* const sA0 = smem;
   char* const sA1 = smem + g.abytes;
-  float4* const sRed = reinterpret_cast<float4*>(smem + 2 * g.abytes);  // [WM][BN]
+  constexpr bool SEP = SEPT && KG == 32;
+  char* const sImg = SEP ? smem + 2 * g.abytes : nullptr;  // [BN][CSO] tile image (SEP)
+  float4* const sRed = reinterpret_cast<float4*>(smem + g.red_off);  // [WM][BN]
   // drain counter: each helper wave adds 1 when its reads of a tile image are done; the halo writes into
   // that buffer wait until all four have (the image and the next halo share the buffer)
-  unsigned* const sCnt = reinterpret_cast<unsigned*>(smem + 2 * g.abytes + WM * BN * 16);
+  unsigned* const sCnt = reinterpret_cast<unsigned*>(smem + g.red_off + WM_MAX * BN * 16);
 
   auto item_tile = [&](int w, int& gi) {  // items past the block's last one are clamped to it
     w = min(w, nitems - 1);
@@ -209,17 +224,22 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
       });
     };
     // finished tile image (column-major [BN][CSO bytes]) -> global rows; BN partials -> global
-    auto drain = [&](int w, const char* img) {
+    auto drain = [&](int w, const char* img, int part = 0, int nparts = 1) {
       int gi;
       const int tile = item_tile(w, gi);
       const TileInfo ti = tile_info(tile, g);
       const int rows_valid = ti.fe * V;
       const int n0 = ti.ct * BN;
-      if (a.stats) {
+      if (a.stats && part == 0) {
         const int rt = tile / g.ncol;
-        for (int c = htid; c < BN; c += NT) {
-          const float4 f0 = sRed[c], f1 = sRed[BN + c];
-          const Welford wv = welford_merge(Welford{f0.x, f0.y, f0.z}, Welford{f1.x, f1.y, f1.z});
+        for (int c = htid; c < BN; c += NTH) {
+          const float4 f0 = sRed[c];
+          Welford wv{f0.x, f0.y, f0.z};
+#pragma unroll
+          for (int k = 1; k < WM; ++k) {
+            const float4 f1 = sRed[k * BN + c];
+            wv = welford_merge(wv, Welford{f1.x, f1.y, f1.z});
+          }
           if (n0 + c < a.Cout_pad)
             reinterpret_cast<float4*>(a.stats)[(long)rt * a.Cout_pad + n0 + c] = make_float4(wv.n, wv.mean, wv.m2, 0.f);
         }
@@ -237,7 +257,7 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
       // column stride the 8 units x 8 quads of one ds_read_b64 land on 32 distinct bank pairs (2-way)
       constexpr int UG = BN / 64;  // groups of 8 units per row
       const int nq = (rows_valid + 3) >> 2, nq8 = (nq + 7) >> 3;
-      for (int idx = htid; idx < UG * nq8 * 64; idx += NT) {
+      for (int idx = htid + part * NTH; idx < UG * nq8 * 64; idx += nparts * NTH) {
         const int cl = idx & 7, ql = (idx >> 3) & 7, rest = idx >> 6;
         const int ug = rest / nq8, qh = rest - ug * nq8;
         const int rq = qh * 8 + ql, cu = ug * 8 + cl;
@@ -283,7 +303,7 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
     auto drain_sync = [&]() {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_fetch_add(sCnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      ndrain += 4;
+      ndrain += NHW;
       while (__hip_atomic_load(sCnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < ndrain)
         __builtin_amdgcn_s_sleep(1);
     };
@@ -294,6 +314,23 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
     if (nitems > 1) issue_A.template operator()<1 % NSET>(1);
     if (NSET == 2 && nitems > 2) issue_A.template operator()<0>(2);
     lds_barrier();  // P
+    for (int w = 0; w < nitems && SEP; w += 2) {
+      // SEP (G = 2: the pair (w, w+1) is one tile): drain the previous tile's image in two halves, one per
+      // window, beside the two halo stores; the next dump comes after E_{w+1}
+      if (w > 0) drain(w - 1, sImg, 0, 2);
+      store_A.template operator()<1 % NSET>(sA1);
+      if (w + 1 + NSET < nitems) issue_A.template operator()<(1 + NSET) % NSET>(w + 1 + NSET);
+      lds_barrier();  // E_w
+      if (w > 0) drain(w - 1, sImg, 1, 2);
+      if (w + 2 < nitems) store_A.template operator()<2 % NSET>(sA0);
+      if (w + 2 + NSET < nitems) issue_A.template operator()<(2 + NSET) % NSET>(w + 2 + NSET);
+      lds_barrier();  // E_{w+1}
+      lds_barrier();  // I_{w+1}
+    }
+    if (SEP) {
+      drain(nitems - 1, sImg);
+      return;
+    }
     for (int w = 0; w < nitems; w += 2) {
       // window w: item w+1 -> sA1, request item w+1+NSET
       if ((DBG & 2) == 0) {
@@ -323,7 +360,7 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
   }
 
   // =============================== MMA waves ===============================
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   const int lr = lane & 31, lh = lane >> 5;
   // B fragment j at k-step (t, ks) of item (ct, gi): the contiguous 1-KiB block
   // [t][c32 = ct*BN/32 + wn*TN + j][k16 = gi*4 + ks] of the fragment image (stgcn_pack_weight_frag)
@@ -467,7 +504,8 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
     asm volatile("" : "+s"(tbytes));
     asm volatile("" : "+s"(kcc_l));
     asm volatile("" : "+s"(cinp_l));
-    bf16x8 fa[2][TM];
+    constexpr int AR = APD + 1;  // A fragment ring: reads APD k-steps ahead inside an item
+    bf16x8 fa[AR][TM];
     // one k-step; hs is a template parameter so every ring index below is a compile-time constant
     auto step = [&]<int hs>() {
       constexpr int h = hs / SPI, s = hs % SPI, t = s / KS, ks = s % KS;
@@ -477,24 +515,26 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
         const int woff = hn < SPI ? woff0 : (hn < PAIR ? woff1 : woff2);
         load_B(fb[hn % NBUF], hn % SPI, woff, wl, kcc_l, cinp_l);
       }
+      auto read_a = [&]<int sd>() {  // A fragments of k-step sd of this item -> ring slot
+        constexpr int td = sd / KS, ksd = sd % KS;
+        const int tb = (qbase + qsign * td) * tbytes + ksd * 32;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          fa[(h * SPI + sd) % AR][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(cur + af[i] + tb));
+      };
       if constexpr (s == 0) {
-        const int tb = (qbase + qsign * t) * tbytes + ks * 32;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-          fa[hs & 1][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(cur + af[i] + tb));
+        static_for<APD>([&]<int d>() { read_a.template operator()<d>(); });
       }
-      if constexpr (s + 1 < SPI) {  // A fragments one k-step ahead inside an item
-        constexpr int t1 = (s + 1) / KS, ks1 = (s + 1) % KS;
-        const int tb1 = (qbase + qsign * t1) * tbytes + ks1 * 32;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-          fa[(hs + 1) & 1][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(cur + af[i] + tb1));
-      }
+      if constexpr (s + APD < SPI) read_a.template operator()<s + APD>();
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[hs & 1][i], fb[hs % NBUF][j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j) {
+          if constexpr ((DBG & 4) != 0)  // timing only: operands consumed without MFMA work
+            acc[i][j][0] += (float)fa[hs % AR][i][0] + (float)fb[hs % NBUF][j][0];
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[hs % AR][i], fb[hs % NBUF][j], acc[i][j], 0, 0, 0);
+        }
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (s == SPI - 1) {
         lds_barrier();  // E_{w+h}
@@ -503,7 +543,7 @@ __global__ __launch_bounds__(2 * NT, 1) void conv_wide_kernel(const stgcn_conv_d
     if (w % g.G == 0) load_bias(w);
     static_for<PAIR>(step);
     if (tile_end(w + 1)) {
-      dump(w + 1, sA1);
+      dump(w + 1, SEP ? sImg : sA1);
       lds_barrier();  // I_{w+1}
     }
   }
@@ -614,16 +654,26 @@ int conv_wide_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
   if (nt <= 0 || nt > 0x7fffffffL) return -1;
   g.ntiles = (int)nt;
   if (a.stats && (long)a.N * g.tiles_n > conv_rows_num_row_blocks((long)a.N * a.T_out * a.V, a.Cout)) return -1;
-  g.abytes = abytes_for(kg);
-  const size_t lds = 2 * (size_t)g.abytes + (size_t)WM * BN * 16 + 16;
+  // C = 64 (two 32-channel items per tile): its own tile-image buffer (SEPT) and 8 helper waves (NHW)
+  const bool sep = kg == 32;
+  if (sep && BN != 64) return -1;
+  if (sep) {  // halo buffers sized for the halo alone; the tile image separate
+    const int upr = kg / 8, nth = 8 * 64, rstep = nth / upr, na = (HR_CAP * upr + nth - 1) / nth;
+    g.abytes = na * rstep * (2 * kg + 16);
+    g.red_off = 2 * g.abytes + BN * CSO;
+  } else {
+    g.abytes = abytes_for(kg);
+    g.red_off = 2 * g.abytes;
+  }
+  const size_t lds = (size_t)g.red_off + (size_t)WM_MAX * BN * 16 + 16;
   if (lds > (size_t)LDS_MAX) return -1;
   const int ncu = stgcn_cu_count(s);
   const int tpb = (g.ntiles + ncu - 1) / ncu;
   const int grid = (g.ntiles + tpb - 1) / tpb;
-  const dim3 gd((unsigned)grid), bd(2 * NT);
+  const dim3 gd((unsigned)grid);
   auto kern = [&]() -> void (*)(const stgcn_conv_desc, const WGeom) {
-    if (kg == 32)
-      return a.pro ? conv_wide_kernel<64, 9, 12, 1, 0, 32> : conv_wide_kernel<64, 9, 12, 0, 0, 32>;
+    if (kg == 32)  // C = 64: 8 helper waves, separate tile image (64.6 vs 70.5 us, tools/bench_conv.py tcn_fwd_c64)
+      return a.pro ? conv_wide_kernel<64, 9, 9, 1, 0, 32, 2, 1, 8, true> : conv_wide_kernel<64, 9, 9, 0, 0, 32, 2, 1, 8, true>;
     // B ring depth 8 (7 k-steps of L2 latency cover): measured 2-3 % faster than 4, 6 or 9 at C = 128/256
     if (ktap == 9) return a.pro ? conv_wide_kernel<128, 9, 8, 1> : conv_wide_kernel<128, 9, 8, 0>;
     // stride-2 folded 5-tap form: ring depth must divide 40 k-steps per item pair.  Depth 8 measured equal
@@ -631,6 +681,8 @@ int conv_wide_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
     return a.pro ? conv_wide_kernel<128, 5, 5, 1> : conv_wide_kernel<128, 5, 5, 0>;
   };
   auto* k = kern();
+  const int nhw = sep ? 8 : 4;
+  const dim3 bd((unsigned)((4 + nhw) * 64));
   if (stgcn_lds_attr((const void*)k, LDS_MAX, s)) return STGCN_EHIP;
   hipLaunchKernelGGL(k, gd, bd, lds, s, a, g);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;

@@ -1140,7 +1140,14 @@ int gconv_launch(const stgcn_gconv_desc& a, int dtype, hipStream_t s) {
   // bf16, Cout <= 64: 128-row tiles (TM = 1, TN = 2) — twice the blocks of the 256-row tile, measured
   // 46 vs 54 us (C=64 fwd), 42 vs 47 us (dgrad), 68 vs 72 us (128 -> 64 dgrad); wider outputs keep
   // 256 x 128 tiles (128-row variants measured 5-10 % slower there)
-  if (dtype == 1) return wide ? launch_gconv<bf16, 4, 2, 2, 2, 32>(a, s) : launch_gconv<bf16, 4, 1, 1, 2, 32>(a, s);
+  // K chunk of 64 channels (one barrier per 64 instead of 32) once Cin >= 128, with 128-row tiles at the
+  // wide outputs (tools/bench_conv.py gconv, us, 32-chunk -> 64-chunk: fwd C=128 63 -> 56.5, C=256 96.5 ->
+  // 92; dgrad 128 -> 64 67 -> 55; at Cin = 64 the 32-chunk tiles stay ahead or even)
+  if (dtype == 1) {
+    const bool k64 = a.Cin >= 128 && a.Cin_pad % 64 == 0;
+    if (wide) return k64 ? launch_gconv<bf16, 4, 2, 1, 2, 64>(a, s) : launch_gconv<bf16, 4, 2, 2, 2, 32>(a, s);
+    return k64 ? launch_gconv<bf16, 4, 1, 1, 2, 64>(a, s) : launch_gconv<bf16, 4, 1, 1, 2, 32>(a, s);
+  }
   return wide ? launch_gconv<float, 4, 2, 2, 2, 16>(a, s) : launch_gconv<float, 4, 1, 2, 2, 16>(a, s);
 }
 
