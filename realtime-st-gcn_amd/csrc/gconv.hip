@@ -44,6 +44,28 @@ DEV void glds16(const void* src, char* lds_base) {
 #endif
 }
 
+// global -> LDS DMA of 16 B per lane at a wave-uniform LDS offset, through asm so the compiler inserts no
+// alias-driven vmcnt drains (the DMA K loop counts its own); m0 saved / restored
+DEV void gdma16(const void* src, unsigned lds_off) {
+  unsigned saved;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(saved) : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_off)) : "memory");
+}
+DEV unsigned glds_off(const void* p) { return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p; }
+// s_waitcnt vmcnt(n) for the counts the DMA K loop uses (n = steps in flight x instructions per step)
+DEV void gwait_vm(int n) {
+  switch (n) {
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
 template <typename T>
 DEV typename Tr<T>::frag frag2(const char* p0, const char* p1) {
   if constexpr (sizeof(T) == 2) {
@@ -68,8 +90,12 @@ struct GGeom {
 // ------------------------------------------------------------------ gather GEMM (fwd and data grad)
 // ACCV: stores (and accumulate, out +=) through the vectorised LDS-scratch epilogue; a separate instantiation so
 // the plain-store kernel keeps its register budget (<= 128 VGPRs: 2 blocks per CU)
-template <typename T, int WM, int WN, int TM, int TN, int KC, bool ACCV>
-__global__ __launch_bounds__(WM * WN * 64, 2) void gconv_kernel(const stgcn_gconv_desc a, const GGeom g) {
+// NSTG > 0 (bf16, KC = 64): the K loop DMAs both operands (gathered x rows and the effective weights,
+// XOR-swizzled 128-B rows) into an NSTG-deep LDS ring, NSTG - 1 K steps ahead, with counted vmcnt waits
+// (every wave issues the same number of DMA instructions per step) and one LDS-only barrier per step;
+// NSTG = 0: rows staged through registers, double-buffered.
+template <typename T, int WM, int WN, int TM, int TN, int KC, bool ACCV, int NSTG = 0>
+__global__ __launch_bounds__(WM * WN * 64, (NSTG && (WM * TM + WN * TN) * 32 * 128 * NSTG > 80 * 1024) ? 1 : 2) void gconv_kernel(const stgcn_gconv_desc a, const GGeom g) {
   typedef GL<T, KC> L;
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
@@ -183,6 +209,70 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gconv_kernel(const stgcn_gcon
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   typedef typename Tr<T>::frag Frag;
+  if constexpr (NSTG > 0) {
+    static_assert(sizeof(T) == 2 && KC == 64, "DMA K loop: bf16, 64-channel chunks");
+    constexpr int RBD = 128, A_B = BM * RBD, STG = A_B + BN * RBD;
+    constexpr int AI = BM / 8 / NW, BI = BN / 8 / NW, OPS = AI + BI;  // DMA instructions per wave and step
+    static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "DMA rows");
+    int* const snbr = reinterpret_cast<int*>(smem + NSTG * STG);  // this joint's neighbour list
+    if (tid < a.J) snbr[tid] = a.nbr[jt * a.J + tid];
+    __syncthreads();
+    // lane -> (row rr of the instruction's 8 rows, 16-B slot); the slot holds unit slot ^ swz(row)
+    const int rr = lane >> 3, slot = lane & 7;
+    long a_src[AI];
+    int b_src[BI];
+#pragma unroll
+    for (int q = 0; q < AI; ++q) {
+      const int r = (wave * AI + q) * 8 + rr;
+      const int rc = min(r, max(rows_valid, 1) - 1);  // rows past the tile's end read a valid row (discarded)
+      a_src[q] = (long)(i0 + rc) * V * a.in_ld + (slot ^ ((r >> 1) & 7)) * 8;
+    }
+#pragma unroll
+    for (int q = 0; q < BI; ++q) {
+      const int r = (wave * BI + q) * 8 + rr;
+      b_src[q] = (n0 + r) * a.Cin_pad + (slot ^ ((r >> 1) & 7)) * 8;
+    }
+    auto issue = [&](int k, int stage) {
+      const int j = k / nch, c = k - j * nch;
+      const long joff = (long)snbr[j] * a.in_ld + c * KC;
+      const T* wsrc = wp + (long)(jt * a.J + j) * a.Cout_pad * a.Cin_pad + c * KC;
+      char* base = smem + stage * STG;
+#pragma unroll
+      for (int q = 0; q < AI; ++q) gdma16(in + a_src[q] + joff, glds_off(base + (wave * AI + q) * 1024));
+#pragma unroll
+      for (int q = 0; q < BI; ++q) gdma16(wsrc + b_src[q], glds_off(base + A_B + (wave * BI + q) * 1024));
+    };
+#pragma unroll
+    for (int sidx = 0; sidx < NSTG - 1; ++sidx)
+      if (sidx < nk) issue(sidx, sidx);
+    for (int k = 0; k < nk; ++k) {
+      const int younger = min(NSTG - 2, nk - 1 - k);  // own DMA steps allowed to stay in flight
+      gwait_vm(younger * OPS);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave's DMAs of step k landed
+      if (k + NSTG - 1 < nk) issue(k + NSTG - 1, (k + NSTG - 1) % NSTG);  // that stage was read in step k-1
+      const char* A_ = smem + (k % NSTG) * STG;
+      const char* B_ = A_ + A_B;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        Frag fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int r = (wm * TM + i) * 32 + lr;
+          fa[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(A_ + r * RBD + (((2 * ks + lh) ^ ((r >> 1) & 7)) << 4)));
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int r = (wn * TN + j) * 32 + lr;
+          fb[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(B_ + r * RBD + (((2 * ks + lh) ^ ((r >> 1) & 7)) << 4)));
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) Tr<T>::mma(acc[i][j], fa[i], fb[j]);
+      }
+    }
+    __syncthreads();  // every wave is done with the ring before the epilogue reuses it
+  } else {
   int cur = 0;
   if (nk > 0) {
     load(0, 0);
@@ -221,6 +311,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gconv_kernel(const stgcn_gcon
     __syncthreads();
     cur ^= 1;
   }
+  }  // NSTG == 0
 
   // ---------------------------------------------------------------- epilogue
   // bias + BN partials on the fp32 accumulators.  accumulate: the values go through a per-wave LDS
@@ -343,12 +434,13 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void gconv_kernel(const stgcn_gcon
   }
 }
 
-template <typename T, int WM, int WN, int TM, int TN, int KC>
+template <typename T, int WM, int WN, int TM, int TN, int KC, int NSTG = 0>
 int launch_gconv(const stgcn_gconv_desc& a, hipStream_t s) {
   constexpr int VEC = 16 / (int)sizeof(T);
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   typedef GL<T, KC> L;
   if (a.Cout_pad % BN || a.Cin_pad % KC) return STGCN_EBADSHAPE;
+  if (NSTG && (a.in_ld % VEC || a.Cin != a.Cin_pad || a.J > 64)) return STGCN_EBADSHAPE;
   GGeom g;
   g.ntile = (a.NT + BM - 1) / BM;
   g.ncol = a.Cout_pad / BN;
@@ -356,11 +448,11 @@ int launch_gconv(const stgcn_gconv_desc& a, hipStream_t s) {
   if (nblk <= 0 || nblk > 0x7fffffffL) return STGCN_EBADSHAPE;
   g.nblk = (int)nblk;
   const int STAGE = ((BM * L::RS + BN * L::RB) + 1023) & ~1023;
-  size_t lds = 2 * (size_t)STAGE;
+  size_t lds = NSTG ? (size_t)NSTG * (BM + BN) * 128 + 256 : 2 * (size_t)STAGE;
   const size_t red = a.stats ? (size_t)WM * BN * 16 : 0;
   if (red > lds) lds = red;
-  if (stgcn_lds_attr((const void*)gconv_kernel<T, WM, WN, TM, TN, KC, false>, 160 * 1024, s) ||
-      stgcn_lds_attr((const void*)gconv_kernel<T, WM, WN, TM, TN, KC, true>, 160 * 1024, s))
+  if (stgcn_lds_attr((const void*)gconv_kernel<T, WM, WN, TM, TN, KC, false, NSTG>, 160 * 1024, s) ||
+      stgcn_lds_attr((const void*)gconv_kernel<T, WM, WN, TM, TN, KC, true, NSTG>, 160 * 1024, s))
     return STGCN_EHIP;
   // 16-B row stores through the LDS scratch whenever rows are 16-B aligned (A/B: STGCN_GCONV_SCATTER=1 keeps
   // the per-element stores for plain outputs)
@@ -368,11 +460,11 @@ int launch_gconv(const stgcn_gconv_desc& a, hipStream_t s) {
   const bool scatter = sce && sce[0] == '1';
   const bool accv = (a.accumulate || !scatter) && (a.out_ld % VEC) == 0 && (a.Cout % VEC) == 0;
   if (accv)
-    hipLaunchKernelGGL((gconv_kernel<T, WM, WN, TM, TN, KC, true>), dim3((unsigned)nblk), dim3(WM * WN * 64), lds, s,
-                       a, g);
+    hipLaunchKernelGGL((gconv_kernel<T, WM, WN, TM, TN, KC, true, NSTG>), dim3((unsigned)nblk), dim3(WM * WN * 64),
+                       lds, s, a, g);
   else
-    hipLaunchKernelGGL((gconv_kernel<T, WM, WN, TM, TN, KC, false>), dim3((unsigned)nblk), dim3(WM * WN * 64), lds,
-                       s, a, g);
+    hipLaunchKernelGGL((gconv_kernel<T, WM, WN, TM, TN, KC, false, NSTG>), dim3((unsigned)nblk), dim3(WM * WN * 64),
+                       lds, s, a, g);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
 
@@ -1144,6 +1236,15 @@ int gconv_launch(const stgcn_gconv_desc& a, int dtype, hipStream_t s) {
   // wide outputs (tools/bench_conv.py gconv, us, 32-chunk -> 64-chunk: fwd C=128 63 -> 56.5, C=256 96.5 ->
   // 92; dgrad 128 -> 64 67 -> 55; at Cin = 64 the 32-chunk tiles stay ahead or even)
   if (dtype == 1) {
+    // DMA K loop (two LDS stages, 64-channel chunks) whenever rows allow it: tools/bench_conv.py gconv, us,
+    // register-staged -> DMA: C=64 fwd 44.7 -> 42.7, dgrad 40.7 -> 36.6; C=128 59.8 -> 56.0 / 51.8 -> 48.9;
+    // 64->128 69.8 -> 67.2 / 58.2 -> 49.8; C=256 (256-row tiles) 95.7 -> 85.2 / 88.1 -> 75.2
+    const char* de = getenv("STGCN_GCONV_DMA");  // A/B: 0 = register-staged kernels
+    const bool dma = !(de && de[0] == '0') && a.Cin % 64 == 0 && a.Cin == a.Cin_pad && a.in_ld % 8 == 0;
+    if (dma) {
+      if (!wide) return launch_gconv<bf16, 4, 1, 1, 2, 64, 2>(a, s);
+      return a.Cin >= 256 ? launch_gconv<bf16, 4, 2, 2, 2, 64, 2>(a, s) : launch_gconv<bf16, 4, 2, 1, 2, 64, 2>(a, s);
+    }
     const bool k64 = a.Cin >= 128 && a.Cin_pad % 64 == 0;
     if (wide) return k64 ? launch_gconv<bf16, 4, 2, 1, 2, 64>(a, s) : launch_gconv<bf16, 4, 2, 2, 2, 32>(a, s);
     return k64 ? launch_gconv<bf16, 4, 1, 1, 2, 64>(a, s) : launch_gconv<bf16, 4, 1, 1, 2, 32>(a, s);
