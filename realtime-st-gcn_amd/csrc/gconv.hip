@@ -472,8 +472,10 @@ int launch_gconv(const stgcn_gconv_desc& a, hipStream_t s) {
 // out[a][j][r][c] (dtype, padded to [R_pad][C_pad]):
 //   trans 0: sum_p A[p][nbr[a][j]][a] * W[p*Cout + r][c]          (r = co < Cout, c = ci < Cin)
 //   trans 1: sum_p A[p][a][nbr[a][j]] * W[p*Cout + c][r]          (r = ci < Cin,  c = co < Cout)
-// One thread per 8 consecutive c (one 16-B bf16 store); slots j >= deg[a] are never read by gconv and
-// are skipped; padding rows / columns are written as zeros (they meet zero-filled operands).
+// One thread per (joint a, 8 consecutive c, r): it loads its P x 8 weights once and writes all deg[a]
+// neighbour slots of joint a (a thread per slot re-read the same weights J times: ~100 MB of L2 reads per
+// C = 256 launch).  Slots j >= deg[a] are never read by gconv and are skipped; padding rows / columns are
+// written as zeros (they meet zero-filled operands).
 constexpr int GW_PMAX = 4;
 template <typename T>
 __global__ void gconv_weights_kernel(const float* __restrict__ A, const float* __restrict__ W, const int* nbr,
@@ -481,34 +483,28 @@ __global__ void gconv_weights_kernel(const float* __restrict__ A, const float* _
                                      int R_pad, int C_pad) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int C8 = C_pad / 8;
-  const long total = (long)V * J * R_pad * C8;
+  const long total = (long)V * R_pad * C8;
   if (idx >= total) return;
   // forward: c (ci) fastest across lanes, so W rows are read as float4 runs; trans: r (ci) fastest, so
   // the 8 scalar reads of W[co][r] per thread are coalesced across lanes
-  int c0, r;
-  long aj;
+  int c0, r, a;
   if (!trans) {
     c0 = (int)(idx % C8) * 8;
     const long t1 = idx / C8;
     r = (int)(t1 % R_pad);
-    aj = t1 / R_pad;
+    a = (int)(t1 / R_pad);
   } else {
     r = (int)(idx % R_pad);
     const long t1 = idx / R_pad;
     c0 = (int)(t1 % C8) * 8;
-    aj = t1 / C8;
+    a = (int)(t1 / C8);
   }
-  const int j = (int)(aj % J), a = (int)(aj / J);
-  if (j >= deg[a]) return;
   const int R = trans ? Cin : Cout, C = trans ? Cout : Cin;
-  const int b = nbr[a * J + j];
-  float coef[GW_PMAX];
+  float wv[GW_PMAX][8];
 #pragma unroll
   for (int p = 0; p < GW_PMAX; ++p)
-    coef[p] = p < P ? (trans ? A[((long)p * V + a) * V + b] : A[((long)p * V + b) * V + a]) : 0.f;
-  float s[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) s[e] = 0.f;
+    for (int e = 0; e < 8; ++e) wv[p][e] = 0.f;
   if (r < R) {
 #pragma unroll
     for (int p = 0; p < GW_PMAX; ++p) {
@@ -517,26 +513,40 @@ __global__ void gconv_weights_kernel(const float* __restrict__ A, const float* _
         const float* w = W + ((long)p * Cout + r) * Cin + c0;
         if (c0 + 8 <= C && (Cin & 3) == 0) {
           const float4 w0 = *reinterpret_cast<const float4*>(w), w1 = *reinterpret_cast<const float4*>(w + 4);
-          s[0] += coef[p] * w0.x; s[1] += coef[p] * w0.y; s[2] += coef[p] * w0.z; s[3] += coef[p] * w0.w;
-          s[4] += coef[p] * w1.x; s[5] += coef[p] * w1.y; s[6] += coef[p] * w1.z; s[7] += coef[p] * w1.w;
+          wv[p][0] = w0.x; wv[p][1] = w0.y; wv[p][2] = w0.z; wv[p][3] = w0.w;
+          wv[p][4] = w1.x; wv[p][5] = w1.y; wv[p][6] = w1.z; wv[p][7] = w1.w;
         } else {
 #pragma unroll
           for (int e = 0; e < 8; ++e)
-            if (c0 + e < C) s[e] += coef[p] * w[e];
+            if (c0 + e < C) wv[p][e] = w[e];
         }
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          if (c0 + e < C) s[e] += coef[p] * W[((long)p * Cout + c0 + e) * Cin + r];
+          if (c0 + e < C) wv[p][e] = W[((long)p * Cout + c0 + e) * Cin + r];
       }
     }
   }
-  T* o = out + ((aj * R_pad) + r) * (long)C_pad + c0;
-  if constexpr (sizeof(T) == 2) {
-    *reinterpret_cast<uint4*>(o) = pack16(s, (T*)nullptr);
-  } else {
+  const int da = deg[a];
+  for (int j = 0; j < da; ++j) {
+    const int b = nbr[a * J + j];
+    float s[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = s[e];
+    for (int e = 0; e < 8; ++e) s[e] = 0.f;
+#pragma unroll
+    for (int p = 0; p < GW_PMAX; ++p) {
+      if (p >= P) break;
+      const float coef = trans ? A[((long)p * V + a) * V + b] : A[((long)p * V + b) * V + a];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[e] += coef * wv[p][e];
+    }
+    T* o = out + (((long)a * J + j) * R_pad + r) * (long)C_pad + c0;
+    if constexpr (sizeof(T) == 2) {
+      *reinterpret_cast<uint4*>(o) = pack16(s, (T*)nullptr);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = s[e];
+    }
   }
 }
 
@@ -1255,7 +1265,7 @@ int gconv_launch(const stgcn_gconv_desc& a, int dtype, hipStream_t s) {
 int gconv_weights_launch(const float* A, const float* W, const int* nbr, const int* deg, int P, int V, int J, int Cout,
                          int Cin, int trans, void* out, int R_pad, int C_pad, int dtype, hipStream_t s) {
   if (C_pad % 8 || P > GW_PMAX) return STGCN_EBADSHAPE;
-  const long total = (long)V * J * R_pad * (C_pad / 8);
+  const long total = (long)V * R_pad * (C_pad / 8);
   const unsigned blocks = (unsigned)((total + 255) / 256);
   if (dtype == 1)
     hipLaunchKernelGGL(gconv_weights_kernel<bf16>, dim3(blocks), dim3(256), 0, s, A, W, nbr, deg, P, V, J, Cout, Cin,

@@ -1,13 +1,11 @@
 #!/bin/bash
-# A/B of an environment switch on ONE box, interleaved: bench_conv cases with and without it.
-# usage: ENVSET="STGCN_GCONV_SCATTER=1" CASES="gconv_fwd_c64 ..." bash tools/ab_env.sh
+# A/B of an env switch on ONE box, interleaved full-step bench runs: tools/ab_env.sh VAR "A B" [steps]
 export TMPDIR=/tmp
-for rep in 1 2; do
-  for mode in base env; do
-    for c in $CASES; do
-      if [ $mode = env ]; then out=$(env $ENVSET timeout -k 10 120 python tools/bench_conv.py 30 $c 2>&1 | grep -v amdgpu.ids)
-      else out=$(timeout -k 10 120 python tools/bench_conv.py 30 $c 2>&1 | grep -v amdgpu.ids); fi
-      echo "$mode $rep $out"
-    done
+mkdir -p gpurun_out
+VAR=$1; VALS=$2; STEPS=${3:-100}
+for rep in 1 2 3; do
+  for v in $VALS; do
+    env $VAR=$v timeout -k 10 300 python bench.py --steps $STEPS --warmup 10 --no-cpu-baseline > gpurun_out/ab_env_$v.json 2>/dev/null || exit 1
+    echo "$VAR=$v rep $rep: $(python -c 'import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(d["ms_per_step"])' gpurun_out/ab_env_$v.json)"
   done
 done
