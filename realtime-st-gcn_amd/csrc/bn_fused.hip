@@ -112,7 +112,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_fused_kernel(const stgcn_bn
 // gradients are contiguous views (no gather copies on the host side).
 __global__ __launch_bounds__(256) void sum4_kernel(const float4* part, int nb, int C, float4* out) {
   __shared__ double sx[256], sy[256], sz[256];
-  const int c = blockIdx.x;
+  const int c = xcd_channel(blockIdx.x, C);
   double x = 0, y = 0, z = 0;
   for (int i = threadIdx.x; i < nb; i += 256) {
     const float4 v = part[(long)i * C + c];

@@ -48,6 +48,12 @@ template <> struct Tr<bf16> {
 };
 
 // 16-byte unit <-> 8 floats (bf16) or 4 floats (fp32)
+// Channel of block b in a one-block-per-channel reduction over [nb][C] partial rows (grid = C): workgroups
+// are dealt round-robin to the 8 XCDs, so with c = b every 128-B line of partials (8 float4 channels) was
+// fetched into all eight L2s; this mapping gives each XCD a contiguous channel range (C % 64 == 0), so each
+// line goes to one L2.
+DEV int xcd_channel(int b, int C) { return (C & 63) ? b : (b & 7) * (C >> 3) + (b >> 3); }
+
 DEV void unpack16(const uint4& u, float* f, bf16*) {
   const bf16x8 v = __builtin_bit_cast(bf16x8, u);
 #pragma unroll

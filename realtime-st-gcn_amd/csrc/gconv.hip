@@ -477,6 +477,7 @@ int launch_gconv(const stgcn_gconv_desc& a, hipStream_t s) {
 // C = 256 launch).  Slots j >= deg[a] are never read by gconv and are skipped; padding rows / columns are
 // written as zeros (they meet zero-filled operands).
 constexpr int GW_PMAX = 4;
+constexpr int GW_JMAX = 8;  // neighbour slots per joint whose loads are issued together
 template <typename T>
 __global__ void gconv_weights_kernel(const float* __restrict__ A, const float* __restrict__ W, const int* nbr,
                                      const int* deg, int P, int V, int J, int Cout, int Cin, int trans, T* out,
@@ -527,25 +528,41 @@ __global__ void gconv_weights_kernel(const float* __restrict__ A, const float* _
       }
     }
   }
-  const int da = deg[a];
-  for (int j = 0; j < da; ++j) {
-    const int b = nbr[a * J + j];
-    float s[8];
+  // the neighbour list and coefficients of up to GW_JMAX slots are requested together (independent loads),
+  // not as a chain of dependent loads per slot: the small launches are latency-bound
+  const int dtot = deg[a];
+  for (int j0 = 0; j0 < dtot; j0 += GW_JMAX) {
+    const int da = min(dtot - j0, GW_JMAX);
+    int nb[GW_JMAX];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) s[e] = 0.f;
+    for (int jj = 0; jj < GW_JMAX; ++jj) nb[jj] = jj < da ? nbr[a * J + j0 + jj] : a;
+    float cf[GW_JMAX][GW_PMAX];
 #pragma unroll
-    for (int p = 0; p < GW_PMAX; ++p) {
-      if (p >= P) break;
-      const float coef = trans ? A[((long)p * V + a) * V + b] : A[((long)p * V + b) * V + a];
+    for (int jj = 0; jj < GW_JMAX; ++jj)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s[e] += coef * wv[p][e];
-    }
-    T* o = out + (((long)a * J + j) * R_pad + r) * (long)C_pad + c0;
-    if constexpr (sizeof(T) == 2) {
-      *reinterpret_cast<uint4*>(o) = pack16(s, (T*)nullptr);
-    } else {
+      for (int p = 0; p < GW_PMAX; ++p)
+        cf[jj][p] = (jj < da && p < P) ? (trans ? A[((long)p * V + a) * V + nb[jj]] : A[((long)p * V + nb[jj]) * V + a])
+                                       : 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = s[e];
+    for (int jj = 0; jj < GW_JMAX; ++jj) {
+      if (jj >= da) break;
+      const int j = j0 + jj;
+      float s[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[e] = 0.f;
+#pragma unroll
+      for (int p = 0; p < GW_PMAX; ++p) {
+        if (p >= P) break;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s[e] += cf[jj][p] * wv[p][e];
+      }
+      T* o = out + (((long)a * J + j) * R_pad + r) * (long)C_pad + c0;
+      if constexpr (sizeof(T) == 2) {
+        *reinterpret_cast<uint4*>(o) = pack16(s, (T*)nullptr);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = s[e];
+      }
     }
   }
 }

@@ -98,7 +98,7 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float4* part, in
   // division chain), a wave reduction and one LDS step; at fp64 the final var = S2/n - mean^2 loses
   // ~1e-16 * mean^2/var, far below the fp32 result
   __shared__ double sred[3][4];
-  const int c = blockIdx.x;
+  const int c = xcd_channel(blockIdx.x, C);
   double n = 0, s1 = 0, s2 = 0;
   for (int b0 = 0; b0 < nb; b0 += 256 * 8) {
     float4 gv[8];
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
 // column sums of float2 partials -> out[c] (double accumulation), one block per channel
 __global__ __launch_bounds__(256) void sum_partials_kernel(const float2* part, int nb, int C, float2* out) {
   __shared__ double sa[256], sb[256];
-  const int c = blockIdx.x;
+  const int c = xcd_channel(blockIdx.x, C);
   double a = 0, b = 0;
   for (int i = threadIdx.x; i < nb; i += 256) {
     const float2 g = part[(long)i * C + c];

@@ -24,11 +24,44 @@ re-packing (tiny tensors) and the (P x V)-sized reshuffles of the A/bias gradien
 """
 from __future__ import annotations
 
+import contextlib
+import os
+
 import torch
 
 from . import native as K
 
 BN, LN = "BatchNorm", "LayerNorm"
+
+_SIDE = {}
+
+
+def _side_stream(dev):
+    """Per-device side stream for the weight-gradient branch of a layer backward (None: run in order).
+
+    The data-gradient chain (BN backward -> transposed temporal conv -> BN1 backward -> transposed graph
+    conv) is the critical path from dy to dx; the weight gradients (temporal-conv wgrad, residual wgrad,
+    graph-conv wgrad + dW/dA finish + bias through A) branch off it.  They are issued on this stream after
+    a fork event and joined before the backward returns, so the latency-bound reduction kernels of the
+    branch fill the gaps and tails of the data-gradient kernels.  Off under stream capture (HIP graphs) and
+    with STGCN_SIDE_STREAM=0 (A/B)."""
+    if os.environ.get("STGCN_SIDE_STREAM", "1") == "0" or torch.cuda.is_current_stream_capturing():
+        return None
+    s = _SIDE.get(dev.index)
+    if s is None:
+        s = _SIDE[dev.index] = torch.cuda.Stream(device=dev)
+    return s
+
+
+@contextlib.contextmanager
+def _fork(side):
+    """Run the body on ``side`` after everything already queued on the current stream."""
+    if side is None:
+        yield
+        return
+    side.wait_stream(torch.cuda.current_stream(side.device))
+    with torch.cuda.stream(side):
+        yield
 
 
 def _flat_ln(p):
@@ -270,6 +303,7 @@ class StgcnLayerFunction(torch.autograd.Function):
         zshapes = [(kt, Cout, Cout), (1, Cout, Cin), (P * Cout, Cin), (P, V, V),
                    ((N, V, Cout) if A32.dim() == 4 else (V, Cout))]
         z_dwt, z_dwr, z_dwg, z_dA, z_S = K.zeros_arena(dev, *zshapes)
+        side = _side_stream(dev)  # weight-gradient branch (joined before returning)
 
         # ---- through relu(norm2(u) + res): dz = dy * [y > 0]
         du = K.cl_empty(N, Cout, T_out, V, dtype, dev)
@@ -320,10 +354,11 @@ class StgcnLayerFunction(torch.autograd.Function):
             # residual conv (1x1, stride s, bias): data grad (transposed), weight grad
             wrT = wr.detach().float().view(Cout, Cin).t().reshape(1, Cin, Cout)
             wrTp, cq, kq = K.pack_weight(wrT, dtype)
+            with _fork(side):
+                grads["wr"] = K.conv_wgrad(x, dr, Cin, Cout, T, T_out, Kt=1, stride=stride, pad=0,
+                                           dw=z_dwr).view(Cout, Cin, 1, 1)
             K.conv_rows(dr, wrTp, Cout, Cin, cq, kq, T_out, T, Kt=1, stride=stride, pad=0, trans=True, out=dx)
             dx_written = True
-            grads["wr"] = K.conv_wgrad(x, dr, Cin, Cout, T, T_out, Kt=1, stride=stride, pad=0,
-                                       dw=z_dwr).view(Cout, Cin, 1, 1)
         elif residual and not fused:
             K.bn_bwd_apply(dy, M2, Cin, dx, mask=1, mref=y)  # dx = dz
             dx_written = True
@@ -331,13 +366,14 @@ class StgcnLayerFunction(torch.autograd.Function):
         # ---- temporal conv: dh = conv^T(du), dWt, dbt
         wtT = wt.detach().float().squeeze(-1).permute(2, 1, 0)  # [Kt][Cin=Cout][Cout]: W[co][ci][dt] -> [dt][ci][co]
         wtTp, cq, kq = K.pack_weight(wtT, dtype, stride=stride, trans=True)
-        dh = K.conv_rows(du, wtTp, Cout, Cout, cq, kq, T_out, T, Kt=kt, stride=stride, pad=pad, trans=True)
         if norm == BN:
             pro1 = dict(pro=1, pro_a=sc1, pro_b=sh1)
         else:
             pro1 = dict(pro=2, pro_a=_flat_ln(n1w), pro_b=_flat_ln(n1b), pro_stats=ls1)
-        dwt = K.conv_wgrad(g, du, Cout, Cout, T, T_out, Kt=kt, stride=stride, pad=pad, dw=z_dwt, **pro1)
-        grads["wt"] = dwt.permute(1, 2, 0).unsqueeze(-1)  # [Kt][co][ci] -> (co, ci, Kt, 1)
+        with _fork(side):
+            dwt = K.conv_wgrad(g, du, Cout, Cout, T, T_out, Kt=kt, stride=stride, pad=pad, dw=z_dwt, **pro1)
+            grads["wt"] = dwt.permute(1, 2, 0).unsqueeze(-1)  # [Kt][co][ci] -> (co, ci, Kt, 1)
+        dh = K.conv_rows(du, wtTp, Cout, Cout, cq, kq, T_out, T, Kt=kt, stride=stride, pad=pad, trans=True)
         if not bt_done:
             grads["bt"] = K.bn_bwd_reduce(du, M2, Cout)[:, 0].clone()
 
@@ -364,6 +400,18 @@ class StgcnLayerFunction(torch.autograd.Function):
             # weight/adjacency grads from dWeff[w][j] = sum_i dg[(i,w)] x[(i,S(w)_j)]^T
             sup = ctx.sup
             wg2 = wg.detach().float().reshape(P * Cout, Cin).contiguous()
+            with _fork(side):
+                fuse_s = A32.dim() == 3 and K.gconv_wgrad_rowsum_ok(sup, Cin, Cout, dtype)
+                dweff = K.gconv_wgrad(x, dg, sup, Cin, Cout, rowsum=z_S if fuse_s else None)
+                dwg2, dA = K.gconv_finish(dweff, A32, wg2, sup, Cout, Cin, dW=z_dwg, dA=z_dA)
+                grads["wg"] = dwg2.view(P * Cout, Cin, 1, 1)
+                if ctx.cfg[6] and ctx.needs_input_grad[1]:
+                    # caller-owned A: the reference's dA is dense (also off the graph's support), so take
+                    # it from the A-first factorisation dA_p[v][w] = sum x[(i,v)] . (dg W_p)[(i,w)]
+                    wgTd = wg.detach().float().view(P, Cout, Cin).permute(0, 2, 1).reshape(1, P * Cin, Cout)
+                    wgTp, cq, kq = K.pack_weight(wgTd, dtype)
+                    dA = K.amix_dA(x, K.conv_rows(dg, wgTp, Cout, P * Cin, cq, kq, T, T), A32)
+                dA = _bias_through_A(dA, A32, bg, bgp, dg, z_S if fuse_s else None, z_S, M1, Cout, V, grads)
             if K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype, trans=True):  # dx = sum_p A_p-mix(dg) W_p^T, fused (gcn_tile.hip)
                 wdf = wg.detach().float().view(P, Cout, Cin).permute(2, 0, 1).reshape(Cin, P * Cout)
                 wimgT, cq, kwT = K.pack_gcn_weight(wdf, dtype)
@@ -371,16 +419,6 @@ class StgcnLayerFunction(torch.autograd.Function):
             else:
                 wgT = K.gconv_weights(A32, wg2, sup, Cout, Cin, True, dtype)
                 K.gconv(dg, wgT, sup, Cout, Cin, trans=True, out=dx, accumulate=dx_written)
-            fuse_s = A32.dim() == 3 and K.gconv_wgrad_rowsum_ok(sup, Cin, Cout, dtype)
-            dweff = K.gconv_wgrad(x, dg, sup, Cin, Cout, rowsum=z_S if fuse_s else None)
-            dwg2, dA = K.gconv_finish(dweff, A32, wg2, sup, Cout, Cin, dW=z_dwg, dA=z_dA)
-            grads["wg"] = dwg2.view(P * Cout, Cin, 1, 1)
-            if ctx.cfg[6] and ctx.needs_input_grad[1]:
-                # caller-owned A: the reference's dA is dense (also off the graph's support), so take
-                # it from the A-first factorisation dA_p[v][w] = sum x[(i,v)] . (dg W_p)[(i,w)]
-                wgTd = wg.detach().float().view(P, Cout, Cin).permute(0, 2, 1).reshape(1, P * Cin, Cout)
-                wgTp, cq, kq = K.pack_weight(wgTd, dtype)
-                dA = K.amix_dA(x, K.conv_rows(dg, wgTp, Cout, P * Cin, cq, kq, T, T), A32)
         else:
             # DW[(n,t,w)][p*Cin+ci] = sum_c dg[(n,t,w)][c] Wg[p*Cout+c][ci]
             wgT = wg.detach().float().view(P, Cout, Cin).permute(0, 2, 1).reshape(1, P * Cin, Cout)
@@ -390,18 +428,13 @@ class StgcnLayerFunction(torch.autograd.Function):
             dA = K.amix_dA(x, DW, A32)
             dwg = K.conv_wgrad(XA, dg, P * Cin, Cout, T, T, Kt=1)              # [1][Cout][P*Cin]
             grads["wg"] = dwg.view(Cout, P, Cin).permute(1, 0, 2).reshape(P * Cout, Cin, 1, 1)
-        # bias pushed through A: dA[p][v][w] += sum_c b_p[c] S[w][c]  (independent of v)
-        if A32.dim() == 4:
-            Sn = K.rowgroup_sum(dg, M1, Cout, V, per_sample=True, out=z_S)   # [N][V(w)][Cout]
-            dA += torch.einsum("pc,nwc->npw", bgp, Sn).unsqueeze(2)
-            colsum = A32.sum(dim=2)                                         # [N][P][W]
-            grads["bg"] = torch.einsum("npw,nwc->pc", colsum, Sn).reshape(-1)
-        else:
-            # [V(w)][Cout]; the joint-grouped weight-gradient kernel already produced it when it ran
-            S = z_S if (ctx.sup is not None and fuse_s) else K.rowgroup_sum(dg, M1, Cout, V, out=z_S)
-            if not dA.is_contiguous():
-                dA = dA.contiguous()
-            grads["bg"] = K.gcn_bias_bwd(A32, bg.detach().float().contiguous(), S, dA, Cout)
+            dA = _bias_through_A(dA, A32, bg, bgp, dg, None, z_S, M1, Cout, V, grads)
+        if side is not None:  # join the weight-gradient branch
+            main = torch.cuda.current_stream(dev)
+            main.wait_stream(side)
+            for t in list(grads.values()) + [dA]:
+                if t is not None:
+                    t.record_stream(main)
 
         def gr(name, like):
             v = grads.get(name)
@@ -413,6 +446,23 @@ class StgcnLayerFunction(torch.autograd.Function):
         return (dx, dA.to(ctx.in_dtype), gr("wg", wg), gr("bg", bg), gr("n1w", n1w), gr("n1b", n1b), gr("wt", wt),
                 grads["bt"], gr("n2w", n2w), gr("n2b", n2b), gr("wr", wr_),
                 grads.get("br"), gr("nrw", nrw_), gr("nrb", nrb_), None)
+
+
+def _bias_through_A(dA, A32, bg, bgp, dg, S_fused, z_S, M1, Cout, V, grads):
+    """Bias pushed through A: dA[p][v][w] += sum_c b_p[c] S[w][c] (independent of v), S = per-joint row
+    sums of dg (already produced by the joint-grouped weight-gradient kernel when S_fused is given);
+    sets grads["bg"] and returns dA."""
+    if A32.dim() == 4:
+        Sn = K.rowgroup_sum(dg, M1, Cout, V, per_sample=True, out=z_S)   # [N][V(w)][Cout]
+        dA = dA + torch.einsum("pc,nwc->npw", bgp, Sn).unsqueeze(2)
+        colsum = A32.sum(dim=2)                                         # [N][P][W]
+        grads["bg"] = torch.einsum("npw,nwc->pc", colsum, Sn).reshape(-1)
+        return dA
+    S = S_fused if S_fused is not None else K.rowgroup_sum(dg, M1, Cout, V, out=z_S)   # [V(w)][Cout]
+    if not dA.is_contiguous():
+        dA = dA.contiguous()
+    grads["bg"] = K.gcn_bias_bwd(A32, bg.detach().float().contiguous(), S, dA, Cout)
+    return dA
 
 
 class GcnFunction(torch.autograd.Function):
