@@ -75,6 +75,7 @@ struct WGeom {
   int cpar;     // fold 1: 64-channel items per input parity; fold 2: output channels per parity
   int wc32, wk16;  // fragment image dims: (output channels / 32, input channels / 16)
   int strided;     // 1: block b takes tiles b, b + grid, ... (A/B switch STGCN_WIDE_STRIDED); 0: a contiguous run
+  int pair;        // ncol == 2: blocks b and b + 8 (one XCD) take the two column tiles of the same row-tile run
   int red_off;     // LDS byte offset of the Welford partials (after the halo buffers and, SEP, the tile image)
 };
 
@@ -130,9 +131,22 @@ __global__ __launch_bounds__((4 + NHW) * 64, 1) void conv_wide_kernel(const stgc
   const int V = a.V;
   const int grid = gridDim.x;
   const int tpb = (g.ntiles + grid - 1) / grid;  // contiguous tile runs: neighbour halos stay in L2
-  const int tile0 = g.strided ? (int)blockIdx.x : (int)blockIdx.x * tpb;
-  const int tstep = g.strided ? grid : 1;
-  const int ntile_b = g.strided ? (g.ntiles - (int)blockIdx.x + grid - 1) / grid : min(tpb, g.ntiles - tile0);
+  int tile0 = g.strided ? (int)blockIdx.x : (int)blockIdx.x * tpb;
+  int tstep = g.strided ? grid : 1;
+  int ntile_b = g.strided ? (g.ntiles - (int)blockIdx.x + grid - 1) / grid : min(tpb, g.ntiles - tile0);
+  if (g.pair) {
+    // workgroups are dealt round-robin to the 8 XCDs: blocks b = x + 8 s share XCD x; the pair (s = 2q, 2q+1)
+    // walks the same run of row tiles, one column tile each, at the same pace, so every halo item one of
+    // them stages from HBM the other finds in the XCD's L2 (a block walking both column tiles of a row tile
+    // in turn re-fetched the halo: 32 CUs' halos overrun the 4 MB L2)
+    const int b = blockIdx.x, sx = b >> 3;
+    const int nrt = g.ntiles >> 1, npair = grid >> 1;
+    const int rpp = (nrt + npair - 1) / npair;
+    const int rt0 = ((b & 7) * (grid >> 4) + (sx >> 1)) * rpp;
+    tile0 = 2 * rt0 + (sx & 1);
+    tstep = 2;
+    ntile_b = min(rpp, nrt - rt0);
+  }
   if (ntile_b <= 0) return;
   const int nitems = ntile_b * g.G;
 
@@ -669,7 +683,12 @@ int conv_wide_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
   if (lds > (size_t)LDS_MAX) return -1;
   const int ncu = stgcn_cu_count(s);
   const int tpb = (g.ntiles + ncu - 1) / ncu;
-  const int grid = (g.ntiles + tpb - 1) / tpb;
+  int grid = (g.ntiles + tpb - 1) / tpb;
+  {
+    static const int pe = getenv("STGCN_WIDE_PAIR") ? atoi(getenv("STGCN_WIDE_PAIR")) : 1;  // A/B switch
+    g.pair = pe && !g.strided && g.ncol == 2 && ncu >= 16;
+    if (g.pair) grid = ncu & ~15;
+  }
   const dim3 gd((unsigned)grid);
   auto kern = [&]() -> void (*)(const stgcn_conv_desc, const WGeom) {
     if (kg == 32)  // C = 64: 8 helper waves, separate tile image (64.6 vs 70.5 us, tools/bench_conv.py tcn_fwd_c64)
