@@ -199,6 +199,23 @@ class StgcnLayerFunction(torch.autograd.Function):
             st_all = K.zeros_arena(dev, *st_shapes)
             st1, st2 = st_all[0], st_all[1]
             str_ = st_all[2] if res_conv else None
+        # ---- residual branch: independent of the graph conv -> temporal conv chain until the output norm,
+        # so on the side stream (x is ready at entry; joined before the norm that adds it)
+        r = None
+        side = _side_stream(dev) if res_conv else None
+        if res_conv:
+            with _fork(side):
+                wr3 = wr.detach().float().view(1, Cout, Cin)
+                wrp, cpr, kpr = K.pack_weight(wr3, dtype)
+                r = K.conv_rows(x, wrp, Cin, Cout, cpr, kpr, T, T_out, Kt=1, stride=stride, pad=0,
+                                bias=br.detach().float().contiguous(), stats=str_ if norm == BN else None)
+                if norm == BN:
+                    mrr, scr, shr = K.bn_finalize(str_, str_.shape[0], cpr, Cout, nrw.detach().float(),
+                                                  nrb.detach().float())
+                else:
+                    lsr = K.ln_stats(r, N * T_out, V, Cout)
+                side_made = [r] + ([mrr, scr, shr] if norm == BN else [lsr])
+
         if tiled:  # A-mix on the fly into the MFMA operand of whole-frame tiles (gcn_tile.hip)
             wgf = wg.detach().float().view(P, Cout, Cin).permute(1, 0, 2).reshape(Cout, P * Cin)  # W'[co][p*Cin+ci]
             wimg, cpg, kwg = K.pack_gcn_weight(wgf, dtype)
@@ -233,24 +250,20 @@ class StgcnLayerFunction(torch.autograd.Function):
         # ---- temporal conv on relu(norm1(g)) (norm applied in the prologue)
         wt3 = wt.detach().float().squeeze(-1).permute(2, 0, 1)  # [Kt][Cout][Cin]
         wtp, cpt, kpt = K.pack_weight(wt3, dtype, stride=stride)
+
         u = K.conv_rows(g, wtp, Cout, Cout, cpt, kpt, T, T_out, Kt=kt, stride=stride, pad=pad,
                         bias=bt.detach().float().contiguous(), stats=st2 if norm == BN else None,
                         tag=f"tcn_fwd_c{Cout}" if stride == 1 else None, **pro1)
-
-        # ---- residual branch
-        r = None
-        if res_conv:
-            wr3 = wr.detach().float().view(1, Cout, Cin)
-            wrp, cpr, kpr = K.pack_weight(wr3, dtype)
-            r = K.conv_rows(x, wrp, Cin, Cout, cpr, kpr, T, T_out, Kt=1, stride=stride, pad=0,
-                            bias=br.detach().float().contiguous(), stats=str_ if norm == BN else None)
+        if side is not None:  # join the residual branch
+            main = torch.cuda.current_stream(dev)
+            main.wait_stream(side)
+            for t_ in side_made:
+                t_.record_stream(main)
 
         # ---- y = relu(norm2(u) + res)
         if norm == BN:
             mr2, sc2, sh2 = K.bn_finalize(st2, st2.shape[0], cpt, Cout, n2w.detach().float(), n2b.detach().float())
             if res_conv:
-                mrr, scr, shr = K.bn_finalize(str_, str_.shape[0], cpr, Cout, nrw.detach().float(),
-                                              nrb.detach().float())
                 y = K.bn_apply(u, sc2, sh2, M2, Cout, res_mode=2, r=r, rsc=scr, rsh=shr)
             else:
                 y = K.bn_apply(u, sc2, sh2, M2, Cout, res_mode=1 if residual else 0, r=x if residual else None)
@@ -258,7 +271,6 @@ class StgcnLayerFunction(torch.autograd.Function):
             ls2 = K.ln_stats(u, N * T_out, V, Cout)
             g2, b2 = _flat_ln(n2w), _flat_ln(n2b)
             if res_conv:
-                lsr = K.ln_stats(r, N * T_out, V, Cout)
                 y = K.ln_apply(u, ls2, g2, b2, M2, V, Cout, res_mode=2, r=r, rst=lsr, rg=_flat_ln(nrw),
                                rb=_flat_ln(nrb))
             else:
