@@ -73,9 +73,14 @@ class Model(nn.Module):
             else:
                 w = self.fcn_in.weight
             x = LF.Conv1x1Function.apply(x, w, self.fcn_in.bias, self.compute_dtype)   # stgcn.py:85
-        for gcn, importance in zip(self.gcn_networks, self.edge_importance):       # stgcn.py:88-89
+        if isinstance(self.edge_importance, nn.ParameterList) and len(self.edge_importance):
+            # A * M_i of every layer as one stacked product (one launch each way instead of one per layer)
+            A_eff = (self.A * torch.stack(list(self.edge_importance))).unbind(0)
+        else:
+            A_eff = [self.A * m for m in self.edge_importance]
+        for gcn, A_i in zip(self.gcn_networks, A_eff):                                # stgcn.py:88-89
             gcn.bind_graph(self.A)  # support of the static graph (cached; no sync after the first call)
-            x = gcn(x, self.A * importance)
+            x = gcn(x, A_i)
         x = LF.PoolFunction.apply(x, self.compute_dtype)                            # stgcn.py:92
         x = LF.Conv1x1Function.apply(x, self.fcn_out.weight, self.fcn_out.bias, self.compute_dtype)  # :95
         return x.squeeze(-1).float()                                                # :97
