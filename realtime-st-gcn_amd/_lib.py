@@ -200,7 +200,9 @@ def require_device(t: torch.Tensor):
 
 
 def stream() -> int:
-    return torch.cuda.current_stream().cuda_stream
+    """Raw handle of the current device's current stream (what torch.cuda.current_stream().cuda_stream
+    returns, without building a Stream object: 0.1 vs 2.6 us per call, and every kernel wrapper calls it)."""
+    return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
 
 
 def dtype_code(dt: torch.dtype) -> int:

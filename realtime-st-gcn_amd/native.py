@@ -501,10 +501,8 @@ def bn_stats_partial(x, M, C, ld=None):
 
 
 def bn_finalize(part, nb, ld_part, C, gamma, beta, eps=1e-5):
-    dev = part.device
-    mr = torch.empty((C, 2), dtype=torch.float32, device=dev)
-    sc = torch.empty(C, dtype=torch.float32, device=dev)
-    sh = torch.empty(C, dtype=torch.float32, device=dev)
+    buf = torch.empty(4 * C, dtype=torch.float32, device=part.device)  # (mean, rstd) pairs | scale | shift
+    mr, sc, sh = buf[:2 * C].view(C, 2), buf[2 * C:3 * C], buf[3 * C:]
     L.check(L.lib().stgcn_bn_finalize(part.data_ptr(), nb, ld_part, C, L.ptr(gamma), L.ptr(beta), eps, mr.data_ptr(),
                                       sc.data_ptr(), sh.data_ptr(), L.stream()), "bn_finalize")
     return mr, sc, sh

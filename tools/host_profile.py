@@ -52,3 +52,13 @@ if __name__ == "__main__":
     host = sum(ph.values()) / steps * 1e3
     print({k: round(v / steps * 1e3, 3) for k, v in ph.items()}, "host ms/step", round(host, 3), "wall ms/step",
           round(wall, 3), flush=True)
+    if "cprofile" in sys.argv:  # where the host time goes (per-function own time over 10 steps)
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        for _ in range(10):
+            step(False)
+        pr.disable()
+        torch.cuda.synchronize()
+        pstats.Stats(pr).sort_stats("tottime").print_stats(40)
