@@ -133,12 +133,18 @@ def layer_roofline(pkg, dev, reps=20, norm="BatchNorm"):
     K.layer_fused = tagged
     prev_hook = K.EVENT_HOOK
     K.EVENT_HOOK = hook
+    prev_env = os.environ.get("STGCN_FUSED_BN")
+    os.environ["STGCN_FUSED_BN"] = "1"  # BatchNorm layers take the fused path on request only
     try:
         with torch.no_grad():
             fused_ms = timed(lambda: layer(x, A))
     finally:
         K.layer_fused = orig
         K.EVENT_HOOK = prev_hook
+        if prev_env is None:
+            os.environ.pop("STGCN_FUSED_BN", None)
+        else:
+            os.environ["STGCN_FUSED_BN"] = prev_env
     xg = x.detach().requires_grad_(True)  # a differentiable input: the training path's forward (unfused)
     unfused_ms = timed(lambda: layer(xg, A))
     pairs = [(kev[i], kev[i + 1]) for i in range(6, len(kev) - 1, 2)]  # skip the warm-up launches

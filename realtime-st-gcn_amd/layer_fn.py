@@ -183,9 +183,12 @@ class StgcnLayerFunction(torch.autograd.Function):
         # ---- graph convolution: g = sum_p A_p-mix(x) W_p + bias2d
         sup = cfg[5] if len(cfg) > 5 else None
         gather = sup is not None and A32.dim() == 3 and not sup.dense(P)
-        if (gather and len(cfg) > 7 and cfg[7]
+        if (gather and len(cfg) > 7 and cfg[7] and (norm == LN or os.environ.get("STGCN_FUSED_BN") == "1")
                 and K.layer_fused_ok(sup, P, Cin, Cout, V, kt, stride, dtype)):
-            # inference: the fused layer kernel (g never leaves the chip; nothing saved for backward)
+            # inference: the fused layer kernel (g never leaves the chip; nothing saved for backward).
+            # LayerNorm layers by default (one kernel, 2.4x the unfused forward); BatchNorm layers only on
+            # request (STGCN_FUSED_BN=1): their two-pass form measured slower than the unfused forward
+            # (DESIGN 4.6), so inference keeps the faster route
             return fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, sup, dtype,
                                        cache=cfg[8] if len(cfg) > 8 else None, norm=norm)
         tiled = gather and K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype)  # fused frame-tiled graph conv

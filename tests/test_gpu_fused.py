@@ -92,7 +92,29 @@ def _count_fused(P, monkeypatch):
         return orig(*a, **k)
 
     monkeypatch.setattr(P.native, "layer_fused", spy)
+    monkeypatch.setenv("STGCN_FUSED_BN", "1")  # BatchNorm layers take the fused path on request only
     return calls
+
+
+def test_bn_inference_default_route(P, monkeypatch):
+    """Without STGCN_FUSED_BN a BatchNorm layer's inference forward takes the unfused route (measured faster
+    than the two-pass fused form) and still matches the fp32 oracle."""
+    calls = _count_fused(P, monkeypatch)
+    monkeypatch.delenv("STGCN_FUSED_BN", raising=False)
+    torch.manual_seed(4)
+    N, T, V = 4, 64, 25
+    A = _graph(P)
+    layer = P.StgcnLayer(64, 64, (9, V), 3, V, stride=1, normalization="BatchNorm")
+    sd = {k: v.clone() for k, v in layer.state_dict().items()}
+    x = torch.randn(N, 64, T, V)
+    ref = O.stgcn_layer(x, A, sd, "", 9, 1, True, "BatchNorm")
+    layer = layer.to(DEV)
+    P.set_compute_dtype(layer, "bf16")
+    with torch.no_grad():
+        y = layer(x.to(DEV), A.to(DEV))
+    torch.cuda.synchronize()
+    assert not calls, "BatchNorm inference took the fused kernel without STGCN_FUSED_BN=1"
+    assert_close(y.float().cpu(), ref, 3e-2, "unfused inference layer")
 
 
 @pytest.mark.parametrize("norm", ["BatchNorm", "LayerNorm"])
