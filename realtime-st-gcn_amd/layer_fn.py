@@ -34,6 +34,7 @@ from . import native as K
 BN, LN = "BatchNorm", "LayerNorm"
 
 _SIDE = {}
+_SIDE_OFF = os.environ.get("STGCN_SIDE_STREAM", "1") == "0"
 
 
 def _side_stream(dev):
@@ -45,7 +46,7 @@ def _side_stream(dev):
     a fork event and joined before the backward returns, so the latency-bound reduction kernels of the
     branch fill the gaps and tails of the data-gradient kernels.  Off under stream capture (HIP graphs) and
     with STGCN_SIDE_STREAM=0 (A/B)."""
-    if os.environ.get("STGCN_SIDE_STREAM", "1") == "0" or torch.cuda.is_current_stream_capturing():
+    if _SIDE_OFF or torch.cuda.is_current_stream_capturing():
         return None
     s = _SIDE.get(dev.index)
     if s is None:
@@ -447,7 +448,9 @@ class StgcnLayerFunction(torch.autograd.Function):
         if side is not None:  # join the weight-gradient branch
             main = torch.cuda.current_stream(dev)
             main.wait_stream(side)
-            for t in list(grads.values()) + [dA]:
+            # tensors allocated on the side stream and used on the main one (the others are views of the
+            # zero arena, allocated on the main stream)
+            for t in (grads.get("bg"), dA):
                 if t is not None:
                     t.record_stream(main)
 
