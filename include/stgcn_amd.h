@@ -167,6 +167,12 @@ long stgcn_gcn_tile_row_blocks(int NT, int V, int Cout);
 long stgcn_gconv_row_blocks(int NT, int V);
 int stgcn_gconv_weights(const float* A, const float* W, const int* nbr, const int* deg, int P, int V, int J, int Cout,
                         int Cin, int trans, void* out, int rows_pad, int cols_pad, int dtype, void* stream);
+/* stgcn_gconv_weights (forward form, trans = 0) and stgcn_gcn_bias for a shared A in ONE launch:
+ * bias2d[w][co] = sum_p b[p*Cout + co] * sum_v A[p][v][w]  (fp32 [V][Cout]; replaces the separate
+ * bias-through-A launch of ConvTemporalGraphical.forward, tgcn.py:71-79, conv bias then einsum with A) */
+int stgcn_gconv_weights_bias(const float* A, const float* W, const float* b, const int* nbr, const int* deg, int P,
+                             int V, int J, int Cout, int Cin, void* out, int rows_pad, int cols_pad, float* bias2d,
+                             int dtype, void* stream);
 /* dweff[w][j][co][ci] = sum_i dy[(i,w)][co] * x[(i, nbr[w][j])][ci]   (fp32 [V][J][Cout][Cin], written
  * whole: 0 for the unused slots j >= deg[w]) */
 typedef struct {

@@ -88,6 +88,8 @@ _SIGS = {
     "stgcn_bn_bwd_fused_reduce": (c_int, [ctypes.POINTER(BnBwdDesc), c_int, c_void_p]),
     "stgcn_bn_bwd_fused_apply": (c_int, [ctypes.POINTER(BnBwdDesc), c_int, c_void_p]),
     "stgcn_gconv_row_blocks": (c_long, [c_int, c_int]),
+    "stgcn_gconv_weights_bias": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_void_p, c_int, c_int, c_void_p, c_int,
+                                                                       c_void_p]),
     "stgcn_gconv_weights": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 6 + [c_void_p, c_int, c_int,
                                                                                            c_int, c_void_p]),
     "stgcn_gconv_wgrad": (c_int, [ctypes.POINTER(GconvWgradDesc), c_int, c_void_p]),

@@ -36,7 +36,8 @@ int bn_bwd_fused_reduce_launch(const stgcn_bn_bwd_desc& a, int dtype, hipStream_
 int bn_bwd_fused_apply_launch(const stgcn_bn_bwd_desc& a, int dtype, hipStream_t s);
 int gconv_launch(const stgcn_gconv_desc& a, int dtype, hipStream_t s);
 int gconv_weights_launch(const float* A, const float* W, const int* nbr, const int* deg, int P, int V, int J, int Cout,
-                         int Cin, int trans, void* out, int R_pad, int C_pad, int dtype, hipStream_t s);
+                         int Cin, int trans, void* out, int R_pad, int C_pad, int dtype, hipStream_t s,
+                         const float* bconv = nullptr, float* bias2d = nullptr);
 long gconv_wgrad_workspace(const stgcn_gconv_wgrad_desc& a, int dtype);
 int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s);
 int gconv_wgrad_finish_launch(const float* dweff, const float* A, const float* W, const int* nbr, const int* deg,
@@ -223,6 +224,16 @@ int stgcn_gconv_weights(const float* A, const float* W, const int* nbr, const in
     return STGCN_EBADSHAPE;
   return gconv_weights_launch(A, W, nbr, deg, P, V, J, Cout, Cin, trans, out, rows_pad, cols_pad, dtype,
                               STREAM(stream));
+}
+int stgcn_gconv_weights_bias(const float* A, const float* W, const float* b, const int* nbr, const int* deg, int P,
+                             int V, int J, int Cout, int Cin, void* out, int rows_pad, int cols_pad, float* bias2d,
+                             int dtype, void* stream) {
+  CHECK_DTYPE(dtype);
+  if (!A || !W || !b || !nbr || !deg || !out || !bias2d || P <= 0 || V <= 0 || J <= 0 || Cout <= 0 || Cin <= 0 ||
+      rows_pad < Cout || cols_pad < Cin || (cols_pad % 8) != 0)
+    return STGCN_EBADSHAPE;
+  return gconv_weights_launch(A, W, nbr, deg, P, V, J, Cout, Cin, 0, out, rows_pad, cols_pad, dtype, STREAM(stream),
+                              b, bias2d);
 }
 long stgcn_gconv_wgrad_workspace(const stgcn_gconv_wgrad_desc* d, int dtype) {
   if (!d || (dtype != 0 && dtype != 1)) return 0;

@@ -481,7 +481,7 @@ constexpr int GW_JMAX = 8;  // neighbour slots per joint whose loads are issued 
 template <typename T>
 __global__ void gconv_weights_kernel(const float* __restrict__ A, const float* __restrict__ W, const int* nbr,
                                      const int* deg, int P, int V, int J, int Cout, int Cin, int trans, T* out,
-                                     int R_pad, int C_pad) {
+                                     int R_pad, int C_pad, const float* __restrict__ bconv, float* __restrict__ bias2d) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int C8 = C_pad / 8;
   const long total = (long)V * R_pad * C8;
@@ -501,6 +501,17 @@ __global__ void gconv_weights_kernel(const float* __restrict__ A, const float* _
     a = (int)(t1 / C8);
   }
   const int R = trans ? Cin : Cout, C = trans ? Cout : Cin;
+  if (bias2d && !trans && c0 == 0 && r < Cout) {
+    // the graph conv's bias pushed through A in the same launch (stgcn_gcn_bias, same summation order):
+    // bias2d[a][co] = sum_p b[p*Cout + co] * colsum_p[a],  colsum_p[a] = sum_v A[p][v][a]
+    float sb = 0.f;
+    for (int p = 0; p < P; ++p) {
+      float cs = 0.f;
+      for (int v = 0; v < V; ++v) cs += A[((long)p * V + v) * V + a];
+      sb += bconv[p * Cout + r] * cs;
+    }
+    bias2d[(long)a * Cout + r] = sb;
+  }
   float wv[GW_PMAX][8];
 #pragma unroll
   for (int p = 0; p < GW_PMAX; ++p)
@@ -1280,16 +1291,17 @@ int gconv_launch(const stgcn_gconv_desc& a, int dtype, hipStream_t s) {
 }
 
 int gconv_weights_launch(const float* A, const float* W, const int* nbr, const int* deg, int P, int V, int J, int Cout,
-                         int Cin, int trans, void* out, int R_pad, int C_pad, int dtype, hipStream_t s) {
+                         int Cin, int trans, void* out, int R_pad, int C_pad, int dtype, hipStream_t s,
+                         const float* bconv, float* bias2d) {
   if (C_pad % 8 || P > GW_PMAX) return STGCN_EBADSHAPE;
   const long total = (long)V * R_pad * (C_pad / 8);
   const unsigned blocks = (unsigned)((total + 255) / 256);
   if (dtype == 1)
     hipLaunchKernelGGL(gconv_weights_kernel<bf16>, dim3(blocks), dim3(256), 0, s, A, W, nbr, deg, P, V, J, Cout, Cin,
-                       trans, (bf16*)out, R_pad, C_pad);
+                       trans, (bf16*)out, R_pad, C_pad, bconv, bias2d);
   else
     hipLaunchKernelGGL(gconv_weights_kernel<float>, dim3(blocks), dim3(256), 0, s, A, W, nbr, deg, P, V, J, Cout,
-                       Cin, trans, (float*)out, R_pad, C_pad);
+                       Cin, trans, (float*)out, R_pad, C_pad, bconv, bias2d);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
 

@@ -193,7 +193,8 @@ class StgcnLayerFunction(torch.autograd.Function):
             return fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, sup, dtype,
                                        cache=cfg[8] if len(cfg) > 8 else None, norm=norm)
         tiled = gather and K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype)  # fused frame-tiled graph conv
-        bias2d = K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
+        # gathered path: bias2d comes out of the effective-weight launch below
+        bias2d = None if (gather and not tiled) else K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
         if norm == BN:  # all BatchNorm partial-statistics buffers of the layer from one zero fill
             cpo = -(-Cout // K.col_tile(Cout)) * K.col_tile(Cout)
             rb1 = (K.gcn_tile_row_blocks(N * T, V, Cout) if tiled else K.gconv_row_blocks(N * T, V)) if gather \
@@ -230,7 +231,7 @@ class StgcnLayerFunction(torch.autograd.Function):
             XA = None
         elif gather:  # joint-gathered GEMM over per-joint effective weights (gconv.hip), no XA in HBM
             wg2 = wg.detach().float().reshape(P * Cout, Cin).contiguous()
-            wgp = K.gconv_weights(A32, wg2, sup, Cout, Cin, False, dtype)
+            wgp, bias2d = K.gconv_weights(A32, wg2, sup, Cout, Cin, False, dtype, bias=bg.detach().float().contiguous())
             cpg, kpg = wgp.shape[2], wgp.shape[3]
             if norm == BN:
                 assert cpg == cpo

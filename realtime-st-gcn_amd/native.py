@@ -282,14 +282,24 @@ class GraphSupport:
         return self.nnz > P * self.V
 
 
-def gconv_weights(A, W, sup, Cout, Cin, trans, dtype):
-    """Effective weights [V][J][R_pad][C_pad]: trans 0 -> (Cout, Cin) from S lists, 1 -> (Cin, Cout) from R lists."""
+def gconv_weights(A, W, sup, Cout, Cin, trans, dtype, bias=None):
+    """Effective weights [V][J][R_pad][C_pad]: trans 0 -> (Cout, Cin) from S lists, 1 -> (Cin, Cout) from R lists.
+
+    ``bias`` (forward only: the conv bias, fp32 [P*Cout]): the same launch also pushes it through A
+    (stgcn_gconv_weights_bias), and the call returns (weights, bias2d [V][Cout]) — gcn_bias's result."""
     A = _dense(A)
     P, V = A.shape[0], A.shape[-1]
     R, C = (Cin, Cout) if trans else (Cout, Cin)
     rp = -(-R // col_tile(R)) * col_tile(R)
     cpad = -(-C // 32) * 32
     out = torch.empty((V, sup.J, rp, cpad), dtype=dtype, device=A.device)
+    if bias is not None:
+        assert not trans
+        b2 = torch.empty((V, Cout), dtype=torch.float32, device=A.device)
+        L.check(L.lib().stgcn_gconv_weights_bias(A.data_ptr(), W.data_ptr(), bias.data_ptr(), sup.nbr.data_ptr(),
+                                                 sup.deg.data_ptr(), P, V, sup.J, Cout, Cin, out.data_ptr(), rp, cpad,
+                                                 b2.data_ptr(), L.dtype_code(dtype), L.stream()), "gconv_weights_bias")
+        return out, b2
     nbr, deg = (sup.rnbr, sup.rdeg) if trans else (sup.nbr, sup.deg)
     L.check(L.lib().stgcn_gconv_weights(A.data_ptr(), W.data_ptr(), nbr.data_ptr(), deg.data_ptr(), P, V, sup.J,
                                         Cout, Cin, int(trans), out.data_ptr(), rp, cpad, L.dtype_code(dtype),

@@ -69,3 +69,25 @@ def test_gconv_fwd_bwd(K, pkg, dtype, tol, Cin, Cout, N, T):
     m = sup.mask.cpu().unsqueeze(0).expand_as(A)
     assert_close(dA.cpu()[m], A.grad[m], tol, "gconv dA")
     assert float(dA.cpu()[~m].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("Cin,Cout", [(64, 64), (128, 256), (24, 40)])
+def test_gconv_weights_bias_one_launch(K, pkg, dtype, Cin, Cout):
+    """stgcn_gconv_weights_bias (effective weights + the bias pushed through A in one launch) writes exactly
+    what stgcn_gconv_weights and stgcn_gcn_bias write separately (same summation orders: bit-equal)."""
+    torch.manual_seed(5)
+    A0 = torch.tensor(pkg.Graph(**pkg.PKU_MMD).A, dtype=torch.float32)
+    A = (A0 * (torch.rand(A0.shape) + 0.5)).to(DEV)
+    P, V = A.shape[0], A.shape[-1]
+    sup = K.GraphSupport(A)
+    W = torch.randn(P * Cout, Cin, device=DEV)
+    b = torch.randn(P * Cout, device=DEV)
+    w_ref = K.gconv_weights(A, W, sup, Cout, Cin, False, dtype)
+    b_ref = K.gcn_bias(A, b, 1, Cout)
+    w_one, b_one = K.gconv_weights(A, W, sup, Cout, Cin, False, dtype, bias=b)
+    torch.cuda.synchronize()
+    for a in range(V):  # slots past deg[a] are never written (nor read by gconv)
+        d = int(sup.deg[a])
+        assert torch.equal(w_one[a, :d], w_ref[a, :d]), a
+    assert torch.equal(b_one, b_ref.view(V, Cout))
