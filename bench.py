@@ -133,18 +133,15 @@ def layer_roofline(pkg, dev, reps=20, norm="BatchNorm"):
     K.layer_fused = tagged
     prev_hook = K.EVENT_HOOK
     K.EVENT_HOOK = hook
-    prev_env = os.environ.get("STGCN_FUSED_BN")
-    os.environ["STGCN_FUSED_BN"] = "1"  # BatchNorm layers take the fused path on request only
+    prev_route = pkg.routing.ROUTING.fused_bn_inference
+    pkg.routing.ROUTING.fused_bn_inference = True  # BatchNorm layers take the fused path on request only
     try:
         with torch.no_grad():
             fused_ms = timed(lambda: layer(x, A))
     finally:
         K.layer_fused = orig
         K.EVENT_HOOK = prev_hook
-        if prev_env is None:
-            os.environ.pop("STGCN_FUSED_BN", None)
-        else:
-            os.environ["STGCN_FUSED_BN"] = prev_env
+        pkg.routing.ROUTING.fused_bn_inference = prev_route
     xg = x.detach().requires_grad_(True)  # a differentiable input: the training path's forward (unfused)
     unfused_ms = timed(lambda: layer(xg, A))
     pairs = [(kev[i], kev[i + 1]) for i in range(6, len(kev) - 1, 2)]  # skip the warm-up launches
@@ -204,6 +201,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-layer-roofline", action="store_true", help="skip the north_star layer timing (profiling)")
     ap.add_argument("--graph", action="store_true",
                     help="capture the step into HIP graphs and replay them (measured slower than eager here)")
     args = ap.parse_args()
@@ -372,8 +370,9 @@ def main():
                     per[g] = json.load(f).get("hbm_bytes_per_launch")
         if kt and all(per.get(g) for g, _ in kt):
             traffic = sum(per[g] for g, _ in kt) / len(kt)
-        lroof = layer_roofline(pkg, dev) if world == 1 else None
-        lroof_ln = layer_roofline(pkg, dev, norm="LayerNorm") if world == 1 else None
+        lay = world == 1 and not args.no_layer_roofline
+        lroof = layer_roofline(pkg, dev) if lay else None
+        lroof_ln = layer_roofline(pkg, dev, norm="LayerNorm") if lay else None
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(pkg, cpu_sd)

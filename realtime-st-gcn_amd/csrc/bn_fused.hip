@@ -255,9 +255,9 @@ Geo geo(long M, int C, int vec) {
   g.RPI = 256 / g.CU;
   // >= 2 iterations of UNR rows per thread and at most ~1024 blocks (partials folded by sum4_kernel)
   const long step = (long)g.RPI * UNR;
-  // block target (A/B knob STGCN_BNF_BLOCKS): 512 / 1024 / 2048 measured 1.67 / 1.68 / 1.8 ms per step for all
-  // fused BN backward passes + sum4 folds (512 speeds up apply, slows reduce)
-  static const long tb = getenv("STGCN_BNF_BLOCKS") ? atol(getenv("STGCN_BNF_BLOCKS")) : 1024;
+  // block target: 512 / 1024 / 2048 measured 1.67 / 1.68 / 1.8 ms per step for all fused BN backward passes +
+  // sum4 folds (512 speeds up apply, slows reduce)
+  constexpr long tb = 1024;
   long it = (M + step * tb - 1) / (step * tb);
   if (it < 2) it = 2;
   g.rpb = step * it;

@@ -320,8 +320,7 @@ long conv_rows_num_row_blocks(long M, int cout);
 
 // returns -1 when the shape is not handled here
 int conv1x1_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
-  static const bool off = getenv("STGCN_NO_CONV1X1") != nullptr;  // A/B switch
-  if (off || dtype != 1 || a.Kt != 1 || a.pad != 0 || a.pro != 0) return -1;
+  if (dtype != 1 || a.Kt != 1 || a.pad != 0 || a.pro != 0) return -1;
   if (a.stride == 1 && a.T_in == a.T_out && !a.stats && a.bias_mode >= 0 && a.bias_mode <= 1 &&
       (long)a.Cout_pad * a.Cin_pad <= 4096) {
     const long M = (long)a.N * a.T_out * a.V;

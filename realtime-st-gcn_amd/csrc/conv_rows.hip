@@ -356,8 +356,7 @@ long conv_rows_num_row_blocks(long M, int cout) { (void)cout; return (M + 127) /
 int conv_tile_launch(const ConvArgs& a, int dtype, hipStream_t s);
 
 int conv_rows_launch(const ConvArgs& a, int dtype, hipStream_t s) {
-  static const bool v1_only = getenv("STGCN_CONV_V1") != nullptr;  // A/B switch for the microbench
-  if (!v1_only) {  // frame-tiled kernel (conv_tile.hip) for the shapes it covers
+  {  // frame-tiled kernels (conv_tile.hip and the kernels it dispatches to) for the shapes they cover
     const int r = conv_tile_launch(a, dtype, s);
     if (r >= 0) return r;
   }

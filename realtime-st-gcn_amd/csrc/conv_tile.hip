@@ -561,31 +561,18 @@ int launch_tile(const stgcn_conv_desc& a, long max_row_blocks, hipStream_t s) {
   const size_t B_BYTES = (size_t)KT * BN * L::RB;
   const size_t pro_bytes = a.pro == 1 ? 2 * sizeof(float) * (size_t)a.Cin_pad : 0;
   const size_t red = a.stats ? (size_t)WM * BN * 16 : 0;
-  // 3 B stages (prefetch distance 2) for the bf16 stride-1 framed convs when they fit the 160 KB LDS
-  // and every chunk is loaded by the unconditional fast path
-  constexpr bool CAN3 = sizeof(T) == 2 && S == 1 && KT > 1;
-  const bool fast = (a.in_ld % (16 / (int)sizeof(T))) == 0 && (a.Cin % KC) == 0;
-  size_t lds3 = 2 * (size_t)A_BYTES + 3 * B_BYTES + pro_bytes;
-  if (red > lds3) lds3 = red;
-  // measured: no gain over 2 stages on the config-2 shapes (the chunk barriers, not load latency, bound
-  // this kernel), so the 3-stage pipeline is opt-in (STGCN_TILE_NB3=1) for experiments
-  static const bool want3 = getenv("STGCN_TILE_NB3") != nullptr;
-  const bool use3 = want3 && CAN3 && fast && a.pro != 2 && !g.parity && lds3 <= 160 * 1024;
+  // two B stages: a 3-stage pipeline (prefetch distance 2) measured no gain on the config-2 shapes (the
+  // chunk barriers, not load latency, bound this kernel) and was removed
   size_t lds = 2 * ((size_t)A_BYTES + B_BYTES) + pro_bytes;
   if (red > lds) lds = red;
-  if (!use3 && lds > 160 * 1024) return -1;
+  if (lds > 160 * 1024) return -1;
   if (stgcn_lds_attr((const void*)conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, false, 2>, 160 * 1024, s) ||
       (S == 2 &&
-       stgcn_lds_attr((const void*)conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, S == 2, 2>, 160 * 1024, s)) ||
-      (CAN3 && stgcn_lds_attr((const void*)conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, false, CAN3 ? 3 : 2>,
-                              160 * 1024, s)))
+       stgcn_lds_attr((const void*)conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, S == 2, 2>, 160 * 1024, s)))
     return STGCN_EHIP;
   if (g.parity)
     hipLaunchKernelGGL((conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, S == 2, 2>), dim3((unsigned)nblk),
                        dim3(WM * WN * 64), lds, s, a, g);
-  else if (use3)
-    hipLaunchKernelGGL((conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, false, CAN3 ? 3 : 2>),
-                       dim3((unsigned)nblk), dim3(WM * WN * 64), lds3, s, a, g);
   else
     hipLaunchKernelGGL((conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, false, 2>), dim3((unsigned)nblk),
                        dim3(WM * WN * 64), lds, s, a, g);
@@ -617,7 +604,6 @@ int conv_wide_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s);
 int conv1x1_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s);
 
 int conv_tile_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
-  static const bool no_persist = getenv("STGCN_NO_PERSIST") != nullptr;  // A/B switch
   if (a.Kt == 1) {  // 1x1 convs (residual, stride 1 or 2, and their input grads): row GEMM (conv1x1.hip)
     const int r = conv1x1_launch(a, dtype, s);
     if (r >= 0) return r;
@@ -628,7 +614,7 @@ int conv_tile_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
     const int r = conv_wide_launch(a, dtype, s);
     if (r >= 0) return r;
   }
-  if (!no_persist) {  // weight-resident persistent kernel for the 64-channel Kt=9 convs
+  {  // weight-resident persistent kernel for the 64-channel Kt=9 convs
     const int r = conv_persist_launch(a, dtype, s);
     if (r >= 0) return r;
   }

@@ -74,7 +74,6 @@ struct WGeom {
   int fold;     // stride-2 folding: 0 none, 1 input parity (forward), 2 output parity (data grad)
   int cpar;     // fold 1: 64-channel items per input parity; fold 2: output channels per parity
   int wc32, wk16;  // fragment image dims: (output channels / 32, input channels / 16)
-  int strided;     // 1: block b takes tiles b, b + grid, ... (A/B switch STGCN_WIDE_STRIDED); 0: a contiguous run
   int pair;        // ncol == 2: blocks b and b + 8 (one XCD) take the two column tiles of the same row-tile run
   int red_off;     // LDS byte offset of the Welford partials (after the halo buffers and, SEP, the tile image)
 };
@@ -131,9 +130,9 @@ __global__ __launch_bounds__((4 + NHW) * 64, 1) void conv_wide_kernel(const stgc
   const int V = a.V;
   const int grid = gridDim.x;
   const int tpb = (g.ntiles + grid - 1) / grid;  // contiguous tile runs: neighbour halos stay in L2
-  int tile0 = g.strided ? (int)blockIdx.x : (int)blockIdx.x * tpb;
-  int tstep = g.strided ? grid : 1;
-  int ntile_b = g.strided ? (g.ntiles - (int)blockIdx.x + grid - 1) / grid : min(tpb, g.ntiles - tile0);
+  int tile0 = (int)blockIdx.x * tpb;
+  int tstep = 1;
+  int ntile_b = min(tpb, g.ntiles - tile0);
   if (g.pair) {
     // workgroups are dealt round-robin to the 8 XCDs: blocks b = x + 8 s share XCD x; the pair (s = 2q, 2q+1)
     // walks the same run of row tiles, one column tile each, at the same pace, so every halo item one of
@@ -608,17 +607,12 @@ int pack_s2frag_launch(const float* src, long s0, long s1, long s2, int Co, int 
 long conv_rows_num_row_blocks(long M, int cout);
 
 int conv_wide_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
-  static const bool off = getenv("STGCN_NO_WIDE") != nullptr;  // A/B switch
-  if (off || dtype != 1 || !a.w_frag) return -1;
+  if (dtype != 1 || !a.w_frag) return -1;
   if (a.Kt != 9 || a.pad != 4) return -1;
   if (a.pro != 0 && a.pro != 1) return -1;
   if (a.bias_mode != 0 && a.bias_mode != 1) return -1;
   if (a.in_ld % 8 || a.V > 32 || a.Cin % 8 || a.Cout % 8 || a.out_ld % 8) return -1;
   WGeom g;
-  {
-    static const int st = getenv("STGCN_WIDE_STRIDED") ? atoi(getenv("STGCN_WIDE_STRIDED")) : 0;
-    g.strided = st;
-  }
   int ktap, cin_f, cout_f;  // folded conv: taps, input / output channels
   if (a.stride == 1) {
     if (a.T_in != a.T_out) return -1;
@@ -684,11 +678,8 @@ int conv_wide_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
   const int ncu = stgcn_cu_count(s);
   const int tpb = (g.ntiles + ncu - 1) / ncu;
   int grid = (g.ntiles + tpb - 1) / tpb;
-  {
-    static const int pe = getenv("STGCN_WIDE_PAIR") ? atoi(getenv("STGCN_WIDE_PAIR")) : 1;  // A/B switch
-    g.pair = pe && !g.strided && g.ncol == 2 && ncu >= 16;
-    if (g.pair) grid = ncu & ~15;
-  }
+  g.pair = g.ncol == 2 && ncu >= 16;
+  if (g.pair) grid = ncu & ~15;
   const dim3 gd((unsigned)grid);
   auto kern = [&]() -> void (*)(const stgcn_conv_desc, const WGeom) {
     if (kg == 32)  // C = 64: 8 helper waves, separate tile image (64.6 vs 70.5 us, tools/bench_conv.py tcn_fwd_c64)

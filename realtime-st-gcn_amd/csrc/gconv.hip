@@ -454,11 +454,8 @@ int launch_gconv(const stgcn_gconv_desc& a, hipStream_t s) {
   if (stgcn_lds_attr((const void*)gconv_kernel<T, WM, WN, TM, TN, KC, false, NSTG>, 160 * 1024, s) ||
       stgcn_lds_attr((const void*)gconv_kernel<T, WM, WN, TM, TN, KC, true, NSTG>, 160 * 1024, s))
     return STGCN_EHIP;
-  // 16-B row stores through the LDS scratch whenever rows are 16-B aligned (A/B: STGCN_GCONV_SCATTER=1 keeps
-  // the per-element stores for plain outputs)
-  const char* sce = getenv("STGCN_GCONV_SCATTER");
-  const bool scatter = sce && sce[0] == '1';
-  const bool accv = (a.accumulate || !scatter) && (a.out_ld % VEC) == 0 && (a.Cout % VEC) == 0;
+  // 16-B row stores through the LDS scratch whenever rows are 16-B aligned (per-element stores otherwise)
+  const bool accv = (a.out_ld % VEC) == 0 && (a.Cout % VEC) == 0;
   if (accv)
     hipLaunchKernelGGL((gconv_kernel<T, WM, WN, TM, TN, KC, true, NSTG>), dim3((unsigned)nblk), dim3(WM * WN * 64),
                        lds, s, a, g);
@@ -1208,21 +1205,16 @@ __global__ void gconv_dA_reduce_kernel(const float* __restrict__ part, const int
 
 // joint-grouped plan (gconv_wgrad2_kernel): COB (output channels per block); 0 = not taken
 int w2_cob(const stgcn_gconv_wgrad_desc& a) {
-  static const bool off = getenv("STGCN_GCONV_WGRAD1") != nullptr;  // A/B switch: the per-pair kernel
-  if (off || a.J > J2 || a.Cin % 64 || a.Cout % 64) return 0;
+  if (a.J > J2 || a.Cin % 64 || a.Cout % 64) return 0;
   // COB = 64: 32-row tiles, 48 KB of LDS, three 4-wave blocks per CU.  Measured against COB = 128 (64-row
   // tiles, one 8-wave block per CU): C=128 78 vs 85 us, C=256 143 vs 153 us, equal at 64 -> 128; and
-  // 56 vs 72 us (per-pair kernel) at C = 64.  COB = 128 stays selectable (STGCN_GCONV_WGRAD2_COB128).
-  static const bool cob128 = getenv("STGCN_GCONV_WGRAD2_COB128") != nullptr;
-  return (cob128 && a.Cout % 128 == 0) ? 128 : 64;
+  // 56 vs 72 us (per-pair kernel) at C = 64.
+  return 64;
 }
 
 // the DMA-ring kernel (gconv_wgrad3) for COB = 64, except 64 -> 128 channels, where the register-staged
-// kernel measured 74 vs 82 us; STGCN_GCONV_WGRAD2_REG forces the register-staged one everywhere
-bool w3_ok(const stgcn_gconv_wgrad_desc& a) {
-  static const bool reg = getenv("STGCN_GCONV_WGRAD2_REG") != nullptr;
-  return !reg && !(a.Cin == 64 && a.Cout == 128);
-}
+// kernel measured 74 vs 82 us
+bool w3_ok(const stgcn_gconv_wgrad_desc& a) { return !(a.Cin == 64 && a.Cout == 128); }
 
 WGG wplan2(const stgcn_gconv_wgrad_desc& a, int cob) {
   WGG g{};
@@ -1233,8 +1225,7 @@ WGG wplan2(const stgcn_gconv_wgrad_desc& a, int cob) {
   const long target = cob == 64 ? 512 : 256;  // COB 64: 3 register-staged / 2 DMA-ring blocks fit a CU
   // DMA ring: block target by the group count, measured per layer (targets 512 / 1024 / 2048): C = 64
   // (25 groups) 49 / 40 / 56 us, C = 128 64 / 81 / 75 us, C = 256 108 / 113 / 130 us
-  static const long t3env = getenv("STGCN_W3_TARGET") ? atol(getenv("STGCN_W3_TARGET")) : 0;
-  const long t3 = t3env > 0 ? t3env : groups <= 32 ? 1024 : 512;
+  const long t3 = groups <= 32 ? 1024 : 512;
   long R = (cob == 64 && w3_ok(a)) ? (t3 + groups - 1) / groups : (target + groups - 1) / groups;
   if (R > g.ntile) R = g.ntile;
   if (R < 1) R = 1;
@@ -1277,8 +1268,7 @@ int gconv_launch(const stgcn_gconv_desc& a, int dtype, hipStream_t s) {
     // DMA K loop (two LDS stages, 64-channel chunks) whenever rows allow it: tools/bench_conv.py gconv, us,
     // register-staged -> DMA: C=64 fwd 44.7 -> 42.7, dgrad 40.7 -> 36.6; C=128 59.8 -> 56.0 / 51.8 -> 48.9;
     // 64->128 69.8 -> 67.2 / 58.2 -> 49.8; C=256 (256-row tiles) 95.7 -> 85.2 / 88.1 -> 75.2
-    const char* de = getenv("STGCN_GCONV_DMA");  // A/B: 0 = register-staged kernels
-    const bool dma = !(de && de[0] == '0') && a.Cin % 64 == 0 && a.Cin == a.Cin_pad && a.in_ld % 8 == 0;
+    const bool dma = a.Cin % 64 == 0 && a.Cin == a.Cin_pad && a.in_ld % 8 == 0;
     if (dma) {
       if (!wide) return launch_gconv<bf16, 4, 1, 1, 2, 64, 2>(a, s);
       return a.Cin >= 256 ? launch_gconv<bf16, 4, 2, 2, 2, 64, 2>(a, s) : launch_gconv<bf16, 4, 2, 1, 2, 64, 2>(a, s);
@@ -1330,7 +1320,7 @@ int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s
     g.rowpart = a.rowsum ? g.slab + (long)g.R * E : nullptr;
     const bool ring = cob == 64 && w3_ok(a);
     const size_t lds = ring ? (size_t)W3_LDS : 2 * (size_t)(cob / 32 + 2 * J2) * w2m(cob) * WPR;
-    auto* k = ring ? gconv_wgrad3_kernel : cob == 128 ? gconv_wgrad2_kernel<128> : gconv_wgrad2_kernel<64>;
+    auto* k = ring ? gconv_wgrad3_kernel : gconv_wgrad2_kernel<64>;
     if (stgcn_lds_attr((const void*)k, 160 * 1024, s)) return STGCN_EHIP;
     const long blocks = (long)a.V * g.nco * g.nci * g.R;
     hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(ring ? 256 : cob / 16 * 64), lds, s, a, g);

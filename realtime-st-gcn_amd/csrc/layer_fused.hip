@@ -44,6 +44,13 @@
 
 namespace {
 
+// Timing ablations (results wrong): build with -DSTGCN_FUSED_DBG=<mask> (tools only, never the shipped library):
+// bit 0 skip the GCN math, bit 1 the TCN math, bit 2 (LN) the residual loads, bit 3 (LN) the LN2 statistics
+#ifndef STGCN_FUSED_DBG
+#define STGCN_FUSED_DBG 0
+#endif
+constexpr int DBG = STGCN_FUSED_DBG;
+
 constexpr int NWT = 4, NWG = 4, NW = NWT + NWG;
 constexpr int C = 64, G = C / 32;      // channels (in = out), 32-channel blocks
 constexpr int HALO = 4, KT = 9;
@@ -124,8 +131,6 @@ DEV float wave_total(float v) {
 DEV unsigned lds_u32(const void* p) { return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p; }
 
 struct FGeom {
-  int dbg;     // A/B timing switch (STGCN_FUSED_DBG; results wrong): bit 0 skip the GCN math, bit 1 the TCN math,
-               // bit 2 (LN) the residual loads, bit 3 (LN) the LN2 statistics reductions
   int runs_n;  // runs per sample
   int run;     // frames per run (multiple of CF)
   int off_tab, off_ring, off_h, off_red;  // LDS offsets
@@ -356,7 +361,7 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
     lds_barrier();  // S_0: frames 0..15 ready
     for (int s = 1; s <= nsteps; ++s) {
       // step s: the TCN waves read frames [8s-8, 8s+8); this wave writes frames base = 8s + 8 ..
-      if (s < nsteps && !(g.dbg & 1)) compute(CF * (s + 1) + gw, s + 1 < nsteps ? CF * (s + 2) + gw : -1);
+      if (s < nsteps && !(DBG & 1)) compute(CF * (s + 1) + gw, s + 1 < nsteps ? CF * (s + 2) + gw : -1);
       lds_barrier();  // S_s
     }
     if (a.stats) lds_barrier();  // R: the TCN waves' statistics hand-off
@@ -404,7 +409,7 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
   // the step loop per row-tile count (compile-time: no per-k-step branches in the MFMA stream)
   auto tcn_run = [&]<int RTN>() {
     for (int s = 1; s <= nsteps; ++s) {
-      if (g.dbg & 2) {
+      if (DBG & 2) {
         lds_barrier();
         continue;
       }
@@ -478,7 +483,7 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
 #pragma unroll
         for (int i = 0; i < RT; ++i) {
           const int r = (rh * RT + i) * 32 + lr;
-          const bool ok = i < RTN && rok[i] && r < vrows && a.residual && !(g.dbg & 4);
+          const bool ok = i < RTN && rok[i] && r < vrows && a.residual && !(DBG & 4);
 #pragma unroll
           for (int q4 = 0; q4 < 4; ++q4) {
             const bf16x4 zr = {};
@@ -486,7 +491,10 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
           }
         }
         // z = acc + bias; per row tile ti and each of the <= 3 frames its 32 rows touch (V > 16): the
-        // (sum, sum of squares) of this wave's 32 channels over the tile's rows of that frame -> LDS
+        // (sum, sum of squares) of this wave's 32 channels over the tile's rows of that frame -> LDS.
+        // Shifted by the pivot mean_c(bias) (the same constant in every wave), so a large common bias does
+        // not cancel catastrophically in sum(z^2) - sum(z) * mean
+        const float piv = a.tbias ? wave_total(a.tbias[lane]) * (1.f / C) : 0.f;
 #pragma unroll
         for (int i = 0; i < RT; ++i) {
           if (i >= RTN) break;
@@ -496,15 +504,16 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
             acc[i][q] += tb[q];
-            su += acc[i][q];
-            sq = fmaf(acc[i][q], acc[i][q], sq);
+            const float d = acc[i][q] - piv;
+            su += d;
+            sq = fmaf(d, d, sq);
           }
           const int ti = rh * RT + i, flo = ti * 32 / V;
 #pragma unroll
           for (int k = 0; k < 3; ++k) {
             const bool m = ok && fo_[i] == flo + k;
             float ts = 0.f, tq = 0.f;
-            if (!(g.dbg & 8)) {
+            if (!(DBG & 8)) {
               ts = wave_total(m ? su : 0.f);
               tq = wave_total(m ? sq : 0.f);
             }
@@ -531,8 +540,8 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
             su += u0.x + u1.x;
             sq += u0.y + u1.y;
           }
-          const float cnt = (float)(V * C), mean = su / cnt;
-          const float2 st = make_float2(mean, 1.f / sqrtf(fmaxf(sq - su * mean, 0.f) / (cnt - 1.f) + 1e-5f));
+          const float cnt = (float)(V * C), dmean = su / cnt;  // mean of z - piv
+          const float2 st = make_float2(piv + dmean, 1.f / sqrtf(fmaxf(sq - su * dmean, 0.f) / (cnt - 1.f) + 1e-5f));
           const int w = jw_[i];
 #pragma unroll
           for (int q4 = 0; q4 < 4; ++q4) {
@@ -634,10 +643,6 @@ int layer_fused_launch(const stgcn_layer_fused_desc& a, hipStream_t s) {
   if (a.N < 1 || a.T < 1 || a.V <= 16 || a.V > VMAX || a.P < 1 || a.P > 3) return STGCN_EBADSHAPE;
   if (a.x_ld < C || a.x_ld % 8 || a.z_ld < C || a.z_ld % 4) return STGCN_EBADSHAPE;
   FGeom g = plan(a.N, a.T);
-  {
-    const char* e = getenv("STGCN_FUSED_DBG");
-    g.dbg = e ? atoi(e) : 0;
-  }
   const long nblk = (long)a.N * g.runs_n;
   if (nblk > 0x7fffffffL) return STGCN_EBADSHAPE;
   const int K16 = a.P * G * 2;

@@ -143,36 +143,37 @@ __global__ __launch_bounds__(1024) void seg_loss_kernel(LossArgs a) {
           gce[k] = a.mode == 2 ? dz / cur.p[k] : dz;  // z = log p
         }
       }
-      const float py = lane_pick(cur.p, y, lane);
-      float above = 0.f;  // classes ranked strictly above y (torch.topk order, ties aside)
+      // top-1 / top-5 from five rounds of argmax (torch.topk order: NaN ranks above every number, equal
+      // values by lowest class index), so the hit counts always agree with the returned top-5 classes
+      float v[kPer];
 #pragma unroll
-      for (int k = 0; k < kPer; ++k)
-        if (lane + 64 * k < C && cur.p[k] > py) above += 1.f;
-      above = wave_sum(above);
-      top1 += above < 0.5f ? 1.f : 0.f;
-      top5 += above < 4.5f ? 1.f : 0.f;
-      if (a.top5) {  // five rounds of argmax (lowest index among equals)
-        float v[kPer];
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) v[k] = lane + 64 * k < C ? cur.p[k] : -INFINITY;
-        for (int r = 0; r < 5 && r < C; ++r) {
-          float bv = -INFINITY;
-          int bc = 1 << 30;
-#pragma unroll
-          for (int k = 0; k < kPer; ++k)
-            if (v[k] > bv) bv = v[k], bc = lane + 64 * k;
-#pragma unroll
-          for (int o = 32; o > 0; o >>= 1) {
-            const float ov = __shfl_xor(bv, o);
-            const int oc = __shfl_xor(bc, o);
-            if (ov > bv || (ov == bv && oc < bc)) bv = ov, bc = oc;
-          }
-          if (lane == 0) a.top5[(long)w * 5 + r] = bc;
-#pragma unroll
-          for (int k = 0; k < kPer; ++k)
-            if (lane + 64 * k == bc) v[k] = -INFINITY;
-        }
+      for (int k = 0; k < kPer; ++k) {
+        const float pv = cur.p[k];
+        v[k] = lane + 64 * k < C ? (pv != pv ? INFINITY : pv) : -INFINITY;
       }
+      bool hit = false;
+      for (int r = 0; r < 5 && r < C; ++r) {
+        float bv = -INFINITY;
+        int bc = 1 << 30;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k)
+          if (v[k] > bv || (v[k] == bv && lane + 64 * k < bc && lane + 64 * k < C)) bv = v[k], bc = lane + 64 * k;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const float ov = __shfl_xor(bv, o);
+          const int oc = __shfl_xor(bc, o);
+          if (ov > bv || (ov == bv && oc < bc)) bv = ov, bc = oc;
+        }
+        if (a.top5 && lane == 0) a.top5[(long)w * 5 + r] = bc;
+        if (bc == y) {
+          hit = true;
+          if (r == 0) top1 += 1.f;
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; ++k)
+          if (lane + 64 * k == bc) v[k] = -INFINITY;
+      }
+      top5 += hit ? 1.f : 0.f;
     }
 
     const float* prow = w > 0 ? a.p + (long)(w - 1) * a.ldp : a.prev;

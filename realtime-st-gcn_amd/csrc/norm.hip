@@ -570,9 +570,9 @@ int grid_for(long work) {
 }
 
 // elementwise kernels: ~2048 blocks (one resident wave of 8 blocks per CU).  bn_apply at C=64..256 measured
-// 41 us at 1024-2048 blocks, 43 at 3072, 45.6 at 4096, 56.5 at 8192.  STGCN_ELT_BLOCKS: A/B knob.
+// 41 us at 1024-2048 blocks, 43 at 3072, 45.6 at 4096, 56.5 at 8192.
 long elt_rows_per_block(long M) {
-  static const long nb = getenv("STGCN_ELT_BLOCKS") ? atol(getenv("STGCN_ELT_BLOCKS")) : 2048;
+  constexpr long nb = 2048;
   long rpb = (M + nb - 1) / nb;
   return rpb < 32 ? 32 : rpb;
 }

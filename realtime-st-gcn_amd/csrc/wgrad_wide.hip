@@ -285,8 +285,6 @@ __global__ void unfold_reduce2_kernel(const float* __restrict__ part, int RS, in
 WPlan wplan(const stgcn_wgrad_desc& a) {
   WPlan p{};
   p.ok = false;
-  static const bool off = getenv("STGCN_NO_WGRAD_WIDE") != nullptr;  // A/B switch
-  if (off) return p;
   if (a.Kt != 9 || a.pad != 4) return p;
   WWGeom& g = p.g;
   if (a.stride == 1 && a.T_in == a.T_out) {

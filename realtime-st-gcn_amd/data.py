@@ -75,9 +75,11 @@ class SkeletonDatasetFromDirectory(torch.utils.data.Dataset):
 def prep_pkummd(dir):
     """PKU-MMD release -> the trial layout above (data_prep/prep.py:15-45): features (L, 150) text ->
     (3, L, 25, 2) float32 .npy; labels ``class,start,end,...`` -> per-frame classes (0 = background) .csv;
-    split by cross-view.txt (second line, comma-separated train ids); the source files are removed."""
+    split by cross-view.txt (second line split on ", " exactly as prep.py:17 does: no stripping, so an id
+    that ends the line keeps its newline, never matches and its trial goes to 'val', as in the reference);
+    the source files are removed."""
     with open(os.path.join(dir, "cross-view.txt")) as f:
-        train = set(s.strip() for s in f.readlines()[1].split(", "))
+        train = set(f.readlines()[1].split(", "))
     for split in ("train", "val"):
         for sub in ("features", "labels"):
             os.makedirs(os.path.join(dir, split, sub), exist_ok=True)

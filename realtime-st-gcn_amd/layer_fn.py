@@ -25,16 +25,15 @@ re-packing (tiny tensors) and the (P x V)-sized reshuffles of the A/bias gradien
 from __future__ import annotations
 
 import contextlib
-import os
 
 import torch
 
 from . import native as K
+from .routing import ROUTING
 
 BN, LN = "BatchNorm", "LayerNorm"
 
 _SIDE = {}
-_SIDE_OFF = os.environ.get("STGCN_SIDE_STREAM", "1") == "0"
 
 
 def _side_stream(dev):
@@ -45,8 +44,8 @@ def _side_stream(dev):
     graph-conv wgrad + dW/dA finish + bias through A) branch off it.  They are issued on this stream after
     a fork event and joined before the backward returns, so the latency-bound reduction kernels of the
     branch fill the gaps and tails of the data-gradient kernels.  Off under stream capture (HIP graphs) and
-    with STGCN_SIDE_STREAM=0 (A/B)."""
-    if _SIDE_OFF or torch.cuda.is_current_stream_capturing():
+    with routing.ROUTING.side_stream off."""
+    if not ROUTING.side_stream or torch.cuda.is_current_stream_capturing():
         return None
     s = _SIDE.get(dev.index)
     if s is None:
@@ -164,6 +163,7 @@ def fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, su
     return K.bn_apply(z, sc2, sh2, N * T * V, Cout, res_mode=1 if residual else 0, r=x if residual else None)
 
 
+@K.on_tensor_device
 class StgcnLayerFunction(torch.autograd.Function):
     """Autograd node for the whole StgcnLayer (BN or LN variant)."""
 
@@ -184,7 +184,7 @@ class StgcnLayerFunction(torch.autograd.Function):
         # ---- graph convolution: g = sum_p A_p-mix(x) W_p + bias2d
         sup = cfg[5] if len(cfg) > 5 else None
         gather = sup is not None and A32.dim() == 3 and not sup.dense(P)
-        if (gather and len(cfg) > 7 and cfg[7] and (norm == LN or os.environ.get("STGCN_FUSED_BN") == "1")
+        if (gather and len(cfg) > 7 and cfg[7] and (norm == LN or ROUTING.fused_bn_inference)
                 and K.layer_fused_ok(sup, P, Cin, Cout, V, kt, stride, dtype)):
             # inference: the fused layer kernel (g never leaves the chip; nothing saved for backward).
             # LayerNorm layers by default (one kernel, 2.4x the unfused forward); BatchNorm layers only on
@@ -484,6 +484,7 @@ def _bias_through_A(dA, A32, bg, bgp, dg, S_fused, z_S, M1, Cout, V, grads):
     return dA
 
 
+@K.on_tensor_device
 class GcnFunction(torch.autograd.Function):
     """ConvTemporalGraphical.forward alone (models/utils/tgcn.py:58-79): conv1x1(+bias) -> @A -> sum_P."""
 
@@ -532,6 +533,7 @@ class GcnFunction(torch.autograd.Function):
         return dx, dA.to(adt), dwg.to(wg.dtype), dbg.to(bg.dtype), None
 
 
+@K.on_tensor_device
 class Conv1x1Function(torch.autograd.Function):
     """Pointwise conv on channels-last rows (fcn_in / fcn_out, stgcn.py:49,74): y = W x + b."""
 
@@ -560,6 +562,7 @@ class Conv1x1Function(torch.autograd.Function):
         return dx, dw.to(w.dtype), db.to(w.dtype), None
 
 
+@K.on_tensor_device
 class InputBatchNormFunction(torch.autograd.Function):
     """BatchNorm1d(V*C) on (N, V*C, T) (models/utils/batchnorm.py:13-23): per-(v,c) batch stats over
     (N,T).  Channels-last NTVC rows are exactly [N*T][V*C], so it is a row BatchNorm with V*C channels."""
@@ -594,6 +597,7 @@ class InputBatchNormFunction(torch.autograd.Function):
         return dx, sums[:, 1].to(w.dtype), sums[:, 0].to(w.dtype), None
 
 
+@K.on_tensor_device
 class WindowStageFunction(torch.autograd.Function):
     """norm_in + fcn_in of a batch of sliding windows (WindowSegment, segment_generator.py:132-145; stgcn.py:
     82-85) straight from the padded capture (1, Cin, Lp, V): windows [n0, n0+nw) of W frames, never formed
@@ -655,6 +659,7 @@ def _bn_apply_flat(dy, x, mr, gamma, sums, F_, CV, dx):
     return out
 
 
+@K.on_tensor_device
 class LayerNormFunction(torch.autograd.Function):
     """Custom LayerNorm([C,1,V]) (models/utils/layernorm.py:22-28) on channels-last rows."""
 
@@ -679,6 +684,7 @@ class LayerNormFunction(torch.autograd.Function):
         return dx, dgb[0].view(w.shape).to(w.dtype), dgb[1].view(b.shape).to(b.dtype), None
 
 
+@K.on_tensor_device
 class PoolFunction(torch.autograd.Function):
     """F.avg_pool2d(x, x.size()[2:]) (stgcn.py:92) -> (N, C, 1, 1); joints_only=True is the RT head's
     AvgPool2d((1, V)) (rtstgcn.py:127,149) -> (N, C, T, 1)."""
@@ -719,6 +725,7 @@ def _strided_rows_ok(t, dtype) -> bool:
     return True
 
 
+@K.on_tensor_device
 class AttentionFunction(torch.autograd.Function):
     """C = softmax(theta^T phi) per (n, p) (models/aagcn/aagcn.py:142-145), theta/phi channels-last rows."""
 
@@ -745,6 +752,7 @@ def attn_proj_ok(x, Cin, Nt, Np, dtype) -> bool:
     return dtype == torch.bfloat16 and Cin % 16 == 0 and Cin <= 256 and Nt % 4 == 0 and Np % 4 == 0
 
 
+@K.on_tensor_device
 class AttnProjFunction(torch.autograd.Function):
     """AgcnLayer's theta and phi 1x1 convs (aagcn.py:139-141) for a bf16 model: one fp32-output projection
     of the bf16 activation (stgcn_attn_proj: no fp32 copy of x, no fp32 GEMM), theta and phi the two
@@ -788,6 +796,7 @@ class AttnProjFunction(torch.autograd.Function):
                 db[Nt:].to(wdt))
 
 
+@K.on_tensor_device
 class RtOfflineLayerFunction(torch.autograd.Function):
     """OfflineLayer.forward (models/rtstgcn/rtstgcn.py:343-389) with the Toeplitz matmul it intends
     (rtstgcn.py:366-379) evaluated as the causal K//S-tap box sum it is:

@@ -7,13 +7,15 @@ keep the reference's call signatures; ``predictions`` is the (1, C, L) series of
 (loss.hip: log-softmax, weighted CE, clamped temporal MSE, top-1/top-5, and the gradient of both
 loss terms in the same pass); the backward is one more launch.  ``shard=`` (parallel.SegmentShard)
 makes a data-parallel rank's share of a trial's loss exact: per-rank values sum to the single-process
-loss and per-rank gradients equal the single-process ones (see parallel.sharded_loss).
+loss and per-rank gradients equal the single-process ones (parallel.sharded_loss adds DDP's world
+scaling and empty shards).
 """
 from __future__ import annotations
 
 import torch
 
 from . import _lib as L
+from . import native as K
 
 _MODES = {"logits": 0, "logsoftmax": 1, "softmax": 2}
 
@@ -57,6 +59,7 @@ def seg_loss(p_rows, labels, weight, first=0, mode=0, prev=None, den=None, pairs
     return out, dce, dmse, t5
 
 
+@K.on_tensor_device
 class SegLossFunction(torch.autograd.Function):
     """(ce, mse) of loss.py:25-41 with the gradients computed in the forward launch."""
 

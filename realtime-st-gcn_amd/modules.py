@@ -11,13 +11,12 @@ parity path, bf16 (fp32 accumulate) for the perf path.  Activations are returned
 """
 from __future__ import annotations
 
-import os
-
 import torch
 import torch.nn as nn
 
 from . import layer_fn as F_
 from . import native as K
+from .routing import ROUTING
 
 _DTYPES = {"fp32": torch.float32, "bf16": torch.bfloat16, torch.float32: torch.float32,
            torch.bfloat16: torch.bfloat16}
@@ -115,6 +114,21 @@ class StgcnLayer(nn.Module):
         self._graph_bound = False
         self._fused_cache = {}  # packed weights of the fused inference forward (layer_fn._packs)
 
+    def _drop_packs(self):
+        """Forget the packed weights of the fused inference forward.  The cache is keyed by each weight's
+        storage and in-place version counter, which optimizer steps and ordinary in-place ops bump; writes
+        through ``param.data`` do not, so call ``train()`` / ``eval()`` (or load a state_dict) after such a
+        write — both drop the cache."""
+        self._fused_cache.clear()
+
+    def train(self, mode: bool = True):
+        self._drop_packs()
+        return super().train(mode)
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        self._drop_packs()
+        return super()._load_from_state_dict(*args, **kwargs)
+
     def bind_graph(self, A, masked=True):
         """Cache the support lists of the static adjacency A (P, V, V) for the joint-gathered graph
         conv.  Every A later passed to forward must have its nonzeros inside this support.  A Model
@@ -127,7 +141,7 @@ class StgcnLayer(nn.Module):
         self._graph_bound = self._graph_bound or masked
 
     def graph_support(self, A):
-        if A.dim() != 3 or os.environ.get("STGCN_GCN_AFIRST"):
+        if A.dim() != 3 or ROUTING.gcn_afirst:
             return None  # per-sample A (AAGCN) or forced A-first path
         self.bind_graph(A, masked=False)
         return self._gsup

@@ -7,11 +7,58 @@ HIP stream; all arithmetic happens in the HIP kernels.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
 from . import _lib as L
+from .routing import ROUTING
+
+class device_of:
+    """Device guard (SURVEY 8(b) threading): make the device of tensor ``t`` current for the body, so that
+    L.stream() — the current stream of the current device — and every allocation belong to the tensor's
+    device even when the caller has another device current (DataParallel-style threads, multi-GPU hosts).
+    Costs one device query when the device is already current."""
+    __slots__ = ("idx", "prev")
+
+    def __init__(self, t):
+        self.idx = t.device.index if getattr(t, "is_cuda", False) else None
+        self.prev = None
+
+    def __enter__(self):
+        if self.idx is not None:
+            cur = torch._C._cuda_getDevice()
+            if cur != self.idx:
+                torch._C._cuda_setDevice(self.idx)
+                self.prev = cur
+        return self
+
+    def __exit__(self, *exc):
+        if self.prev is not None:
+            torch._C._cuda_setDevice(self.prev)
+            self.prev = None
+        return False
+
+
+def on_tensor_device(cls):
+    """Class decorator for the autograd Functions: run forward / backward under device_of(the first CUDA
+    tensor argument)."""
+    import functools
+
+    def wrap(fn):
+        @functools.wraps(fn)
+        def g(ctx, *args):
+            t = next((a for a in args if isinstance(a, torch.Tensor) and a.is_cuda), None)
+            if t is None:
+                return fn(ctx, *args)
+            with device_of(t):
+                return fn(ctx, *args)
+        return staticmethod(g)
+
+    for name in ("forward", "backward"):
+        if name in cls.__dict__:
+            setattr(cls, name, wrap(cls.__dict__[name].__func__))
+    return cls
+
 
 # Optional instrumentation: callable(tag, phase) invoked right before ("start") and after ("end")
 # a tagged launch, on the launching stream (bench.py records HIP events with it).  None = off.
@@ -326,9 +373,6 @@ def pack_frag1(w2: torch.Tensor, dtype) -> tuple:
     return buf[cp * kp:], cp, kp
 
 
-_GCN_TILE = os.environ.get("STGCN_GCN_TILE", "0")  # "0" never (default), "1" every shape it takes, "auto"
-
-
 def gcn_tile_ok(sup, P, Cin, Cout, V, dtype, trans=False) -> bool:
     """Whether the graph conv of a layer (Cin -> Cout) runs on the fused kernel (gcn_tile.hip: joint mix
     + 1x1 conv as two chained MFMA products) in the forward (trans False) or data-grad direction.
@@ -337,11 +381,11 @@ def gcn_tile_ok(sup, P, Cin, Cout, V, dtype, trans=False) -> bool:
     MFMA work of the gathered one (stage-1 mix per 64-channel column tile, joints padded 25 -> 32) and
     loses.  Default "0": inside the training step (cold HBM inputs) "auto" measured equal to gconv.hip
     (0.46 ms/step either way), so the gathered path stays the default."""
-    if _GCN_TILE == "0" or dtype != torch.bfloat16 or sup is None or P > 3 or not 16 < V <= 32:
+    if ROUTING.gcn_tile == "0" or dtype != torch.bfloat16 or sup is None or P > 3 or not 16 < V <= 32:
         return False
     if Cin not in (64, 128, 256) or Cout not in (64, 128, 256):
         return False
-    return _GCN_TILE == "1" or (Cin if trans else Cout) == 64
+    return ROUTING.gcn_tile == "1" or (Cin if trans else Cout) == 64
 
 
 def gcn_tile_row_blocks(NT: int, V: int, Cout: int) -> int:
@@ -390,14 +434,11 @@ def gcn_tile(x, A, wimg, kw_pad, Cin, Cout, cp, sup, trans_a=False, bias=None, s
     return out
 
 
-_FUSED = os.environ.get("STGCN_FUSED", "1")
-
-
 def layer_fused_ok(sup, P, Cin, Cout, V, kt, stride, dtype) -> bool:
     """Whether a layer's forward can run as the fused graph conv + BN1 + ReLU + temporal conv kernel
     (layer_fused.hip): bf16, 64 -> 64 channels, stride 1, Kt = 9, a batch-shared graph, 16 < V <= 25.
-    STGCN_FUSED=0 disables it (A/B)."""
-    return (_FUSED != "0" and dtype == torch.bfloat16 and sup is not None and P <= 3 and 16 < V <= 25
+    routing.ROUTING.fused_inference off disables it."""
+    return (ROUTING.fused_inference and dtype == torch.bfloat16 and sup is not None and P <= 3 and 16 < V <= 25
             and Cin == 64 and Cout == 64 and kt == 9 and stride == 1)
 
 
@@ -459,8 +500,7 @@ def gconv(x, wpk, sup, Cin, Cout, trans=False, bias=None, stats=None, out=None, 
 
 def gconv_wgrad_rowsum_ok(sup, Cin, Cout, dtype) -> bool:
     """Whether gconv_wgrad can also return the per-joint row sums of dy (joint-grouped kernel only)."""
-    return (dtype == torch.bfloat16 and Cin % 64 == 0 and Cout % 64 == 0 and sup.J <= 5
-            and "STGCN_GCONV_WGRAD1" not in os.environ)
+    return dtype == torch.bfloat16 and Cin % 64 == 0 and Cout % 64 == 0 and sup.J <= 5
 
 
 def gconv_wgrad(x, dy, sup, Cin, Cout, rowsum=None):

@@ -102,6 +102,20 @@ def exchange_shard(pred_local, labels_full, weight, start, L, group=None):
     return SegmentShard(prev, den, L - 1, start == 0)
 
 
+def sharded_loss(crit, i, pred_local, labels_local, shard: SegmentShard, world: int):
+    """This rank's share of a sharded trial's loss, ready for DDP: ``crit`` (loss.Loss) on the local
+    predictions (1, C, n) and their labels with the shard's cross-rank terms, each term multiplied by
+    ``world`` because DistributedDataParallel averages the gradients over ranks (the shares sum to the
+    trial's loss, so the averaged gradient is the single-process one).  A rank whose shard is empty
+    (n = 0, possible when a trial has fewer units than ranks) contributes zeros connected to its
+    predictions, so its backward still takes part in the all-reduce."""
+    if pred_local.shape[2] == 0:
+        z = pred_local.sum() * 0.0
+        return z, z
+    ce, mse = crit(i, pred_local, labels_local, shard=shard)
+    return ce * world, mse * world
+
+
 def ddp(model: torch.nn.Module, device: torch.device, bucket_cap_mb: int = 16):
     """DistributedDataParallel over the initialised process group (RCCL on the GPU box, gloo in tests)."""
     from torch.nn.parallel import DistributedDataParallel as DDP

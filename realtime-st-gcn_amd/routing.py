@@ -1,0 +1,29 @@
+"""Kernel-routing switches of the package, in one place.
+
+Every switch only chooses between kernels that compute the same result (each route is covered by the -m gpu
+suite); none changes numerics beyond the rounding order of its kernels.  Defaults are the measured-fastest
+routes on MI355X.  The environment variables are read once at import; code (tests, tools) may
+also assign the attributes directly.
+
+    side_stream         STGCN_SIDE_STREAM=0   weight-gradient branch of a layer backward on a per-device side
+                                              stream (default on)
+    fused_inference     STGCN_FUSED=0         no_grad forward of 64->64 stride-1 layers through the fused layer
+                                              kernel layer_fused.hip (default on for LayerNorm layers)
+    fused_bn_inference  STGCN_FUSED_BN=1      BatchNorm layers too (default off: measured slower)
+    gcn_tile            STGCN_GCN_TILE=0|1|auto  graph conv on the two-stage MFMA kernel gcn_tile.hip (default 0)
+    gcn_afirst          STGCN_GCN_AFIRST=1    force the A-first graph conv (amix + GEMM) for shared graphs
+"""
+import os
+
+
+class _Routing:
+    def __init__(self):
+        e = os.environ.get
+        self.side_stream = e("STGCN_SIDE_STREAM", "1") != "0"
+        self.fused_inference = e("STGCN_FUSED", "1") != "0"
+        self.fused_bn_inference = e("STGCN_FUSED_BN", "0") == "1"
+        self.gcn_tile = e("STGCN_GCN_TILE", "0")
+        self.gcn_afirst = e("STGCN_GCN_AFIRST", "0") not in ("0", "")
+
+
+ROUTING = _Routing()

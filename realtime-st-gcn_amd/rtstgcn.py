@@ -122,14 +122,25 @@ class OnlineLayer(nn.Module):
         self._packed = None
         return
 
+    def train(self, mode: bool = True):
+        """Also drops the per-frame weight packs (see _weights: writes through ``param.data`` are not seen
+        by the version counters, so train()/eval()/eval_()/load_state_dict re-pack)."""
+        self._packed = None
+        return super().train(mode)
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        self._packed = None
+        return super()._load_from_state_dict(*args, **kwargs)
+
     def _weights(self, Cin):
         """Per-frame constants (packed GCN weight, A-pushed conv bias, packed residual weight), built once and
         reused while the parameters are unchanged (keyed by their in-place version counters): the per-frame
         step then launches only data-dependent kernels."""
         A = self.aggregate.A
         rw = self.residual[0].weight if self.is_residual_conv else None
-        key = (A.data_ptr(), A._version, self.conv.weight._version, self.conv.bias._version,
-               None if rw is None else rw._version)
+        key = (A.data_ptr(), A._version, self.conv.weight.data_ptr(), self.conv.weight._version,
+               self.conv.bias.data_ptr(), self.conv.bias._version,
+               None if rw is None else (rw.data_ptr(), rw._version))
         pk = getattr(self, "_packed", None)
         if pk is not None and pk[0] == key:
             return pk[1]

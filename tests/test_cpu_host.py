@@ -93,3 +93,64 @@ def test_bench_multi_gpu_launch_rejected_cleanly_without_devices():
     r = subprocess.run([sys.executable, bench, "--gpus", "0", "--steps", "1"], capture_output=True, text=True,
                        timeout=300, env=env)
     assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr and "Traceback" not in r.stderr
+
+
+class _FakeDev:
+    def __init__(self, i):
+        self.index = i
+
+
+class _FakeCuda:
+    """Stands in for a CUDA tensor on device ``i`` (the guard only reads .is_cuda and .device.index)."""
+
+    def __init__(self, i):
+        self.is_cuda = True
+        self.device = _FakeDev(i)
+
+
+def test_device_guard_follows_tensor(pkg, monkeypatch):
+    """SURVEY 8(b) threading: every autograd Function runs under native.device_of(first CUDA input), so a
+    launch takes the tensor's device (its current stream, its allocations) even when the caller has another
+    device current, and the caller's device is restored afterwards (also on error)."""
+    K = pkg.native
+    state = {"cur": 0, "sets": []}
+    monkeypatch.setattr(torch._C, "_cuda_getDevice", lambda: state["cur"])
+
+    def setdev(i):
+        state["sets"].append(i)
+        state["cur"] = i
+    monkeypatch.setattr(torch._C, "_cuda_setDevice", setdev)
+    seen = []
+    with K.device_of(_FakeCuda(1)):
+        seen.append(state["cur"])
+    assert seen == [1] and state["cur"] == 0 and state["sets"] == [1, 0]
+    state["sets"].clear()
+    with K.device_of(_FakeCuda(0)):  # already current: no device switch at all
+        pass
+    assert state["sets"] == []
+    with pytest.raises(ValueError):
+        with K.device_of(_FakeCuda(3)):
+            raise ValueError("inside")
+    assert state["cur"] == 0
+
+    @K.on_tensor_device
+    class Fn:
+        @staticmethod
+        def forward(ctx, x, y):
+            return state["cur"]
+
+        @staticmethod
+        def backward(ctx, g):
+            return state["cur"]
+
+    # the decorator picks the first CUDA torch.Tensor argument: a CPU tensor that reports cuda:2
+    t = torch.zeros(1)
+    monkeypatch.setattr(torch.Tensor, "is_cuda", property(lambda self: True))
+    monkeypatch.setattr(torch.Tensor, "device", property(lambda self: _FakeDev(2)))
+    assert Fn.forward(None, 5, t) == 2 and Fn.backward(None, t) == 2 and state["cur"] == 0
+    # every autograd Function of the package is wrapped
+    import inspect
+    for mod in (pkg.layer_fn, pkg.loss):
+        for name, cls in inspect.getmembers(mod, inspect.isclass):
+            if issubclass(cls, torch.autograd.Function) and cls.__module__ == mod.__name__:
+                assert cls.forward.__wrapped__ is not None, name

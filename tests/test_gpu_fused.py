@@ -92,15 +92,15 @@ def _count_fused(P, monkeypatch):
         return orig(*a, **k)
 
     monkeypatch.setattr(P.native, "layer_fused", spy)
-    monkeypatch.setenv("STGCN_FUSED_BN", "1")  # BatchNorm layers take the fused path on request only
+    monkeypatch.setattr(P.routing.ROUTING, "fused_bn_inference", True)  # BatchNorm: fused path on request only
     return calls
 
 
 def test_bn_inference_default_route(P, monkeypatch):
-    """Without STGCN_FUSED_BN a BatchNorm layer's inference forward takes the unfused route (measured faster
+    """Without routing.fused_bn_inference a BatchNorm layer's inference forward takes the unfused route (measured faster
     than the two-pass fused form) and still matches the fp32 oracle."""
     calls = _count_fused(P, monkeypatch)
-    monkeypatch.delenv("STGCN_FUSED_BN", raising=False)
+    monkeypatch.setattr(P.routing.ROUTING, "fused_bn_inference", False)
     torch.manual_seed(4)
     N, T, V = 4, 64, 25
     A = _graph(P)
@@ -113,7 +113,7 @@ def test_bn_inference_default_route(P, monkeypatch):
     with torch.no_grad():
         y = layer(x.to(DEV), A.to(DEV))
     torch.cuda.synchronize()
-    assert not calls, "BatchNorm inference took the fused kernel without STGCN_FUSED_BN=1"
+    assert not calls, "BatchNorm inference took the fused kernel without fused_bn_inference"
     assert_close(y.float().cpu(), ref, 3e-2, "unfused inference layer")
 
 
@@ -198,3 +198,65 @@ def test_model_inference_fused_config2(P, monkeypatch, norm):
     torch.cuda.synchronize()
     assert len(calls) == 3
     assert_close(y.float().cpu(), ref, 3e-2, "model logits (fused inference)")
+
+
+def _ln_layer(P, seed, tcn_bias=None):
+    torch.manual_seed(seed)
+    layer = P.StgcnLayer(64, 64, (9, 25), 3, 25, stride=1, normalization="LayerNorm")
+    if tcn_bias is not None:
+        with torch.no_grad():
+            layer.tcn[2].bias.copy_(tcn_bias)
+    return layer
+
+
+def test_fused_pack_cache_invalidation(P, monkeypatch):
+    """The fused inference forward caches its packed weights (keyed by storage + in-place version):
+    an optimizer-style in-place update is seen at once; a write through ``param.data`` (invisible to the
+    version counter) is seen after train()/eval(), as documented (modules.StgcnLayer._drop_packs).  Each
+    result equals the unfused route on the same weights."""
+    calls = _count_fused(P, monkeypatch)
+    A = _graph(P).to(DEV)
+    layer = _ln_layer(P, 11).to(DEV).eval()
+    P.set_compute_dtype(layer, "bf16")
+    x = cl(torch.randn(4, 64, 40, 25), BF)
+
+    def both():
+        with torch.no_grad():
+            y_f = layer(x, A)
+            monkeypatch.setattr(P.routing.ROUTING, "fused_inference", False)
+            y_u = layer(x, A)
+            monkeypatch.setattr(P.routing.ROUTING, "fused_inference", True)
+        torch.cuda.synchronize()
+        return y_f.float(), y_u.float()
+
+    y0, u0 = both()
+    assert_close(y0, u0, 3e-2, "fused vs unfused")
+    with torch.no_grad():  # optimizer-style in-place step: bumps the version counter
+        layer.tcn[2].weight.mul_(-0.5)
+        layer.gcn.conv.weight.add_(0.05)
+    y1, u1 = both()
+    assert (u1 - u0).abs().max() > 0.1
+    assert_close(y1, u1, 3e-2, "after an in-place update")
+    layer.tcn[2].weight.data.mul_(2.0)  # through .data: re-pack on eval()
+    layer.eval()
+    y2, u2 = both()
+    assert (u2 - u1).abs().max() > 0.1
+    assert_close(y2, u2, 3e-2, "after a .data write + eval()")
+    assert len(calls) == 3
+
+
+def test_fused_ln_large_bias(P):
+    """LayerNorm statistics of z = tcn(...) + b with a large common bias (frame mean >> frame std): the
+    fused kernel shifts its sums by the mean bias, so LN2 keeps fp32 precision (vs the fp32 oracle)."""
+    A = _graph(P)
+    g = torch.Generator().manual_seed(12)
+    layer = _ln_layer(P, 12, tcn_bias=3000.0 + 0.5 * torch.randn(64, generator=g))
+    sd = {k: v.clone() for k, v in layer.state_dict().items()}
+    x = torch.randn(4, 64, 50, 25, generator=g)
+    ref = O.stgcn_layer(x, A, sd, "", 9, 1, True, "LayerNorm")
+    layer = layer.to(DEV).eval()
+    P.set_compute_dtype(layer, "bf16")
+    with torch.no_grad():
+        y = layer(x.to(DEV), A.to(DEV))
+    torch.cuda.synchronize()
+    assert_close(y.float().cpu(), ref, 3e-2, "fused LN layer, bias 3000")

@@ -68,6 +68,23 @@ def test_prep_pkummd_single_action_row(data, tmp_path):
     assert lab.tolist() == [0, 0, 4, 4, 4, 4, 0, 0, 0, 0]
 
 
+def test_prep_pkummd_split_like_reference(data, tmp_path):
+    """prep.py:17 splits the train line on ", " without stripping: an id that ends the line (no trailing
+    ", ") keeps its newline, never matches, and its trial lands in 'val' — reproduced, not 'fixed'."""
+    root = str(tmp_path)
+    for sub in ("features", "labels"):
+        os.makedirs(os.path.join(root, sub))
+    for n in ("0001-L", "0002-L"):
+        np.savetxt(os.path.join(root, "features", n + ".txt"), np.ones((8, 150), np.float32), fmt="%.6f")
+        np.savetxt(os.path.join(root, "labels", n + ".txt"), np.array([[4, 2, 6, 1], [3, 6, 8, 1]]), fmt="%d",
+                   delimiter=",")
+    with open(os.path.join(root, "cross-view.txt"), "w") as fo:
+        fo.write("Training videos:\n0001-L, 0002-L\nValidation videos:\n")
+    data.prep_pkummd(root)
+    assert os.path.exists(os.path.join(root, "train", "features", "0001-L.npy"))
+    assert os.path.exists(os.path.join(root, "val", "features", "0002-L.npy"))
+
+
 def _dataset_dir(root):
     os.makedirs(os.path.join(root, "f"))
     os.makedirs(os.path.join(root, "l"))
