@@ -1,20 +1,27 @@
 """Benchmark: skeleton-frames/sec (fwd+bwd) of the 10-layer ST-GCN (fcn_in + 9 StgcnLayers, as_is BN,
 Kt=9) at N=64 T=300 V=25 (BASELINE.json config 2), bf16 MFMA path, synthetic data.
 
-One step = forward of the whole model on one (64, 3, 300, 25) batch + the reference loss
-(weighted CE + clamped temporal MSE, utils/loss.py:25-41, windows as the time axis like
-WindowSegment.mask_segment) + backward + Adam step.  Inputs are resident in HBM before timing.
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--graph] [--config 2|4]
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
-Kernels are launched eagerly from Python (the GPU stays busy: launch cost < kernel time); --graph
-captures the step into HIP graphs (torch.cuda.CUDAGraph) and replays them instead.
-N > 1: one process per GPU, DistributedDataParallel over RCCL (backend "nccl").  Under
-torch.distributed.run (WORLD_SIZE set) the ranks are the launcher's; `python bench.py --gpus N` alone
-starts `torch.distributed.run --nproc-per-node N` as a child process (before anything touches the GPU)
-and exits with its status.  Each rank processes its own 64 consecutive windows of one synthetic trial
-of N*64 windows (weak scaling); the loss is the trial's (parallel.exchange_shard: the boundary MSE pair
-crosses ranks), so the gradient equals the single-process one up to per-replica BatchNorm statistics,
-as in the reference's DataParallel.
+Config 2 (default): one step = forward of the whole model on one (64, 3, 300, 25) batch of windows + the
+reference loss (weighted CE + clamped temporal MSE, utils/loss.py:25-41, windows as the time axis like
+WindowSegment.mask_segment) + backward + Adam step.  Inputs are resident in HBM before timing.  Kernels are
+launched eagerly from Python; --graph replays the step as HIP graphs (parallel.GraphedStep).
+N > 1: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) the ranks are the launcher's;
+`python bench.py --gpus N` alone starts `torch.distributed.run --nproc-per-node N` as a child process
+(before anything touches the GPU) and exits with its status.  Each rank trains on its own trial's
+64-window subsegment (weak scaling; the subsegment's loss is self-contained, processor.py:377-392, so the
+data path has no collective); gradients are averaged over ranks by DistributedDataParallel (RCCL
+all-reduce in 16 MB buckets overlapped with backward) or, with --graph, by one all-reduce of the flat
+gradient between the two graphs — the reference's accumulation of ``loss / batch_size`` over trials.
+
+Config 4 (--config 4): the long-trial DDP workload of SURVEY 8(d): synthetic trials of U[4000, 8000]
+frames (seed 2), cut into WindowSegment subsegments of 64 windows of T = 300 frames (the reference's
+receptive-field windows at config 2's T), every subsegment a unit with its own loss term (ce + mse) /
+num_subsegments; the units of all trials are dealt round-robin to the ranks
+(parallel.segment_units / units_for_rank).  A step = one unit per rank (64-65 windows staged on the GPU
+from the padded capture, window.hip), fwd + loss + bwd; the optimizer steps (and DDP all-reduces) every
+--accum steps, DDP.no_sync on the others (processor.py:531-564).
 Rank 0 prints ONE JSON line (metric/value/..., roofline, cpu_baseline).
 """
 from __future__ import annotations
@@ -106,7 +113,7 @@ def layer_roofline(pkg, dev, reps=20, norm="BatchNorm"):
         memory_format=torch.channels_last)
     kev = []
 
-    def hook(tag, phase):
+    def hook(tag, phase, work=None):
         if tag == "layer_fused":
             ev = torch.cuda.Event(enable_timing=True)
             ev.record(torch.cuda.current_stream())
@@ -194,17 +201,32 @@ def cpu_baseline(pkg, model_cpu_sd):
     return out
 
 
+def trial_lengths(n_units, W=T_LEN, seg=N_BATCH, seed=2):
+    """Config 4's synthetic trial lengths ~ U[4000, 8000] (seed 2), as many trials as n_units needs."""
+    import random
+    rng = random.Random(seed)
+    out, units = [], 0
+    while units < n_units:
+        L = rng.randint(4000, 8000)
+        out.append(L)
+        units += (L + L % seg) // seg
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=250)  # >= 2 s timed, so utilisation sampling sees it
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--config", type=int, default=2, choices=(2, 4))
+    ap.add_argument("--accum", type=int, default=8, help="config 4: micro-steps per optimizer step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-layer-roofline", action="store_true", help="skip the north_star layer timing (profiling)")
-    ap.add_argument("--graph", action="store_true",
-                    help="capture the step into HIP graphs and replay them (measured slower than eager here)")
+    ap.add_argument("--graph", action="store_true", help="config 2: replay the step as HIP graphs")
     args = ap.parse_args()
+    if args.config == 4 and args.graph:
+        sys.exit("bench.py: --graph needs fixed shapes (config 2); config 4's units have 49-65 windows")
 
     ndev = torch.cuda.device_count()  # does not initialise HIP (safe before spawning the ranks)
     if ndev < args.gpus:
@@ -225,6 +247,7 @@ def main():
     import __graft_entry__ as ge
     pkg = ge.load_package()
     K = pkg.native
+    par = pkg.parallel
 
     torch.manual_seed(1538574472)  # config seed (stgcn_local.json optimizer.seed)
     model = pkg.MODELS["st-gcn"](rank=None, **dict(ARCH, graph=pkg.PKU_MMD))
@@ -233,102 +256,100 @@ def main():
     params = [p for p in model.parameters() if p.requires_grad]
     train_model = model
     if world > 1 and not args.graph:
-        train_model = pkg.parallel.ddp(model, dev, bucket_cap_mb=16)  # RCCL all-reduce overlapped with bwd
+        train_model = par.ddp(model, dev, bucket_cap_mb=16)  # RCCL all-reduce overlapped with bwd
     elif world > 1:  # identical replicas (DistributedDataParallel's broadcast from rank 0)
         for p in params:
             torch.distributed.broadcast(p.data, 0)
     # the reference's optimizer (Adam, lr 5e-4); the fused multi-tensor implementation is the same update
     # rule in one launch per parameter chunk instead of one foreach launch per elementwise op
     opt = torch.optim.Adam(params, lr=5e-4, fused=True, capturable=args.graph)
-
-    gen = torch.Generator(device=dev).manual_seed(rank)
-    x = torch.randn(N_BATCH, 3, T_LEN, V_J, device=dev, generator=gen)
-    # the trial's labels and class distribution are the same on every rank (seeded alike)
     gen_t = torch.Generator(device=dev).manual_seed(12345)
-    labels_trial = torch.randint(0, CLASSES, (1, N_BATCH * world), device=dev, generator=gen_t)
     class_dist = torch.rand(CLASSES, device=dev, generator=gen_t) + 0.5
     crit = pkg.loss.Loss(dev, class_dist)
-    w0, w1 = rank * N_BATCH, (rank + 1) * N_BATCH
-    labels = labels_trial[:, w0:w1]
 
-    # Gradient exchange (N > 1): eager mode uses DistributedDataParallel (RCCL all-reduce of 16 MB
-    # buckets overlapped with backward); graph mode all-reduces one flat fp32 buffer between the
-    # backward graph and the optimizer graph.  BatchNorm statistics stay per replica in both.
-    numels = [p.numel() for p in params]
-    flat = torch.zeros(sum(numels), device=dev) if world > 1 and args.graph else None
-
-    def fwd_bwd():
-        pred = train_model(x).permute(2, 1, 0)  # (1, classes, windows): WindowSegment.mask_segment
-        shard = pkg.parallel.exchange_shard(pred, labels_trial, crit.weight, w0, N_BATCH * world) \
-            if world > 1 else None
-        ce, mse = crit(0, pred, labels, shard=shard)
-        loss = (ce + mse) * world  # DDP averages over ranks; the shares sum to the trial's loss
-        loss.backward()
-        if flat is not None:
-            torch.cat([p.grad.reshape(-1) for p in params], out=flat)
-        return loss
-
-    def opt_step():
-        if flat is not None:
-            for p, g in zip(params, torch.split(flat, numels)):
-                p.grad.copy_(g.view_as(p.grad)).div_(world)
-        opt.step()
-
-    def eager_step():
-        opt.zero_grad(set_to_none=flat is None)  # as the reference's optimizer.zero_grad() (set_to_none)
-        fwd_bwd()
-        if flat is not None:
-            torch.distributed.all_reduce(flat)
-        opt_step()
-
-    # live timing of the roofline kernel (ROOF_TAGS: temporal-conv forward of the C=128/256 layers): HIP events on
-    # the stream the kernel is launched on.  ROCm refuses timing events inside a captured graph, so in
-    # graph mode the events bracket the launches of one eager step run right after the timed region.
+    # live timing of the roofline kernel (ROOF_TAGS: temporal-conv forward of the C=128/256 layers): HIP events
+    # on the stream the kernel is launched on, with each launch's algorithmic flops.  ROCm refuses timing
+    # events inside a captured graph, so in graph mode the events bracket the launches of one eager step run
+    # right after the timed region.
     events = []
     timing = {"on": False}
 
-    def hook(tag, phase):
+    def hook(tag, phase, work=None):
         if tag not in ROOF_TAGS or not timing["on"]:
             return
         ev = torch.cuda.Event(enable_timing=True)
         ev.record(torch.cuda.current_stream())
-        events.append((tag, ev))
+        events.append((tag, ev, work))
 
     K.EVENT_HOOK = hook
-    for _ in range(max(args.warmup, 2)):
-        eager_step()
-    torch.cuda.synchronize()
+    frames_done = [0]
 
-    graphs = None
-    if args.graph:
-        # capture: [zero grads, fwd, loss, bwd (+ flatten)] and [unflatten/average, Adam]; grads keep
-        # their addresses, so replays overwrite them in place
-        opt.zero_grad(set_to_none=False)
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g1):
-                for p in params:
-                    p.grad.zero_()
-                fwd_bwd()
-            with torch.cuda.graph(g2):
-                opt_step()
-        torch.cuda.current_stream().wait_stream(s)
-        graphs = (g1, g2)
+    if args.config == 2:
+        gen = torch.Generator(device=dev).manual_seed(rank)
+        x = torch.randn(N_BATCH, 3, T_LEN, V_J, device=dev, generator=gen)
+        labels = torch.randint(0, CLASSES, (1, N_BATCH), device=dev, generator=gen)
+
+        def fwd_loss():
+            pred = train_model(x).permute(2, 1, 0)  # (1, classes, windows): WindowSegment.mask_segment
+            ce, mse = crit(0, pred, labels)
+            return ce + mse  # DDP / the flat all-reduce average over ranks: loss / batch_size (processor.py:538)
+
+        def eager_step():
+            opt.zero_grad(set_to_none=True)  # as the reference's optimizer.zero_grad() (set_to_none)
+            fwd_loss().backward()
+            opt.step()
+            frames_done[0] += N_BATCH * T_LEN
+
+        if args.graph:  # its first (eager) step all-reduces too: the replicas stay identical
+            gstep = par.GraphedStep(fwd_loss, params, opt, world)
+
+            def step():
+                gstep()
+                frames_done[0] += N_BATCH * T_LEN
+        else:
+            step = eager_step
+        for _ in range(max(args.warmup, 2)):
+            step()
+        torch.cuda.synchronize()
+    else:
+        units = par.units_for_rank(par.segment_units(trial_lengths(world * (args.warmup + args.steps + 2)),
+                                                     T_LEN, N_BATCH), world, rank)
+        gen = torch.Generator(device=dev).manual_seed(100 + rank)
+        caps, labs = {}, {}
+
+        def capture(k, L):
+            if k not in caps:  # padded capture (1, 3, L + W - 1, V), labels (1, L): resident in HBM
+                caps[k] = torch.nn.functional.pad(torch.randn(1, 3, L, V_J, device=dev, generator=gen),
+                                                  (0, 0, T_LEN - 1, 0))
+                labs[k] = torch.randint(0, CLASSES, (1, L), device=dev, generator=gen)
+            return caps[k], labs[k]
+
+        lengths = trial_lengths(world * (args.warmup + args.steps + 2))
+        for u in units[:args.warmup + args.steps + 2]:
+            capture(u.trial, lengths[u.trial])
+        it = iter(units)
+        micro = [0]
 
         def step():
-            g1.replay()
-            if flat is not None:
-                torch.distributed.all_reduce(flat)
-            g2.replay()
-        for _ in range(2):
-            step()
-    else:
-        step = eager_step
+            u = next(it)
+            cap, lab = caps[u.trial], labs[u.trial]
+            last = (micro[0] + 1) % args.accum == 0
+            with par.accumulate(train_model, last=last):
+                pred = train_model(pkg.segment.WindowBatch(cap, u.n0, u.nw, T_LEN)).permute(2, 1, 0)
+                ce, mse = crit(u.i, pred, lab[:, u.y0:u.y1])
+                ((ce + mse) / u.count).backward()  # processor.py:392 (ce, mse / num_subsegments)
+            if last:
+                opt.step()
+                opt.zero_grad(set_to_none=True)
+            micro[0] += 1
+            frames_done[0] += u.nw * T_LEN
 
-    if not args.graph:
-        timing["on"] = True
+        for _ in range(max(args.warmup, 2)):
+            step()
+        torch.cuda.synchronize()
+
+    timing["on"] = not args.graph
+    frames_done[0] = 0
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -339,6 +360,7 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
+    frames = frames_done[0]
     if args.graph:
         timing["on"] = True
         eager_step()
@@ -346,17 +368,17 @@ def main():
     timing["on"] = False
     K.EVENT_HOOK = None
     if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = t.item()
+        t = torch.tensor([elapsed, float(frames)], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t[:1], op=torch.distributed.ReduceOp.MAX)
+        torch.distributed.all_reduce(t[1:], op=torch.distributed.ReduceOp.SUM)
+        elapsed, frames = t[0].item(), t[1].item()
 
-    # eager mode: every launch of the timed region; graph mode: the 6 launches of the step after it
     # (start, end) event pairs of the roofline launches: achieved = their algorithmic flops / their time
-    kt = [(events[i][0], events[i][1].elapsed_time(events[i + 1][1])) for i in range(0, len(events) - 1, 2)]
-    k_ms = sum(t for _, t in kt) / len(kt) if kt else float("nan")
-    achieved = sum(ROOF_TAGS[g] for g, _ in kt) / (sum(t for _, t in kt) * 1e-3) / 1e12 if kt else None
+    kt = [(events[i][0], events[i][1].elapsed_time(events[i + 1][1]), events[i][2])
+          for i in range(0, len(events) - 1, 2)]
+    k_ms = sum(t for _, t, _ in kt) / len(kt) if kt else float("nan")
+    achieved = sum(w for _, _, w in kt) / (sum(t for _, t, _ in kt) * 1e-3) / 1e12 if kt else None
 
-    frames = world * args.steps * N_BATCH * T_LEN
     value = frames / elapsed
     if rank == 0:
         traffic = None
@@ -368,23 +390,30 @@ def main():
             if os.path.exists(pmc):
                 with open(pmc) as f:
                     per[g] = json.load(f).get("hbm_bytes_per_launch")
-        if kt and all(per.get(g) for g, _ in kt):
-            traffic = sum(per[g] for g, _ in kt) / len(kt)
-        lay = world == 1 and not args.no_layer_roofline
+        if kt and all(per.get(g) for g, _, _ in kt) and args.config == 2:
+            traffic = sum(per[g] for g, _, _ in kt) / len(kt)
+        lay = world == 1 and not args.no_layer_roofline and args.config == 2
         lroof = layer_roofline(pkg, dev) if lay else None
         lroof_ln = layer_roofline(pkg, dev, norm="LayerNorm") if lay else None
         cpu = None
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and args.config == 2:
             cpu = cpu_baseline(pkg, cpu_sd)
+        if args.config == 2:
+            workload = "config 2: as_is st-gcn (fcn_in + 9 StgcnLayer, BatchNorm, Kt=9), fwd + loss + bwd + Adam"
+            metric = "skeleton-frames/sec/GPU (fwd+bwd), 10-layer ST-GCN N=64 T=300 V=25"
+        else:
+            workload = ("config 4: as_is st-gcn DDP training on long unequal trials (U[4000,8000] frames, seed 2), "
+                        f"WindowSegment units of 64 windows x T=300 dealt round-robin to ranks, fwd + loss + bwd "
+                        f"per unit, no_sync + Adam every {args.accum} units")
+            metric = "skeleton-frames/sec (fwd+bwd), 10-layer ST-GCN DDP, long trials, windows of T=300 V=25"
         out = {
-            "metric": "skeleton-frames/sec/GPU (fwd+bwd), 10-layer ST-GCN N=64 T=300 V=25",
+            "metric": metric,
             "value": round(value, 1), "unit": "skeleton-frames/s", "per_gpu": round(value / world, 1),
             "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (randn skeletons, random labels/class weights), random-init weights",
-            "config": {"workload": "config 2: as_is st-gcn (fcn_in + 9 StgcnLayer, BatchNorm, Kt=9), fwd + loss + "
-                                   "bwd + Adam", "global_batch": N_BATCH * world, "seq_len": T_LEN, "joints": V_J,
+            "config": {"workload": workload, "global_batch": N_BATCH * world, "seq_len": T_LEN, "joints": V_J,
                        "parallelism": f"dp{world}" if world > 1 else "single",
                        "launch": "eager" if not args.graph else "hip-graph replay (fwd+bwd | allreduce | Adam)"},
             "roofline": {"kernel": "conv_wide_kernel<128,9,8,1,0,64> (persistent warp-specialised Kt=9 stride-1 "
@@ -398,7 +427,6 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    del graphs
     if world > 1:
         torch.distributed.destroy_process_group()
 

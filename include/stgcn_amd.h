@@ -414,6 +414,41 @@ int stgcn_window_grad(const void* dy, int ldd, int dtype, const float* x, int Ci
                       int mode, const float* st, const float* gamma, const float* beta, const float* w, int Cout,
                       void* work, float* dgamma, float* dbeta, float* dw, float* db, void* stream);
 
+/* Batched weight preparation (prep.hip): every packed operand a model's layers read in one training step —
+ * the GEMM packs and MFMA-fragment images of the temporal / residual / head 1x1 convs (stgcn_pack_weight,
+ * _frag, _s2frag) and the graph conv's per-joint effective weights with the bias pushed through A
+ * (stgcn_gconv_weights_bias), for the forward and the data gradient — in ONE launch instead of ~50
+ * (stgcn.py:80-97 as a whole; replaces the per-layer packing of the reference's nn.Conv2d weights, which
+ * PyTorch's own kernels read in place).  A job is one of those single-job entry points with the same
+ * argument meaning:
+ *   kind 0 (pack): src + strides (s0, s1, s2), Kt, Co, Ci -> dst [Kt][cp][kp] (dtype), and the fragment
+ *                  image into dst_frag when non-NULL (cp % 32 == 0, kp % 16 == 0);
+ *   kind 1 (stride-2 fold, bf16): src + strides, Co, Ci, trans -> dst (stgcn_pack_weight_s2frag);
+ *   kind 2 (graph conv): A [P][V][V] (times the edge importance M [P][V][V] when non-NULL: the product the
+ *                  model feeds the layer, formed here exactly as a rounded fp32 product), W = src
+ *                  [P*Cout][Cin] (Co = Cout, Ci = Cin), nbr / deg support lists, trans, dst [V][J][R_pad]
+ *                  [C_pad] (dtype), and for trans 0 with bconv non-NULL bias2d [V][Cout].
+ * stgcn_prep_check validates a host-side job array and fills each job's thread count (threads);
+ * stgcn_prep_run launches the jobs from a DEVICE copy of that array with block_start [njobs + 1] (device,
+ * block_start[j] = first 256-thread block of job j, block_start[njobs] = nblocks). */
+typedef struct {
+  int kind, dtype, trans, Kt, Co, Ci, cp, kp;
+  long s0, s1, s2, threads;
+  const float* src;
+  void* dst;
+  void* dst_frag;
+  const float* A;
+  const float* M;
+  const int* nbr;
+  const int* deg;
+  int P, V, J, R_pad, C_pad, pad_;
+  const float* bconv;
+  float* bias2d;
+} stgcn_prep_job;
+int stgcn_prep_check(stgcn_prep_job* jobs, int njobs);
+int stgcn_prep_run(const stgcn_prep_job* jobs_dev, const long* block_start_dev, int njobs, long nblocks,
+                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

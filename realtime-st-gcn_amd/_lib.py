@@ -75,6 +75,14 @@ class BnBwdDesc(ctypes.Structure):
                                                        "acc2")]
 
 
+class PrepJob(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in ("kind", "dtype", "trans", "Kt", "Co", "Ci", "cp", "kp")] + \
+               [(n, c_long) for n in ("s0", "s1", "s2", "threads")] + \
+               [(n, c_void_p) for n in ("src", "dst", "dst_frag", "A", "M", "nbr", "deg")] + \
+               [(n, c_int) for n in ("P", "V", "J", "R_pad", "C_pad", "pad_")] + \
+               [(n, c_void_p) for n in ("bconv", "bias2d")]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "stgcn_abi_version": (c_int, []),
@@ -162,6 +170,8 @@ _SIGS = {
     "stgcn_seg_loss": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                                c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "stgcn_seg_loss_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p]),
+    "stgcn_prep_check": (c_int, [ctypes.POINTER(PrepJob), c_int]),
+    "stgcn_prep_run": (c_int, [c_void_p, c_void_p, c_int, c_long, c_void_p]),
 }
 
 EXPORTS = tuple(_SIGS)

@@ -22,6 +22,7 @@
 // tap dt) pairs; A (gathered rows) and B (packed weights) tiles are double-buffered in LDS with
 // register prefetch of the next pair, XOR-swizzled so fragment reads are bank-conflict free.
 #include "common.h"
+#include "pack.h"
 #include <stdlib.h>
 
 #include "../../include/stgcn_amd.h"
@@ -310,26 +311,11 @@ int launch_conv(const ConvArgs& a, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
 
-// dst[k][co][ci] = src[k*s0 + co*s1 + ci*s2] (0 in the padding), cast to T: any strided view of the
-// fp32 parameter (permuted / transposed) packs in one pass
 template <typename T>
 __global__ void pack_weight_kernel(const float* __restrict__ src, long s0, long s1, long s2, int Co, int Ci, int cp,
                                    int kp, long total, T* __restrict__ dst, T* __restrict__ dst_frag) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const int ci = (int)(i % kp);
-  const long r = i / kp;
-  const int co = (int)(r % cp);
-  const long k = r / cp;
-  const float v = (co < Co && ci < Ci) ? src[k * s0 + co * s1 + ci * s2] : 0.f;
-  dst[i] = Tr<T>::from_f(v);
-  if (dst_frag) {
-    // MFMA-fragment image (conv_wide.hip): 1-KiB blocks [k][co/32][ci/16], lane l = (ci%16)/8*32 + co%32
-    // holding 8 consecutive ci: a wave's B fragment is one contiguous 1-KiB load
-    const long blk = ((long)k * (cp / 32) + co / 32) * (kp / 16) + ci / 16;
-    const int l = ((ci & 15) >> 3) * 32 + (co & 31);
-    dst_frag[blk * 512 + l * 8 + (ci & 7)] = Tr<T>::from_f(v);
-  }
+  if (i < total) pack_weight_elem<T>(src, s0, s1, s2, Co, Ci, cp, kp, i, dst, dst_frag);
 }
 
 }  // namespace

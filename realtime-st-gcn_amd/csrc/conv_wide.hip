@@ -27,6 +27,7 @@
 //   * epilogue per tile: + bias, bf16 store, BatchNorm Welford partials per (tile, channel) (the
 //     float4 (count, mean, M2) layout bn_finalize merges; row-tile index = n * tiles_n + tile).
 #include "common.h"
+#include "pack.h"
 #include "../../include/stgcn_amd.h"
 #include <stdlib.h>
 #include <utility>
@@ -562,33 +563,10 @@ __global__ __launch_bounds__((4 + NHW) * 64, 1) void conv_wide_kernel(const stgc
   }
 }
 
-// Parity-folded fragment image of a stride-2 Kt = 9 weight [9][Co][Ci] (fp32, any strides): the 5-tap
-// conv the wide kernel runs instead (see conv_wide_launch) —
-//   forward   W'[t][co][par*Ci + ci] = W[2t + par][co][ci]
-//   data grad W'[t][par*Co + co][ci] = W[8 - 2t + par][co][ci]      (taps outside 0..8 are zero)
-// laid out like stgcn_pack_weight_frag (1-KiB blocks [t][co'/32][ci'/16]).
 __global__ void pack_s2frag_kernel(const float* __restrict__ src, long s0, long s1, long s2, int Co, int Ci, int trans,
                                    int co_f, int ci_f, bf16* __restrict__ dst) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long total = 5L * co_f * ci_f;
-  if (idx >= total) return;
-  const int cip = (int)(idx % ci_f);
-  const int cop = (int)((idx / ci_f) % co_f);
-  const int t = (int)(idx / ((long)co_f * ci_f));
-  int co = cop, ci = cip, dt;
-  if (trans) {
-    const int par = cop >= Co;
-    co = cop - par * Co;
-    dt = 8 - 2 * t + par;
-  } else {
-    const int par = cip >= Ci;
-    ci = cip - par * Ci;
-    dt = 2 * t + par;
-  }
-  const float v = (dt >= 0 && dt <= 8) ? src[dt * s0 + co * s1 + ci * s2] : 0.f;
-  const long blk = ((long)t * (co_f / 32) + cop / 32) * (ci_f / 16) + cip / 16;
-  const int l = ((cip & 15) >> 3) * 32 + (cop & 31);
-  dst[blk * 512 + l * 8 + (cip & 7)] = (bf16)v;
+  if (idx < 5L * co_f * ci_f) pack_s2frag_elem(src, s0, s1, s2, Co, Ci, trans, co_f, ci_f, idx, dst);
 }
 
 }  // namespace

@@ -23,6 +23,7 @@
 // tile); A rows staged through registers into padded LDS rows, B (packed Weff) by LDS-DMA with the
 // XOR swizzle on the source, fragment double-buffering, BN partial statistics in the epilogue.
 #include "common.h"
+#include "pack.h"
 #include <stdlib.h>
 #include <utility>
 #include "../../include/stgcn_amd.h"
@@ -465,114 +466,14 @@ int launch_gconv(const stgcn_gconv_desc& a, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
 
-// ------------------------------------------------------------------ effective weights
-// out[a][j][r][c] (dtype, padded to [R_pad][C_pad]):
-//   trans 0: sum_p A[p][nbr[a][j]][a] * W[p*Cout + r][c]          (r = co < Cout, c = ci < Cin)
-//   trans 1: sum_p A[p][a][nbr[a][j]] * W[p*Cout + c][r]          (r = ci < Cin,  c = co < Cout)
-// One thread per (joint a, 8 consecutive c, r): it loads its P x 8 weights once and writes all deg[a]
-// neighbour slots of joint a (a thread per slot re-read the same weights J times: ~100 MB of L2 reads per
-// C = 256 launch).  Slots j >= deg[a] are never read by gconv and are skipped; padding rows / columns are
-// written as zeros (they meet zero-filled operands).
-constexpr int GW_PMAX = 4;
-constexpr int GW_JMAX = 8;  // neighbour slots per joint whose loads are issued together
+// ------------------------------------------------------------------ effective weights (pack.h)
 template <typename T>
 __global__ void gconv_weights_kernel(const float* __restrict__ A, const float* __restrict__ W, const int* nbr,
                                      const int* deg, int P, int V, int J, int Cout, int Cin, int trans, T* out,
                                      int R_pad, int C_pad, const float* __restrict__ bconv, float* __restrict__ bias2d) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int C8 = C_pad / 8;
-  const long total = (long)V * R_pad * C8;
-  if (idx >= total) return;
-  // forward: c (ci) fastest across lanes, so W rows are read as float4 runs; trans: r (ci) fastest, so
-  // the 8 scalar reads of W[co][r] per thread are coalesced across lanes
-  int c0, r, a;
-  if (!trans) {
-    c0 = (int)(idx % C8) * 8;
-    const long t1 = idx / C8;
-    r = (int)(t1 % R_pad);
-    a = (int)(t1 / R_pad);
-  } else {
-    r = (int)(idx % R_pad);
-    const long t1 = idx / R_pad;
-    c0 = (int)(t1 % C8) * 8;
-    a = (int)(t1 / C8);
-  }
-  const int R = trans ? Cin : Cout, C = trans ? Cout : Cin;
-  if (bias2d && !trans && c0 == 0 && r < Cout) {
-    // the graph conv's bias pushed through A in the same launch (stgcn_gcn_bias, same summation order):
-    // bias2d[a][co] = sum_p b[p*Cout + co] * colsum_p[a],  colsum_p[a] = sum_v A[p][v][a]
-    float sb = 0.f;
-    for (int p = 0; p < P; ++p) {
-      float cs = 0.f;
-      for (int v = 0; v < V; ++v) cs += A[((long)p * V + v) * V + a];
-      sb += bconv[p * Cout + r] * cs;
-    }
-    bias2d[(long)a * Cout + r] = sb;
-  }
-  float wv[GW_PMAX][8];
-#pragma unroll
-  for (int p = 0; p < GW_PMAX; ++p)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) wv[p][e] = 0.f;
-  if (r < R) {
-#pragma unroll
-    for (int p = 0; p < GW_PMAX; ++p) {
-      if (p >= P) break;
-      if (!trans) {
-        const float* w = W + ((long)p * Cout + r) * Cin + c0;
-        if (c0 + 8 <= C && (Cin & 3) == 0) {
-          const float4 w0 = *reinterpret_cast<const float4*>(w), w1 = *reinterpret_cast<const float4*>(w + 4);
-          wv[p][0] = w0.x; wv[p][1] = w0.y; wv[p][2] = w0.z; wv[p][3] = w0.w;
-          wv[p][4] = w1.x; wv[p][5] = w1.y; wv[p][6] = w1.z; wv[p][7] = w1.w;
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            if (c0 + e < C) wv[p][e] = w[e];
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if (c0 + e < C) wv[p][e] = W[((long)p * Cout + c0 + e) * Cin + r];
-      }
-    }
-  }
-  // the neighbour list and coefficients of up to GW_JMAX slots are requested together (independent loads),
-  // not as a chain of dependent loads per slot: the small launches are latency-bound
-  const int dtot = deg[a];
-  for (int j0 = 0; j0 < dtot; j0 += GW_JMAX) {
-    const int da = min(dtot - j0, GW_JMAX);
-    int nb[GW_JMAX];
-#pragma unroll
-    for (int jj = 0; jj < GW_JMAX; ++jj) nb[jj] = jj < da ? nbr[a * J + j0 + jj] : a;
-    float cf[GW_JMAX][GW_PMAX];
-#pragma unroll
-    for (int jj = 0; jj < GW_JMAX; ++jj)
-#pragma unroll
-      for (int p = 0; p < GW_PMAX; ++p)
-        cf[jj][p] = (jj < da && p < P) ? (trans ? A[((long)p * V + a) * V + nb[jj]] : A[((long)p * V + nb[jj]) * V + a])
-                                       : 0.f;
-#pragma unroll
-    for (int jj = 0; jj < GW_JMAX; ++jj) {
-      if (jj >= da) break;
-      const int j = j0 + jj;
-      float s[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) s[e] = 0.f;
-#pragma unroll
-      for (int p = 0; p < GW_PMAX; ++p) {
-        if (p >= P) break;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) s[e] += cf[jj][p] * wv[p][e];
-      }
-      T* o = out + (((long)a * J + j) * R_pad + r) * (long)C_pad + c0;
-      if constexpr (sizeof(T) == 2) {
-        *reinterpret_cast<uint4*>(o) = pack16(s, (T*)nullptr);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = s[e];
-      }
-    }
-  }
+  if (idx < (long)V * R_pad * (C_pad / 8))
+    gconv_weights_elem<T>(A, nullptr, W, nbr, deg, P, V, J, Cout, Cin, trans, out, R_pad, C_pad, bconv, bias2d, idx);
 }
 
 // ------------------------------------------------------------------ weight gradient (bf16 + fp32)

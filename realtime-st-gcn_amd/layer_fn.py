@@ -43,9 +43,10 @@ def _side_stream(dev):
     conv) is the critical path from dy to dx; the weight gradients (temporal-conv wgrad, residual wgrad,
     graph-conv wgrad + dW/dA finish + bias through A) branch off it.  They are issued on this stream after
     a fork event and joined before the backward returns, so the latency-bound reduction kernels of the
-    branch fill the gaps and tails of the data-gradient kernels.  Off under stream capture (HIP graphs) and
-    with routing.ROUTING.side_stream off."""
-    if not ROUTING.side_stream or torch.cuda.is_current_stream_capturing():
+    branch fill the gaps and tails of the data-gradient kernels.  Under stream capture (parallel.GraphedStep)
+    the fork/join events pull the side stream into the capture: the branch becomes a parallel branch of the
+    HIP graph.  Off with routing.ROUTING.side_stream off."""
+    if not ROUTING.side_stream:
         return None
     s = _SIDE.get(dev.index)
     if s is None:
@@ -130,6 +131,43 @@ def _packs(cache, wg, wt, P, Cin, Cout, dtype):
     return val
 
 
+class LayerPacks:
+    """Packed operands of one StgcnLayer's training step, filled by the model's PrepPlan launch
+    (native.PrepPlan): graph-conv effective weights + bias through A (forward), their data-gradient form,
+    temporal conv (forward / data gradient) and residual 1x1 conv (forward / data gradient) packs, each as
+    the (tensor, Cout_pad, Cin_pad) triple pack_weight returns (gw: (weights, bias2d))."""
+    __slots__ = ("gw", "gwT", "wt", "wtT", "wr", "wrT")
+
+    def __init__(self):
+        self.gw = self.gwT = self.wt = self.wtT = self.wr = self.wrT = None
+
+
+def plan_layer_packs(plan, layer, A, M, dtype):
+    """Record in ``plan`` every pack StgcnLayerFunction builds per call for ``layer`` fed ``A * M`` (the
+    model's graph and the layer's edge importance, M None without importance); None when the layer takes a
+    route that packs differently (per-sample or dense A, the opt-in gcn_tile kernel)."""
+    sup = layer._gsup
+    P, V = A.shape[0], A.shape[-1]
+    conv = layer.tcn[2]
+    Cout, Cin = conv.out_channels, layer.gcn.conv.in_channels
+    kt, stride = layer.kernel_size[0], layer.stride
+    if sup is None or A.dim() != 3 or sup.dense(P) or K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype):
+        return None
+    pk = LayerPacks()
+    wg2 = layer.gcn.conv.weight.detach().reshape(P * Cout, Cin)
+    pk.gw = K.gconv_weights(A, wg2, sup, Cout, Cin, False, dtype, bias=layer.gcn.conv.bias.detach(), plan=plan, M=M)
+    if not K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype, trans=True):
+        pk.gwT = K.gconv_weights(A, wg2, sup, Cout, Cin, True, dtype, plan=plan, M=M)
+    wt = conv.weight.detach().squeeze(-1)
+    pk.wt = K.pack_weight(wt.permute(2, 0, 1), dtype, stride=stride, plan=plan)
+    pk.wtT = K.pack_weight(wt.permute(2, 1, 0), dtype, stride=stride, trans=True, plan=plan)
+    if layer.is_residual_conv:
+        wr = layer.residual[0].weight.detach().view(Cout, Cin)
+        pk.wr = K.pack_weight(wr.unsqueeze(0), dtype, plan=plan)
+        pk.wrT = K.pack_weight(wr.t().unsqueeze(0), dtype, plan=plan)
+    return pk
+
+
 def _ln_vc(p, V, C):
     """LayerNorm([C,1,V]) parameter -> [V][C] fp32 (the fused kernel's per-joint rows)."""
     return p.detach().float().reshape(C, V).t().contiguous()
@@ -180,6 +218,7 @@ class StgcnLayerFunction(torch.autograd.Function):
         M1, M2 = N * T * V, N * T_out * V
         A32 = A.detach().float().contiguous()
         res_conv = residual and not (Cin == Cout and stride == 1)
+        packs = cfg[9] if len(cfg) > 9 else None  # LayerPacks of the model's PrepPlan launch, or None
 
         # ---- graph convolution: g = sum_p A_p-mix(x) W_p + bias2d
         sup = cfg[5] if len(cfg) > 5 else None
@@ -210,8 +249,8 @@ class StgcnLayerFunction(torch.autograd.Function):
         side = _side_stream(dev) if res_conv else None
         if res_conv:
             with _fork(side):
-                wr3 = wr.detach().float().view(1, Cout, Cin)
-                wrp, cpr, kpr = K.pack_weight(wr3, dtype)
+                wrp, cpr, kpr = packs.wr if packs is not None else \
+                    K.pack_weight(wr.detach().float().view(1, Cout, Cin), dtype)
                 r = K.conv_rows(x, wrp, Cin, Cout, cpr, kpr, T, T_out, Kt=1, stride=stride, pad=0,
                                 bias=br.detach().float().contiguous(), stats=str_ if norm == BN else None)
                 if norm == BN:
@@ -230,8 +269,12 @@ class StgcnLayerFunction(torch.autograd.Function):
             g = K.gcn_tile(x, A32, wimg, kwg, Cin, Cout, cpg, sup, bias=bias2d, stats=st1 if norm == BN else None)
             XA = None
         elif gather:  # joint-gathered GEMM over per-joint effective weights (gconv.hip), no XA in HBM
-            wg2 = wg.detach().float().reshape(P * Cout, Cin).contiguous()
-            wgp, bias2d = K.gconv_weights(A32, wg2, sup, Cout, Cin, False, dtype, bias=bg.detach().float().contiguous())
+            if packs is not None:
+                wgp, bias2d = packs.gw
+            else:
+                wg2 = wg.detach().float().reshape(P * Cout, Cin).contiguous()
+                wgp, bias2d = K.gconv_weights(A32, wg2, sup, Cout, Cin, False, dtype,
+                                              bias=bg.detach().float().contiguous())
             cpg, kpg = wgp.shape[2], wgp.shape[3]
             if norm == BN:
                 assert cpg == cpo
@@ -253,8 +296,8 @@ class StgcnLayerFunction(torch.autograd.Function):
             pro1 = dict(pro=2, pro_a=g1, pro_b=b1, pro_stats=ls1)
 
         # ---- temporal conv on relu(norm1(g)) (norm applied in the prologue)
-        wt3 = wt.detach().float().squeeze(-1).permute(2, 0, 1)  # [Kt][Cout][Cin]
-        wtp, cpt, kpt = K.pack_weight(wt3, dtype, stride=stride)
+        wtp, cpt, kpt = packs.wt if packs is not None else \
+            K.pack_weight(wt.detach().float().squeeze(-1).permute(2, 0, 1), dtype, stride=stride)  # [Kt][Cout][Cin]
 
         u = K.conv_rows(g, wtp, Cout, Cout, cpt, kpt, T, T_out, Kt=kt, stride=stride, pad=pad,
                         bias=bt.detach().float().contiguous(), stats=st2 if norm == BN else None,
@@ -315,6 +358,7 @@ class StgcnLayerFunction(torch.autograd.Function):
         dev = x.device
         dy = K.to_rows(dy, dtype)
         M1, M2 = N * T * V, N * T_out * V
+        packs = ctx.cfg[9] if len(ctx.cfg) > 9 else None
         grads = {}
         # every fp32 accumulation target of this backward from one zero fill
         zshapes = [(kt, Cout, Cout), (1, Cout, Cin), (P * Cout, Cin), (P, V, V),
@@ -369,8 +413,8 @@ class StgcnLayerFunction(torch.autograd.Function):
                     grads["nrw"], grads["nrb"] = dgbr[0].view(nrw.shape), dgbr[1].view(nrb.shape)
                 grads["br"] = K.bn_bwd_reduce(dr, M2, Cout)[:, 0].clone()
             # residual conv (1x1, stride s, bias): data grad (transposed), weight grad
-            wrT = wr.detach().float().view(Cout, Cin).t().reshape(1, Cin, Cout)
-            wrTp, cq, kq = K.pack_weight(wrT, dtype)
+            wrTp, cq, kq = packs.wrT if packs is not None else \
+                K.pack_weight(wr.detach().float().view(Cout, Cin).t().unsqueeze(0), dtype)
             with _fork(side):
                 grads["wr"] = K.conv_wgrad(x, dr, Cin, Cout, T, T_out, Kt=1, stride=stride, pad=0,
                                            dw=z_dwr).view(Cout, Cin, 1, 1)
@@ -381,8 +425,9 @@ class StgcnLayerFunction(torch.autograd.Function):
             dx_written = True
 
         # ---- temporal conv: dh = conv^T(du), dWt, dbt
-        wtT = wt.detach().float().squeeze(-1).permute(2, 1, 0)  # [Kt][Cin=Cout][Cout]: W[co][ci][dt] -> [dt][ci][co]
-        wtTp, cq, kq = K.pack_weight(wtT, dtype, stride=stride, trans=True)
+        # [Kt][Cin=Cout][Cout]: W[co][ci][dt] -> [dt][ci][co]
+        wtTp, cq, kq = packs.wtT if packs is not None else \
+            K.pack_weight(wt.detach().float().squeeze(-1).permute(2, 1, 0), dtype, stride=stride, trans=True)
         if norm == BN:
             pro1 = dict(pro=1, pro_a=sc1, pro_b=sh1)
         else:
@@ -434,7 +479,8 @@ class StgcnLayerFunction(torch.autograd.Function):
                 wimgT, cq, kwT = K.pack_gcn_weight(wdf, dtype)
                 K.gcn_tile(dg, A32, wimgT, kwT, Cout, Cin, cq, sup, trans_a=True, out=dx, accumulate=dx_written)
             else:
-                wgT = K.gconv_weights(A32, wg2, sup, Cout, Cin, True, dtype)
+                wgT = packs.gwT if packs is not None and packs.gwT is not None else \
+                    K.gconv_weights(A32, wg2, sup, Cout, Cin, True, dtype)
                 K.gconv(dg, wgT, sup, Cout, Cin, trans=True, out=dx, accumulate=dx_written)
         else:
             # DW[(n,t,w)][p*Cin+ci] = sum_c dg[(n,t,w)][c] Wg[p*Cout+c][ci]
@@ -533,19 +579,31 @@ class GcnFunction(torch.autograd.Function):
         return dx, dA.to(adt), dwg.to(wg.dtype), dbg.to(bg.dtype), None
 
 
+def plan_conv1x1_packs(plan, w, dtype):
+    """Forward and data-gradient packs of a 1x1 conv weight (Cout, Cin', 1, 1) for Conv1x1Function; Cin' may
+    be below the activation's channel count (fcn_in: 3 input features in 8-channel rows), the packs pad."""
+    Cout, Ci = w.shape[0], w.shape[1]
+    w2 = w.detach().view(Cout, Ci)
+    return K.pack_weight(w2.unsqueeze(0), dtype, plan=plan), K.pack_weight(w2.t().unsqueeze(0), dtype, plan=plan)
+
+
 @K.on_tensor_device
 class Conv1x1Function(torch.autograd.Function):
-    """Pointwise conv on channels-last rows (fcn_in / fcn_out, stgcn.py:49,74): y = W x + b."""
+    """Pointwise conv on channels-last rows (fcn_in / fcn_out, stgcn.py:49,74): y = W x + b.  w may have fewer
+    input channels than x (fcn_in's 3 features in 8-channel rows: the missing columns act as zeros); packs =
+    plan_conv1x1_packs(...) filled by the model's PrepPlan launch, or None (packed here)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, dtype):
+    def forward(ctx, x, w, b, dtype, packs=None):
         x = K.to_rows(x, dtype)
         N, Cin, T, V = x.shape
-        Cout = w.shape[0]
-        wp, cp, kp = K.pack_weight(w.detach().float().view(1, Cout, Cin), dtype)
+        Cout, Ci = w.shape[0], w.shape[1]
+        wp, cp, kp = packs[0] if packs is not None else \
+            K.pack_weight(w.detach().float().view(Cout, Ci).unsqueeze(0), dtype)
         y = K.conv_rows(x, wp, Cin, Cout, cp, kp, T, T, bias=b.detach().float().contiguous())
         ctx.save_for_backward(x, w)
         ctx.dtype = dtype
+        ctx.packT = packs[1] if packs is not None else None
         return y
 
     @staticmethod
@@ -553,13 +611,16 @@ class Conv1x1Function(torch.autograd.Function):
         x, w = ctx.saved_tensors
         dtype = ctx.dtype
         N, Cin, T, V = x.shape
-        Cout = w.shape[0]
+        Cout, Ci = w.shape[0], w.shape[1]
         dy = K.to_rows(dy, dtype)
-        wT, cq, kq = K.pack_weight(w.detach().float().view(Cout, Cin).t().reshape(1, Cin, Cout), dtype)
+        wT, cq, kq = ctx.packT if ctx.packT is not None else \
+            K.pack_weight(w.detach().float().view(Cout, Ci).t().unsqueeze(0), dtype)
         dx = K.conv_rows(dy, wT, Cout, Cin, cq, kq, T, T, trans=True)
         dw = K.conv_wgrad(x, dy, Cin, Cout, T, T).view(Cout, Cin, 1, 1)
+        if Ci < Cin:
+            dw = dw[:, :Ci]
         db = K.bn_bwd_reduce(dy, N * T * V, Cout)[:, 0]
-        return dx, dw.to(w.dtype), db.to(w.dtype), None
+        return dx, dw.to(w.dtype), db.to(w.dtype), None, None
 
 
 @K.on_tensor_device

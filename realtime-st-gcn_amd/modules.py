@@ -146,7 +146,9 @@ class StgcnLayer(nn.Module):
         self.bind_graph(A, masked=False)
         return self._gsup
 
-    def forward(self, x, A):
+    def forward(self, x, A, packs=None):
+        """``packs``: this layer's layer_fn.LayerPacks from the owning model's one-launch weight preparation
+        (stgcn.Model._prepared), or None (the layer packs per call)."""
         if self.dropout and self.training:
             raise NotImplementedError("stgcn_amd: dropout > 0 in training is not implemented (every reference "
                                       "config uses dropout 0)")
@@ -164,7 +166,7 @@ class StgcnLayer(nn.Module):
         infer = not torch.is_grad_enabled() or not (
             x.requires_grad or A.requires_grad or any(p.requires_grad for p in self.parameters()))
         cfg = (self.kernel_size[0], self.stride, self.is_residual, self.normalization, self.compute_dtype,
-               self.graph_support(A), not self._graph_bound, infer, self._fused_cache)
+               self.graph_support(A), not self._graph_bound, infer, self._fused_cache, None if infer else packs)
         return F_.StgcnLayerFunction.apply(x, A, self.gcn.conv.weight, self.gcn.conv.bias, n1.weight, n1.bias,
                                            conv.weight, conv.bias, n2.weight, n2.bias, wr, br, nrw, nrb, cfg)
 

@@ -60,8 +60,9 @@ def on_tensor_device(cls):
     return cls
 
 
-# Optional instrumentation: callable(tag, phase) invoked right before ("start") and after ("end")
-# a tagged launch, on the launching stream (bench.py records HIP events with it).  None = off.
+# Optional instrumentation: callable(tag, phase, work) invoked right before ("start", with the launch's
+# algorithmic flops where the wrapper knows them, else None) and after ("end", None) a tagged launch, on the
+# launching stream (bench.py records HIP events with it).  None = off.
 EVENT_HOOK = None
 
 
@@ -111,14 +112,16 @@ def row_blocks(M: int, cout: int) -> int:
     return L.lib().stgcn_conv_rows_row_blocks(M, cout)
 
 
-def pack_weight(w3: torch.Tensor, dtype, stride: int = 1, trans: bool = False) -> tuple:
+def pack_weight(w3: torch.Tensor, dtype, stride: int = 1, trans: bool = False, plan=None) -> tuple:
     """[Kt][Cout][Cin] float weight -> padded contiguous [Kt][Cout_pad][Cin_pad] of ``dtype``.
 
     bf16 Kt=9 weights with >= 128 (padded) channels on both sides also get the MFMA-fragment image the
     wide-channel conv kernel reads (stgcn_pack_weight_frag), in the same allocation; ``out.frag_ptr``
     is its address and ``out.frag_stride`` the conv stride it is for (conv_rows passes it as ``w_frag``
     to calls of that stride).  For ``stride=2`` the image is the parity-folded 5-tap form
-    (stgcn_pack_weight_s2frag, ``trans`` selecting the data-gradient fold)."""
+    (stgcn_pack_weight_s2frag, ``trans`` selecting the data-gradient fold).
+    ``plan`` (a PrepPlan): allocate the same buffers but only record the jobs; PrepPlan.run() fills them
+    (with every other pack of the model) in one launch."""
     Kt, Co, Ci = w3.shape
     cp = -(-Co // col_tile(Co)) * col_tile(Co)
     kp = -(-Ci // 32) * 32
@@ -126,37 +129,95 @@ def pack_weight(w3: torch.Tensor, dtype, stride: int = 1, trans: bool = False) -
         w3 = w3.float()
     s0, s1, s2 = w3.stride()
     n = Kt * cp * kp
+    code = L.dtype_code(dtype)
     if dtype == torch.bfloat16 and Kt == 9 and stride == 2 and Co % 64 == 0 and Ci % 64 == 0:
         nf = 5 * 2 * Co * Ci
         buf = torch.empty(n + nf, dtype=dtype, device=w3.device)
         out = buf[:n].view(Kt, cp, kp)
-        L.check(L.lib().stgcn_pack_weight(w3.data_ptr(), s0, s1, s2, Kt, Co, Ci, out.data_ptr(), cp, kp,
-                                          L.dtype_code(dtype), L.stream()), "pack_weight")
-        L.check(L.lib().stgcn_pack_weight_s2frag(w3.data_ptr(), s0, s1, s2, Co, Ci, buf[n:].data_ptr(), int(trans),
-                                                 L.dtype_code(dtype), L.stream()), "pack_weight_s2frag")
+        if plan is not None:
+            plan.add(kind=0, dtype=code, src=w3, Kt=Kt, Co=Co, Ci=Ci, cp=cp, kp=kp, dst=out)
+            plan.add(kind=1, dtype=code, src=w3, Co=Co, Ci=Ci, trans=int(trans), dst=buf[n:])
+        else:
+            L.check(L.lib().stgcn_pack_weight(w3.data_ptr(), s0, s1, s2, Kt, Co, Ci, out.data_ptr(), cp, kp,
+                                              code, L.stream()), "pack_weight")
+            L.check(L.lib().stgcn_pack_weight_s2frag(w3.data_ptr(), s0, s1, s2, Co, Ci, buf[n:].data_ptr(),
+                                                     int(trans), code, L.stream()), "pack_weight_s2frag")
         out.frag_ptr, out.frag_stride = buf[n:].data_ptr(), 2
         return out, cp, kp
+    frag = None
     if dtype == torch.bfloat16 and Kt == 9 and stride == 1 and cp % 64 == 0 and kp % 64 == 0:
+        frag = 1
+    elif dtype == torch.bfloat16 and Kt == 1 and kp == Ci and Ci in (64, 128, 192, 256) and Co % 64 == 0:
+        frag = 0  # 1x1 weights: fragment image for the row-GEMM kernel (conv1x1.hip), valid at any stride
+    if frag is not None:
         buf = torch.empty(2 * n, dtype=dtype, device=w3.device)
         out = buf[:n].view(Kt, cp, kp)
-        L.check(L.lib().stgcn_pack_weight_frag(w3.data_ptr(), s0, s1, s2, Kt, Co, Ci, out.data_ptr(),
-                                               buf[n:].data_ptr(), cp, kp, L.dtype_code(dtype), L.stream()),
-                "pack_weight_frag")
-        out.frag_ptr, out.frag_stride = buf[n:].data_ptr(), 1
-        return out, cp, kp
-    if dtype == torch.bfloat16 and Kt == 1 and kp == Ci and Ci in (64, 128, 192, 256) and Co % 64 == 0:
-        # 1x1 weights: fragment image for the row-GEMM kernel (conv1x1.hip), valid at any stride
-        buf = torch.empty(2 * n, dtype=dtype, device=w3.device)
-        out = buf[:n].view(Kt, cp, kp)
-        L.check(L.lib().stgcn_pack_weight_frag(w3.data_ptr(), s0, s1, s2, Kt, Co, Ci, out.data_ptr(),
-                                               buf[n:].data_ptr(), cp, kp, L.dtype_code(dtype), L.stream()),
-                "pack_weight_frag")
-        out.frag_ptr, out.frag_stride = buf[n:].data_ptr(), 0
+        if plan is not None:
+            plan.add(kind=0, dtype=code, src=w3, Kt=Kt, Co=Co, Ci=Ci, cp=cp, kp=kp, dst=out, dst_frag=buf[n:])
+        else:
+            L.check(L.lib().stgcn_pack_weight_frag(w3.data_ptr(), s0, s1, s2, Kt, Co, Ci, out.data_ptr(),
+                                                   buf[n:].data_ptr(), cp, kp, code, L.stream()), "pack_weight_frag")
+        out.frag_ptr, out.frag_stride = buf[n:].data_ptr(), frag
         return out, cp, kp
     out = torch.empty((Kt, cp, kp), dtype=dtype, device=w3.device)
-    L.check(L.lib().stgcn_pack_weight(w3.data_ptr(), s0, s1, s2, Kt, Co, Ci, out.data_ptr(), cp, kp,
-                                      L.dtype_code(dtype), L.stream()), "pack_weight")
+    if plan is not None:
+        plan.add(kind=0, dtype=code, src=w3, Kt=Kt, Co=Co, Ci=Ci, cp=cp, kp=kp, dst=out)
+    else:
+        L.check(L.lib().stgcn_pack_weight(w3.data_ptr(), s0, s1, s2, Kt, Co, Ci, out.data_ptr(), cp, kp,
+                                          code, L.stream()), "pack_weight")
     return out, cp, kp
+
+
+class PrepPlan:
+    """Every packed operand of a model's training step, prepared by ONE launch (stgcn_prep_run): the jobs
+    pack_weight / gconv_weights would launch one by one are recorded once (their output buffers are
+    allocated here and stay put), the job table is validated (stgcn_prep_check) and uploaded once, and
+    run() re-fills every buffer from the current parameter values.  ``key`` identifies the parameter
+    storages the jobs read; the owner rebuilds the plan when it changes (e.g. after .to())."""
+
+    def __init__(self, device, key=None):
+        self.device = device
+        self.key = key
+        self._jobs = []
+        self._keep = []  # sources and outputs: the table holds raw pointers into them
+        self._table = self._starts = None
+        self.nblocks = 0
+
+    def add(self, kind, dtype, src, dst, Kt=1, Co=0, Ci=0, cp=0, kp=0, dst_frag=None, trans=0, A=None, M=None,
+            nbr=None, deg=None, P=0, V=0, J=0, R_pad=0, C_pad=0, bconv=None, bias2d=None):
+        if self._table is not None:
+            raise RuntimeError("stgcn_amd: PrepPlan is finalized")
+        j = L.PrepJob()
+        j.kind, j.dtype, j.trans, j.Kt, j.Co, j.Ci, j.cp, j.kp = kind, dtype, int(trans), Kt, Co, Ci, cp, kp
+        j.s0, j.s1, j.s2 = src.stride() if src.dim() == 3 else (0,) + tuple(src.stride())
+        j.src, j.dst, j.dst_frag = src.data_ptr(), dst.data_ptr(), L.ptr(dst_frag)
+        j.A, j.M, j.nbr, j.deg, j.bconv, j.bias2d = L.ptr(A), L.ptr(M), L.ptr(nbr), L.ptr(deg), L.ptr(bconv), \
+            L.ptr(bias2d)
+        j.P, j.V, j.J, j.R_pad, j.C_pad = P, V, J, R_pad, C_pad
+        self._jobs.append(j)
+        self._keep += [t for t in (src, dst, dst_frag, A, M, nbr, deg, bconv, bias2d) if t is not None]
+
+    def finalize(self):
+        n = len(self._jobs)
+        arr = (L.PrepJob * n)(*self._jobs)
+        L.check(L.lib().stgcn_prep_check(arr, n), "prep_check")
+        starts, b = [], 0
+        for j in arr:
+            starts.append(b)
+            b += -(-j.threads // 256)
+        starts.append(b)
+        self.nblocks = b
+        raw = bytes(memoryview(arr).cast("B"))
+        self._table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
+        self._starts = torch.tensor(starts, dtype=torch.int64).to(self.device)
+        self.njobs = n
+        return self
+
+    def run(self):
+        if self._table is None:
+            self.finalize()
+        L.check(L.lib().stgcn_prep_run(self._table.data_ptr(), self._starts.data_ptr(), self.njobs, self.nblocks,
+                                       L.stream()), "prep_run")
 
 
 def conv_rows(x, w3p, Cin, Cout, cp, kp, T_in, T_out, Kt=1, stride=1, pad=0, trans=False, bias=None, bias_mode=None,
@@ -181,11 +242,11 @@ def conv_rows(x, w3p, Cin, Cout, cp, kp, T_in, T_out, Kt=1, stride=1, pad=0, tra
     d.accumulate = int(accumulate)
     d.in_ld, d.out_ld = rows_ld(x), rows_ld(out)
     hook = EVENT_HOOK if tag is not None else None
-    if hook:
-        hook(tag, "start")
+    if hook:  # (tag, phase, algorithmic flops of the launch)
+        hook(tag, "start", 2.0 * N * T_out * V * Cout * Cin * Kt)
     L.check(L.lib().stgcn_conv_rows(d, L.dtype_code(x.dtype), L.stream()), "conv_rows")
     if hook:
-        hook(tag, "end")
+        hook(tag, "end", None)
     return out
 
 
@@ -329,17 +390,26 @@ class GraphSupport:
         return self.nnz > P * self.V
 
 
-def gconv_weights(A, W, sup, Cout, Cin, trans, dtype, bias=None):
+def gconv_weights(A, W, sup, Cout, Cin, trans, dtype, bias=None, plan=None, M=None):
     """Effective weights [V][J][R_pad][C_pad]: trans 0 -> (Cout, Cin) from S lists, 1 -> (Cin, Cout) from R lists.
 
     ``bias`` (forward only: the conv bias, fp32 [P*Cout]): the same launch also pushes it through A
-    (stgcn_gconv_weights_bias), and the call returns (weights, bias2d [V][Cout]) — gcn_bias's result."""
+    (stgcn_gconv_weights_bias), and the call returns (weights, bias2d [V][Cout]) — gcn_bias's result.
+    ``plan``: record the job in a PrepPlan instead of launching; the coefficients are then A * M (``M`` the
+    layer's edge importance, or None), formed inside the batched launch."""
     A = _dense(A)
     P, V = A.shape[0], A.shape[-1]
     R, C = (Cin, Cout) if trans else (Cout, Cin)
     rp = -(-R // col_tile(R)) * col_tile(R)
     cpad = -(-C // 32) * 32
     out = torch.empty((V, sup.J, rp, cpad), dtype=dtype, device=A.device)
+    if plan is not None:
+        nbr, deg = (sup.rnbr, sup.rdeg) if trans else (sup.nbr, sup.deg)
+        b2 = torch.empty((V, Cout), dtype=torch.float32, device=A.device) if bias is not None else None
+        plan.add(kind=2, dtype=L.dtype_code(dtype), src=W, dst=out, Co=Cout, Ci=Cin, trans=int(trans), A=A,
+                 M=None if M is None else _dense(M), nbr=nbr, deg=deg, P=P, V=V, J=sup.J, R_pad=rp, C_pad=cpad,
+                 bconv=bias, bias2d=b2)
+        return (out, b2) if bias is not None else out
     if bias is not None:
         assert not trans
         b2 = torch.empty((V, Cout), dtype=torch.float32, device=A.device)
@@ -470,10 +540,10 @@ def layer_fused(x, A, wimg, gbias, n1_scale, n1_shift, wt_packed, tbias, stats=N
         d._keep = ln
     hook = EVENT_HOOK if tag is not None else None
     if hook:
-        hook(tag, "start")
+        hook(tag, "start", None)
     L.check(L.lib().stgcn_layer_fused_fwd(d, L.stream()), "layer_fused")
     if hook:
-        hook(tag, "end")
+        hook(tag, "end", None)
     return z
 
 
@@ -491,10 +561,10 @@ def gconv(x, wpk, sup, Cin, Cout, trans=False, bias=None, stats=None, out=None, 
     d.in_ld, d.out_ld, d.accumulate = rows_ld(x), rows_ld(out), int(accumulate)
     hook = EVENT_HOOK if tag is not None else None
     if hook:
-        hook(tag, "start")
+        hook(tag, "start", None)
     L.check(L.lib().stgcn_gconv(d, L.dtype_code(x.dtype), L.stream()), "gconv")
     if hook:
-        hook(tag, "end")
+        hook(tag, "end", None)
     return out
 
 

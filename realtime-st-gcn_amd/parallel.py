@@ -133,3 +133,103 @@ def accumulate(model, last: bool):
             yield
     else:
         yield
+
+
+@dataclass
+class SegmentUnit:
+    """One WindowSegment subsegment of one trial: the unit of work the data-parallel path distributes.
+
+    trial: index of the trial; i / count: the subsegment's index and the trial's subsegment count (the
+    reference's ``i`` and ``num_subsegments``, processor.py:377-392); n0 / nw: windows [n0, n0 + nw) of the
+    padded capture; y0 / y1: its label frames."""
+    trial: int
+    i: int
+    count: int
+    n0: int
+    nw: int
+    y0: int
+    y1: int
+
+
+def segment_units(lengths, W: int, segment: int):
+    """Every subsegment of every trial (lengths = frames per trial), in trial order.  The subsegments of a
+    trial are independent units — each has its own loss term ce/count + mse/count (processor.py:377-392,
+    utils/loss.py:25-41, with the one-frame overlap that carries the MSE pair across the boundary) and the
+    reference accumulates their gradients — so they shard across ranks with no data-path collective: the
+    ranks' gradient sum (DDP's all-reduce) is the reference's accumulated gradient."""
+    from .segment import window_segments
+    out = []
+    for k, L in enumerate(lengths):
+        segs = window_segments(L, L + W - 1, L, W, segment)
+        for i, (sx, ex, sy, ey) in enumerate(segs):
+            out.append(SegmentUnit(k, i, len(segs), sx, ex - sx - (W - 1), sy, ey))
+    return out
+
+
+def units_for_rank(units, world: int, rank: int):
+    """Round-robin deal of the units (sizes of consecutive units are alike, so every rank gets the same
+    work within one unit)."""
+    return units[rank::world]
+
+
+class GraphedStep:
+    """A fixed-shape training step replayed as HIP graphs (processor.py:531-564 inner loop with the batch in
+    static buffers): one graph launch for ~370 kernels, the weight-gradient side stream captured as a
+    parallel branch (layer_fn._fork: event fork/join inside the capture).
+
+        graph 1: zero the gradients, ``fwd_loss()`` (forward + loss), backward, [N > 1: copy the fp32
+                 gradients into one flat buffer]
+        N > 1:   all-reduce of the flat buffer over ``group`` (eager, one RCCL launch; not captured)
+        graph 2: [N > 1: the averaged flat gradient back into .grad] + ``opt.step()``
+
+    ``fwd_loss`` must only read tensors whose storage stays put between replays (copy new batches into the
+    tensors it closes over).  The optimizer must be capturable (torch.optim.Adam(capturable=True)).  One
+    eager step runs first (on a side stream, as graph capture requires) so that every gradient and optimizer
+    state tensor exists and keeps its address."""
+
+    def __init__(self, fwd_loss, params, opt, world: int = 1, group=None):
+        self.fwd_loss, self.params, self.opt = fwd_loss, list(params), opt
+        self.world, self.group = world, group
+        self.numels = [p.numel() for p in self.params]
+        dev = self.params[0].device
+        self.flat = torch.zeros(sum(self.numels), device=dev) if world > 1 else None
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            self.opt.zero_grad(set_to_none=False)
+            self._fwd_bwd()
+            if self.flat is not None:
+                self._allreduce()
+            self._apply()
+            self.g1, self.g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g1, stream=s):
+                for p in self.params:
+                    p.grad.zero_()
+                self.loss = self._fwd_bwd()
+            with torch.cuda.graph(self.g2, stream=s):
+                self._apply()
+        torch.cuda.current_stream(dev).wait_stream(s)
+
+    def _fwd_bwd(self):
+        loss = self.fwd_loss()
+        loss.backward()
+        if self.flat is not None:
+            torch.cat([p.grad.reshape(-1) for p in self.params], out=self.flat)
+        return loss.detach()
+
+    def _allreduce(self):
+        import torch.distributed as dist
+        dist.all_reduce(self.flat, group=self.group)
+
+    def _apply(self):
+        if self.flat is not None:
+            for p, g in zip(self.params, torch.split(self.flat, self.numels)):
+                p.grad.copy_(g.view_as(p.grad)).div_(self.world)
+        self.opt.step()
+
+    def __call__(self):
+        self.g1.replay()
+        if self.flat is not None:
+            self._allreduce()
+        self.g2.replay()
+        return self.loss

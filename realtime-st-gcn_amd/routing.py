@@ -12,6 +12,8 @@ also assign the attributes directly.
     fused_bn_inference  STGCN_FUSED_BN=1      BatchNorm layers too (default off: measured slower)
     gcn_tile            STGCN_GCN_TILE=0|1|auto  graph conv on the two-stage MFMA kernel gcn_tile.hip (default 0)
     gcn_afirst          STGCN_GCN_AFIRST=1    force the A-first graph conv (amix + GEMM) for shared graphs
+    prep_plan           STGCN_PREP_PLAN=0     stgcn.Model training forwards pack every weight per call instead of
+                                              in the one-launch plan (native.PrepPlan; default on)
 """
 import os
 
@@ -24,6 +26,7 @@ class _Routing:
         self.fused_bn_inference = e("STGCN_FUSED_BN", "0") == "1"
         self.gcn_tile = e("STGCN_GCN_TILE", "0")
         self.gcn_afirst = e("STGCN_GCN_AFIRST", "0") not in ("0", "")
+        self.prep_plan = e("STGCN_PREP_PLAN", "1") != "0"
 
 
 ROUTING = _Routing()

@@ -55,6 +55,17 @@ class WindowBatch:
         return frames.unfold(2, self.W, 1).permute(0, 2, 1, 4, 3).contiguous().view(self.nw, C, self.W, V)
 
 
+def window_segments(S, Lp, L_labels, W, seg):
+    """[(startX, endX, startY, endY)] of WindowSegment.get_segment (segment_generator.py:133-139) for a trial
+    of S frames: capture frames [startX, endX) of the padded capture (Lp = S + W - 1 frames) give windows
+    startX .. endX - W, predicting label frames [startY, endY).  (S + S % seg) // seg segments; every one
+    after the first starts one window early (the frame its temporal MSE pairs with); the last runs to the
+    end of the capture."""
+    n = (S + S % seg) // seg
+    return [(seg * i - (1 if i > 0 else 0), seg * (i + 1) + (W - 1) if i < n - 1 else Lp,
+             seg * i, seg * (i + 1) if i < n - 1 else L_labels) for i in range(n)]
+
+
 class Segment:
     """segment_generator.py:5-15."""
 
@@ -89,10 +100,7 @@ class WindowSegment(Segment):
 
     def segments(self, Lp, L_labels):
         """[(startX, endX, startY, endY)] of segment_generator.py:133-139 (capture frames / label frames)."""
-        seg = self.subsegment_size
-        n = (self.S + self.S % seg) // seg
-        return [(seg * i - (1 if i > 0 else 0), seg * (i + 1) + (self.W - 1) if i < n - 1 else Lp,
-                 seg * i, seg * (i + 1) if i < n - 1 else L_labels) for i in range(n)]
+        return window_segments(self.S, Lp, L_labels, self.W, self.subsegment_size)
 
     def get_segment(self, captures, labels):
         segs = self.segments(captures.size(2), labels.size(1))

@@ -154,3 +154,27 @@ def test_device_guard_follows_tensor(pkg, monkeypatch):
         for name, cls in inspect.getmembers(mod, inspect.isclass):
             if issubclass(cls, torch.autograd.Function) and cls.__module__ == mod.__name__:
                 assert cls.forward.__wrapped__ is not None, name
+
+
+def test_prep_plan_builds_and_validates(pkg):
+    """The one-launch weight preparation of the config-2 model (stgcn.Model._prepared -> native.PrepPlan):
+    the per-layer jobs are recorded and validated on the host (stgcn_prep_check fills each job's thread
+    count) — 9 layers x (graph conv fwd + data grad, temporal conv fwd + data grad) + 2 residual convs x 2 +
+    the head's 2 x 2, where the stride-2 temporal packs take two jobs each (plain + folded image)."""
+    import bench
+    m = pkg.MODELS["st-gcn"](rank=None, **dict(bench.ARCH, graph=pkg.PKU_MMD)).set_compute_dtype("bf16")
+    K, LF = pkg.native, pkg.layer_fn
+    plan = K.PrepPlan(torch.device("cpu"))
+    layers = []
+    for i, gcn in enumerate(m.gcn_networks):
+        gcn.bind_graph(m.A)
+        layers.append(LF.plan_layer_packs(plan, gcn, m.A, m.edge_importance[i], torch.bfloat16))
+    head = (LF.plan_conv1x1_packs(plan, m.fcn_in.weight, torch.bfloat16),
+            LF.plan_conv1x1_packs(plan, m.fcn_out.weight, torch.bfloat16))
+    plan.finalize()
+    assert all(p is not None for p in layers)
+    assert plan.njobs == 9 * 4 + 2 * 2 + 2 * 2 + 2 * 2
+    assert plan.nblocks > 0
+    # frag images where the kernels expect them
+    assert layers[0].wt[0].frag_stride == 1 and layers[3].wt[0].frag_stride == 2 and layers[3].wtT[0].frag_stride == 2
+    assert head[0][0][1] == 64 and head[0][0][2] == 32

@@ -152,7 +152,7 @@ def test_layer_bf16_vs_oracle(P, cin, cout, stride, gcn_mode, monkeypatch):
     route the graph conv through the fused gcn_tile kernel in one or both directions) vs the fp32
     oracle: forward and every gradient within bf16 tolerance, with the graph conv on the gathered
     gconv.hip ("0") and on the fused gcn_tile.hip ("1")."""
-    monkeypatch.setattr(P.native, "_GCN_TILE", gcn_mode)
+    monkeypatch.setattr(P.routing.ROUTING, "gcn_tile", gcn_mode)
     torch.manual_seed(5)
     N, T = 3, 40
     A = torch.tensor(P.Graph(**P.PKU_MMD).A, dtype=torch.float32)

@@ -53,3 +53,66 @@ def test_rt_online_golden(P, case):
     with torch.no_grad():
         y2 = torch.cat([m(x[:, :, i:i + 1]) for i in range(x.shape[2])], dim=2)
     assert_close(y2, y, 1e-6, "online after reset")
+
+
+CONFIG3_LAYERS = {"layers": 9, "kernel": 9, "in_ch": [64, 64, 64, 64, 128, 128, 128, 256, 256],
+                  "out_ch": [64, 64, 64, 128, 128, 128, 256, 256, 256], "residual": [1] * 9, "dropout": [0.0] * 9,
+                  "latency": False, "importance": True, "in_feat": 3, "buffer": 1, "stages": 1}
+
+
+@pytest.mark.parametrize("strides", [[1] * 9, [1, 1, 1, 2, 1, 1, 2, 1, 1]], ids=["stride1", "ref_strides"])
+def test_rt_online_config3_widths(P, strides):
+    """Config 3 at its own widths (config/pku-mmd/ln/rtstgcn_local.json: LayerNorm, K = 9, 64 -> 256 channels,
+    V*C up to 6 400): the per-frame kernels (rt_fused.hip; rt_norm's several values per thread, rt_gcn at
+    Cin 64-256) over 48 frames (> every FIFO: 17 frames at stride 2), eager and replayed as a HIP graph, vs
+    the oracle's online form (rtstgcn.py:528-553, 591-627), fp32 1e-3."""
+    from oracle import stgcn_oracle as O
+    arch = {"strategy": "spatial", "in_feat": 3, "stages": 1, "kernel": 9, "output_type": "logits",
+            "normalization": "LayerNorm", "segment": 500, "num_classes": 52,
+            "rt-st-gcn": dict(CONFIG3_LAYERS, stride=strides), "graph": P.PKU_MMD}
+    torch.manual_seed(21)
+    m = P.MODELS["rt-st-gcn"](rank=None, **arch)
+    sd = m.state_dict()
+    g = torch.Generator().manual_seed(22)
+    for k in sd:  # non-trivial norms, biases and edge importance
+        if "edge_importance" in k:
+            sd[k] = 1 + 0.1 * torch.randn(sd[k].shape, generator=g)
+        elif ("bn_relu" in k or "residual.1" in k or "norm_in" in k) and k.endswith("weight"):
+            sd[k] = 1 + 0.2 * torch.randn(sd[k].shape, generator=g)
+        elif k.endswith("bias"):
+            sd[k] = 0.1 * torch.randn(sd[k].shape, generator=g)
+    m.load_state_dict(sd, strict=True)
+    F_ = 48
+    x = torch.randn(1, 3, F_, 25, generator=g)
+    with torch.no_grad():
+        ref = O.rt_model_online(x, {k: v.clone() for k, v in sd.items()}, arch)
+    m = m.to(DEV).eval()
+    m.prepare_benchmark(arch)
+    xd = x.to(DEV)
+    with torch.no_grad():
+        y = torch.cat([m(xd[:, :, i:i + 1]) for i in range(F_)], dim=2)
+    torch.cuda.synchronize()
+    assert_close(y, ref, TOL, f"config-3 online eager {strides}")
+    # the same stream replayed as a HIP graph of one per-frame step (FIFO state on the device)
+    m.reset_state()
+    x_static = torch.zeros_like(xd[:, :, :1])
+    with torch.no_grad():
+        for i in range(3):
+            x_static.copy_(xd[:, :, i:i + 1])
+            m(x_static)
+        m.reset_state()
+        graph = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(graph):
+                y_static = m(x_static)
+        torch.cuda.current_stream().wait_stream(s)
+        m.reset_state()
+        outs = []
+        for i in range(F_):
+            x_static.copy_(xd[:, :, i:i + 1])
+            graph.replay()
+            outs.append(y_static.clone())
+    torch.cuda.synchronize()
+    assert_close(torch.cat(outs, dim=2), ref, TOL, f"config-3 online graph {strides}")

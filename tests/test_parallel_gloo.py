@@ -192,3 +192,30 @@ def test_sharded_stgcn_step_matches_single_process(pkg):
     for g, p in zip(got, net.p):
         g = torch.tensor(g, dtype=torch.float64)
         assert torch.allclose(g, p.grad, rtol=1e-7, atol=1e-10), (g - p.grad).abs().max()  # fp64 sum order
+
+
+def test_segment_units_partition(pkg):
+    """Config 4's units (parallel.segment_units) are exactly WindowSegment.get_segment's subsegments of each
+    trial (segment_generator.py:132-145: window ranges, label ranges, index, count), and the round-robin deal
+    gives every unit to exactly one rank with per-rank window counts within one unit of each other."""
+    par, seg = pkg.parallel, pkg.segment
+    lengths = [4123, 301, 7999, 64, 640]
+    W, S = 300, 64
+    units = par.segment_units(lengths, W, S)
+    k = 0
+    for t, L in enumerate(lengths):
+        ws = seg.WindowSegment(staged=True, stages=1, num_classes=52, graph={"num_node": 25}, in_feat=3,
+                               rank="cpu", world_size=1, receptive_field=W, segment=S)
+        P0, _ = ws.pad_sequence(L)
+        cap = torch.zeros(1, 3, L + P0, 25)
+        lab = torch.zeros(1, L, dtype=torch.long)
+        for i, (b, y, n) in enumerate(ws.get_segment(cap, lab)):
+            u = units[k]
+            assert (u.trial, u.i, u.count, u.n0, u.nw) == (t, i, n, b.n0, b.nw)
+            assert u.y1 - u.y0 == y.shape[1] and u.nw == y.shape[1] + (1 if i > 0 else 0)
+            k += 1
+    assert k == len(units)
+    for world in (1, 2, 3, 8):
+        parts = [par.units_for_rank(units, world, r) for r in range(world)]
+        assert sorted(id(u) for p in parts for u in p) == sorted(id(u) for u in units)
+        assert max(len(p) for p in parts) - min(len(p) for p in parts) <= 1
