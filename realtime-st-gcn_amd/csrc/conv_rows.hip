@@ -322,9 +322,9 @@ __global__ void pack_weight_kernel(const float* __restrict__ src, long s0, long 
 
 int pack_weight_launch(const float* src, long s0, long s1, long s2, int Kt, int Co, int Ci, void* dst, int cp, int kp,
                        int dtype, hipStream_t s, void* dst_frag) {
-  const long total = (long)Kt * cp * kp;
+  const long total = (long)Kt * cp * kp / 8;  // threads: 8 consecutive ci each
   const unsigned blocks = (unsigned)((total + 255) / 256);
-  if (dst_frag && (cp % 32 || kp % 16)) return STGCN_EBADSHAPE;
+  if (kp % 8 || (dst_frag && (cp % 32 || kp % 16))) return STGCN_EBADSHAPE;
   if (dtype == 1)
     hipLaunchKernelGGL(pack_weight_kernel<bf16>, dim3(blocks), dim3(256), 0, s, src, s0, s1, s2, Co, Ci, cp, kp, total,
                        (bf16*)dst, (bf16*)dst_frag);

@@ -566,7 +566,7 @@ __global__ __launch_bounds__((4 + NHW) * 64, 1) void conv_wide_kernel(const stgc
 __global__ void pack_s2frag_kernel(const float* __restrict__ src, long s0, long s1, long s2, int Co, int Ci, int trans,
                                    int co_f, int ci_f, bf16* __restrict__ dst) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx < 5L * co_f * ci_f) pack_s2frag_elem(src, s0, s1, s2, Co, Ci, trans, co_f, ci_f, idx, dst);
+  if (idx < 5L * co_f * ci_f / 8) pack_s2frag_elem(src, s0, s1, s2, Co, Ci, trans, co_f, ci_f, idx, dst);
 }
 
 }  // namespace
@@ -575,7 +575,8 @@ int pack_s2frag_launch(const float* src, long s0, long s1, long s2, int Co, int 
                        hipStream_t s) {
   const int co_f = trans ? 2 * Co : Co, ci_f = trans ? Ci : 2 * Ci;
   if (co_f % 32 || ci_f % 16) return STGCN_EBADSHAPE;
-  const long total = 5L * co_f * ci_f;
+  if (Ci % 8 || Co % 8) return STGCN_EBADSHAPE;
+  const long total = 5L * co_f * ci_f / 8;  // threads: 8 consecutive folded input channels each
   hipLaunchKernelGGL(pack_s2frag_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, src, s0, s1, s2, Co,
                      Ci, trans, co_f, ci_f, (bf16*)dst);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;

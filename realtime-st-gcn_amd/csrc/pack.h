@@ -4,23 +4,39 @@
 #pragma once
 #include "common.h"
 
+// 8 consecutive elements of T as 16 (bf16) or 32 (fp32) bytes
+template <typename T>
+DEV void store8(T* p, const float* v) {
+  if constexpr (sizeof(T) == 2) {
+    *reinterpret_cast<uint4*>(p) = pack16(v, (T*)nullptr);
+  } else {
+    *reinterpret_cast<uint4*>(p) = pack16(v, (T*)nullptr);
+    *reinterpret_cast<uint4*>(p + 4) = pack16(v + 4, (T*)nullptr);
+  }
+}
+
 // dst[k][co][ci] = src[k*s0 + co*s1 + ci*s2] (0 in the padding), cast to T: any strided view of the
-// fp32 parameter (permuted / transposed) packs in one pass.  Thread i of Kt * cp * kp.
+// fp32 parameter (permuted / transposed) packs in one pass.  Thread i of Kt * cp * kp / 8 handles 8
+// consecutive ci (kp % 8 == 0): one 16/32-byte store into dst and one into the fragment image.
 template <typename T>
 DEV void pack_weight_elem(const float* __restrict__ src, long s0, long s1, long s2, int Co, int Ci, int cp, int kp,
                           long i, T* __restrict__ dst, T* __restrict__ dst_frag) {
-  const int ci = (int)(i % kp);
-  const long r = i / kp;
+  const int k8 = kp >> 3;
+  const int ci0 = (int)(i % k8) * 8;
+  const long r = i / k8;
   const int co = (int)(r % cp);
   const long k = r / cp;
-  const float v = (co < Co && ci < Ci) ? src[k * s0 + co * s1 + ci * s2] : 0.f;
-  dst[i] = Tr<T>::from_f(v);
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+    v[e] = (co < Co && ci0 + e < Ci) ? src[k * s0 + co * s1 + (long)(ci0 + e) * s2] : 0.f;
+  store8(dst + ((k * cp + co) * (long)kp + ci0), v);
   if (dst_frag) {
     // MFMA-fragment image (conv_wide.hip): 1-KiB blocks [k][co/32][ci/16], lane l = (ci%16)/8*32 + co%32
     // holding 8 consecutive ci: a wave's B fragment is one contiguous 1-KiB load
-    const long blk = ((long)k * (cp / 32) + co / 32) * (kp / 16) + ci / 16;
-    const int l = ((ci & 15) >> 3) * 32 + (co & 31);
-    dst_frag[blk * 512 + l * 8 + (ci & 7)] = Tr<T>::from_f(v);
+    const long blk = ((long)k * (cp / 32) + co / 32) * (kp / 16) + ci0 / 16;
+    const int l = ((ci0 & 15) >> 3) * 32 + (co & 31);
+    store8(dst_frag + blk * 512 + l * 8, v);
   }
 }
 
@@ -28,12 +44,14 @@ DEV void pack_weight_elem(const float* __restrict__ src, long s0, long s1, long 
 // conv the wide kernel runs instead (see conv_wide_launch) —
 //   forward   W'[t][co][par*Ci + ci] = W[2t + par][co][ci]
 //   data grad W'[t][par*Co + co][ci] = W[8 - 2t + par][co][ci]      (taps outside 0..8 are zero)
-// laid out like stgcn_pack_weight_frag (1-KiB blocks [t][co'/32][ci'/16]).  Thread idx of 5 * co_f * ci_f.
+// laid out like stgcn_pack_weight_frag (1-KiB blocks [t][co'/32][ci'/16]).  Thread idx of 5 * co_f * ci_f / 8
+// handles 8 consecutive ci' (Ci % 8 == 0, so they share the parity).
 DEV void pack_s2frag_elem(const float* __restrict__ src, long s0, long s1, long s2, int Co, int Ci, int trans,
                           int co_f, int ci_f, long idx, bf16* __restrict__ dst) {
-  const int cip = (int)(idx % ci_f);
-  const int cop = (int)((idx / ci_f) % co_f);
-  const int t = (int)(idx / ((long)co_f * ci_f));
+  const int c8 = ci_f >> 3;
+  const int cip = (int)(idx % c8) * 8;
+  const int cop = (int)((idx / c8) % co_f);
+  const int t = (int)(idx / ((long)co_f * c8));
   int co = cop, ci = cip, dt;
   if (trans) {
     const int par = cop >= Co;
@@ -44,10 +62,12 @@ DEV void pack_s2frag_elem(const float* __restrict__ src, long s0, long s1, long 
     ci = cip - par * Ci;
     dt = 2 * t + par;
   }
-  const float v = (dt >= 0 && dt <= 8) ? src[dt * s0 + co * s1 + ci * s2] : 0.f;
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = (dt >= 0 && dt <= 8) ? src[dt * s0 + co * s1 + (long)(ci + e) * s2] : 0.f;
   const long blk = ((long)t * (co_f / 32) + cop / 32) * (ci_f / 16) + cip / 16;
   const int l = ((cip & 15) >> 3) * 32 + (cop & 31);
-  dst[blk * 512 + l * 8 + (cip & 7)] = (bf16)v;
+  store8(dst + blk * 512 + l * 8, v);
 }
 
 // Graph conv effective weights (gconv.hip):
@@ -87,12 +107,26 @@ DEV void gconv_weights_elem(const float* __restrict__ A, const float* __restrict
   if (bias2d && !trans && c0 == 0 && r < Cout) {
     // the graph conv's bias pushed through A in the same launch (stgcn_gcn_bias, same summation order):
     // bias2d[a][co] = sum_p b[p*Cout + co] * colsum_p[a],  colsum_p[a] = sum_v A[p][v][a]
+    // (the V <= 32 coefficients of a column are loaded together: a dependent chain of loads per partition
+    // was the tail of the batched launch)
     float sb = 0.f;
     for (int p = 0; p < P; ++p) {
       float cs = 0.f;
-      for (int v = 0; v < V; ++v) {
-        const long ia = ((long)p * V + v) * V + a;
-        cs += M ? __fmul_rn(A[ia], M[ia]) : A[ia];  // rounded product, never fused into the sum
+      if (V <= 32) {
+        float c[32];
+#pragma unroll
+        for (int v = 0; v < 32; ++v) {
+          const long ia = ((long)p * V + v) * V + a;
+          c[v] = v < V ? (M ? __fmul_rn(A[ia], M[ia]) : A[ia]) : 0.f;  // rounded product, never fused
+        }
+#pragma unroll
+        for (int v = 0; v < 32; ++v)
+          if (v < V) cs += c[v];
+      } else {
+        for (int v = 0; v < V; ++v) {
+          const long ia = ((long)p * V + v) * V + a;
+          cs += M ? __fmul_rn(A[ia], M[ia]) : A[ia];
+        }
       }
       sb += bconv[p * Cout + r] * cs;
     }

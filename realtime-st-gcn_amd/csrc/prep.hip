@@ -49,13 +49,13 @@ extern "C" int stgcn_prep_check(stgcn_prep_job* jobs, int njobs) {
     if (!j.src || !j.dst || j.Co <= 0 || j.Ci <= 0) return STGCN_EBADSHAPE;
     if (j.kind == 0) {
       if (j.Kt <= 0 || j.cp < j.Co || j.kp < j.Ci) return STGCN_EBADSHAPE;
-      if (j.dst_frag && (j.cp % 32 || j.kp % 16)) return STGCN_EBADSHAPE;
-      j.threads = (long)j.Kt * j.cp * j.kp;
+      if (j.kp % 8 || (j.dst_frag && (j.cp % 32 || j.kp % 16))) return STGCN_EBADSHAPE;
+      j.threads = (long)j.Kt * j.cp * j.kp / 8;
     } else if (j.kind == 1) {
       if (j.dtype != 1) return STGCN_EDTYPE;
       const int co_f = j.trans ? 2 * j.Co : j.Co, ci_f = j.trans ? j.Ci : 2 * j.Ci;
-      if (co_f % 32 || ci_f % 16) return STGCN_EBADSHAPE;
-      j.threads = 5L * co_f * ci_f;
+      if (co_f % 32 || ci_f % 16 || j.Ci % 8 || j.Co % 8) return STGCN_EBADSHAPE;
+      j.threads = 5L * co_f * ci_f / 8;
     } else if (j.kind == 2) {
       if (!j.A || !j.nbr || !j.deg || j.P <= 0 || j.P > GW_PMAX || j.V <= 0 || j.J <= 0 || j.C_pad % 8 ||
           j.R_pad < (j.trans ? j.Ci : j.Co) || j.C_pad < (j.trans ? j.Co : j.Ci) || (j.bias2d && (j.trans || !j.bconv)))

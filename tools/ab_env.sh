@@ -1,11 +1,16 @@
 #!/bin/bash
-# A/B of an env switch on ONE box, interleaved full-step bench runs: tools/ab_env.sh VAR "A B" [steps]
+# Interleaved A/B of bench.py variants on ONE box: each argument is "NAME:ENV=VAL,ENV2=VAL:extra bench flags"
+# (empty env / flags allowed), run REPS times in turn; prints ms/step per run.  Example:
+#   bash tools/ab_env.sh "plan::" "noplan:STGCN_PREP_PLAN=0:" "graph::--graph"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-VAR=$1; VALS=$2; STEPS=${3:-100}
-for rep in ${REPS:-1 2 3}; do
-  for v in $VALS; do
-    env $VAR=$v timeout -k 10 300 python bench.py --steps $STEPS --warmup 10 --no-cpu-baseline > gpurun_out/ab_env_$v.json 2>/dev/null || exit 1
-    echo "$VAR=$v rep $rep: $(python -c 'import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(d["ms_per_step"])' gpurun_out/ab_env_$v.json)"
+REPS=${REPS:-3}
+STEPS=${STEPS:-100}
+for rep in $(seq $REPS); do
+  for spec in "$@"; do
+    name=${spec%%:*}; rest=${spec#*:}; envs=${rest%%:*}; flags=${rest#*:}
+    out=gpurun_out/ab_$name.json
+    env $(echo $envs | tr ',' ' ') timeout -k 10 300 python bench.py --steps $STEPS --warmup 10 --no-cpu-baseline --no-layer-roofline $flags > $out 2> gpurun_out/ab_$name.err || { tail -5 gpurun_out/ab_$name.err; exit 1; }
+    echo "$name rep $rep: $(python -c 'import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(d["ms_per_step"], d["roofline"]["avg_launch_ms"])' $out)"
   done
 done
