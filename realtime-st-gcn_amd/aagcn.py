@@ -60,7 +60,9 @@ class Model(nn.Module):
         super().__init__()
         conf = kwargs["aa-gcn"]
         self.graph = Graph(strategy=kwargs["strategy"], **kwargs["graph"])
-        A = torch.tensor(self.graph.A, dtype=torch.float32, requires_grad=False)
+        # contiguous: graph.A is a transposed view (graph.py:179) and torch.tensor keeps its strides, so every
+        # A * edge_importance product (and each layer's dense copy of it) would be permuted
+        A = torch.tensor(self.graph.A, dtype=torch.float32, requires_grad=False).contiguous()
         self.register_buffer("A", A)
         kernel_size = (conf["kernel"], kwargs["graph"]["num_node"])
         self.num_classes = kwargs["num_classes"]

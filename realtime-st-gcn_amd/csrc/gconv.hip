@@ -471,9 +471,12 @@ template <typename T>
 __global__ void gconv_weights_kernel(const float* __restrict__ A, const float* __restrict__ W, const int* nbr,
                                      const int* deg, int P, int V, int J, int Cout, int Cin, int trans, T* out,
                                      int R_pad, int C_pad, const float* __restrict__ bconv, float* __restrict__ bias2d) {
+  __shared__ float colsum[GW_COLSUM_MAX];
+  if (bias2d) gconv_colsum_block(A, nullptr, P, V, colsum);  // block-uniform
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx < (long)V * R_pad * (C_pad / 8))
-    gconv_weights_elem<T>(A, nullptr, W, nbr, deg, P, V, J, Cout, Cin, trans, out, R_pad, C_pad, bconv, bias2d, idx);
+    gconv_weights_elem<T>(A, nullptr, W, nbr, deg, P, V, J, Cout, Cin, trans, out, R_pad, C_pad, bconv, bias2d, colsum,
+                          idx);
 }
 
 // ------------------------------------------------------------------ weight gradient (bf16 + fp32)
@@ -1184,7 +1187,7 @@ int gconv_launch(const stgcn_gconv_desc& a, int dtype, hipStream_t s) {
 int gconv_weights_launch(const float* A, const float* W, const int* nbr, const int* deg, int P, int V, int J, int Cout,
                          int Cin, int trans, void* out, int R_pad, int C_pad, int dtype, hipStream_t s,
                          const float* bconv, float* bias2d) {
-  if (C_pad % 8 || P > GW_PMAX) return STGCN_EBADSHAPE;
+  if (C_pad % 8 || P > GW_PMAX || (bconv && P * V > GW_COLSUM_MAX)) return STGCN_EBADSHAPE;
   const long total = (long)V * R_pad * (C_pad / 8);
   const unsigned blocks = (unsigned)((total + 255) / 256);
   if (dtype == 1)

@@ -82,12 +82,41 @@ constexpr int GW_PMAX = 4;
 constexpr int GW_JMAX = 8;  // neighbour slots per joint whose loads are issued together
 // M (optional, the layer's edge importance [P][V][V]): coefficients are A * M, the same fp32 product the
 // model forms for the layer (stgcn.py:89), so a model can prepare every layer before that product exists.
-// Thread idx of V * R_pad * (C_pad / 8).
+// Column sums of A * M for the bias through A, colsum[p * V + a] = sum_v (A * M)[p][v][a] (summed in v order),
+// computed once per block into LDS by every thread of the block (call before any thread returns; the loads
+// of a column are issued together) — per-thread sums were a chain of 75 dependent loads per output.
+DEV void gconv_colsum_block(const float* __restrict__ A, const float* __restrict__ M, int P, int V, float* colsum) {
+  for (int t = threadIdx.x; t < P * V; t += blockDim.x) {
+    const int p = t / V, a = t - p * V;
+    float cs = 0.f;
+    if (V <= 32) {
+      float c[32];
+#pragma unroll
+      for (int v = 0; v < 32; ++v) {
+        const long ia = ((long)p * V + v) * V + a;
+        c[v] = v < V ? (M ? __fmul_rn(A[ia], M[ia]) : A[ia]) : 0.f;  // rounded product, never fused into the sum
+      }
+#pragma unroll
+      for (int v = 0; v < 32; ++v)
+        if (v < V) cs += c[v];
+    } else {
+      for (int v = 0; v < V; ++v) {
+        const long ia = ((long)p * V + v) * V + a;
+        cs += M ? __fmul_rn(A[ia], M[ia]) : A[ia];
+      }
+    }
+    colsum[t] = cs;
+  }
+  __syncthreads();
+}
+constexpr int GW_COLSUM_MAX = GW_PMAX * 64;  // LDS floats for the column sums (P <= 4, V <= 64)
+
+// Thread idx of V * R_pad * (C_pad / 8); colsum: gconv_colsum_block's LDS table when bias2d != NULL.
 template <typename T>
 DEV void gconv_weights_elem(const float* __restrict__ A, const float* __restrict__ M, const float* __restrict__ W,
                             const int* nbr, const int* deg, int P, int V, int J, int Cout, int Cin, int trans, T* out,
                             int R_pad, int C_pad, const float* __restrict__ bconv, float* __restrict__ bias2d,
-                            long idx) {
+                            const float* colsum, long idx) {
   const int C8 = C_pad / 8;
   // forward: c (ci) fastest across lanes, so W rows are read as float4 runs; trans: r (ci) fastest, so
   // the 8 scalar reads of W[co][r] per thread are coalesced across lanes
@@ -106,30 +135,9 @@ DEV void gconv_weights_elem(const float* __restrict__ A, const float* __restrict
   const int R = trans ? Cin : Cout, C = trans ? Cout : Cin;
   if (bias2d && !trans && c0 == 0 && r < Cout) {
     // the graph conv's bias pushed through A in the same launch (stgcn_gcn_bias, same summation order):
-    // bias2d[a][co] = sum_p b[p*Cout + co] * colsum_p[a],  colsum_p[a] = sum_v A[p][v][a]
-    // (the V <= 32 coefficients of a column are loaded together: a dependent chain of loads per partition
-    // was the tail of the batched launch)
+    // bias2d[a][co] = sum_p b[p*Cout + co] * colsum_p[a], colsum_p[a] = sum_v A[p][v][a] (gconv_colsum_block)
     float sb = 0.f;
-    for (int p = 0; p < P; ++p) {
-      float cs = 0.f;
-      if (V <= 32) {
-        float c[32];
-#pragma unroll
-        for (int v = 0; v < 32; ++v) {
-          const long ia = ((long)p * V + v) * V + a;
-          c[v] = v < V ? (M ? __fmul_rn(A[ia], M[ia]) : A[ia]) : 0.f;  // rounded product, never fused
-        }
-#pragma unroll
-        for (int v = 0; v < 32; ++v)
-          if (v < V) cs += c[v];
-      } else {
-        for (int v = 0; v < V; ++v) {
-          const long ia = ((long)p * V + v) * V + a;
-          cs += M ? __fmul_rn(A[ia], M[ia]) : A[ia];
-        }
-      }
-      sb += bconv[p * Cout + r] * cs;
-    }
+    for (int p = 0; p < P; ++p) sb += bconv[p * Cout + r] * colsum[p * V + a];
     bias2d[(long)a * Cout + r] = sb;
   }
   float wv[GW_PMAX][8];

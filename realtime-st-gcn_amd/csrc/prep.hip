@@ -19,6 +19,8 @@ __global__ __launch_bounds__(256) void prep_kernel(const stgcn_prep_job* __restr
     else hi = mid - 1;
   }
   const stgcn_prep_job& j = jobs[lo];
+  __shared__ float colsum[GW_COLSUM_MAX];
+  if (j.kind == 2 && j.bias2d) gconv_colsum_block(j.A, j.M, j.P, j.V, colsum);  // block-uniform: one job per block
   const long i = (b - start[lo]) * 256 + threadIdx.x;
   if (i >= j.threads) return;
   if (j.kind == 0) {
@@ -32,10 +34,10 @@ __global__ __launch_bounds__(256) void prep_kernel(const stgcn_prep_job* __restr
   } else {
     if (j.dtype == 1)
       gconv_weights_elem<bf16>(j.A, j.M, j.src, j.nbr, j.deg, j.P, j.V, j.J, j.Co, j.Ci, j.trans, (bf16*)j.dst,
-                               j.R_pad, j.C_pad, j.bconv, j.bias2d, i);
+                               j.R_pad, j.C_pad, j.bconv, j.bias2d, colsum, i);
     else
       gconv_weights_elem<float>(j.A, j.M, j.src, j.nbr, j.deg, j.P, j.V, j.J, j.Co, j.Ci, j.trans, (float*)j.dst,
-                                j.R_pad, j.C_pad, j.bconv, j.bias2d, i);
+                                j.R_pad, j.C_pad, j.bconv, j.bias2d, colsum, i);
   }
 }
 
@@ -58,7 +60,8 @@ extern "C" int stgcn_prep_check(stgcn_prep_job* jobs, int njobs) {
       j.threads = 5L * co_f * ci_f / 8;
     } else if (j.kind == 2) {
       if (!j.A || !j.nbr || !j.deg || j.P <= 0 || j.P > GW_PMAX || j.V <= 0 || j.J <= 0 || j.C_pad % 8 ||
-          j.R_pad < (j.trans ? j.Ci : j.Co) || j.C_pad < (j.trans ? j.Co : j.Ci) || (j.bias2d && (j.trans || !j.bconv)))
+          j.R_pad < (j.trans ? j.Ci : j.Co) || j.C_pad < (j.trans ? j.Co : j.Ci) ||
+          (j.bias2d && (j.trans || !j.bconv || j.P * j.V > GW_COLSUM_MAX)))
         return STGCN_EBADSHAPE;
       j.threads = (long)j.V * j.R_pad * (j.C_pad / 8);
     } else {

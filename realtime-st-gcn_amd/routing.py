@@ -5,8 +5,10 @@ suite); none changes numerics beyond the rounding order of its kernels.  Default
 routes on MI355X.  The environment variables are read once at import; code (tests, tools) may
 also assign the attributes directly.
 
-    side_stream         STGCN_SIDE_STREAM=0   weight-gradient branch of a layer backward on a per-device side
-                                              stream (default on)
+    side_stream         STGCN_SIDE_STREAM=1   weight-gradient branch of a layer backward (and the residual branch
+                                              of the forward) on a per-device side stream (default off: with
+                                              the one-launch weight preparation the config-2 step measured 8.59
+                                              ms on one stream vs 8.72 with the side stream, same box)
     fused_inference     STGCN_FUSED=0         no_grad forward of 64->64 stride-1 layers through the fused layer
                                               kernel layer_fused.hip (default on for LayerNorm layers)
     fused_bn_inference  STGCN_FUSED_BN=1      BatchNorm layers too (default off: measured slower)
@@ -21,7 +23,7 @@ import os
 class _Routing:
     def __init__(self):
         e = os.environ.get
-        self.side_stream = e("STGCN_SIDE_STREAM", "1") != "0"
+        self.side_stream = e("STGCN_SIDE_STREAM", "0") == "1"
         self.fused_inference = e("STGCN_FUSED", "1") != "0"
         self.fused_bn_inference = e("STGCN_FUSED_BN", "0") == "1"
         self.gcn_tile = e("STGCN_GCN_TILE", "0")
