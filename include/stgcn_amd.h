@@ -324,7 +324,8 @@ int stgcn_seg_loss_bwd(const float* dce, const float* dmse, const float* gce, co
  * through A, gbias [V][64], is added first), and the Kt = 9 temporal conv (+ tbias) runs on h from LDS:
  *   z[(n,t,w)][co] = tbias[co] + sum_{dt<9, ci} W[dt][co][ci] h[(n, t+dt-4, w)][ci]   (h = 0 outside [0,T))
  * g never reaches HBM.  BatchNorm statistics of g come from pass 1 (stgcn_gcn_tile with out = NULL +
- * stgcn_bn_finalize); z's partials (count, mean, M2) go to stats [stgcn_layer_fused_row_blocks][64]
+ * stgcn_bn_finalize); z's partials (count, mean, M2), one row per (block, 8-frame step, row half), go to
+ * stats [stgcn_layer_fused_row_blocks][64]
  * (or NULL) for bn_finalize.  bf16; Cin = Cout = 64; stride 1; P <= 3; 16 < V <= 25.
  * wg_frag: the stgcn_gcn_tile weight image of W'[co][p*64+ci] = W[p*64+co][ci] (Kw_pad = P*64);
  * wt_frag: the stgcn_pack_weight_frag image of the temporal weight [9][64][64].

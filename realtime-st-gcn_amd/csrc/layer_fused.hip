@@ -133,6 +133,7 @@ DEV unsigned lds_u32(const void* p) { return (unsigned)(size_t)(const __attribut
 struct FGeom {
   int runs_n;  // runs per sample
   int run;     // frames per run (multiple of CF)
+  int nsm;     // steps per run (run / CF): BN2 partial rows per block = 2 * nsm (one per step and row half)
   int off_tab, off_ring, off_h, off_red;  // LDS offsets
 };
 
@@ -364,7 +365,6 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
       if (s < nsteps && !(DBG & 1)) compute(CF * (s + 1) + gw, s + 1 < nsteps ? CF * (s + 2) + gw : -1);
       lds_barrier();  // S_s
     }
-    if (a.stats) lds_barrier();  // R: the TCN waves' statistics hand-off
     return;
   }
 
@@ -398,11 +398,10 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
   bf16x8 fw[NB];  // k-step k's fragment in slot k % NB, the same every step
 #pragma unroll
   for (int k = 0; k < NB - 1; ++k) fw[k] = load_w(k);
-  // BN2 (sum, sum of squares) of the run per channel, accumulated in LDS step by step (registers stay free
-  // for the k-loop); one writer per (row half, channel): deterministic
-  if (!LN)
-    for (int c = lane; c < C; c += 64)
-      if (ct == 0) sRed[rh * C + c] = make_float2(0.f, 0.f);
+  // BN2 partials: per step and row half, the (count, mean, M2) of the step's rows of each channel go straight
+  // to global memory (row (block * nsm + step) * 2 + rh of stats); fire-and-forget stores, no LDS
+  // read-modify-write chain and no end-of-run hand-off
+  float4* const st_out = a.stats ? reinterpret_cast<float4*>(a.stats) + ((long)blockIdx.x * g.nsm * 2 + rh) * C : nullptr;
   const f32x16 zero = {};
   unsigned arrivals = 0;  // LN: TCN-wave arrivals expected at the counter so far
   lds_barrier();  // S_0
@@ -581,18 +580,22 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
           }
         }
       }
-      if (a.stats) {  // the step's sums over this wave's rows (lanes) -> the run totals in LDS
+      if (st_out) {  // the step's sums over this wave's rows (lanes) -> (count, mean, M2) partials
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           s1[r] = half_sum(s1[r]);
           s2[r] = half_sum(s2[r]);
         }
         if (lr == 31) {
+          const int cnt = max(0, min(vrows - rh * RT * 32, RTN * 32));
+          const float inv = cnt ? 1.f / (float)cnt : 0.f;
+          float4* o = st_out + (long)(s - 1) * 2 * C;
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            float2* p = sRed + rh * C + 32 * ct + 8 * (r >> 2) + 4 * lh + (r & 3);
-            const float2 o = *p;
-            *p = make_float2(o.x + s1[r], o.y + s2[r]);
+            const float mu = s1[r] * inv;  // mean of z - bias over the step's rows (bias added back below)
+            o[32 * ct + 8 * (r >> 2) + 4 * lh + (r & 3)] =
+                cnt ? make_float4((float)cnt, tb[r] + mu, fmaxf(s2[r] - s1[r] * mu, 0.f), 0.f)
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
           }
         }
       }
@@ -607,16 +610,11 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
     tcn_run.template operator()<2>();
   else
     tcn_run.template operator()<1>();
-  if (!a.stats) return;
-  lds_barrier();  // R (the GCN waves join it before they exit)
-  if (tid < C) {
-    const float2 u0 = sRed[tid], u1 = sRed[C + tid];
-    const float t1 = u0.x + u1.x, t2 = u0.y + u1.y;
-    const float cntr = (float)((R1 - R0) * V);
-    const float mu = t1 / cntr;
-    const float b = a.tbias ? a.tbias[tid] : 0.f;
-    reinterpret_cast<float4*>(a.stats)[(long)blockIdx.x * C + tid] = make_float4(cntr, b + mu, fmaxf(t2 - t1 * mu, 0.f), 0.f);
-  }
+  if (st_out && lr == 31)  // steps past this run's end (the last run of a sample): empty partials
+    for (int s = nsteps + 1; s <= g.nsm; ++s)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        st_out[(long)(s - 1) * 2 * C + 32 * ct + 8 * (r >> 2) + 4 * lh + (r & 3)] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 FGeom plan(int N, int T) {
@@ -626,6 +624,7 @@ FGeom plan(int N, int T) {
   const int span = (T + per - 1) / per;
   g.run = (span + CF - 1) / CF * CF;
   g.runs_n = (T + g.run - 1) / g.run;
+  g.nsm = g.run / CF;
   return g;
 }
 
@@ -633,7 +632,8 @@ FGeom plan(int N, int T) {
 
 long layer_fused_row_blocks(int N, int T) {
   if (N < 1 || T < 1) return 1;
-  return (long)N * plan(N, T).runs_n;
+  const FGeom g = plan(N, T);
+  return (long)N * g.runs_n * g.nsm * 2;
 }
 
 int layer_fused_launch(const stgcn_layer_fused_desc& a, hipStream_t s) {
