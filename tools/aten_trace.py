@@ -34,6 +34,9 @@ class Log(TorchDispatchMode):
                 if "realtime-st-gcn_amd" in f.filename or "bench.py" in f.filename or "torch/optim" in f.filename:
                     fr = "%s:%d %s" % (os.path.basename(f.filename), f.lineno, f.line)
                     break
+            if fr == "?":  # autograd-engine ops (no Python frame): identify by operand shapes / strides
+                fr = " ".join("%s%s" % (tuple(t.shape), tuple(t.stride())) for t in args
+                              if isinstance(t, torch.Tensor))[:110]
             self.c[(name, fr)] += 1
         return func(*args, **(kwargs or {}))
 
