@@ -194,6 +194,16 @@ long stgcn_gconv_wgrad_workspace(const stgcn_gconv_wgrad_desc* d, int dtype);
  * work: stgcn_gconv_wgrad_finish_workspace() bytes (chunked dA partials, fixed-order reduce) or NULL
  * (slower per-partition path).  Deterministic either way. */
 long stgcn_gconv_wgrad_finish_workspace(int P, int V, int J, int Cout, int Cin);
+/* The same finish with the conv bias pushed through A folded in (stgcn_gcn_bias_bwd), in two launches, every
+ * output OVERWRITTEN (no zero fill needed):
+ *   dW[p*Cout+co][ci] = sum_{w,j} A[p][S(w)_j][w] dweff[w][j][co][ci]
+ *   dA[p][v][w]       = [v in S(w)] sum_{co,ci} W[p*Cout+co][ci] dweff[pair(v,w)][co][ci] + sum_c bconv[p*Cout+c] S[w][c]
+ *   db[p*Cout+c]      = sum_w colsum_p(A)[w] S[w][c]
+ * S = the per-joint row sums of dy [V][Cout] (stgcn_gconv_wgrad's rowsum); work as above (required);
+ * P <= 4, V <= 32.  Bit-identical to stgcn_gconv_wgrad_finish into zeros followed by stgcn_gcn_bias_bwd. */
+int stgcn_gconv_wgrad_finish_bias(const float* dweff, const float* A, const float* W, const int* nbr, const int* deg,
+                                  int P, int V, int J, int Cout, int Cin, const float* bconv, const float* S, float* dW,
+                                  float* dA, float* db, void* work, void* stream);
 int stgcn_gconv_wgrad_finish(const float* dweff, const float* A, const float* W, const int* nbr, const int* deg, int P,
                              int V, int J, int Cout, int Cin, float* dW, float* dA, void* work, void* stream);
 

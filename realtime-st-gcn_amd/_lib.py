@@ -104,6 +104,7 @@ _SIGS = {
     "stgcn_gconv_wgrad_workspace": (c_long, [ctypes.POINTER(GconvWgradDesc), c_int]),
     "stgcn_gconv_wgrad_finish_workspace": (ctypes.c_long, [c_int] * 5),
     "stgcn_gconv_wgrad_finish": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "stgcn_gconv_wgrad_finish_bias": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_void_p] * 7),
     "stgcn_amix_fwd": (c_int, [ctypes.POINTER(AmixDesc), c_int, c_void_p]),
     "stgcn_amix_trans": (c_int, [ctypes.POINTER(AmixDesc), c_int, c_void_p]),
     "stgcn_gcn_bias_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),

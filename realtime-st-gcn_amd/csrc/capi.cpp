@@ -43,6 +43,9 @@ int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s
 int gconv_wgrad_finish_launch(const float* dweff, const float* A, const float* W, const int* nbr, const int* deg,
                               int P, int V, int J, int Cout, int Cin, float* dW, float* dA, void* work, hipStream_t s);
 long gconv_wgrad_finish_workspace(int P, int V, int J, int Cout, int Cin);
+int gconv_wgrad_finish_bias_launch(const float* dweff, const float* A, const float* W, const int* nbr, const int* deg,
+                                   int P, int V, int J, int Cout, int Cin, const float* bconv, const float* S, float* dW,
+                                   float* dA, float* db, void* work, hipStream_t s);
 int amix_trans_launch(const AmixArgs& a, int dtype, hipStream_t s);
 int amix_dA_launch(const AmixArgs& a, const void* dw, float* dA, void* work, int dtype, hipStream_t s);
 long amix_dA_workspace(const AmixArgs& a);
@@ -245,6 +248,15 @@ int stgcn_gconv_wgrad(const stgcn_gconv_wgrad_desc* d, int dtype, void* stream) 
       d->Cin <= 0 || d->Cout <= 0)
     return STGCN_EBADSHAPE;
   return gconv_wgrad_launch(*d, dtype, STREAM(stream));
+}
+int stgcn_gconv_wgrad_finish_bias(const float* dweff, const float* A, const float* W, const int* nbr, const int* deg,
+                                  int P, int V, int J, int Cout, int Cin, const float* bconv, const float* S, float* dW,
+                                  float* dA, float* db, void* work, void* stream) {
+  if (!dweff || !A || !W || !nbr || !deg || !bconv || !S || !dW || !dA || !db || !work || P <= 0 || V <= 0 || J <= 0 ||
+      Cout <= 0 || Cin <= 0)
+    return STGCN_EBADSHAPE;
+  return gconv_wgrad_finish_bias_launch(dweff, A, W, nbr, deg, P, V, J, Cout, Cin, bconv, S, dW, dA, db, work,
+                                        STREAM(stream));
 }
 long stgcn_gconv_wgrad_finish_workspace(int P, int V, int J, int Cout, int Cin) {
   return gconv_wgrad_finish_workspace(P, V, J, Cout, Cin);

@@ -971,6 +971,27 @@ __global__ void rowpart_sum_kernel(const float* __restrict__ part, int R, long E
   out[e] = s;
 }
 
+// gslab_reduce (blocks [0, nb1)) and rowpart_sum (the rest) of one joint-grouped wgrad in one launch
+__global__ void gslab_rowpart_kernel(const float* __restrict__ slab, int R, long E, long EC, const int* deg, int J,
+                                     float* __restrict__ dweff, int nb1, const float* __restrict__ rpart, long ER,
+                                     float* __restrict__ rowsum) {
+  if ((int)blockIdx.x < nb1) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    const int pair = (int)(e / EC);
+    float s = 0.f;
+    if (pair % J < deg[pair / J])
+      for (int r = 0; r < R; ++r) s += slab[(long)r * E + e];
+    dweff[e] = s;
+    return;
+  }
+  const long e = (long)(blockIdx.x - nb1) * blockDim.x + threadIdx.x;
+  if (e >= ER) return;
+  float s = 0.f;
+  for (int r = 0; r < R; ++r) s += rpart[(long)r * ER + e];
+  rowsum[e] = s;
+}
+
 // slab reduction (rows of the slab are whole [V*J][Cout][Cin] images): dweff[e] = sum_r slab[r][e]
 __global__ void gslab_reduce_kernel(const float* __restrict__ slab, int R, long E, long EC, const int* deg, int J,
                                     float* __restrict__ out) {
@@ -1024,9 +1045,10 @@ constexpr int PMAX = 4;
 // staged in LDS first: the per-pair deg -> nbr -> A chain of dependent global loads was this kernel's
 // cost); fixed-order LDS combine.
 constexpr int DW_PAIRS = 32 * 8;  // V * J upper bound for the LDS tables
-__global__ __launch_bounds__(256) void gconv_dw_all_kernel(const float* __restrict__ dweff, const float* __restrict__ A,
-                                                           const int* nbr, const int* deg, int P, int V, int J, long E,
-                                                           float* dW) {
+// one block's work (block index bb of ceil(E / 64)); ``acc_out``: dW += (else dW =, the caller's buffer
+// needs no zero fill)
+DEV void gconv_dw_all_body(const float* __restrict__ dweff, const float* __restrict__ A, const int* nbr,
+                           const int* deg, int P, int V, int J, long E, float* dW, long bb, bool acc_out) {
   __shared__ int spair[DW_PAIRS];
   __shared__ float scoef[DW_PAIRS][PMAX];
   __shared__ int snp;
@@ -1045,7 +1067,7 @@ __global__ __launch_bounds__(256) void gconv_dw_all_kernel(const float* __restri
   }
   __syncthreads();
   const int g = threadIdx.x >> 6;
-  const long e = (long)blockIdx.x * 64 + (threadIdx.x & 63);
+  const long e = bb * 64 + (threadIdx.x & 63);
   float acc[PMAX] = {0.f, 0.f, 0.f, 0.f};
   if (e < E) {
 #pragma unroll 4
@@ -1063,18 +1085,25 @@ __global__ __launch_bounds__(256) void gconv_dw_all_kernel(const float* __restri
     const int l = threadIdx.x;
 #pragma unroll
     for (int p = 0; p < PMAX; ++p)
-      if (p < P) dW[(long)p * E + e] += ((part[0][p][l] + part[1][p][l]) + part[2][p][l]) + part[3][p][l];
+      if (p < P) {
+        const float t = ((part[0][p][l] + part[1][p][l]) + part[2][p][l]) + part[3][p][l];
+        dW[(long)p * E + e] = acc_out ? dW[(long)p * E + e] + t : t;
+      }
   }
+}
+__global__ __launch_bounds__(256) void gconv_dw_all_kernel(const float* __restrict__ dweff, const float* __restrict__ A,
+                                                           const int* nbr, const int* deg, int P, int V, int J, long E,
+                                                           float* dW) {
+  gconv_dw_all_body(dweff, A, nbr, deg, P, V, J, E, dW, blockIdx.x, true);
 }
 
 // dA[p][v][w] += <W_p, dWeff[pair]> for all p, in two deterministic steps: block (pair, chunk) writes the
 // P partial dots of its DA_CHUNK-element slice to part[pair][chunk][p]; gconv_dA_reduce sums the chunks in
 // order.  (pair, chunk) grid keeps >= ~1000 blocks in flight even for C = 64.
 constexpr int DA_CHUNK = 2048;
-__global__ __launch_bounds__(256) void gconv_dA_part_kernel(const float* __restrict__ dweff, const float* __restrict__ W,
-                                                            const int* deg, int P, int J, long E, float* part) {
-  const int pair = blockIdx.x, c = blockIdx.y, nch = gridDim.y;
-  if (pair % J >= deg[pair / J]) return;
+DEV void gconv_dA_part_body(const float* __restrict__ dweff, const float* __restrict__ W, const int* deg, int P, int J,
+                           long E, float* part, int pair, int c, int nch) {
+  if (pair % J >= deg[pair / J]) return;  // block-uniform, no barrier after it
   const float* d = dweff + (long)pair * E;
   float acc[PMAX] = {0.f, 0.f, 0.f, 0.f};
   const long e1 = min(E, (long)(c + 1) * DA_CHUNK);
@@ -1094,6 +1123,72 @@ __global__ __launch_bounds__(256) void gconv_dA_part_kernel(const float* __restr
   if (threadIdx.x < P)
     part[((long)pair * nch + c) * PMAX + threadIdx.x] =
         ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+}
+__global__ __launch_bounds__(256) void gconv_dA_part_kernel(const float* __restrict__ dweff, const float* __restrict__ W,
+                                                            const int* deg, int P, int J, long E, float* part) {
+  gconv_dA_part_body(dweff, W, deg, P, J, E, part, blockIdx.x, blockIdx.y, gridDim.y);
+}
+
+// The finish of the graph-conv weight / adjacency gradient with the conv bias pushed through A folded in, two
+// launches instead of four (stgcn_gconv_wgrad_finish_bias).  Launch 1: blocks [0, nb_dw) the dW pass
+// (overwriting), the rest the dA partial dots of (pair, chunk) = (b' / nch, b' % nch).
+__global__ __launch_bounds__(256) void gconv_finish1_kernel(const float* __restrict__ dweff, const float* __restrict__ A,
+                                                            const float* __restrict__ W, const int* nbr, const int* deg,
+                                                            int P, int V, int J, long E, float* dW, int nb_dw, int nch,
+                                                            float* part) {
+  const int b = blockIdx.x;
+  if (b < nb_dw) {
+    gconv_dw_all_body(dweff, A, nbr, deg, P, V, J, E, dW, b, false);
+  } else {
+    const int b2 = b - nb_dw;
+    gconv_dA_part_body(dweff, W, deg, P, J, E, part, b2 / nch, b2 % nch, nch);
+  }
+}
+
+// Launch 2: blocks [0, P*V): (p, w) — every dA[p][v][w] written once: the support entries' chunk sums
+// (fixed order) plus the bias term sum_c b[p][c] S[w][c] (v-independent; gcn_bias_bwd's value and order);
+// blocks [P*V, ...): db[p*C + c] = sum_w colsum_p(A)[w] S[w][c] (gcn_bias_bwd's).
+constexpr int FV_MAX = 32;
+__global__ __launch_bounds__(256) void gconv_finish2_kernel(const float* __restrict__ part, const float* __restrict__ A,
+                                                            const float* __restrict__ b, const float* __restrict__ S,
+                                                            const int* nbr, const int* deg, int P, int V, int J, int C,
+                                                            int nch, float* dA, float* db) {
+  const int bx = blockIdx.x;
+  if (bx < P * V) {
+    const int p = bx / V, w = bx % V;
+    float t = 0.f;
+    for (int c = threadIdx.x; c < C; c += 256) t += b[p * C + c] * S[w * C + c];
+    t = wave_sum(t);
+    __shared__ float red[4];
+    __shared__ float sup[FV_MAX];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+    if (threadIdx.x < V) sup[threadIdx.x] = 0.f;
+    __syncthreads();
+    const float tot = ((red[0] + red[1]) + red[2]) + red[3];
+    if (threadIdx.x < deg[w]) {  // the support entries of column w: chunk sums in order
+      const int j = threadIdx.x, pair = w * J + j;
+      float s = 0.f;
+      for (int c = 0; c < nch; ++c) s += part[((long)pair * nch + c) * PMAX + p];
+      sup[nbr[pair]] = s;
+    }
+    __syncthreads();
+    for (int v = threadIdx.x; v < V; v += 256) dA[(p * V + v) * V + w] = sup[v] + tot;
+    return;
+  }
+  __shared__ float cs[PMAX * FV_MAX];
+  for (int i = threadIdx.x; i < P * V; i += 256) {
+    const int p = i / V, w = i % V;
+    float t = 0.f;
+    for (int v = 0; v < V; ++v) t += A[(p * V + v) * V + w];
+    cs[i] = t;
+  }
+  __syncthreads();
+  const int i = (bx - P * V) * 256 + threadIdx.x;  // (p, c)
+  if (i >= P * C) return;
+  const int p = i / C, c = i % C;
+  float t = 0.f;
+  for (int w = 0; w < V; ++w) t += cs[p * V + w] * S[w * C + c];
+  db[i] = t;
 }
 
 __global__ void gconv_dA_reduce_kernel(const float* __restrict__ part, const int* nbr, const int* deg, int P, int V,
@@ -1228,12 +1323,15 @@ int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s
     if (stgcn_lds_attr((const void*)k, 160 * 1024, s)) return STGCN_EHIP;
     const long blocks = (long)a.V * g.nco * g.nci * g.R;
     hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(ring ? 256 : cob / 16 * 64), lds, s, a, g);
-    hipLaunchKernelGGL(gslab_reduce_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, (const float*)g.slab,
-                       g.R, E, (long)a.Cout * a.Cin, a.deg, a.J, a.dweff);
-    if (a.rowsum) {
+    if (a.rowsum) {  // slab reduction and row sums in one launch
       const long ER = (long)a.V * a.Cout;
-      hipLaunchKernelGGL(rowpart_sum_kernel, dim3((unsigned)((ER + 255) / 256)), dim3(256), 0, s,
-                         (const float*)g.rowpart, g.R, ER, a.rowsum);
+      const int nb1 = (int)((E + 255) / 256);
+      hipLaunchKernelGGL(gslab_rowpart_kernel, dim3((unsigned)(nb1 + (ER + 255) / 256)), dim3(256), 0, s,
+                         (const float*)g.slab, g.R, E, (long)a.Cout * a.Cin, a.deg, a.J, a.dweff, nb1,
+                         (const float*)g.rowpart, ER, a.rowsum);
+    } else {
+      hipLaunchKernelGGL(gslab_reduce_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, (const float*)g.slab,
+                         g.R, E, (long)a.Cout * a.Cin, a.deg, a.J, a.dweff);
     }
     return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
   }
@@ -1253,6 +1351,23 @@ int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s
 long gconv_wgrad_finish_workspace(int P, int V, int J, int Cout, int Cin) {
   const long E = (long)Cout * Cin;
   return P > PMAX ? 0 : (long)V * J * ((E + DA_CHUNK - 1) / DA_CHUNK) * PMAX * (long)sizeof(float);
+}
+
+bool gconv_finish_bias_ok(int P, int V, int J) { return P <= PMAX && V <= FV_MAX && V * J <= DW_PAIRS; }
+
+int gconv_wgrad_finish_bias_launch(const float* dweff, const float* A, const float* W, const int* nbr, const int* deg,
+                                   int P, int V, int J, int Cout, int Cin, const float* bconv, const float* S, float* dW,
+                                   float* dA, float* db, void* work, hipStream_t s) {
+  if (!gconv_finish_bias_ok(P, V, J) || !work) return STGCN_EBADSHAPE;
+  const long E = (long)Cout * Cin;
+  const int nch = (int)((E + DA_CHUNK - 1) / DA_CHUNK);
+  const int nb_dw = (int)((E + 63) / 64);
+  float* part = reinterpret_cast<float*>(work);
+  hipLaunchKernelGGL(gconv_finish1_kernel, dim3((unsigned)(nb_dw + V * J * nch)), dim3(256), 0, s, dweff, A, W, nbr,
+                     deg, P, V, J, E, dW, nb_dw, nch, part);
+  hipLaunchKernelGGL(gconv_finish2_kernel, dim3((unsigned)(P * V + (P * Cout + 255) / 256)), dim3(256), 0, s,
+                     (const float*)part, A, bconv, S, nbr, deg, P, V, J, Cout, nch, dA, db);
+  return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
 
 int gconv_wgrad_finish_launch(const float* dweff, const float* A, const float* W, const int* nbr, const int* deg,

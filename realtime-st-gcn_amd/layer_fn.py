@@ -464,16 +464,25 @@ class StgcnLayerFunction(torch.autograd.Function):
             wg2 = wg.detach().float().reshape(P * Cout, Cin).contiguous()
             with _fork(side):
                 fuse_s = A32.dim() == 3 and K.gconv_wgrad_rowsum_ok(sup, Cin, Cout, dtype)
+                dense_dA = ctx.cfg[6] and ctx.needs_input_grad[1]
                 dweff = K.gconv_wgrad(x, dg, sup, Cin, Cout, rowsum=z_S if fuse_s else None)
-                dwg2, dA = K.gconv_finish(dweff, A32, wg2, sup, Cout, Cin, dW=z_dwg, dA=z_dA)
+                if fuse_s and not dense_dA and K.gconv_finish_bias_ok(A32, sup):
+                    # dW, dA (support + bias through A) and db in two launches, outputs overwritten
+                    dwg2, dA, grads["bg"] = K.gconv_finish_bias(dweff, A32, wg2, sup, Cout, Cin,
+                                                                bg.detach().float().contiguous(), z_S)
+                    dA_done = True
+                else:
+                    dwg2, dA = K.gconv_finish(dweff, A32, wg2, sup, Cout, Cin, dW=z_dwg, dA=z_dA)
+                    dA_done = False
                 grads["wg"] = dwg2.view(P * Cout, Cin, 1, 1)
-                if ctx.cfg[6] and ctx.needs_input_grad[1]:
+                if dense_dA:
                     # caller-owned A: the reference's dA is dense (also off the graph's support), so take
                     # it from the A-first factorisation dA_p[v][w] = sum x[(i,v)] . (dg W_p)[(i,w)]
                     wgTd = wg.detach().float().view(P, Cout, Cin).permute(0, 2, 1).reshape(1, P * Cin, Cout)
                     wgTp, cq, kq = K.pack_weight(wgTd, dtype)
                     dA = K.amix_dA(x, K.conv_rows(dg, wgTp, Cout, P * Cin, cq, kq, T, T), A32)
-                dA = _bias_through_A(dA, A32, bg, bgp, dg, z_S if fuse_s else None, z_S, M1, Cout, V, grads)
+                if not dA_done:
+                    dA = _bias_through_A(dA, A32, bg, bgp, dg, z_S if fuse_s else None, z_S, M1, Cout, V, grads)
             if K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype, trans=True):  # dx = sum_p A_p-mix(dg) W_p^T, fused (gcn_tile.hip)
                 wdf = wg.detach().float().view(P, Cout, Cin).permute(2, 0, 1).reshape(Cin, P * Cout)
                 wimgT, cq, kwT = K.pack_gcn_weight(wdf, dtype)

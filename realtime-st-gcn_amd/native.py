@@ -607,6 +607,29 @@ def gconv_finish(dweff, A, W, sup, Cout, Cin, dW=None, dA=None):
     return dW, dA
 
 
+def gconv_finish_bias(dweff, A, W, sup, Cout, Cin, bconv, S):
+    """(dW [P*Cout][Cin], dA [P][V][V], db [P*Cout]) fp32, all overwritten (stgcn_gconv_wgrad_finish_bias): the
+    graph-conv weight / adjacency gradient from dWeff with the conv bias pushed through A (S = per-joint row sums
+    of dy [V][Cout]) in two launches; fresh outputs, no zero fill."""
+    A = _dense(A)
+    P, V = A.shape[0], A.shape[-1]
+    dev = A.device
+    out = torch.empty(P * Cout * Cin + P * V * V + P * Cout, dtype=torch.float32, device=dev)
+    dW = out[:P * Cout * Cin].view(P * Cout, Cin)
+    dA = out[P * Cout * Cin:P * Cout * Cin + P * V * V].view(P, V, V)
+    db = out[P * Cout * Cin + P * V * V:]
+    work = _workspace(L.lib().stgcn_gconv_wgrad_finish_workspace(P, V, sup.J, Cout, Cin), dev)
+    L.check(L.lib().stgcn_gconv_wgrad_finish_bias(dweff.data_ptr(), A.data_ptr(), W.data_ptr(), sup.nbr.data_ptr(),
+                                                  sup.deg.data_ptr(), P, V, sup.J, Cout, Cin, bconv.data_ptr(),
+                                                  S.data_ptr(), dW.data_ptr(), dA.data_ptr(), db.data_ptr(),
+                                                  work.data_ptr(), L.stream()), "gconv_finish_bias")
+    return dW, dA, db
+
+
+def gconv_finish_bias_ok(A, sup) -> bool:
+    return A.dim() == 3 and A.shape[0] <= 4 and A.shape[-1] <= 32 and A.shape[-1] * sup.J <= 256
+
+
 # ------------------------------------------------------------------------------------ BatchNorm
 def bn_stat_blocks(M: int) -> int:
     return L.lib().stgcn_bn_stat_blocks(M)

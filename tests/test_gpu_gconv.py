@@ -91,3 +91,29 @@ def test_gconv_weights_bias_one_launch(K, pkg, dtype, Cin, Cout):
         d = int(sup.deg[a])
         assert torch.equal(w_one[a, :d], w_ref[a, :d]), a
     assert torch.equal(b_one, b_ref.view(V, Cout))
+
+
+@pytest.mark.parametrize("Cin,Cout", [(64, 64), (64, 128), (256, 256)])
+def test_gconv_finish_bias_merged(K, pkg, Cin, Cout):
+    """stgcn_gconv_wgrad_finish_bias (dW, dA and the bias through A in two launches, outputs overwritten) is
+    bit-equal to stgcn_gconv_wgrad_finish into zeros followed by stgcn_gcn_bias_bwd, and stgcn_gconv_wgrad's
+    one-launch slab + row-sum reduction gives the per-joint row sums of dy."""
+    torch.manual_seed(6)
+    A0 = torch.tensor(pkg.Graph(**pkg.PKU_MMD).A, dtype=torch.float32)
+    A = (A0 * (torch.rand(A0.shape) + 0.5)).to(DEV).contiguous()
+    P, V = A.shape[0], A.shape[-1]
+    sup = K.GraphSupport(A)
+    N, T = 4, 40
+    x = torch.randn(N, Cin, T, V)
+    dy = torch.randn(N, Cout, T, V)
+    W = torch.randn(P * Cout, Cin, device=DEV) / Cin ** 0.5
+    b = torch.randn(P * Cout, device=DEV)
+    assert K.gconv_wgrad_rowsum_ok(sup, Cin, Cout, torch.bfloat16)
+    S = torch.empty((V, Cout), device=DEV)
+    dweff = K.gconv_wgrad(cl(x, torch.bfloat16), cl(dy, torch.bfloat16), sup, Cin, Cout, rowsum=S)
+    assert_close(S.cpu(), dy.to(torch.bfloat16).float().sum(dim=(0, 2)).t(), 1e-4, "row sums")
+    dW_ref, dA_ref = K.gconv_finish(dweff, A, W, sup, Cout, Cin)
+    db_ref = K.gcn_bias_bwd(A, b, S, dA_ref, Cout)
+    dW, dA, db = K.gconv_finish_bias(dweff, A, W, sup, Cout, Cin, b, S)
+    torch.cuda.synchronize()
+    assert torch.equal(dW, dW_ref) and torch.equal(dA, dA_ref) and torch.equal(db, db_ref)
