@@ -28,6 +28,16 @@
 #include <utility>
 #include "../../include/stgcn_amd.h"
 
+#ifndef GCONV_NSTG_N
+#define GCONV_NSTG_N 2
+#endif
+#ifndef GCONV_NSTG_M
+#define GCONV_NSTG_M 2
+#endif
+#ifndef GCONV_NSTG_W
+#define GCONV_NSTG_W 2
+#endif
+
 namespace {
 
 template <typename T, int KC>
@@ -1269,8 +1279,9 @@ int gconv_launch(const stgcn_gconv_desc& a, int dtype, hipStream_t s) {
     // 64->128 69.8 -> 67.2 / 58.2 -> 49.8; C=256 (256-row tiles) 95.7 -> 85.2 / 88.1 -> 75.2
     const bool dma = a.Cin % 64 == 0 && a.Cin == a.Cin_pad && a.in_ld % 8 == 0;
     if (dma) {
-      if (!wide) return launch_gconv<bf16, 4, 1, 1, 2, 64, 2>(a, s);
-      return a.Cin >= 256 ? launch_gconv<bf16, 4, 2, 2, 2, 64, 2>(a, s) : launch_gconv<bf16, 4, 2, 1, 2, 64, 2>(a, s);
+      if (!wide) return launch_gconv<bf16, 4, 1, 1, 2, 64, GCONV_NSTG_N>(a, s);
+      return a.Cin >= 256 ? launch_gconv<bf16, 4, 2, 2, 2, 64, GCONV_NSTG_W>(a, s)
+                          : launch_gconv<bf16, 4, 2, 1, 2, 64, GCONV_NSTG_M>(a, s);
     }
     const bool k64 = a.Cin >= 128 && a.Cin_pad % 64 == 0;
     if (wide) return k64 ? launch_gconv<bf16, 4, 2, 1, 2, 64>(a, s) : launch_gconv<bf16, 4, 2, 2, 2, 32>(a, s);

@@ -45,11 +45,21 @@
 namespace {
 
 // Timing ablations (results wrong): build with -DSTGCN_FUSED_DBG=<mask> (tools only, never the shipped library):
-// bit 0 skip the GCN math, bit 1 the TCN math, bit 2 (LN) the residual loads, bit 3 (LN) the LN2 statistics
+// bit 0 skip the GCN math, bit 1 the TCN math, bit 2 (LN) the residual loads, bit 3 (LN) the LN2 statistics,
+// bit 4 the TCN z / BN2-partial stores, bit 5 the TCN weight-fragment loads, bit 6 the TCN h-fragment LDS reads,
+// bit 7 three of the four z stores per row tile, bit 8 the BN2-partial stores
 #ifndef STGCN_FUSED_DBG
 #define STGCN_FUSED_DBG 0
 #endif
 constexpr int DBG = STGCN_FUSED_DBG;
+// bit 10: per-wave cycle accounts (s_memtime) into g_fused_prof, read back with stgcn_fused_prof (tools only)
+constexpr bool PROF = (DBG & 1024) != 0;
+constexpr int PROF_BLOCKS = 4096;
+__device__ long long g_fused_prof[PROF ? PROF_BLOCKS * 8 * 6 : 1];
+DEV long long ptime() {
+  if constexpr (PROF) return __builtin_amdgcn_s_memtime();
+  return 0;
+}
 
 constexpr int NWT = 4, NWG = 4, NW = NWT + NWG;
 constexpr int C = 64, G = C / 32;      // channels (in = out), 32-channel blocks
@@ -59,10 +69,15 @@ constexpr int RF = 24;                 // h ring frames (16 read + 8 written per
 constexpr int FPW = CF / NWG;          // h frames per GCN wave per step (2)
 constexpr int PRO = 2 * HALO + CF;     // h frames before the first step (16)
 constexpr int RSH = 2 * C + 16;        // h row bytes (144: conflict-free ds_read_b128 for any row offset)
+// per-joint LDS tables read by 32 lanes of 32 different joints at once: row strides padded off the 256-B
+// bank period (16 B further per joint), or every lane of a ds_read_b128 group hits the same four banks
+constexpr int CBP = C + 4;             // BN: bias2d * scale + shift row, floats
+constexpr int CG2 = C + 2;             // LN: (gamma2, beta2) row, float2
+constexpr int ZSB = 32 * 16;  // BN: per temporal-conv wave, 32 float4 BN2 partials
 constexpr int PANEL = 32 * 64;         // [32 joint rows][32 ch] bf16
 constexpr int SLOTS = FPW * G;         // panel slots per GCN wave (one step's panels)
 constexpr int RT = 4;                  // 32-row output tiles per TCN wave (8 frames x 25 joints = 7 tiles)
-constexpr int NB = 12;                 // temporal-conv weight fragment ring depth
+constexpr int NB = 9;                  // temporal-conv weight fragment ring depth (divides KSTEPS)
 constexpr int KSTEPS = KT * C / 16;    // 36 k-steps of the temporal conv
 constexpr int VMAX = 25;
 constexpr int TARGET_BLOCKS = 256;     // MI355X CUs: runs per sample = 256 / N (fixed: the host sizes stats by it)
@@ -76,6 +91,7 @@ DEV void static_for(F&& f) {
 }
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2n __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 // A operand of a 32x32x16 MFMA (m = channel, k = joint row) from a [row][32 ch] panel (gcn_tile.hip)
@@ -133,8 +149,8 @@ DEV unsigned lds_u32(const void* p) { return (unsigned)(size_t)(const __attribut
 struct FGeom {
   int runs_n;  // runs per sample
   int run;     // frames per run (multiple of CF)
-  int nsm;     // steps per run (run / CF): BN2 partial rows per block = 2 * nsm (one per step and row half)
-  int off_tab, off_ring, off_h, off_red;  // LDS offsets
+  int nsm;     // steps per run (run / CF)
+  int off_tab, off_ring, off_h, off_red, off_zs;  // LDS offsets
 };
 
 template <int P, bool LN>
@@ -154,13 +170,14 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
 
   char* const sW = smem;                                          // [2][K16] 1-KiB W' fragment blocks
   float* const sSc = reinterpret_cast<float*>(smem + g.off_tab);  // [64] BN1 scale
-  float* const sBp = sSc + C;                                     // [V][64] bias2d * scale + shift
+  float* const sBp = sSc + C;                                     // [V][CBP] bias2d * scale + shift
   char* const sH = smem + g.off_h;                                // [RF * V][RSH]
   float2* const sRed = reinterpret_cast<float2*>(smem + g.off_red);  // BN: [2][64] (sum, sum of squares);
   // LN: [row tile][frame slot k < 3][channel half] (sum, sum of squares) of the step's output rows
-  float2* const sG2 = reinterpret_cast<float2*>(smem + g.off_tab);     // LN: [V][64] (gamma2, beta2)
+  float2* const sG2 = reinterpret_cast<float2*>(smem + g.off_tab);     // LN: [V][CG2] (gamma2, beta2)
   unsigned* const sCnt = reinterpret_cast<unsigned*>(smem + g.off_red + 2 * RT * 3 * 2 * 8);  // LN arrivals
   const int vrs = V * RSH;  // bytes per h frame
+  float* const sTb = reinterpret_cast<float*>(smem + g.off_tab + (LN ? V * CG2 * 8 : (C + V * CBP) * 4));  // [64] tcn bias
 
   // ---- per block: W' slice, BN1 tables, zeroed panel rings (rows V..31 stay zero)
   {
@@ -168,21 +185,29 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
     uint4* wdst = reinterpret_cast<uint4*>(sW);
     for (int e = tid; e < 2 * K16 * 64; e += NW * 64) wdst[e] = wsrc[e];
     if (LN) {
-      for (int e = tid; e < V * C; e += NW * 64) sG2[e] = make_float2(a.ln2_g[e], a.ln2_b[e]);
+      for (int e = tid; e < V * C; e += NW * 64) sG2[(e / C) * CG2 + e % C] = make_float2(a.ln2_g[e], a.ln2_b[e]);
       if (tid == 0) *sCnt = 0u;
     } else {
       for (int c = tid; c < C; c += NW * 64) sSc[c] = a.n1_scale[c];
       for (int e = tid; e < V * C; e += NW * 64) {
         const int c = e % C;
         const float b = a.gbias ? a.gbias[e] : 0.f;
-        sBp[e] = fmaf(b, a.n1_scale[c], a.n1_shift[c]);
+        sBp[(e / C) * CBP + c] = fmaf(b, a.n1_scale[c], a.n1_shift[c]);
       }
     }
+    for (int c = tid; c < C; c += NW * 64) sTb[c] = a.tbias ? a.tbias[c] : 0.f;
     uint4* z = reinterpret_cast<uint4*>(smem + g.off_ring);
     for (int e = tid; e < NWG * SLOTS * PANEL / 16; e += NW * 64) z[e] = make_uint4(0, 0, 0, 0);
   }
   __syncthreads();
 
+  long long pa[6] = {0, 0, 0, 0, 0, 0};  // PROF: cycle accounts of this wave
+  const long long pstart = ptime();
+  auto prof_out = [&]() {
+    pa[3] = ptime() - pstart;
+    if (lane == 0 && blockIdx.x < PROF_BLOCKS)
+      for (int j = 0; j < 6; ++j) g_fused_prof[((long)blockIdx.x * 8 + wave) * 6 + j] = pa[j];
+  };
   if (wave >= NWT) {
     // =============================== GCN waves: h frames ===============================
     const int gw = wave - NWT;
@@ -236,7 +261,10 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
     };
     // compute the FPW frames whose panels sit in the ring; `next` >= 0: DMA that batch once the panels are read
     auto compute = [&](int fa0, int next) {
+      const long long pt0 = ptime();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const long long pt1 = ptime();
+      pa[0] += pt1 - pt0;
       bf16x8 fx[FPW][G][2];
 #pragma unroll
       for (int i = 0; i < FPW; ++i)
@@ -248,6 +276,43 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
         }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ring read: refill it with the next batch
       if (next >= 0) issue(next);
+      // the FPW frames' chains interleaved per (channel block, partition): mix (stage 1) of every frame, then
+      // bf16 + 1x1 conv (stage 2) of every frame, so one frame's MFMA latency hides under the other's MFMAs
+      // (padding frames are computed too and replaced by zeros below)
+      f32x16 accf[FPW][2];
+#pragma unroll
+      for (int i = 0; i < FPW; ++i) accf[i][0] = accf[i][1] = zero;
+      if (fa0 < nfr) {
+#pragma unroll
+        for (int cb = 0; cb < G; ++cb)
+#pragma unroll
+          for (int p = 0; p < P; ++p) {
+            f32x16 c1[FPW];
+#pragma unroll
+            for (int i = 0; i < FPW; ++i) {
+              c1[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fx[i][cb][0], ac[p][0], zero, 0, 0, 0);
+              c1[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fx[i][cb][1], ac[p][1], c1[i], 0, 0, 0);
+            }
+            bf16x8 wf[2][2];
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+              for (int t = 0; t < 2; ++t)
+                wf[s][t] = __builtin_bit_cast(
+                    bf16x8, *reinterpret_cast<const uint4*>(wl + (t * K16 + (p * G + cb) * 2 + s) * 1024));
+#pragma unroll
+            for (int i = 0; i < FPW; ++i)
+#pragma unroll
+              for (int s = 0; s < 2; ++s) {
+                bf16x8 xb;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) xb[j] = (bf16)c1[i][8 * s + j];
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+                  accf[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[s][t], xb, accf[i][t], 0, 0, 0);
+              }
+          }
+      }
 #pragma unroll
       for (int i = 0; i < FPW; ++i) {
         const int fa = fa0 + NWG * i;
@@ -258,34 +323,7 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
             *reinterpret_cast<uint4*>(hrow + (e >> 3) * RSH + (e & 7) * 16) = make_uint4(0, 0, 0, 0);
           continue;
         }
-        f32x16 acc[2];
-        acc[0] = zero;
-        acc[1] = zero;
-        // per (channel block, partition): mix (stage 1) -> bf16 -> 1x1 conv (stage 2); one mix accumulator
-        // live at a time (register budget of two waves per SIMD; the TCN wave fills the dependency gaps)
-#pragma unroll
-        for (int cb = 0; cb < G; ++cb)
-#pragma unroll
-          for (int p = 0; p < P; ++p) {
-            f32x16 c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fx[i][cb][0], ac[p][0], zero, 0, 0, 0);
-            c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fx[i][cb][1], ac[p][1], c1, 0, 0, 0);
-            bf16x8 wf[2][2];
-#pragma unroll
-            for (int s = 0; s < 2; ++s)
-#pragma unroll
-              for (int t = 0; t < 2; ++t)
-                wf[s][t] = __builtin_bit_cast(
-                    bf16x8, *reinterpret_cast<const uint4*>(wl + (t * K16 + (p * G + cb) * 2 + s) * 1024));
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-              bf16x8 xb;
-#pragma unroll
-              for (int j = 0; j < 8; ++j) xb[j] = (bf16)c1[8 * s + j];
-#pragma unroll
-              for (int t = 0; t < 2; ++t)
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[s][t], xb, acc[t], 0, 0, 0);
-            }
-          }
+        f32x16 (&acc)[2] = accf[i];
         // epilogue: lane = joint lr, acc[t][r] = g^T[co = 32t + 8(r>>2) + 4lh + (r&3)][lr]
         if constexpr (LN) {
           // g = acc + gbias; the frame's LayerNorm statistics over its 64 x V values (lanes lr < V)
@@ -337,7 +375,7 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
           }
         } else if (lr < V) {
           char* hr = hrow + lr * RSH;
-          const float* bp = sBp + lr * C;
+          const float* bp = sBp + lr * CBP;
 #pragma unroll
           for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -354,6 +392,7 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
             }
         }
       }
+      pa[1] += ptime() - pt1;
     };
     // prologue: frames 0..15 in two batches of 8 (base 0 and 8); then step s produces base 8s + 8
     issue(gw);
@@ -363,8 +402,11 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
     for (int s = 1; s <= nsteps; ++s) {
       // step s: the TCN waves read frames [8s-8, 8s+8); this wave writes frames base = 8s + 8 ..
       if (s < nsteps && !(DBG & 1)) compute(CF * (s + 1) + gw, s + 1 < nsteps ? CF * (s + 2) + gw : -1);
+      const long long pb = ptime();
       lds_barrier();  // S_s
+      pa[2] += ptime() - pb;
     }
+    if constexpr (PROF) prof_out();
     return;
   }
 
@@ -384,12 +426,16 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
     jw_[i] = rr - fo_[i] * V;
     hw_[i] = jw_[i] * RSH + lh * 16;
   }
-  const bf16* wlane = wt + ct * 4 * 512 + lane * 8;  // 1-KiB block [dt][ct][ks] of the [9][2][4] image
-  const bf16* wcur = wlane;  // re-materialised per step (opaque): LICM would otherwise hoist all 36 weight
-                              // fragments of the step out of the step loop and spill them
+  const int wlane = ct * 4 * 512 + lane * 8;  // 1-KiB block [dt][ct][ks] of the [9][2][4] image
+  int wcur = wlane;  // element offset re-materialised per step (opaque): LICM would otherwise hoist all 36
+                     // weight fragments of the step out of the step loop and spill them.  An integer, not the
+                     // pointer: a pointer laundered through asm loses its address space, and the loads become
+                     // flat loads that also count on lgkmcnt (every LDS wait then drained the weight ring)
   auto load_w = [&](int s) {
     const int dt = s >> 2, ks = s & 3;
-    return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(wcur + (dt * 8 + ks) * 512));
+    int o = wcur + dt * 8 * 512;  // per-load opaque tap base (ks offsets fit the instruction's immediate)
+    asm volatile("" : "+v"(o));
+    return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(wt + o + ks * 512));
   };
   // row tiles of this wave: CF*V rows = nrt tiles of 32, the first RT to row half 0
   const int nrt = (CF * V + 31) / 32;
@@ -398,15 +444,24 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
   bf16x8 fw[NB];  // k-step k's fragment in slot k % NB, the same every step
 #pragma unroll
   for (int k = 0; k < NB - 1; ++k) fw[k] = load_w(k);
-  // BN2 partials: per step and row half, the (count, mean, M2) of the step's rows of each channel go straight
-  // to global memory (row (block * nsm + step) * 2 + rh of stats); fire-and-forget stores, no LDS
-  // read-modify-write chain and no end-of-run hand-off
-  float4* const st_out = a.stats ? reinterpret_cast<float4*>(a.stats) + ((long)blockIdx.x * g.nsm * 2 + rh) * C : nullptr;
+  if (DBG & 32) fw[NB - 1] = load_w(NB - 1);
+  // BN2 partials: per row half, the (count, mean, M2) of the run's rows of each channel (row block * 2 + rh of
+  // stats): per-lane sums over the whole run in registers, reduced across the lanes once at the run's end (a
+  // per-step reduction measured 28.6 K of the role's 147 K cycles)
+  float4* const st_out = a.stats ? reinterpret_cast<float4*>(a.stats) + ((long)blockIdx.x * 2 + rh) * C : nullptr;
   const f32x16 zero = {};
   unsigned arrivals = 0;  // LN: TCN-wave arrivals expected at the counter so far
+  // LN: statistics shifted by the pivot mean_c(bias) (the same constant in every wave), so a large common
+  // bias does not cancel catastrophically in sum(z^2) - sum(z) * mean
+  const float piv = LN ? wave_total(sTb[lane]) * (1.f / C) : 0.f;
+  char* const zs = smem + g.off_zs + wave * ZSB;  // BN: this wave's partials scratch
   lds_barrier();  // S_0
   // the step loop per row-tile count (compile-time: no per-k-step branches in the MFMA stream)
   auto tcn_run = [&]<int RTN>() {
+    float s1[16], s2[16];  // BN: per-lane (sum, sum of squares) of z - bias over the run's rows
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s1[r] = s2[r] = 0.f;
+    int cnt_run = 0;
     for (int s = 1; s <= nsteps; ++s) {
       if (DBG & 2) {
         lds_barrier();
@@ -437,11 +492,13 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
         if (i < RTN) {
           fb[0][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sH + ad[i]));
           fb[1][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sH + ad[i] + 32));
+          if (DBG & 64) fb[2][i] = fb[0][i];
         }
       }
+      const long long pk0 = ptime();
       static_for<KSTEPS>([&]<int k>() {
-        fw[(k + NB - 1) % NB] = load_w((k + NB - 1) % KSTEPS);  // runs into the next step's first k-steps
-        if constexpr (k + 2 < KSTEPS) {
+        if constexpr (!(DBG & 32)) fw[(k + NB - 1) % NB] = load_w((k + NB - 1) % KSTEPS);  // runs into the next step's first k-steps
+        if constexpr (k + 2 < KSTEPS && !(DBG & 64)) {
           constexpr int dt2 = (k + 2) >> 2, ks2 = (k + 2) & 3;
           if constexpr (ks2 == 0) {
 #pragma unroll
@@ -460,21 +517,23 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
           if (i < RTN) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[k % NB], fb[k % 3][i], acc[i], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
       });
+      const long long pk1 = ptime();
+      pa[0] += pk1 - pk0;
       // epilogue: acc[i][r] = out^T[co = 32ct + 8(r>>2) + 4lh + (r&3)][row (rh*RT + i)*32 + lr]
       const int vrows = min(CF, R1 - f0) * V;
       bf16* zt = zg + ((long)n * T + f0) * V * a.z_ld;
-      float tb[16], s1[16], s2[16];
+      // the temporal-conv bias from LDS: a global load here would sit behind the weight-fragment prefetch and,
+      // on gfx9's single in-order vmcnt, behind the z stores of the row tiles before it (each tile's stores
+      // were waited out by the next: measured 60 of the 84 us of the temporal-conv role)
+      float tb[16];
 #pragma unroll
       for (int q4 = 0; q4 < 4; ++q4) {
-        const int co = 32 * ct + 8 * q4 + 4 * lh;
-        const float4 b4 = a.tbias ? *reinterpret_cast<const float4*>(a.tbias + co) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 b4 = *reinterpret_cast<const float4*>(sTb + 32 * ct + 8 * q4 + 4 * lh);
         tb[4 * q4] = b4.x;
         tb[4 * q4 + 1] = b4.y;
         tb[4 * q4 + 2] = b4.z;
         tb[4 * q4 + 3] = b4.w;
       }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) s1[r] = s2[r] = 0.f;
       if constexpr (LN) {
         // the residual rows first: their L2 latency runs under the statistics phase
         const bf16* xres = reinterpret_cast<const bf16*>(a.x) + ((long)n * T + f0) * V * a.x_ld;
@@ -490,10 +549,8 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
           }
         }
         // z = acc + bias; per row tile ti and each of the <= 3 frames its 32 rows touch (V > 16): the
-        // (sum, sum of squares) of this wave's 32 channels over the tile's rows of that frame -> LDS.
-        // Shifted by the pivot mean_c(bias) (the same constant in every wave), so a large common bias does
-        // not cancel catastrophically in sum(z^2) - sum(z) * mean
-        const float piv = a.tbias ? wave_total(a.tbias[lane]) * (1.f / C) : 0.f;
+        // (sum, sum of squares) of this wave's 32 channels over the tile's rows of that frame -> LDS,
+        // shifted by the pivot
 #pragma unroll
         for (int i = 0; i < RT; ++i) {
           if (i >= RTN) break;
@@ -545,8 +602,8 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
 #pragma unroll
           for (int q4 = 0; q4 < 4; ++q4) {
             const int co = 32 * ct + 8 * q4 + 4 * lh;
-            const float4 gb0 = *reinterpret_cast<const float4*>(sG2 + w * C + co);
-            const float4 gb1 = *reinterpret_cast<const float4*>(sG2 + w * C + co + 2);
+            const float4 gb0 = *reinterpret_cast<const float4*>(sG2 + w * CG2 + co);
+            const float4 gb1 = *reinterpret_cast<const float4*>(sG2 + w * CG2 + co + 2);
             const float4 g4 = make_float4(gb0.x, gb0.z, gb1.x, gb1.z), b4 = make_float4(gb0.y, gb0.w, gb1.y, gb1.w);
             float rv[4];
 #pragma unroll
@@ -559,9 +616,14 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
             *reinterpret_cast<bf16x4*>(zt + (long)r * a.z_ld + co) = o;
           }
         }
+        const long long pl2 = ptime();
+        pa[4] += pl2 - pk1;
         lds_barrier();  // S_s
+        pa[2] += ptime() - pl2;
         continue;
       }
+      // z = acc + bias (8-B stores of 4 channels per lane and row: routing them through LDS into 64-B row runs
+      // measured slower, 90 vs 84.5 us)
 #pragma unroll
       for (int i = 0; i < RT; ++i) {
         const int r = (rh * RT + i) * 32 + lr;
@@ -576,30 +638,44 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
               s2[4 * q4 + e] = fmaf(v, v, s2[4 * q4 + e]);
               o[e] = (bf16)(v + tb[4 * q4 + e]);
             }
-            *reinterpret_cast<bf16x4*>(zt + (long)r * a.z_ld + 32 * ct + 8 * q4 + 4 * lh) = o;
+            bf16* const zp = zt + (long)r * a.z_ld + 32 * ct + 8 * q4 + 4 * lh;
+            if (DBG & 16) {
+            } else if (DBG & 512) {
+              __builtin_nontemporal_store(__builtin_bit_cast(u32x2n, o), reinterpret_cast<u32x2n*>(zp));
+            } else {
+              *reinterpret_cast<bf16x4*>(zp) = o;
+            }
           }
         }
       }
-      if (st_out) {  // the step's sums over this wave's rows (lanes) -> (count, mean, M2) partials
+      const long long pk15 = ptime();
+      pa[4] += pk15 - pk1;
+      cnt_run += max(0, min(vrows - rh * RT * 32, RTN * 32));
+      const long long pk2 = ptime();
+      pa[1] += pk2 - pk15;
+      lds_barrier();  // S_s: the GCN waves may overwrite the frames this step read
+      pa[2] += ptime() - pk2;
+    }
+    if (st_out && !(DBG & (16 | 256))) {  // the run's sums over this wave's rows (lanes) -> (count, mean, M2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s1[r] = half_sum(s1[r]);
+        s2[r] = half_sum(s2[r]);
+      }
+      // the 32 channels' partials gathered in LDS by the two lanes holding them, then one 512-B store
+      float4* const ss = reinterpret_cast<float4*>(zs);
+      if (lr == 31) {
+        const float inv = cnt_run ? 1.f / (float)cnt_run : 0.f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          s1[r] = half_sum(s1[r]);
-          s2[r] = half_sum(s2[r]);
-        }
-        if (lr == 31) {
-          const int cnt = max(0, min(vrows - rh * RT * 32, RTN * 32));
-          const float inv = cnt ? 1.f / (float)cnt : 0.f;
-          float4* o = st_out + (long)(s - 1) * 2 * C;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float mu = s1[r] * inv;  // mean of z - bias over the step's rows (bias added back below)
-            o[32 * ct + 8 * (r >> 2) + 4 * lh + (r & 3)] =
-                cnt ? make_float4((float)cnt, tb[r] + mu, fmaxf(s2[r] - s1[r] * mu, 0.f), 0.f)
-                    : make_float4(0.f, 0.f, 0.f, 0.f);
-          }
+          const float mu = s1[r] * inv;  // mean of z - bias over the run's rows (bias added back below)
+          ss[8 * (r >> 2) + 4 * lh + (r & 3)] =
+              cnt_run ? make_float4((float)cnt_run, sTb[32 * ct + 8 * (r >> 2) + 4 * lh + (r & 3)] + mu,
+                                    fmaxf(s2[r] - s1[r] * mu, 0.f), 0.f)
+                      : make_float4(0.f, 0.f, 0.f, 0.f);
         }
       }
-      lds_barrier();  // S_s: the GCN waves may overwrite the frames this step read
+      if (lane < 32) st_out[32 * ct + lane] = ss[lane];
     }
   };
   if (rtn >= 4)
@@ -610,11 +686,7 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
     tcn_run.template operator()<2>();
   else
     tcn_run.template operator()<1>();
-  if (st_out && lr == 31)  // steps past this run's end (the last run of a sample): empty partials
-    for (int s = nsteps + 1; s <= g.nsm; ++s)
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        st_out[(long)(s - 1) * 2 * C + 32 * ct + 8 * (r >> 2) + 4 * lh + (r & 3)] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (PROF) prof_out();
 }
 
 FGeom plan(int N, int T) {
@@ -630,10 +702,18 @@ FGeom plan(int N, int T) {
 
 }  // namespace
 
+// PROF builds: copy the per-wave cycle accounts [block][8 waves][6] (long long; GCN: DMA wait, compute, barrier,
+// total; TCN: k-loop, BN2 partials, barrier, total, z stores) to host memory; -1 in the shipped library
+extern "C" int stgcn_fused_prof(void* dst, long n) {
+  if (!PROF) return -1;
+  if (n > (long)PROF_BLOCKS * 8 * 6) n = (long)PROF_BLOCKS * 8 * 6;
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_fused_prof), n * sizeof(long long), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+
 long layer_fused_row_blocks(int N, int T) {
   if (N < 1 || T < 1) return 1;
   const FGeom g = plan(N, T);
-  return (long)N * g.runs_n * g.nsm * 2;
+  return (long)N * g.runs_n * 2;  // one BN2 partial row per block and row half
 }
 
 int layer_fused_launch(const stgcn_layer_fused_desc& a, hipStream_t s) {
@@ -647,10 +727,11 @@ int layer_fused_launch(const stgcn_layer_fused_desc& a, hipStream_t s) {
   if (nblk > 0x7fffffffL) return STGCN_EBADSHAPE;
   const int K16 = a.P * G * 2;
   g.off_tab = 2 * K16 * 1024;
-  g.off_ring = g.off_tab + ((a.ln ? a.V * C * 8 : (C + a.V * C) * 4) + 255) / 256 * 256;
+  g.off_ring = g.off_tab + ((a.ln ? a.V * CG2 * 8 : (C + a.V * CBP) * 4) + C * 4 + 255) / 256 * 256;
   g.off_h = g.off_ring + NWG * SLOTS * PANEL;
   g.off_red = g.off_h + (RF * a.V * RSH + 255) / 256 * 256;
-  const size_t lds = (size_t)g.off_red + (a.ln ? 2 * RT * 3 * 2 * 8 + 16 : 2 * C * 8);
+  g.off_zs = g.off_red + 2 * C * 8;
+  const size_t lds = (size_t)g.off_red + (a.ln ? 2 * RT * 3 * 2 * 8 + 16 : 2 * C * 8 + NWT * ZSB);
   if (lds > (size_t)LDS_MAX) return STGCN_EBADSHAPE;
   typedef void (*KFn)(const stgcn_layer_fused_desc, const FGeom);
   static const KFn tab[2][3] = {{layer_fused_kernel<1, false>, layer_fused_kernel<2, false>, layer_fused_kernel<3, false>},
