@@ -275,13 +275,35 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
           fx[i][cb][1] = trfrag(pan, 16, lane);
         }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ring read: refill it with the next batch
-      if (next >= 0) issue(next);
+      // LN: the DMA goes out after the epilogue instead, whose parameter loads (global) would otherwise wait
+      // behind it on the in-order vmcnt
+      if (!LN && next >= 0) issue(next);
       // the FPW frames' chains interleaved per (channel block, partition): mix (stage 1) of every frame, then
       // bf16 + 1x1 conv (stage 2) of every frame, so one frame's MFMA latency hides under the other's MFMAs
       // (padding frames are computed too and replaced by zeros below)
       f32x16 accf[FPW][2];
 #pragma unroll
       for (int i = 0; i < FPW; ++i) accf[i][0] = accf[i][1] = zero;
+      if constexpr (LN) {
+        // LN: the graph-conv bias enters as the accumulators' initial value (acc layout: lane = joint lr,
+        // register r of tile t = channel 32t + 8(r>>2) + 4lh + (r&3)), loaded before the MFMAs run
+        if (a.gbias) {
+          const int lc = min(lr, V - 1);
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+              const float4 b4 = *reinterpret_cast<const float4*>(a.gbias + lc * C + 32 * t + 8 * q4 + 4 * lh);
+#pragma unroll
+              for (int i = 0; i < FPW; ++i) {
+                accf[i][t][4 * q4 + 0] = b4.x;
+                accf[i][t][4 * q4 + 1] = b4.y;
+                accf[i][t][4 * q4 + 2] = b4.z;
+                accf[i][t][4 * q4 + 3] = b4.w;
+              }
+            }
+        }
+      }
       if (fa0 < nfr) {
 #pragma unroll
         for (int cb = 0; cb < G; ++cb)
@@ -313,85 +335,114 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
               }
           }
       }
+      if constexpr (LN) {
+        // the frames' LayerNorm statistics over their 64 x V values (lanes lr < V), both frames' wave reductions
+        // interleaved; gamma1 / beta1 of this lane's joint and channels loaded once for both frames
+        const int lc = min(lr, V - 1);
+        const bool jv = lr < V;
+        float4 g4[2][4], b4[2][4];
 #pragma unroll
-      for (int i = 0; i < FPW; ++i) {
-        const int fa = fa0 + NWG * i;
-        if (fa >= nfr) continue;
-        char* hrow = sH + (fa % RF) * vrs;
-        if (!frame_ok(fa)) {  // padding frame: h = 0
-          for (int e = lane; e < V * 8; e += 64)
-            *reinterpret_cast<uint4*>(hrow + (e >> 3) * RSH + (e & 7) * 16) = make_uint4(0, 0, 0, 0);
-          continue;
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4) {
+            const int co = 32 * t + 8 * q4 + 4 * lh;
+            g4[t][q4] = *reinterpret_cast<const float4*>(a.ln1_g + lc * C + co);
+            b4[t][q4] = *reinterpret_cast<const float4*>(a.ln1_b + lc * C + co);
+          }
+        const float cnt = (float)(V * C);
+        float mean[FPW], rstd[FPW];
+        {
+          float sum[FPW];
+#pragma unroll
+          for (int i = 0; i < FPW; ++i) {
+            sum[i] = 0.f;
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) sum[i] += accf[i][t][r];
+            sum[i] = jv ? sum[i] : 0.f;
+          }
+#pragma unroll
+          for (int i = 0; i < FPW; ++i) mean[i] = wave_total(sum[i]) / cnt;
+          float sq[FPW];
+#pragma unroll
+          for (int i = 0; i < FPW; ++i) {
+            sq[i] = 0.f;
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) {
+                const float d = accf[i][t][r] - mean[i];
+                sq[i] = fmaf(d, d, sq[i]);
+              }
+            sq[i] = jv ? sq[i] : 0.f;
+          }
+#pragma unroll
+          for (int i = 0; i < FPW; ++i) rstd[i] = 1.f / sqrtf(wave_total(sq[i]) / (cnt - 1.f) + 1e-5f);
         }
-        f32x16 (&acc)[2] = accf[i];
-        // epilogue: lane = joint lr, acc[t][r] = g^T[co = 32t + 8(r>>2) + 4lh + (r&3)][lr]
-        if constexpr (LN) {
-          // g = acc + gbias; the frame's LayerNorm statistics over its 64 x V values (lanes lr < V)
-          const int lc = min(lr, V - 1);
-          const bool jv = lr < V;
-          float sum = 0.f;
 #pragma unroll
-          for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int q4 = 0; q4 < 4; ++q4) {
-              const int co = 32 * t + 8 * q4 + 4 * lh;
-              const float4 b4 = a.gbias ? *reinterpret_cast<const float4*>(a.gbias + lc * C + co)
-                                        : make_float4(0.f, 0.f, 0.f, 0.f);
-              acc[t][4 * q4 + 0] += b4.x;
-              acc[t][4 * q4 + 1] += b4.y;
-              acc[t][4 * q4 + 2] += b4.z;
-              acc[t][4 * q4 + 3] += b4.w;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) sum += jv ? acc[t][4 * q4 + e] : 0.f;
-            }
-          const float cnt = (float)(V * C);
-          const float mean = wave_total(sum) / cnt;
-          float sq = 0.f;
-#pragma unroll
-          for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const float d = acc[t][r] - mean;
-              sq = fmaf(d, d, sq);
-            }
-          sq = jv ? sq : 0.f;
-          const float rstd = 1.f / sqrtf(wave_total(sq) / (cnt - 1.f) + 1e-5f);
+        for (int i = 0; i < FPW; ++i) {
+          const int fa = fa0 + NWG * i;
+          if (fa >= nfr) continue;
+          char* hrow = sH + (fa % RF) * vrs;
+          if (!frame_ok(fa)) {  // padding frame: h = 0
+            for (int e = lane; e < V * 8; e += 64)
+              *reinterpret_cast<uint4*>(hrow + (e >> 3) * RSH + (e & 7) * 16) = make_uint4(0, 0, 0, 0);
+            continue;
+          }
           if (jv) {
             char* hr = hrow + lr * RSH;
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
               for (int q4 = 0; q4 < 4; ++q4) {
-                const int co = 32 * t + 8 * q4 + 4 * lh;
-                const float4 g4 = *reinterpret_cast<const float4*>(a.ln1_g + lr * C + co);
-                const float4 b4 = *reinterpret_cast<const float4*>(a.ln1_b + lr * C + co);
+                const float4 gg = g4[t][q4], bb = b4[t][q4];
+                const float v[4] = {accf[i][t][4 * q4], accf[i][t][4 * q4 + 1], accf[i][t][4 * q4 + 2],
+                                    accf[i][t][4 * q4 + 3]};
                 bf16x4 hv;
-                hv[0] = (bf16)fmaxf(fmaf((acc[t][4 * q4 + 0] - mean) * rstd, g4.x, b4.x), 0.f);
-                hv[1] = (bf16)fmaxf(fmaf((acc[t][4 * q4 + 1] - mean) * rstd, g4.y, b4.y), 0.f);
-                hv[2] = (bf16)fmaxf(fmaf((acc[t][4 * q4 + 2] - mean) * rstd, g4.z, b4.z), 0.f);
-                hv[3] = (bf16)fmaxf(fmaf((acc[t][4 * q4 + 3] - mean) * rstd, g4.w, b4.w), 0.f);
+                hv[0] = (bf16)fmaxf(fmaf((v[0] - mean[i]) * rstd[i], gg.x, bb.x), 0.f);
+                hv[1] = (bf16)fmaxf(fmaf((v[1] - mean[i]) * rstd[i], gg.y, bb.y), 0.f);
+                hv[2] = (bf16)fmaxf(fmaf((v[2] - mean[i]) * rstd[i], gg.z, bb.z), 0.f);
+                hv[3] = (bf16)fmaxf(fmaf((v[3] - mean[i]) * rstd[i], gg.w, bb.w), 0.f);
+                *reinterpret_cast<bf16x4*>(hr + (32 * t + 8 * q4 + 4 * lh) * 2) = hv;
+              }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < FPW; ++i) {
+          const int fa = fa0 + NWG * i;
+          if (fa >= nfr) continue;
+          char* hrow = sH + (fa % RF) * vrs;
+          if (!frame_ok(fa)) {  // padding frame: h = 0
+            for (int e = lane; e < V * 8; e += 64)
+              *reinterpret_cast<uint4*>(hrow + (e >> 3) * RSH + (e & 7) * 16) = make_uint4(0, 0, 0, 0);
+            continue;
+          }
+          // epilogue: lane = joint lr, acc[t][r] = g^T[co = 32t + 8(r>>2) + 4lh + (r&3)][lr]; BN1 folded
+          if (lr < V) {
+            char* hr = hrow + lr * RSH;
+            const float* bp = sBp + lr * CBP;
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+              for (int q4 = 0; q4 < 4; ++q4) {
+                const int co = 32 * t + 8 * q4 + 4 * lh;
+                const float4 s4 = *reinterpret_cast<const float4*>(sSc + co);
+                const float4 b4 = *reinterpret_cast<const float4*>(bp + co);
+                const float v[4] = {accf[i][t][4 * q4], accf[i][t][4 * q4 + 1], accf[i][t][4 * q4 + 2],
+                                    accf[i][t][4 * q4 + 3]};
+                bf16x4 hv;
+                hv[0] = (bf16)fmaxf(fmaf(v[0], s4.x, b4.x), 0.f);
+                hv[1] = (bf16)fmaxf(fmaf(v[1], s4.y, b4.y), 0.f);
+                hv[2] = (bf16)fmaxf(fmaf(v[2], s4.z, b4.z), 0.f);
+                hv[3] = (bf16)fmaxf(fmaf(v[3], s4.w, b4.w), 0.f);
                 *reinterpret_cast<bf16x4*>(hr + co * 2) = hv;
               }
           }
-        } else if (lr < V) {
-          char* hr = hrow + lr * RSH;
-          const float* bp = sBp + lr * CBP;
-#pragma unroll
-          for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int q4 = 0; q4 < 4; ++q4) {
-              const int co = 32 * t + 8 * q4 + 4 * lh;
-              const float4 s4 = *reinterpret_cast<const float4*>(sSc + co);
-              const float4 b4 = *reinterpret_cast<const float4*>(bp + co);
-              bf16x4 hv;
-              hv[0] = (bf16)fmaxf(fmaf(acc[t][4 * q4 + 0], s4.x, b4.x), 0.f);
-              hv[1] = (bf16)fmaxf(fmaf(acc[t][4 * q4 + 1], s4.y, b4.y), 0.f);
-              hv[2] = (bf16)fmaxf(fmaf(acc[t][4 * q4 + 2], s4.z, b4.z), 0.f);
-              hv[3] = (bf16)fmaxf(fmaf(acc[t][4 * q4 + 3], s4.w, b4.w), 0.f);
-              *reinterpret_cast<bf16x4*>(hr + co * 2) = hv;
-            }
         }
       }
+      if (LN && next >= 0) issue(next);
       pa[1] += ptime() - pt1;
     };
     // prologue: frames 0..15 in two batches of 8 (base 0 and 8); then step s produces base 8s + 8
@@ -579,10 +630,14 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
         // hand-off among the 4 TCN waves only (a block barrier would also wait for the GCN waves' next
         // frames and serialise the two roles): an LDS arrival counter
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const long long pl0 = ptime();
+        pa[1] += pl0 - pk1;
         if (lane == 0) __hip_atomic_fetch_add(sCnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         arrivals += NWT;
         while (__hip_atomic_load(sCnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < arrivals)
           __builtin_amdgcn_s_sleep(1);
+        const long long pl1 = ptime();
+        pa[5] += pl1 - pl0;
 #pragma unroll
         for (int i = 0; i < RT; ++i) {
           const int r = (rh * RT + i) * 32 + lr;
@@ -617,7 +672,7 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
           }
         }
         const long long pl2 = ptime();
-        pa[4] += pl2 - pk1;
+        pa[4] += pl2 - pl1;
         lds_barrier();  // S_s
         pa[2] += ptime() - pl2;
         continue;

@@ -33,5 +33,6 @@ if __name__ == "__main__":
     tcn, gcn = a[:, :4], a[:, 4:]
     print(f"total cycles per wave: mean {a[:, :, 3].mean():.0f} (max {a[:, :, 3].max():.0f})")
     m = tcn.mean(axis=(0, 1))
-    print(f"TCN waves: k-loop {m[0]:.0f}  z stores (LN: whole epilogue) {m[4]:.0f}  BN2 partials {m[1]:.0f}  barrier {m[2]:.0f}")
+    print(f"TCN waves: k-loop {m[0]:.0f}  z stores (LN: normalise + stores) {m[4]:.0f}  BN2 partials (LN: statistics) "
+          f"{m[1]:.0f}  LN hand-off {m[5]:.0f}  barrier {m[2]:.0f}")
     print("GCN waves: DMA wait {:.0f}  compute {:.0f}  barrier {:.0f}".format(*gcn[:, :, :3].mean(axis=(0, 1))))
