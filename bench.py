@@ -141,7 +141,7 @@ def layer_roofline(pkg, dev, reps=20, norm="BatchNorm"):
     prev_hook = K.EVENT_HOOK
     K.EVENT_HOOK = hook
     prev_route = pkg.routing.ROUTING.fused_bn_inference
-    pkg.routing.ROUTING.fused_bn_inference = True  # BatchNorm layers take the fused path on request only
+    pkg.routing.ROUTING.fused_bn_inference = True  # the fused route, whatever the environment chose
     try:
         with torch.no_grad():
             fused_ms = timed(lambda: layer(x, A))
@@ -151,6 +151,31 @@ def layer_roofline(pkg, dev, reps=20, norm="BatchNorm"):
         pkg.routing.ROUTING.fused_bn_inference = prev_route
     xg = x.detach().requires_grad_(True)  # a differentiable input: the training path's forward (unfused)
     unfused_ms = timed(lambda: layer(xg, A))
+
+    def graphed(fn):
+        # the same forward captured once into a HIP graph and replayed: device time of the layer's kernels
+        # without the per-launch host work of the eager Python path
+        st = torch.cuda.Stream()
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            for _ in range(3):
+                fn()
+        torch.cuda.current_stream().wait_stream(st)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            fn()
+        return timed(g.replay)
+
+    R = pkg.routing.ROUTING
+    prev = (R.fused_bn_inference, R.fused_inference)
+    try:
+        with torch.no_grad():
+            R.fused_bn_inference, R.fused_inference = True, True
+            fused_graph_ms = graphed(lambda: layer(x, A))
+            R.fused_bn_inference, R.fused_inference = False, False
+            unfused_graph_ms = graphed(lambda: layer(x, A))
+    finally:
+        R.fused_bn_inference, R.fused_inference = prev
     pairs = [(kev[i], kev[i + 1]) for i in range(6, len(kev) - 1, 2)]  # skip the warm-up launches
     k_ms = sum(a.elapsed_time(b) for a, b in pairs) / len(pairs) if pairs else None
     achieved = LAYER_FWD_FLOP / (fused_ms * 1e-3) / 1e12
@@ -160,7 +185,11 @@ def layer_roofline(pkg, dev, reps=20, norm="BatchNorm"):
             "fused_kernel_ms": round(k_ms, 4) if k_ms else None,
             "achieved": round(achieved, 2), "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4),
-            "unfused_frac": round(LAYER_FWD_FLOP / (unfused_ms * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS, 4)}
+            "unfused_frac": round(LAYER_FWD_FLOP / (unfused_ms * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS, 4),
+            "graph": {"fused_fwd_ms": round(fused_graph_ms, 4), "unfused_fwd_ms": round(unfused_graph_ms, 4),
+                      "frac": round(LAYER_FWD_FLOP / (fused_graph_ms * 1e-3) / 1e12 / BF16_DENSE_PEAK_TFLOPS, 4),
+                      "unfused_frac": round(LAYER_FWD_FLOP / (unfused_graph_ms * 1e-3) / 1e12
+                                            / BF16_DENSE_PEAK_TFLOPS, 4)}}
 
 
 def cpu_baseline(pkg, model_cpu_sd):

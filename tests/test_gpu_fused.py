@@ -92,13 +92,13 @@ def _count_fused(P, monkeypatch):
         return orig(*a, **k)
 
     monkeypatch.setattr(P.native, "layer_fused", spy)
-    monkeypatch.setattr(P.routing.ROUTING, "fused_bn_inference", True)  # BatchNorm: fused path on request only
+    monkeypatch.setattr(P.routing.ROUTING, "fused_bn_inference", True)  # whatever the environment chose
     return calls
 
 
-def test_bn_inference_default_route(P, monkeypatch):
-    """Without routing.fused_bn_inference a BatchNorm layer's inference forward takes the unfused route (measured faster
-    than the two-pass fused form) and still matches the fp32 oracle."""
+def test_bn_inference_unfused_route(P, monkeypatch):
+    """With routing.fused_bn_inference off a BatchNorm layer's inference forward takes the unfused route and
+    still matches the fp32 oracle."""
     calls = _count_fused(P, monkeypatch)
     monkeypatch.setattr(P.routing.ROUTING, "fused_bn_inference", False)
     torch.manual_seed(4)
