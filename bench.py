@@ -249,6 +249,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--config", type=int, default=2, choices=(2, 4))
+    ap.add_argument("--torch-adam", action="store_true", help="torch's fused Adam instead of the package's")
     ap.add_argument("--accum", type=int, default=8, help="config 4: micro-steps per optimizer step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-layer-roofline", action="store_true", help="skip the north_star layer timing (profiling)")
@@ -289,9 +290,10 @@ def main():
     elif world > 1:  # identical replicas (DistributedDataParallel's broadcast from rank 0)
         for p in params:
             torch.distributed.broadcast(p.data, 0)
-    # the reference's optimizer (Adam, lr 5e-4); the fused multi-tensor implementation is the same update
-    # rule in one launch per parameter chunk instead of one foreach launch per elementwise op
-    opt = torch.optim.Adam(params, lr=5e-4, fused=True, capturable=args.graph)
+    # the reference's optimizer (Adam, lr 5e-4, processor.py:579): the package's Adam is torch's update rule with
+    # every parameter in ONE launch (csrc/adam.hip; test_gpu_optim.py); --torch-adam: torch's fused Adam
+    opt = torch.optim.Adam(params, lr=5e-4, fused=True, capturable=args.graph) if args.torch_adam else \
+        pkg.optim.Adam(params, lr=5e-4)
     gen_t = torch.Generator(device=dev).manual_seed(12345)
     class_dist = torch.rand(CLASSES, device=dev, generator=gen_t) + 0.5
     crit = pkg.loss.Loss(dev, class_dist)

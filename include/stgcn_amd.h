@@ -460,6 +460,30 @@ int stgcn_prep_check(stgcn_prep_job* jobs, int njobs);
 int stgcn_prep_run(const stgcn_prep_job* jobs_dev, const long* block_start_dev, int njobs, long nblocks,
                    void* stream);
 
+/* Adam over every parameter tensor of a model in one launch (adam.hip).
+ * Replaces: the reference's optimizer step, torch.optim.Adam (processor.py:561, built at processor.py:579; optimizer
+ * config learning_rate 5e-4, default betas / eps), with torch's update rule:
+ *   g' = g + weight_decay * p;  m = lerp(m, g', 1 - b1);  v = b2 v + (1 - b2) g'^2;
+ *   p += (-lr / (1 - b1^t)) * (m / (sqrt(v) / sqrt(1 - b2^t) + eps)),   t = the tensor's step count
+ * (the default foreach implementation's operation order; hyper-parameters in double, as Python floats).
+ * table_dev: device array of stgcn_adam_entry (p: the fp32 parameter, m / v: its moment slices, n elements,
+ * b0 = first block of the tensor, b0 increasing, block counts from stgcn_adam_blocks(n); vec = 1 when p, m
+ * and v are 16-B aligned).  grads: HOST array of ntensors device gradient pointers (NULL = no gradient:
+ * the tensor is skipped, its step count unchanged).  steps: device float [nblocks], every block's copy of
+ * its tensor's step count (zero-initialised; the caller reads a tensor's count at its first block). */
+#define STGCN_ADAM_MAXT 256
+typedef struct {
+  float* p;
+  float* m;
+  float* v;
+  long n, b0;
+  int vec, pad_;
+} stgcn_adam_entry;
+long stgcn_adam_blocks(long n);
+int stgcn_adam_step(const stgcn_adam_entry* table_dev, int ntensors, long nblocks, const float* const* grads,
+                    float* steps, double lr, double beta1, double beta2, double eps, double weight_decay,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif

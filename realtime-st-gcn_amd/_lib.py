@@ -21,6 +21,11 @@ c_long = ctypes.c_long
 c_float = ctypes.c_float
 
 
+class AdamEntry(ctypes.Structure):
+    _fields_ = [("p", c_void_p), ("m", c_void_p), ("v", c_void_p), ("n", c_long), ("b0", c_long), ("vec", c_int),
+                ("pad_", c_int)]
+
+
 class ConvDesc(ctypes.Structure):
     _fields_ = [("in_", c_void_p), ("out", c_void_p), ("w", c_void_p), ("bias", c_void_p), ("pro_a", c_void_p),
                 ("pro_b", c_void_p), ("pro_stats", c_void_p), ("stats", c_void_p)] + \
@@ -173,6 +178,8 @@ _SIGS = {
     "stgcn_seg_loss_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p]),
     "stgcn_prep_check": (c_int, [ctypes.POINTER(PrepJob), c_int]),
     "stgcn_prep_run": (c_int, [c_void_p, c_void_p, c_int, c_long, c_void_p]),
+    "stgcn_adam_blocks": (ctypes.c_long, [c_long]),
+    "stgcn_adam_step": (c_int, [c_void_p, c_int, c_long, c_void_p, c_void_p] + [ctypes.c_double] * 5 + [c_void_p]),
 }
 
 EXPORTS = tuple(_SIGS)

@@ -16,7 +16,10 @@
 
 namespace {
 
-constexpr int UNR = 2;  // rows per thread per iteration (raw 16-B units held until use)
+// rows per thread per iteration (raw 16-B units held until use, all loads issued first): 4 for the passes
+// with at most three input streams, 2 for the four-stream ones (register budget)
+constexpr int UNR_MAX = 4;
+constexpr int ur_for(int streams) { return streams <= 3 ? 4 : 2; }
 
 template <typename T, int VEC>
 DEV void ld8(const T* p, float* f) {
@@ -34,7 +37,7 @@ struct Geo {
   int nb;
 };
 
-template <typename T, int VEC, int MASK, bool X2>
+template <typename T, int VEC, int MASK, bool X2, int UNR>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_fused_kernel(const stgcn_bn_bwd_desc a, const Geo g) {
   __shared__ float4 red[256 * 8];  // [RPI][C]
   const int tid = threadIdx.x;
@@ -138,7 +141,7 @@ __global__ __launch_bounds__(256) void sum4_kernel(const float4* part, int nb, i
   }
 }
 
-template <typename T, int VEC, int MASK, int O2, bool OSUM>
+template <typename T, int VEC, int MASK, int O2, bool OSUM, int UNR>
 __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(const stgcn_bn_bwd_desc a, const Geo g) {
   __shared__ float2 red[256 * 8];
   const int tid = threadIdx.x;
@@ -253,8 +256,9 @@ Geo geo(long M, int C, int vec) {
   Geo g;
   g.CU = C / vec;
   g.RPI = 256 / g.CU;
-  // >= 2 iterations of UNR rows per thread and at most ~1024 blocks (partials folded by sum4_kernel)
-  const long step = (long)g.RPI * UNR;
+  // >= 2 iterations of UNR_MAX rows per thread and at most ~1024 blocks (partials folded by sum4_kernel); one
+  // row split for every UNR, so the reduce and apply passes of one BN see the same blocks
+  const long step = (long)g.RPI * UNR_MAX;
   // block target: 512 / 1024 / 2048 measured 1.67 / 1.68 / 1.8 ms per step for all fused BN backward passes +
   // sum4 folds (512 speeds up apply, slows reduce)
   constexpr long tb = 1024;
@@ -280,7 +284,9 @@ long bn_bwd_fused_work_floats_impl(long M, int C, int dtype) {
 
 template <typename T, int VEC, int MASK, bool X2>
 void launch_reduce(const stgcn_bn_bwd_desc& a, const Geo& g, hipStream_t s) {
-  hipLaunchKernelGGL((bn_bwd_reduce_fused_kernel<T, VEC, MASK, X2>), dim3(g.nb), dim3(256), 0, s, a, g);
+  // input streams: dy, the mask reference, x1 (shared with the mask reference for BN1), x2
+  constexpr int UR = ur_for(2 + (MASK == 2 ? 0 : 1) + (X2 ? 1 : 0));
+  hipLaunchKernelGGL((bn_bwd_reduce_fused_kernel<T, VEC, MASK, X2, UR>), dim3(g.nb), dim3(256), 0, s, a, g);
 }
 template <typename T, int VEC>
 void reduce_dispatch(const stgcn_bn_bwd_desc& a, const Geo& g, hipStream_t s) {
@@ -295,10 +301,11 @@ void reduce_dispatch(const stgcn_bn_bwd_desc& a, const Geo& g, hipStream_t s) {
 
 template <typename T, int VEC, int MASK, int O2>
 void launch_apply(const stgcn_bn_bwd_desc& a, const Geo& g, hipStream_t s) {
+  constexpr int UR = ur_for(2 + (MASK == 2 ? 0 : 1) + (O2 == 1 ? 1 : 0));  // (+ out2 read-back when acc2)
   if (a.osum)
-    hipLaunchKernelGGL((bn_bwd_apply_fused_kernel<T, VEC, MASK, O2, true>), dim3(g.nb), dim3(256), 0, s, a, g);
+    hipLaunchKernelGGL((bn_bwd_apply_fused_kernel<T, VEC, MASK, O2, true, UR>), dim3(g.nb), dim3(256), 0, s, a, g);
   else
-    hipLaunchKernelGGL((bn_bwd_apply_fused_kernel<T, VEC, MASK, O2, false>), dim3(g.nb), dim3(256), 0, s, a, g);
+    hipLaunchKernelGGL((bn_bwd_apply_fused_kernel<T, VEC, MASK, O2, false, UR>), dim3(g.nb), dim3(256), 0, s, a, g);
 }
 template <typename T, int VEC>
 void apply_dispatch(const stgcn_bn_bwd_desc& a, const Geo& g, hipStream_t s) {

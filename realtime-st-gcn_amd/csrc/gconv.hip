@@ -515,6 +515,7 @@ struct WGG {
   int ntile, tpb, R, nco, nci;
   float* slab;     // [R][V*J][Cout][Cin]
   float* rowpart;  // joint-grouped kernel: [R][V][Cout] partial row sums of dy per joint, or NULL
+  int zero_unused;  // direct plan (slab = dWeff): also write zeros into the slots j in [deg, J)
 };
 
 __global__ __launch_bounds__(256, 2) void gconv_wgrad_kernel(const stgcn_gconv_wgrad_desc a, const WGG g) {
@@ -904,6 +905,12 @@ DEV void wgrad3_body(const stgcn_gconv_wgrad_desc& a, const WGG& g, char* smem, 
 #pragma unroll
     for (int r = 0; r < 16; ++r) slab[(long)(co0 + cq * 32 + acc_row(r, lane)) * a.Cin + cc] = acc[j][r];
   }
+  if (g.zero_unused)
+    for (int j = DEG; j < a.J; ++j) {
+      float* slab = g.slab + ((long)w * a.J + j) * a.Cout * a.Cin;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) slab[(long)(co0 + cq * 32 + acc_row(r, lane)) * a.Cin + cc] = 0.f;
+    }
 }
 
 __global__ __launch_bounds__(256, 2) void gconv_wgrad3_kernel(const stgcn_gconv_wgrad_desc a, const WGG g) {
@@ -945,6 +952,13 @@ __global__ __launch_bounds__(256, 2) void gconv_wgrad3_kernel(const stgcn_gconv_
         float s = 0.f;
         for (int i = rr * g.tpb * 32; i < i1; ++i) s += (float)dy[((long)i * a.V + wj) * a.dy_ld + co];
         g.rowpart[((long)rr * a.V + wj) * a.Cout + co] = s;
+      }
+      if (g.zero_unused) {  // direct plan: this joint's J slots of the (64 co, 64 ci) group are zero
+        const int co0 = (grp % g.nco) * 64, ci0 = (grp / g.nco) * 64;
+        for (int i = threadIdx.x; i < a.J * 64 * 64; i += blockDim.x) {
+          const int j = i >> 12, co = (i >> 6) & 63, ci = i & 63;
+          g.slab[(((long)wj * a.J + j) * a.Cout + co0 + co) * a.Cin + ci0 + ci] = 0.f;
+        }
       }
       break;
   }
@@ -1225,6 +1239,12 @@ int w2_cob(const stgcn_gconv_wgrad_desc& a) {
 // kernel measured 74 vs 82 us
 bool w3_ok(const stgcn_gconv_wgrad_desc& a) { return !(a.Cin == 64 && a.Cout == 128); }
 
+// DMA-ring block target once a joint has several channel groups (C >= 128); a plan with R = 1 (one row range
+// per block: the 400 groups of C = 256) writes dWeff and the row sums directly, with no slab and no reduction
+// launch.  Config-2 step, interleaved A/B (3 x 100 steps): target 256 8.16 ms, 512 8.19, 1024 8.25
+#ifndef STGCN_W3_WIDE_TARGET
+#define STGCN_W3_WIDE_TARGET 256
+#endif
 WGG wplan2(const stgcn_gconv_wgrad_desc& a, int cob) {
   WGG g{};
   g.ntile = (a.NT + w2m(cob) - 1) / w2m(cob);
@@ -1234,7 +1254,7 @@ WGG wplan2(const stgcn_gconv_wgrad_desc& a, int cob) {
   const long target = cob == 64 ? 512 : 256;  // COB 64: 3 register-staged / 2 DMA-ring blocks fit a CU
   // DMA ring: block target by the group count, measured per layer (targets 512 / 1024 / 2048): C = 64
   // (25 groups) 49 / 40 / 56 us, C = 128 64 / 81 / 75 us, C = 256 108 / 113 / 130 us
-  const long t3 = groups <= 32 ? 1024 : 512;
+  const long t3 = groups <= 32 ? 1024 : STGCN_W3_WIDE_TARGET;
   long R = (cob == 64 && w3_ok(a)) ? (t3 + groups - 1) / groups : (target + groups - 1) / groups;
   if (R > g.ntile) R = g.ntile;
   if (R < 1) R = 1;
@@ -1309,6 +1329,7 @@ long gconv_wgrad_workspace(const stgcn_gconv_wgrad_desc& a, int dtype) {
   if (dtype != 1) return 0;
   const int cob = w2_cob(a);
   const WGG g = cob ? wplan2(a, cob) : wplan(a);
+  if (cob && w3_ok(a) && g.R == 1) return 0;  // direct
   if (cob && a.rowsum)
     return ((long)g.R * a.V * a.J * a.Cout * a.Cin + (long)g.R * a.V * a.Cout) * (long)sizeof(float);
   return (long)g.R * a.V * a.J * a.Cout * a.Cin * (long)sizeof(float);
@@ -1324,16 +1345,24 @@ int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s
   const int cob = w2_cob(a);
   if (cob) {
     WGG g = wplan2(a, cob);
-    const long need = (long)g.R * E + (a.rowsum ? (long)g.R * a.V * a.Cout : 0);
-    if (!a.work || a.work_bytes < need * (long)sizeof(float)) return STGCN_EBADSHAPE;
-    g.slab = reinterpret_cast<float*>(a.work);
-    g.rowpart = a.rowsum ? g.slab + (long)g.R * E : nullptr;
     const bool ring = cob == 64 && w3_ok(a);
+    const bool direct = ring && g.R == 1;  // the only row range: partials are the result
+    const long need = (long)g.R * E + (a.rowsum ? (long)g.R * a.V * a.Cout : 0);
+    if (direct) {
+      g.slab = a.dweff;
+      g.rowpart = a.rowsum;
+      g.zero_unused = 1;
+    } else {
+      if (!a.work || a.work_bytes < need * (long)sizeof(float)) return STGCN_EBADSHAPE;
+      g.slab = reinterpret_cast<float*>(a.work);
+      g.rowpart = a.rowsum ? g.slab + (long)g.R * E : nullptr;
+    }
     const size_t lds = ring ? (size_t)W3_LDS : 2 * (size_t)(cob / 32 + 2 * J2) * w2m(cob) * WPR;
     auto* k = ring ? gconv_wgrad3_kernel : gconv_wgrad2_kernel<64>;
     if (stgcn_lds_attr((const void*)k, 160 * 1024, s)) return STGCN_EHIP;
     const long blocks = (long)a.V * g.nco * g.nci * g.R;
     hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(ring ? 256 : cob / 16 * 64), lds, s, a, g);
+    if (direct) return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
     if (a.rowsum) {  // slab reduction and row sums in one launch
       const long ER = (long)a.V * a.Cout;
       const int nb1 = (int)((E + 255) / 256);

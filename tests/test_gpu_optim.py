@@ -1,0 +1,110 @@
+"""optim.Adam (csrc/adam.hip: every parameter of a group in one launch) against torch.optim.Adam — the
+reference's optimizer (processor.py:579, stepped at processor.py:561) — on the same parameters and gradients:
+sizes below / across / far above one 2048-element block and not multiples of 4, a parameter without a gradient
+(skipped, its step count unchanged, as torch does), a non-contiguous gradient, weight decay, several steps;
+the state_dict round trip in both directions; and the config-2 model's parameters through one training step."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def P(pkg):
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return pkg
+
+
+def _params(seed):
+    g = torch.Generator().manual_seed(seed)
+    shapes = [(3,), (64,), (2048,), (2049,), (5, 7, 11), (256, 256, 9, 1), (75,), (1,)]
+    return [torch.randn(s, generator=g).to(DEV) for s in shapes]
+
+
+def _grads(params, seed):
+    g = torch.Generator().manual_seed(seed)
+    return [torch.randn(p.shape, generator=g).to(DEV) for p in params]
+
+
+# the kernel follows the default (foreach) implementation's operations in fp32; fused-vs-foreach style reordering
+# would show at ~1e-6
+TOL = dict(rtol=2e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("wd", [0.0, 0.01])
+def test_adam_matches_torch(P, wd):
+    ref = [p.clone().requires_grad_(True) for p in _params(0)]
+    got = [p.clone().requires_grad_(True) for p in _params(0)]
+    o_ref = torch.optim.Adam(ref, lr=5e-4, weight_decay=wd)
+    o_got = P.optim.Adam(got, lr=5e-4, weight_decay=wd)
+    for it in range(6):
+        gs = _grads(ref, 10 + it)
+        for k, (a, b, g) in enumerate(zip(ref, got, gs)):
+            if k == 1 and it in (2, 3):  # no gradient this step: skipped, step count not advanced
+                a.grad = b.grad = None
+                continue
+            a.grad = g.clone()
+            # k == 4: a non-contiguous gradient of the right shape
+            b.grad = g.clone() if k != 4 else g.transpose(0, 2).contiguous().transpose(0, 2)
+        o_ref.step()
+        o_got.step()
+        torch.cuda.synchronize()
+        for k, (a, b) in enumerate(zip(ref, got)):
+            torch.testing.assert_close(b.detach(), a.detach(), **TOL, msg=lambda m: f"step {it} param {k}: {m}")
+            sa, sb = o_ref.state[a], o_got.state[b]
+            assert float(sb["step"]) == float(sa["step"]), (it, k)
+            torch.testing.assert_close(sb["exp_avg"], sa["exp_avg"], **TOL)
+            torch.testing.assert_close(sb["exp_avg_sq"], sa["exp_avg_sq"], **TOL)
+
+
+def test_adam_state_dict_round_trip(P):
+    ref = [p.clone().requires_grad_(True) for p in _params(1)]
+    got = [p.clone().requires_grad_(True) for p in _params(1)]
+    o_ref = torch.optim.Adam(ref, lr=1e-3)
+    for it in range(3):
+        for a, g in zip(ref, _grads(ref, 20 + it)):
+            a.grad = g
+        o_ref.step()
+    with torch.no_grad():
+        for a, b in zip(ref, got):
+            b.copy_(a)
+    o_got = P.optim.Adam(got, lr=1e-3)
+    o_got.load_state_dict(o_ref.state_dict())  # torch -> package
+    for it in range(2):
+        gs = _grads(ref, 30 + it)
+        for a, b, g in zip(ref, got, gs):
+            a.grad, b.grad = g.clone(), g.clone()
+        o_ref.step()
+        o_got.step()
+    for a, b in zip(ref, got):
+        torch.testing.assert_close(b.detach(), a.detach(), **TOL)
+    back = torch.optim.Adam([p.clone() for p in got], lr=1e-3)
+    back.load_state_dict(o_got.state_dict())  # package -> torch
+    for pa, pb in zip(o_got.param_groups[0]["params"], back.param_groups[0]["params"]):
+        sa, sb = o_got.state[pa], back.state[pb]
+        assert float(sa["step"]) == float(sb["step"]) == 5.0
+        torch.testing.assert_close(sb["exp_avg"], sa["exp_avg"], rtol=0, atol=0)
+
+
+def test_adam_model_step(P):
+    """The config-2 model's 96 parameters (bench.py's optimizer) after one training step: same update as torch."""
+    import bench
+    torch.manual_seed(5)
+    m = P.MODELS["st-gcn"](rank=None, **dict(bench.ARCH, graph=P.PKU_MMD)).to(DEV)
+    params = [p for p in m.parameters() if p.requires_grad]
+    g = torch.Generator().manual_seed(6)
+    for p in params:
+        p.grad = torch.randn(p.shape, generator=g).to(DEV)
+    ref = [p.detach().clone().requires_grad_(True) for p in params]
+    for a, p in zip(ref, params):
+        a.grad = p.grad.clone()
+    o_ref = torch.optim.Adam(ref, lr=5e-4)
+    o_got = P.optim.Adam(params, lr=5e-4)
+    assert len(params) <= 256
+    for _ in range(2):
+        o_ref.step()
+        o_got.step()
+    for a, p in zip(ref, params):
+        torch.testing.assert_close(p.detach(), a.detach(), **TOL)
