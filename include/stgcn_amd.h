@@ -83,6 +83,10 @@ typedef struct {
   long rows_per_block; /* filled by the library */
   void* work;          /* optional workspace (bf16 frame-tiled path: per-block fp32 partials) */
   long work_bytes;     /* its size; stgcn_conv_wgrad_workspace() tells how much the fast path needs */
+  int out_mode;        /* 0: dw[Kt][Cout][Cin] += gradient; 1: dw OVERWRITTEN in nn.Conv2d weight order
+                        * [Cout][Cin][Kt] (no zero fill, no permute copy) — the workspace paths only
+                        * (stgcn_conv_wgrad_workspace() > 0), else STGCN_EBADSHAPE */
+  int pad_;
 } stgcn_wgrad_desc;
 
 int stgcn_conv_wgrad(const stgcn_wgrad_desc* d, int dtype, void* stream);

@@ -46,7 +46,7 @@ class WgradDesc(ctypes.Structure):
                 ("pro_stats", c_void_p)] + \
                [(n, c_int) for n in ("N", "T_in", "T_out", "V", "Cin", "Cout", "Kt", "stride", "pad", "pro",
                                      "in_ld", "dy_ld")] + [("rows_per_block", c_long), ("work", c_void_p),
-                                                           ("work_bytes", c_long)]
+                                                           ("work_bytes", c_long), ("out_mode", c_int), ("pad_", c_int)]
 
 
 class AmixDesc(ctypes.Structure):

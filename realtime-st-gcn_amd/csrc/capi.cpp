@@ -182,12 +182,14 @@ int stgcn_conv_wgrad(const stgcn_wgrad_desc* d, int dtype, void* stream) {
   CHECK_DTYPE(dtype);
   if (!d || !d->in || !d->dy || !d->dw || d->N <= 0 || d->Kt <= 0 || d->stride <= 0) return STGCN_EBADSHAPE;
   if (d->pro && (!d->pro_a || !d->pro_b || (d->pro == 2 && !d->pro_stats))) return STGCN_EBADSHAPE;
+  if (d->out_mode != 0 && d->out_mode != 1) return STGCN_EBADSHAPE;
   const int rw = wgrad_wide_launch(*d, dtype, STREAM(stream));  // bf16 >= 128-channel ring path (needs work)
   if (rw >= 0) return rw;
   const int r1 = wgrad1x1_launch(*d, dtype, STREAM(stream));  // bf16 1x1 split-K row reduction (needs work)
   if (r1 >= 0) return r1;
   const int r = wgrad_tile_launch(*d, dtype, STREAM(stream));  // bf16 frame-tiled path (needs work)
   if (r >= 0) return r;
+  if (d->out_mode) return STGCN_EBADSHAPE;  // the accumulating paths below: += [Kt][Cout][Cin] only
   return conv_wgrad_launch(*d, dtype, STREAM(stream));
 }
 

@@ -160,9 +160,10 @@ __global__ __launch_bounds__(NT1) void wgrad1x1_kernel(const stgcn_wgrad_desc a,
   }
 }
 
-// dw[e] += sum over chunks of slab[c][e], fixed order: 64 entries x 16 chunk groups per block
+// dw[e] (+)= sum over chunks of slab[c][e], fixed order: 64 entries x 16 chunk groups per block (overwrite: the
+// desc's out_mode 1; Kt = 1, so both layouts agree)
 __global__ __launch_bounds__(1024) void wgrad1x1_reduce_kernel(const float* __restrict__ slab, int nchunk, long E,
-                                                               float* __restrict__ dw) {
+                                                               float* __restrict__ dw, int overwrite) {
   __shared__ float part[16][64];
   const int le = threadIdx.x & 63, q = threadIdx.x >> 6;
   const long e = (long)blockIdx.x * 64 + le;
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(1024) void wgrad1x1_reduce_kernel(const float* __re
   s = 0.f;
 #pragma unroll
   for (int j = 0; j < 16; ++j) s += part[j][le];
-  dw[e] += s;
+  dw[e] = overwrite ? s : dw[e] + s;
 }
 
 bool w1_ok(const stgcn_wgrad_desc& a, int dtype) {
@@ -222,6 +223,6 @@ int wgrad1x1_launch(const stgcn_wgrad_desc& a, int dtype, hipStream_t s) {
   if (hipGetLastError() != hipSuccess) return STGCN_EHIP;
   const long E = (long)a.Cout * a.Cin;
   hipLaunchKernelGGL(wgrad1x1_reduce_kernel, dim3((unsigned)((E + 63) / 64)), dim3(1024), 0, s, (const float*)slab,
-                     g.nchunk, E, a.dw);
+                     g.nchunk, E, a.dw, a.out_mode);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }

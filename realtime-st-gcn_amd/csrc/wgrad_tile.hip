@@ -96,38 +96,48 @@ __global__ __launch_bounds__(256, LN ? 1 : 2) void wgrad_tile_kernel(const stgcn
   const int dy_u = tid & 7;                  // dy: 8 units per row (co0 + 8*dy_u)
   const int x_u = tid % X_UPR;               // halo: X_UPR units per row
   const int x_ci = ci0 + x_u * 8;
-  float sc[8], sh[8];
-  if (a.pro == 1) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      sc[j] = x_ci + j < a.Cin ? a.pro_a[x_ci + j] : 0.f;
-      sh[j] = x_ci + j < a.Cin ? a.pro_b[x_ci + j] : 0.f;
-    }
+  // BatchNorm prologue scale / shift of the block's 32*NB input channels in LDS after the two stages (read at
+  // each halo store instead of held in 16 registers for the whole kernel)
+  float* const sScSh = reinterpret_cast<float*>(smem + 2 * STAGE);  // [2][32 * NB]
+  if (a.pro == 1 && tid < 32 * NB) {
+    const int c = ci0 + tid;
+    sScSh[tid] = c < a.Cin ? a.pro_a[c] : 0.f;
+    sScSh[32 * NB + tid] = c < a.Cin ? a.pro_b[c] : 0.f;
   }
 
-  // tile-invariant part of each halo unit: frame offset from the tile's first halo frame, joint
-  int x_fo[X_PT], x_v[X_PT];
+  // tile-invariant part of each halo unit: frame offset from the tile's first halo frame (fo, -1 = unused unit)
+  // and joint (v < 32), packed as fo * 32 + v (registers: two staged sets are live in the tile loop)
+  int x_fv[X_PT];
 #pragma unroll
   for (int i = 0; i < X_PT; ++i) {
     const int prow = (tid + i * 256) / X_UPR;
     const int par = prow / g.HRS, j = prow - par * g.HRS;
     if (prow >= SP * g.HRS) {
-      x_fo[i] = -1;
-      x_v[i] = 0;
+      x_fv[i] = -32;
     } else if (g.F) {
       const int fl = j / V;
-      x_fo[i] = S * fl + par;
-      x_v[i] = j - fl * V;
+      x_fv[i] = (S * fl + par) * 32 + (j - fl * V);
     } else {
-      x_fo[i] = j;  // flat: row within the tile
-      x_v[i] = 0;
+      x_fv[i] = j * 32;  // flat: row within the tile
     }
   }
+  auto x_fo = [&](int i) { return x_fv[i] >> 5; };
+  auto x_v = [&](int i) { return x_fv[i] & 31; };
 
-  uint4 ry[DY_PT], rx[X_PT];
-  int rxs[X_PT];  // input frame n*T_in + t of the halo unit (LN prologue), -1 = zero
+  // Two register sets of staged loads: tile j's in set j & 1.  Tile j + 2's loads are issued at the start of
+  // tile j, tile j + 1's set goes to LDS at its end, so two tiles of MFMA work cover each load's latency (one
+  // tile's 32-40 k-steps per wave did not; AHEAD2 below).  Loads are unconditional (invalid units read an in-bounds row of
+  // the same sample and are zeroed at the store through a per-set validity mask), so the count in flight is
+  // fixed and the wait before storing set j+1 leaves tile j+2's loads pending.
+  static_assert(DY_PT + X_PT <= 32, "validity mask");
+  uint4 ry[2][DY_PT], rx[2][X_PT];
+  int rxs[2][X_PT];  // input frame n*T_in + t of the halo unit (LN prologue), -1 = zero
+  unsigned msk[2];
+  const int coc = co0 + dy_u * 8 < a.Cout ? co0 + dy_u * 8 : 0;
+  const int xcc = x_ci < a.Cin ? x_ci : 0;
 
-  auto load = [&](int t) {
+  auto load = [&]<int SS>(int t) {
+    t = min(t, t_end - 1);  // past the block's range: re-read its last tile (never stored)
     long orow0, irow0;
     int rows_valid, fi0 = 0, nT = 0;
     if (g.F) {
@@ -142,42 +152,46 @@ __global__ __launch_bounds__(256, LN ? 1 : 2) void wgrad_tile_kernel(const stgcn
       rows_valid = (int)min((long)KM, (long)a.N * a.T_out * V - orow0);
       irow0 = orow0;
     }
+    unsigned m = 0;
 #pragma unroll
     for (int i = 0; i < DY_PT; ++i) {
       const int id = tid + i * 256, row = id >> 3;
-      const int co = co0 + dy_u * 8;
-      ry[i] = make_uint4(0, 0, 0, 0);
-      if (row < rows_valid && co < a.Cout)
-        ry[i] = *reinterpret_cast<const uint4*>(dy + (orow0 + row) * a.dy_ld + co);
+      const bool ok = row < rows_valid && co0 + dy_u * 8 < a.Cout;
+      ry[SS][i] = *reinterpret_cast<const uint4*>(dy + (orow0 + (ok ? row : 0)) * a.dy_ld + coc);
+      m |= (unsigned)ok << i;
     }
 #pragma unroll
     for (int i = 0; i < X_PT; ++i) {
-      rx[i] = make_uint4(0, 0, 0, 0);
-      rxs[i] = -1;
       long src = -1;
-      if (x_fo[i] >= 0) {
+      int fr = -1;
+      if (x_fo(i) >= 0) {
         if (g.F) {
-          const int fi = fi0 + x_fo[i];
+          const int fi = fi0 + x_fo(i);
           if (fi >= 0 && fi < a.T_in) {
-            src = irow0 + (long)fi * V + x_v[i];
-            rxs[i] = nT + fi;
+            src = irow0 + (long)fi * V + x_v(i);
+            fr = nT + fi;
           }
-        } else if (x_fo[i] < rows_valid) {
-          src = irow0 + x_fo[i];
+        } else if (x_fo(i) < rows_valid) {
+          src = irow0 + x_fo(i);
         }
       }
-      if (src >= 0 && x_ci < a.Cin) rx[i] = *reinterpret_cast<const uint4*>(in + src * a.in_ld + x_ci);
-      else rxs[i] = -1;
+      const bool ok = src >= 0 && x_ci < a.Cin;
+      rx[SS][i] = *reinterpret_cast<const uint4*>(in + (ok ? src : irow0) * a.in_ld + xcc);
+      rxs[SS][i] = ok ? fr : -1;
+      m |= (unsigned)ok << (DY_PT + i);
     }
+    msk[SS] = m;
   };
 
-  auto store = [&](int buf) {
+  auto store = [&]<int SS>(int buf) {
     char* sdy = smem + buf * STAGE;
     char* sx = sdy + DY_BYTES;
+    const unsigned m = msk[SS];
 #pragma unroll
     for (int i = 0; i < DY_PT; ++i) {
       const int id = tid + i * 256, row = id >> 3;
-      *reinterpret_cast<uint4*>(sdy + (dy_u >> 2) * (KM * PR) + row * PR + (dy_u & 3) * 16) = ry[i];
+      *reinterpret_cast<uint4*>(sdy + (dy_u >> 2) * (KM * PR) + row * PR + (dy_u & 3) * 16) =
+          (m >> i) & 1u ? ry[SS][i] : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < X_PT; ++i) {
@@ -185,16 +199,23 @@ __global__ __launch_bounds__(256, LN ? 1 : 2) void wgrad_tile_kernel(const stgcn
       const int id = tid + i * 256;
       const int prow = id / X_UPR;
       if (prow < SP * g.HRS) {
-        uint4 v = rx[i];
-        if (a.pro != 0 && rxs[i] >= 0) {
+        const bool ok = (m >> (DY_PT + i)) & 1u;
+        uint4 v = ok ? rx[SS][i] : make_uint4(0, 0, 0, 0);
+        if (a.pro != 0 && ok && (!LN || rxs[SS][i] >= 0)) {
           float f[8];
           unpack16(v, f, (bf16*)nullptr);
           if constexpr (!LN) {
+            const float4 s0 = *reinterpret_cast<const float4*>(sScSh + x_u * 8);
+            const float4 s1 = *reinterpret_cast<const float4*>(sScSh + x_u * 8 + 4);
+            const float4 h0 = *reinterpret_cast<const float4*>(sScSh + 32 * NB + x_u * 8);
+            const float4 h1 = *reinterpret_cast<const float4*>(sScSh + 32 * NB + x_u * 8 + 4);
+            const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+            const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
 #pragma unroll
             for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], sc[j], sh[j]), 0.f);
           } else {
-            const float2 st = reinterpret_cast<const float2*>(a.pro_stats)[rxs[i]];
-            const int av = x_v[i];  // LN prologue only in framed tiles (plan())
+            const float2 st = reinterpret_cast<const float2*>(a.pro_stats)[rxs[SS][i]];
+            const int av = x_v(i);  // LN prologue only in framed tiles (plan())
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
               const int gi = (x_ci + j) * V + av;
@@ -216,18 +237,21 @@ __global__ __launch_bounds__(256, LN ? 1 : 2) void wgrad_tile_kernel(const stgcn
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  int cur = 0;
-  if (t_begin < t_end) {
-    load(t_begin);
-    store(0);
+  // two tiles ahead for the stride-1 convs; the stride-2 instantiations keep one (a second live set spills)
+  constexpr bool AHEAD2 = S == 1;
+  const int nt = t_end - t_begin;
+  if (nt > 0) {
+    load.template operator()<0>(t_begin);
+    store.template operator()<0>(0);
+    if constexpr (AHEAD2) load.template operator()<1>(t_begin + 1);
   }
   __syncthreads();
-  for (int t = t_begin; t < t_end; ++t) {
-    const bool more = t + 1 < t_end;
-    if (more) load(t + 1);
-    const char* sdy = smem + cur * STAGE;
+  auto tile = [&]<int SET>(int j) {  // tile j from LDS buffer j & 1 (= SET); tile j+1's loads go to set SET^1
+    if constexpr (AHEAD2) load.template operator()<SET>(t_begin + j + 2);
+    else load.template operator()<SET ^ 1>(t_begin + j + 1);
+    const char* sdy = smem + SET * STAGE;
     const char* sx = sdy + DY_BYTES;
-#pragma unroll 2
+#pragma unroll 1
     for (int ks = 0; ks < KM / 16; ++ks) {
       const bf16x8 fa = trfrag(sdy + wa * (KM * PR), ks * 16, lane);
 #pragma unroll
@@ -236,17 +260,20 @@ __global__ __launch_bounds__(256, LN ? 1 : 2) void wgrad_tile_kernel(const stgcn
         if (dt < tw1) {  // wave-uniform
           const int par = dt % S, e = dt / S;
 #pragma unroll
-          for (int j = 0; j < NBW; ++j) {
-            const char* panel = sx + (bw0 + j) * XP_BYTES + par * g.HRS * PR;
+          for (int jb = 0; jb < NBW; ++jb) {
+            const char* panel = sx + (bw0 + jb) * XP_BYTES + par * g.HRS * PR;
             const bf16x8 fb = trfrag(panel, ks * 16 + e * V, lane);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, acc[i][j], 0, 0, 0);
+            acc[i][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, acc[i][jb], 0, 0, 0);
           }
         }
       }
     }
-    if (more) store(cur ^ 1);
+    if (j + 1 < nt) store.template operator()<SET ^ 1>(SET ^ 1);
     __syncthreads();
-    cur ^= 1;
+  };
+  for (int j = 0; j < nt; j += 2) {
+    tile.template operator()<0>(j);
+    if (j + 1 < nt) tile.template operator()<1>(j + 1);
   }
 
   // ---- partial of this block -> slab [rr][dt][co][ci] (full Kt x Cout x Cin image per rr)
@@ -283,15 +310,27 @@ __global__ void slab_reduce1_kernel(const float* __restrict__ slab, int R, int R
   *reinterpret_cast<float4*>(part + (long)sidx * E + e4) = acc;
 }
 
-__global__ void slab_reduce2_kernel(const float* __restrict__ part, int RS, long E, float* __restrict__ dw) {
+// level 2: dw (+)= sum_r part[r]; mode 0: dw[e] += (layout [Kt][Cout][Cin] of e); mode 1: dw overwritten in the
+// nn.Conv2d order [Cout][Cin][Kt] (CoCi = Cout * Cin, Kt taps)
+__global__ void slab_reduce2_kernel(const float* __restrict__ part, int RS, long E, float* __restrict__ dw, int mode,
+                                    int Kt, long CoCi) {
   const long e4 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (e4 >= E) return;
-  float4 s = *reinterpret_cast<const float4*>(dw + e4);
+  float4 s = mode ? make_float4(0.f, 0.f, 0.f, 0.f) : *reinterpret_cast<const float4*>(dw + e4);
   for (int r = 0; r < RS; ++r) {
     const float4 v = *reinterpret_cast<const float4*>(part + (long)r * E + e4);
     s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
   }
-  *reinterpret_cast<float4*>(dw + e4) = s;
+  if (mode == 0 || Kt == 1) {
+    *reinterpret_cast<float4*>(dw + e4) = s;
+  } else {  // e = k * CoCi + (co * Cin + ci) -> (co * Cin + ci) * Kt + k; 4 consecutive ci never cross a co row
+    const long k = e4 / CoCi, r = e4 - k * CoCi;
+    float* d = dw + r * Kt + k;
+    d[0] = s.x;
+    d[Kt] = s.y;
+    d[2 * Kt] = s.z;
+    d[3 * Kt] = s.w;
+  }
 }
 
 constexpr int RS_MAX = 16;
@@ -346,7 +385,7 @@ Plan plan(const stgcn_wgrad_desc& a) {
   if (R < 1) R = 1;
   g.tpb = (g.ntiles + R - 1) / R;
   g.R = (g.ntiles + g.tpb - 1) / g.tpb;
-  p.lds = 2 * (size_t)(2 * KM * PR + NB * (a.Kt >= S ? S : 1) * g.HRS * PR);
+  p.lds = 2 * (size_t)(2 * KM * PR + NB * (a.Kt >= S ? S : 1) * g.HRS * PR) + 2 * 32 * NB * sizeof(float);
   if (p.lds > 160 * 1024) return p;
   // slabs + level-1 partials; E % 4 == 0 holds since Cin % 8 == 0
   p.slab_elems = (long)(g.R + RS_MAX) * a.Kt * a.Cout * a.Cin;
@@ -381,12 +420,13 @@ int slab_reduce1_launch(const float* slab, int R, long E, float* part, hipStream
   return hipGetLastError() == hipSuccess ? RS : -STGCN_EHIP;
 }
 
-// deterministic two-level sum of R fp32 slabs [R][E] into dw (+=); part holds RS_MAX * E floats
-int slab_reduce_launch(const float* slab, int R, long E, float* part, float* dw, hipStream_t s) {
+// deterministic two-level sum of R fp32 slabs [R][E] into dw (out mode as slab_reduce2); part holds RS_MAX * E floats
+int slab_reduce_launch(const float* slab, int R, long E, float* part, float* dw, hipStream_t s, int mode, int Kt,
+                       long CoCi) {
   const int RS = R < RS_MAX ? R : RS_MAX;
   const unsigned blocks = (unsigned)((E / 4 + 255) / 256);
   hipLaunchKernelGGL(slab_reduce1_kernel, dim3(blocks, RS), dim3(256), 0, s, slab, R, RS, E, part);
-  hipLaunchKernelGGL(slab_reduce2_kernel, dim3(blocks), dim3(256), 0, s, (const float*)part, RS, E, dw);
+  hipLaunchKernelGGL(slab_reduce2_kernel, dim3(blocks), dim3(256), 0, s, (const float*)part, RS, E, dw, mode, Kt, CoCi);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
 
@@ -418,6 +458,7 @@ int wgrad_tile_launch(const stgcn_wgrad_desc& a, int dtype, hipStream_t s) {
   const unsigned blocks = (unsigned)((E / 4 + 255) / 256);
   hipLaunchKernelGGL(slab_reduce1_kernel, dim3(blocks, RS), dim3(256), 0, s, (const float*)p.g.slab, p.g.R, RS, E,
                      part);
-  hipLaunchKernelGGL(slab_reduce2_kernel, dim3(blocks), dim3(256), 0, s, (const float*)part, RS, E, a.dw);
+  hipLaunchKernelGGL(slab_reduce2_kernel, dim3(blocks), dim3(256), 0, s, (const float*)part, RS, E, a.dw, a.out_mode,
+                     a.Kt, (long)a.Cout * a.Cin);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }

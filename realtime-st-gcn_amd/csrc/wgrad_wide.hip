@@ -117,45 +117,52 @@ __global__ __launch_bounds__(NT, 1) void wgrad_wide_kernel(const stgcn_wgrad_des
       sh[j] = c < a.Cin ? a.pro_b[c] : 0.f;
     }
   }
-  uint4 ry[DY_U], rx[X_U];
-  auto load_dy = [&](int n, int f0) {  // rows of output frames f0 .. f0+F-1 (zero past T_out / F*V)
+  // Two register sets: tile j's staged loads live in set j & 1, and tile j + 1's set goes to LDS at the end of
+  // tile j.  5-tap (stride-2 folded) tiles have 40 k-steps, too few to cover one tile's load latency: there
+  // tile j + 2's loads are issued at the start of tile j (AHEAD2).  The 9-tap tiles keep one tile ahead (a
+  // second live set pushes them past 256 VGPRs).  Every load is unconditional (out-of-range rows clamp to an
+  // in-bounds row and are zeroed at the LDS store), so the number of loads in flight is fixed and the vmcnt wait
+  // before the store of set j+1 leaves tile j+2's loads pending.
+  constexpr bool AHEAD2 = KT < 9;
+  uint4 ry[2][DY_U], rx[2][X_U];
+  const bool ycok = co0 + ycu * 8 < a.Cout, xcok = ci0 + xcu * 8 < a.Cin;
+  const bf16* __restrict__ dyb = dy + co0 + (ycok ? ycu * 8 : 0);
+  const bf16* __restrict__ xb = xin + ci0 + (xcok ? xcu * 8 : 0);
+  auto load_dy = [&]<int S>(int n, int f0) {  // rows of output frames f0 .. f0+F-1 (f0 clamped into the sample)
+    f0 = min(f0, a.T_out - 1);
     const int rows_valid = min(F, a.T_out - f0) * V;
-    const bf16* base = dy + ((long)n * a.T_out + f0) * V * a.dy_ld + co0 + ycu * 8;
-    const bool cok = co0 + ycu * 8 < a.Cout;
+    const bf16* base = dyb + ((long)n * a.T_out + f0) * V * a.dy_ld;
     static_for<DY_U>([&]<int i>() {
       const int r = (tid >> 4) + 32 * i;
-      ry[i] = make_uint4(0, 0, 0, 0);
-      if (cok && r < rows_valid) ry[i] = *reinterpret_cast<const uint4*>(base + (long)r * a.dy_ld);
+      ry[S][i] = *reinterpret_cast<const uint4*>(base + (long)(r < rows_valid ? r : 0) * a.dy_ld);
     });
   };
-  auto store_dy = [&](int buf) {
+  auto store_dy = [&]<int S>(int buf, int f0) {  // rows past T_out / F*V and channels past Cout: zero
+    const int rows_valid = ycok ? min(F, a.T_out - f0) * V : 0;
     char* p = sY + buf * DY_BYTES + (ycu >> 2) * DY_PANEL + (ycu & 3) * 16;
     static_for<DY_U>([&]<int i>() {
       const int r = (tid >> 4) + 32 * i;
-      *reinterpret_cast<uint4*>(p + r * PR) = ry[i];
+      *reinterpret_cast<uint4*>(p + r * PR) = r < rows_valid ? ry[S][i] : make_uint4(0, 0, 0, 0);
     });
   };
-  // input frames [fa, fa + nf) of sample n (nf * V <= 128) -> registers
-  auto load_x = [&](int n, int fa, int nf) {
-    const bool cok = ci0 + xcu * 8 < a.Cin;
+  // input frames [fa, fa + nf) of sample n (nf * V <= 128) -> register set S (source frames clamped into [0, T_in))
+  auto load_x = [&]<int S>(int n, int fa, int nf) {
     static_for<X_U>([&]<int i>() {
       const int r = (tid >> 3) + 64 * i;
-      rx[i] = make_uint4(0, 0, 0, 0);
-      if (r < nf * V) {
-        const int fl = r / V, v = r - fl * V, f = fa + fl;
-        const int fs = fmul * f + par;  // source frame
-        if (cok && f >= 0 && fs < a.T_in)
-          rx[i] = *reinterpret_cast<const uint4*>(xin + (((long)n * a.T_in + fs) * V + v) * a.in_ld + ci0 + xcu * 8);
-      }
+      const int rr = r < nf * V ? r : 0;
+      const int fl = rr / V, v = rr - fl * V, f = fa + fl;
+      const int fs = min(max(fmul * f + par, 0), a.T_in - 1);
+      rx[S][i] = *reinterpret_cast<const uint4*>(xb + (((long)n * a.T_in + fs) * V + v) * a.in_ld);
     });
   };
-  auto store_x = [&](int fa, int nf) {  // slot f mod RS and its mirror
+  auto store_x = [&]<int S>(int fa, int nf) {  // slot f mod RS and its mirror; frames outside [0, T_in) zero
     static_for<X_U>([&]<int i>() {
       const int r = (tid >> 3) + 64 * i;
       if (r < nf * V) {
         const int fl = r / V, v = r - fl * V, f = fa + fl;
-        uint4 u = rx[i];
-        if (PRO == 1 && f >= 0 && fmul * f + par < a.T_in) {
+        const bool ok = xcok && f >= 0 && fmul * f + par < a.T_in;
+        uint4 u = ok ? rx[S][i] : make_uint4(0, 0, 0, 0);
+        if (PRO == 1 && ok) {
           float e[8];
           unpack16(u, e, (bf16*)nullptr);
 #pragma unroll
@@ -170,12 +177,12 @@ __global__ __launch_bounds__(NT, 1) void wgrad_wide_kernel(const stgcn_wgrad_des
       }
     });
   };
-  // the whole window of a range's / sample's first tile (F + 8 frames) in batches of F frames
-  auto stage_window = [&](int n, int f0) {
+  // the whole window of a range's / sample's first tile (F + 8 frames) in batches of F frames, through set S
+  auto stage_window = [&]<int S>(int n, int f0) {
     for (int fb = f0 - PADT; fb < f0 + F + PADT; fb += F) {
       const int nf = min(F, f0 + F + PADT - fb);
-      load_x(n, fb, nf);
-      store_x(fb, nf);
+      load_x.template operator()<S>(n, fb, nf);
+      store_x.template operator()<S>(fb, nf);
     }
   };
 
@@ -195,22 +202,32 @@ __global__ __launch_bounds__(NT, 1) void wgrad_wide_kernel(const stgcn_wgrad_des
   __syncthreads();
 
   const int tapb = V * PR;  // bytes between taps
-  for (int k = k_begin; k < k_end; ++k) {
+  const int nk = k_end - k_begin;
+  auto tile = [&]<int S>(int j) {
+    const int k = k_begin + j;
     const int n = k / tiles_n, tt = k - n * tiles_n, f0 = tt * F;
-    if (tt == 0 || k == k_begin) {  // range/sample start: dY of this tile and the whole input window
+    const bool next1 = j + 1 < nk && tt + 1 < tiles_n;  // tile j+1: same sample (else it restages itself)
+    if (tt == 0 || j == 0) {  // range/sample start: dY of this tile and the whole input window, then tile j+1's loads
       __syncthreads();
-      load_dy(n, f0);
-      store_dy(k & 1);
-      stage_window(n, f0);
+      load_dy.template operator()<S>(n, f0);
+      store_dy.template operator()<S>(k & 1, f0);
+      stage_window.template operator()<S>(n, f0);
       __syncthreads();
+      if constexpr (AHEAD2) {
+        load_dy.template operator()<S ^ 1>(n, f0 + F);
+        load_x.template operator()<S ^ 1>(n, f0 + F + PADT, F);
+      }
     }
-    // prefetch tile k+1 (same sample only: a new sample restages above)
-    const bool pre = k + 1 < k_end && tt + 1 < tiles_n;
-    if (pre) {
-      load_dy(n, f0 + F);
-      load_x(n, f0 + F + PADT, F);
+    // loads of tile j+2 (two ahead) or j+1 (one ahead), always issued: past the sample / range they re-read
+    // rows of this sample, unused
+    if constexpr (AHEAD2) {
+      load_dy.template operator()<S>(n, f0 + 2 * F);
+      load_x.template operator()<S>(n, f0 + 2 * F + PADT, F);
+    } else {
+      load_dy.template operator()<S ^ 1>(n, f0 + F);
+      load_x.template operator()<S ^ 1>(n, f0 + F + PADT, F);
     }
-    // ---- compute tile k: 72 tap-steps u = (ks, t), fragments read D steps ahead
+    // ---- compute tile j: NU tap-steps u = (ks, t), fragments read D steps ahead
     int s0 = (f0 - PADT) % g.RS;
     s0 += s0 < 0 ? g.RS : 0;
     const char* Y = sY + (k & 1) * DY_BYTES + wc * DY_PANEL + colb + rlo * PR;
@@ -230,12 +247,16 @@ __global__ __launch_bounds__(NT, 1) void wgrad_wide_kernel(const stgcn_wgrad_des
       constexpr int ks = u / KT, t = u % KT;
       acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fy[ks & 1], fx[u % (D + 1)], acc[t], 0, 0, 0);
     });
-    // ---- hand the prefetched tile to LDS (ring slots / dY buffer not read by tile k)
-    if (pre) {
-      store_dy((k + 1) & 1);
-      store_x(f0 + F + PADT, F);
+    // ---- hand tile j+1's set to LDS (ring slots / dY buffer not read by tile j)
+    if (next1) {
+      store_dy.template operator()<S ^ 1>((k + 1) & 1, f0 + F);
+      store_x.template operator()<S ^ 1>(f0 + F + PADT, F);
     }
     lds_barrier();
+  };
+  for (int j = 0; j < nk; j += 2) {
+    tile.template operator()<0>(j);
+    if (j + 1 < nk) tile.template operator()<1>(j + 1);
   }
 
   // ---- block partial -> slab [rg][t][co][ci]: lane holds ci = ci0 + 32 wi + (lane&31), co rows acc_row
@@ -261,7 +282,9 @@ struct WPlan {
 constexpr int RS_PART = 16;  // level-1 partials of slab_reduce
 
 // level 2 of the folded reduction: dW[2t + par][co][ci] += sum_r part[r][t][co][par*Cin + ci]
-__global__ void unfold_reduce2_kernel(const float* __restrict__ part, int RS, int Cout, int Cin, float* __restrict__ dw) {
+// (mode 1: dw overwritten in the nn.Conv2d order [Cout][Cin][9])
+__global__ void unfold_reduce2_kernel(const float* __restrict__ part, int RS, int Cout, int Cin, float* __restrict__ dw,
+                                      int mode) {
   const long E4 = 5L * Cout * 2 * Cin / 4;
   const long e4 = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e4 >= E4) return;
@@ -275,6 +298,14 @@ __global__ void unfold_reduce2_kernel(const float* __restrict__ part, int RS, in
   for (int r = 0; r < RS; ++r) {
     const float4 v = *reinterpret_cast<const float4*>(part + (long)r * 4 * E4 + e);
     acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  if (mode) {
+    float* d = dw + ((long)co * Cin + ci) * 9 + dt;
+    d[0] = acc.x;
+    d[9] = acc.y;
+    d[18] = acc.z;
+    d[27] = acc.w;
+    return;
   }
   float4* d = reinterpret_cast<float4*>(dw + ((long)dt * Cout + co) * Cin + ci);
   float4 o = *d;
@@ -330,7 +361,8 @@ WPlan wplan(const stgcn_wgrad_desc& a) {
 
 }  // namespace
 
-int slab_reduce_launch(const float* slab, int R, long E, float* part, float* dw, hipStream_t s);
+int slab_reduce_launch(const float* slab, int R, long E, float* part, float* dw, hipStream_t s, int mode, int Kt,
+                       long CoCi);
 int slab_reduce1_launch(const float* slab, int R, long E, float* part, hipStream_t s);
 
 long wgrad_wide_workspace(const stgcn_wgrad_desc& a, int dtype) {
@@ -353,10 +385,10 @@ int wgrad_wide_launch(const stgcn_wgrad_desc& a, int dtype, hipStream_t s) {
   if (hipGetLastError() != hipSuccess) return STGCN_EHIP;
   const long E = (long)p.ktap * a.Cout * p.g.cin_f;
   float* part = p.g.slab + (long)p.g.R * E;
-  if (!p.g.fold) return slab_reduce_launch(p.g.slab, p.g.R, E, part, a.dw, s);
+  if (!p.g.fold) return slab_reduce_launch(p.g.slab, p.g.R, E, part, a.dw, s, a.out_mode, 9, (long)a.Cout * a.Cin);
   const int RS = slab_reduce1_launch(p.g.slab, p.g.R, E, part, s);
   if (RS < 0) return -RS;
   hipLaunchKernelGGL(unfold_reduce2_kernel, dim3((unsigned)((E / 4 + 255) / 256)), dim3(256), 0, s, (const float*)part,
-                     RS, a.Cout, a.Cin, a.dw);
+                     RS, a.Cout, a.Cin, a.dw, a.out_mode);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }

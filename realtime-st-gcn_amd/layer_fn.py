@@ -208,6 +208,25 @@ def fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, su
     return K.bn_apply(z, sc2, sh2, N * T * V, Cout, res_mode=1 if residual else 0, r=x if residual else None)
 
 
+def _stats_arena(cache, dev, dtype, shapes, route):
+    """The BatchNorm partial-statistics buffers of a layer's forward.  The producing GEMM epilogues overwrite
+    the same (row block, channel) entries on every call of one route and shape, and the entries they never
+    write (rows past the kernel's row-block count, padded channels) must read as zero for bn_finalize — so a
+    buffer kept per (device, dtype, shapes, route) in the layer's cache is zero-filled ONCE, not per forward.
+    Streams: consumed by the layer's own bn_finalize right after, in stream order; the layer's next forward
+    writes it again only after that.  Without a cache (bare calls): a fresh zeroed arena."""
+    if cache is None:
+        return K.zeros_arena(dev, *shapes)
+    key = ("bn_stats", str(dev), dtype, tuple(map(tuple, shapes)), route)
+    st = cache.get(key)
+    if st is None:
+        old = [k for k in cache if isinstance(k, tuple) and k[:1] == ("bn_stats",)]
+        for k in old[:-3]:  # keep a few shapes (config 4 alternates 64- and 65-window units)
+            del cache[k]
+        st = cache[key] = K.zeros_arena(dev, *shapes)
+    return st
+
+
 @K.on_tensor_device
 class StgcnLayerFunction(torch.autograd.Function):
     """Autograd node for the whole StgcnLayer (BN or LN variant)."""
@@ -246,7 +265,7 @@ class StgcnLayerFunction(torch.autograd.Function):
                 else K.row_blocks(M1, Cout)
             st_shapes = [(rb1, cpo, 4),
                          (K.row_blocks(M2, Cout), cpo, 4)] + ([(K.row_blocks(M2, Cout), cpo, 4)] if res_conv else [])
-            st_all = K.zeros_arena(dev, *st_shapes)
+            st_all = _stats_arena(cfg[8] if len(cfg) > 8 else None, dev, x.dtype, st_shapes, (tiled, gather))
             st1, st2 = st_all[0], st_all[1]
             str_ = st_all[2] if res_conv else None
         # ---- residual branch: independent of the graph conv -> temporal conv chain until the output norm,
@@ -366,10 +385,16 @@ class StgcnLayerFunction(torch.autograd.Function):
         M1, M2 = N * T * V, N * T_out * V
         packs = ctx.cfg[9] if len(ctx.cfg) > 9 else None
         grads = {}
-        # every fp32 accumulation target of this backward from one zero fill
-        zshapes = [(kt, Cout, Cout), (1, Cout, Cin), (P * Cout, Cin), (P, V, V),
-                   ((N, V, Cout) if A32.dim() == 4 else (V, Cout))]
-        z_dwt, z_dwr, z_dwg, z_dA, z_S = K.zeros_arena(dev, *zshapes)
+        # the temporal / residual weight gradients come back in nn.Conv2d order, overwritten (conv_wgrad_w); the
+        # graph-conv accumulation targets (dW, dA, per-joint row sums) are zero-filled only on the routes that
+        # accumulate into them (one fill for all three)
+        zl = {}
+
+        def zero_targets():
+            if not zl:
+                zl["t"] = K.zeros_arena(dev, (P * Cout, Cin), (P, V, V),
+                                        (N, V, Cout) if A32.dim() == 4 else (V, Cout))
+            return zl["t"]
         side = _side_stream(dev)  # weight-gradient branch (joined before returning)
 
         # ---- through relu(norm2(u) + res): dz = dy * [y > 0]
@@ -422,8 +447,8 @@ class StgcnLayerFunction(torch.autograd.Function):
             wrTp, cq, kq = packs.wrT if packs is not None else \
                 K.pack_weight(wr.detach().float().view(Cout, Cin).t().unsqueeze(0), dtype)
             with _fork(side):
-                grads["wr"] = K.conv_wgrad(x, dr, Cin, Cout, T, T_out, Kt=1, stride=stride, pad=0,
-                                           dw=z_dwr).view(Cout, Cin, 1, 1)
+                grads["wr"] = K.conv_wgrad_w(x, dr, Cin, Cout, T, T_out, Kt=1, stride=stride,
+                                             pad=0).view(Cout, Cin, 1, 1)
             K.conv_rows(dr, wrTp, Cout, Cin, cq, kq, T_out, T, Kt=1, stride=stride, pad=0, trans=True, out=dx)
             dx_written = True
         elif residual and not fused:
@@ -439,8 +464,8 @@ class StgcnLayerFunction(torch.autograd.Function):
         else:
             pro1 = dict(pro=2, pro_a=_flat_ln(n1w), pro_b=_flat_ln(n1b), pro_stats=ls1)
         with _fork(side):
-            dwt = K.conv_wgrad(g, du, Cout, Cout, T, T_out, Kt=kt, stride=stride, pad=pad, dw=z_dwt, **pro1)
-            grads["wt"] = dwt.permute(1, 2, 0).unsqueeze(-1)  # [Kt][co][ci] -> (co, ci, Kt, 1)
+            grads["wt"] = K.conv_wgrad_w(g, du, Cout, Cout, T, T_out, Kt=kt, stride=stride, pad=pad,
+                                         **pro1).unsqueeze(-1)  # (co, ci, Kt, 1)
         dh = K.conv_rows(du, wtTp, Cout, Cout, cq, kq, T_out, T, Kt=kt, stride=stride, pad=pad, trans=True)
         if not bt_done:
             grads["bt"] = K.bn_bwd_reduce(du, M2, Cout)[:, 0].clone()
@@ -471,13 +496,16 @@ class StgcnLayerFunction(torch.autograd.Function):
             with _fork(side):
                 fuse_s = A32.dim() == 3 and K.gconv_wgrad_rowsum_ok(sup, Cin, Cout, dtype)
                 dense_dA = ctx.cfg[6] and ctx.needs_input_grad[1]
-                dweff = K.gconv_wgrad(x, dg, sup, Cin, Cout, rowsum=z_S if fuse_s else None)
+                # row sums: overwritten by the joint-grouped wgrad kernel
+                S_rows = torch.empty((V, Cout), dtype=torch.float32, device=dev) if fuse_s else None
+                dweff = K.gconv_wgrad(x, dg, sup, Cin, Cout, rowsum=S_rows)
                 if fuse_s and not dense_dA and K.gconv_finish_bias_ok(A32, sup):
                     # dW, dA (support + bias through A) and db in two launches, outputs overwritten
                     dwg2, dA, grads["bg"] = K.gconv_finish_bias(dweff, A32, wg2, sup, Cout, Cin,
-                                                                bg.detach().float().contiguous(), z_S)
+                                                                bg.detach().float().contiguous(), S_rows)
                     dA_done = True
                 else:
+                    z_dwg, z_dA, z_S = zero_targets()
                     dwg2, dA = K.gconv_finish(dweff, A32, wg2, sup, Cout, Cin, dW=z_dwg, dA=z_dA)
                     dA_done = False
                 grads["wg"] = dwg2.view(P * Cout, Cin, 1, 1)
@@ -488,7 +516,7 @@ class StgcnLayerFunction(torch.autograd.Function):
                     wgTp, cq, kq = K.pack_weight(wgTd, dtype)
                     dA = K.amix_dA(x, K.conv_rows(dg, wgTp, Cout, P * Cin, cq, kq, T, T), A32)
                 if not dA_done:
-                    dA = _bias_through_A(dA, A32, bg, bgp, dg, z_S if fuse_s else None, z_S, M1, Cout, V, grads)
+                    dA = _bias_through_A(dA, A32, bg, bgp, dg, S_rows, zero_targets()[2], M1, Cout, V, grads)
             if K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype, trans=True):  # dx = sum_p A_p-mix(dg) W_p^T, fused (gcn_tile.hip)
                 wdf = wg.detach().float().view(P, Cout, Cin).permute(2, 0, 1).reshape(Cin, P * Cout)
                 wimgT, cq, kwT = K.pack_gcn_weight(wdf, dtype)
@@ -506,13 +534,12 @@ class StgcnLayerFunction(torch.autograd.Function):
             dA = K.amix_dA(x, DW, A32)
             dwg = K.conv_wgrad(XA, dg, P * Cin, Cout, T, T, Kt=1)              # [1][Cout][P*Cin]
             grads["wg"] = dwg.view(Cout, P, Cin).permute(1, 0, 2).reshape(P * Cout, Cin, 1, 1)
-            dA = _bias_through_A(dA, A32, bg, bgp, dg, None, z_S, M1, Cout, V, grads)
+            dA = _bias_through_A(dA, A32, bg, bgp, dg, None, zero_targets()[2], M1, Cout, V, grads)
         if side is not None:  # join the weight-gradient branch
             main = torch.cuda.current_stream(dev)
             main.wait_stream(side)
-            # tensors allocated on the side stream and used on the main one (the others are views of the
-            # zero arena, allocated on the main stream)
-            for t in (grads.get("bg"), dA):
+            # tensors allocated on the side stream and used on the main one
+            for t in (grads.get("bg"), grads.get("wg"), grads.get("wt"), grads.get("wr"), dA):
                 if t is not None:
                     t.record_stream(main)
 
@@ -631,7 +658,7 @@ class Conv1x1Function(torch.autograd.Function):
         wT, cq, kq = ctx.packT if ctx.packT is not None else \
             K.pack_weight(w.detach().float().view(Cout, Ci).t().unsqueeze(0), dtype)
         dx = K.conv_rows(dy, wT, Cout, Cin, cq, kq, T, T, trans=True)
-        dw = K.conv_wgrad(x, dy, Cin, Cout, T, T).view(Cout, Cin, 1, 1)
+        dw = K.conv_wgrad_w(x, dy, Cin, Cout, T, T).view(Cout, Cin, 1, 1)
         if Ci < Cin:
             dw = dw[:, :Ci]
         db = K.bn_bwd_reduce(dy, N * T * V, Cout)[:, 0]
@@ -971,7 +998,7 @@ class RtOfflineLayerFunction(torch.autograd.Function):
             wrT, cq, kq = K.pack_weight(wr.detach().float().view(Cout, Cin).t().reshape(1, Cin, Cout), dtype)
             K.conv_rows(dr, wrT, Cout, Cin, cq, kq, L, L, trans=True, out=dx)
             dx_written = True
-            g["wr"] = K.conv_wgrad(x, dr, Cin, Cout, L, L).view(Cout, Cin, 1, 1)
+            g["wr"] = K.conv_wgrad_w(x, dr, Cin, Cout, L, L).view(Cout, Cin, 1, 1)
         elif residual:
             K.bn_bwd_apply(dq, M, Cin, dx)  # dx = dq
             dx_written = True

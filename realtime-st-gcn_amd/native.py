@@ -271,6 +271,29 @@ def conv_wgrad(x, dy, Cin, Cout, T_in, T_out, Kt=1, stride=1, pad=0, pro=0, pro_
     return dw
 
 
+def conv_wgrad_w(x, dy, Cin, Cout, T_in, T_out, Kt=1, stride=1, pad=0, pro=0, pro_a=None, pro_b=None, pro_stats=None):
+    """The weight gradient as a FRESH fp32 tensor in nn.Conv2d weight order (Cout, Cin, Kt): the workspace paths
+    write it directly (out_mode 1: no zero fill, no permute copy); the others accumulate into zeros and permute."""
+    N, V = x.shape[0], x.shape[3]
+    d = L.WgradDesc()
+    d.in_, d.dy = x.data_ptr(), dy.data_ptr()
+    d.pro_a, d.pro_b, d.pro_stats = L.ptr(pro_a), L.ptr(pro_b), L.ptr(pro_stats)
+    d.N, d.T_in, d.T_out, d.V, d.Cin, d.Cout, d.Kt, d.stride, d.pad, d.pro = \
+        N, T_in, T_out, V, Cin, Cout, Kt, stride, pad, pro
+    d.in_ld, d.dy_ld = rows_ld(x), rows_ld(dy)
+    code = L.dtype_code(x.dtype)
+    nbytes = L.lib().stgcn_conv_wgrad_workspace(d, code)
+    if nbytes <= 0:
+        return conv_wgrad(x, dy, Cin, Cout, T_in, T_out, Kt, stride, pad, pro, pro_a, pro_b,
+                          pro_stats).permute(1, 2, 0).contiguous()
+    work = torch.empty(nbytes // 4, dtype=torch.float32, device=x.device)
+    d.work, d.work_bytes = work.data_ptr(), nbytes
+    dw = torch.empty((Cout, Cin, Kt), dtype=torch.float32, device=x.device)
+    d.dw, d.out_mode = dw.data_ptr(), 1
+    L.check(L.lib().stgcn_conv_wgrad(d, code, L.stream()), "conv_wgrad")
+    return dw
+
+
 def _amix_desc(x, out, A, N, T, V, P, Cin, accumulate=False, x_ld=None, out_ld=None):
     A = _dense(A)
     d = L.AmixDesc()

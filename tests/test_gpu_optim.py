@@ -80,7 +80,7 @@ def test_adam_state_dict_round_trip(P):
         o_got.step()
     for a, b in zip(ref, got):
         torch.testing.assert_close(b.detach(), a.detach(), **TOL)
-    back = torch.optim.Adam([p.clone() for p in got], lr=1e-3)
+    back = torch.optim.Adam([p.detach().clone() for p in got], lr=1e-3)
     back.load_state_dict(o_got.state_dict())  # package -> torch
     for pa, pb in zip(o_got.param_groups[0]["params"], back.param_groups[0]["params"]):
         sa, sb = o_got.state[pa], back.state[pb]
