@@ -124,9 +124,8 @@ __global__ __launch_bounds__(256, LN ? 1 : 2) void wgrad_tile_kernel(const stgcn
   auto x_fo = [&](int i) { return x_fv[i] >> 5; };
   auto x_v = [&](int i) { return x_fv[i] & 31; };
 
-  // Two register sets of staged loads: tile j's in set j & 1.  Tile j + 2's loads are issued at the start of
-  // tile j, tile j + 1's set goes to LDS at its end, so two tiles of MFMA work cover each load's latency (one
-  // tile's 32-40 k-steps per wave did not; AHEAD2 below).  Loads are unconditional (invalid units read an in-bounds row of
+  // Two register sets of staged loads: tile j's in set j & 1, tile j + 1's set goes to LDS at the end of tile j;
+  // with AHEAD2 (below) tile j + 2's loads are issued at the start of tile j.  Loads are unconditional (invalid units read an in-bounds row of
   // the same sample and are zeroed at the store through a per-set validity mask), so the count in flight is
   // fixed and the wait before storing set j+1 leaves tile j+2's loads pending.
   static_assert(DY_PT + X_PT <= 32, "validity mask");
@@ -237,8 +236,13 @@ __global__ __launch_bounds__(256, LN ? 1 : 2) void wgrad_tile_kernel(const stgcn
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  // two tiles ahead for the stride-1 convs; the stride-2 instantiations keep one (a second live set spills)
-  constexpr bool AHEAD2 = S == 1;
+  // two tiles ahead: measured equal or slower here (config-2 step 8.037 vs 8.027 ms with one tile ahead, 3
+  // interleaved runs; the C = 64 wgrad's 2 blocks per CU already hide the loads), so off; the stride-2
+  // instantiations could not take it anyway (a second live set spills).  -DSTGCN_WT_AHEAD2=1: A/B builds.
+#ifndef STGCN_WT_AHEAD2
+#define STGCN_WT_AHEAD2 0
+#endif
+  constexpr bool AHEAD2 = STGCN_WT_AHEAD2 && S == 1;
   const int nt = t_end - t_begin;
   if (nt > 0) {
     load.template operator()<0>(t_begin);

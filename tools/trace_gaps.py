@@ -1,6 +1,6 @@
 """GPU busy time vs wall time per training step from a rocprofv3 kernel trace (--kernel-trace, csv).
 
-Steps are delimited by the optimizer (the fused Adam multi_tensor_apply launches end every step).  For the
+Steps are delimited by the optimizer (the Adam launch(es) end every step: the package's adam_kernel, or torch's multi_tensor_apply).  For the
 last `n` complete steps it prints: wall time (first kernel start -> last kernel end), GPU busy time (union of
 all kernel intervals, so overlapping streams count once), the sum of kernel durations, and the launch count.
 busy << wall means the step waits on the host (launch-bound); sum >> busy means the streams overlap.
@@ -26,7 +26,7 @@ def steps(ks):
     """Split the trace after the last Adam launch of each group of consecutive Adam launches."""
     out, cur, in_adam = [], [], False
     for k in ks:
-        adam = "multi_tensor_apply" in k[2] or "fused_adam" in k[2].lower()
+        adam = "multi_tensor_apply" in k[2] or "fused_adam" in k[2].lower() or "adam_kernel" in k[2]
         if in_adam and not adam:
             out.append(cur)
             cur = []
