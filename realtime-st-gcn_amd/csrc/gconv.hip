@@ -791,9 +791,10 @@ __global__ __launch_bounds__(COB / 16 * 64, COB == 64 ? 3 : 1) void gconv_wgrad2
 // while one is consumed instead of one.  The register-staged kernel kept at most one tile (~16 KB)
 // per block in flight and sat at ~13 % of the MFMA peak, latency-bound on L2/MALL.  Body per degree
 // (DEG = deg[w], a block-uniform value) so the vmcnt counts are immediates.
-constexpr int W3_LDS = 80 * 1024;  // two blocks per CU
+// LDS per block: 80 KB (two blocks per CU) or, for the direct plans (R = 1: fewer, longer blocks), 160 KB for a
+// deeper ring (one block per CU)
 constexpr int w3_stage(int deg) { return (2 + 2 * deg) * 32 * WPR; }
-constexpr int w3d(int deg) { return W3_LDS / w3_stage(deg) > 8 ? 8 : W3_LDS / w3_stage(deg); }
+constexpr int w3d(int deg, int lds) { return lds / w3_stage(deg) > 8 ? 8 : lds / w3_stage(deg); }
 
 template <int N, typename F>
 DEV void sfor(F&& f) {
@@ -813,9 +814,9 @@ DEV void glds16m(const void* src, unsigned lds_off) {
                : "=&s"(saved) : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_off)) : "memory");
 }
 
-template <int DEG>
+template <int DEG, int LDSB>
 DEV void wgrad3_body(const stgcn_gconv_wgrad_desc& a, const WGG& g, char* smem, int w, int rr, int grp) {
-  constexpr int D = w3d(DEG), PANEL = 32 * WPR, STAGE = w3_stage(DEG), NU = 1 + DEG;
+  constexpr int D = w3d(DEG, LDSB), PANEL = 32 * WPR, STAGE = w3_stage(DEG), NU = 1 + DEG;
   static_assert(D >= 3 && (D - 2) * NU <= 63, "ring");
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int cq = wave & 1, ch = wave >> 1;  // co half (32), ci half (32)
@@ -913,7 +914,9 @@ DEV void wgrad3_body(const stgcn_gconv_wgrad_desc& a, const WGG& g, char* smem, 
     }
 }
 
-__global__ __launch_bounds__(256, 2) void gconv_wgrad3_kernel(const stgcn_gconv_wgrad_desc a, const WGG g) {
+template <int LDSB>
+__global__ __launch_bounds__(256, LDSB > 80 * 1024 ? 1 : 2) void gconv_wgrad3_kernel(const stgcn_gconv_wgrad_desc a,
+                                                                                    const WGG g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int ngrp = g.nco * g.nci;
   const int w = blockIdx.x / (ngrp * g.R);
@@ -939,11 +942,11 @@ __global__ __launch_bounds__(256, 2) void gconv_wgrad3_kernel(const stgcn_gconv_
     __syncthreads();
   }
   switch (a.deg[wj]) {
-    case 1: wgrad3_body<1>(a, g, smem, wj, rr, grp); break;
-    case 2: wgrad3_body<2>(a, g, smem, wj, rr, grp); break;
-    case 3: wgrad3_body<3>(a, g, smem, wj, rr, grp); break;
-    case 4: wgrad3_body<4>(a, g, smem, wj, rr, grp); break;
-    case 5: wgrad3_body<5>(a, g, smem, wj, rr, grp); break;
+    case 1: wgrad3_body<1, LDSB>(a, g, smem, wj, rr, grp); break;
+    case 2: wgrad3_body<2, LDSB>(a, g, smem, wj, rr, grp); break;
+    case 3: wgrad3_body<3, LDSB>(a, g, smem, wj, rr, grp); break;
+    case 4: wgrad3_body<4, LDSB>(a, g, smem, wj, rr, grp); break;
+    case 5: wgrad3_body<5, LDSB>(a, g, smem, wj, rr, grp); break;
     default:  // deg 0: no pairs (the reduction skips j >= deg); the row sums still come from here
       if (g.rowpart != nullptr && grp / g.nco == 0 && threadIdx.x < 64) {
         const int co = (grp % g.nco) * 64 + threadIdx.x;
@@ -1239,9 +1242,15 @@ int w2_cob(const stgcn_gconv_wgrad_desc& a) {
 // kernel measured 74 vs 82 us
 bool w3_ok(const stgcn_gconv_wgrad_desc& a) { return !(a.Cin == 64 && a.Cout == 128); }
 
-// DMA-ring block target once a joint has several channel groups (C >= 128); a plan with R = 1 (one row range
-// per block: the 400 groups of C = 256) writes dWeff and the row sums directly, with no slab and no reduction
-// launch.  Config-2 step, interleaved A/B (3 x 100 steps): target 256 8.16 ms, 512 8.19, 1024 8.25
+// DMA-ring block target once a joint has several channel groups: 512 at C = 128 (100 groups: R = 6, 67 + 12 us
+// with the slab reduction, against 87 + 9 at R = 3), 256 from 200 groups up (128 -> 256: R = 2, 114 + 13 us vs
+// 127 + 15 at R = 3; C = 256: R = 1).  A plan with R = 1 (one row range per block) writes dWeff and the row
+// sums directly, with no slab and no reduction launch (C = 256: 114-123 us vs 117 + 25 us at R = 2)
+// STGCN_W3_DEEP (A/B build flag): the direct plans with 160 KB of LDS, one block per CU and a deeper ring —
+// measured slower in the step (8.09 vs 8.01 ms, 3 interleaved runs), off
+#ifndef STGCN_W3_DEEP
+#define STGCN_W3_DEEP 0
+#endif
 #ifndef STGCN_W3_WIDE_TARGET
 #define STGCN_W3_WIDE_TARGET 256
 #endif
@@ -1254,7 +1263,7 @@ WGG wplan2(const stgcn_gconv_wgrad_desc& a, int cob) {
   const long target = cob == 64 ? 512 : 256;  // COB 64: 3 register-staged / 2 DMA-ring blocks fit a CU
   // DMA ring: block target by the group count, measured per layer (targets 512 / 1024 / 2048): C = 64
   // (25 groups) 49 / 40 / 56 us, C = 128 64 / 81 / 75 us, C = 256 108 / 113 / 130 us
-  const long t3 = groups <= 32 ? 1024 : STGCN_W3_WIDE_TARGET;
+  const long t3 = groups <= 32 ? 1024 : groups < 200 ? 512 : STGCN_W3_WIDE_TARGET;
   long R = (cob == 64 && w3_ok(a)) ? (t3 + groups - 1) / groups : (target + groups - 1) / groups;
   if (R > g.ntile) R = g.ntile;
   if (R < 1) R = 1;
@@ -1357,8 +1366,9 @@ int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s
       g.slab = reinterpret_cast<float*>(a.work);
       g.rowpart = a.rowsum ? g.slab + (long)g.R * E : nullptr;
     }
-    const size_t lds = ring ? (size_t)W3_LDS : 2 * (size_t)(cob / 32 + 2 * J2) * w2m(cob) * WPR;
-    auto* k = ring ? gconv_wgrad3_kernel : gconv_wgrad2_kernel<64>;
+    const bool deep = direct && STGCN_W3_DEEP;  // one block per CU, deeper ring
+    const size_t lds = ring ? (size_t)(deep ? 160 : 80) * 1024 : 2 * (size_t)(cob / 32 + 2 * J2) * w2m(cob) * WPR;
+    auto* k = ring ? (deep ? gconv_wgrad3_kernel<160 * 1024> : gconv_wgrad3_kernel<80 * 1024>) : gconv_wgrad2_kernel<64>;
     if (stgcn_lds_attr((const void*)k, 160 * 1024, s)) return STGCN_EHIP;
     const long blocks = (long)a.V * g.nco * g.nci * g.R;
     hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(ring ? 256 : cob / 16 * 64), lds, s, a, g);
