@@ -252,16 +252,19 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(const stgcn_bn_
   }
 }
 
-Geo geo(long M, int C, int vec) {
+// block target of the apply pass (the reduce pass keeps 1024: its partials are folded by sum4_kernel, and it
+// measured slower with fewer blocks); A/B build flag
+#ifndef STGCN_BN_APPLY_TB
+#define STGCN_BN_APPLY_TB 512
+#endif
+Geo geo(long M, int C, int vec, long tb = 1024) {
   Geo g;
   g.CU = C / vec;
   g.RPI = 256 / g.CU;
-  // >= 2 iterations of UNR_MAX rows per thread and at most ~1024 blocks (partials folded by sum4_kernel); one
-  // row split for every UNR, so the reduce and apply passes of one BN see the same blocks
+  // >= 2 iterations of UNR_MAX rows per thread and at most ~tb blocks
   const long step = (long)g.RPI * UNR_MAX;
-  // block target: 512 / 1024 / 2048 measured 1.67 / 1.68 / 1.8 ms per step for all fused BN backward passes +
-  // sum4 folds (512 speeds up apply, slows reduce)
-  constexpr long tb = 1024;
+  // block target (both passes): 512 / 1024 / 2048 measured 1.67 / 1.68 / 1.8 ms per step for all fused BN
+  // backward passes + sum4 folds (512 speeds up apply, slows reduce)
   long it = (M + step * tb - 1) / (step * tb);
   if (it < 2) it = 2;
   g.rpb = step * it;
@@ -278,8 +281,8 @@ bool fits(const stgcn_bn_bwd_desc& a, int dtype, int& vec) {
 }
 
 long bn_bwd_fused_work_floats_impl(long M, int C, int dtype) {
-  const Geo g = geo(M, C, dtype == 1 ? 8 : 4);
-  return (long)g.nb * C * 4;
+  const Geo g = geo(M, C, dtype == 1 ? 8 : 4), ga = geo(M, C, dtype == 1 ? 8 : 4, STGCN_BN_APPLY_TB);
+  return (long)(g.nb > ga.nb ? g.nb : ga.nb) * C * 4;
 }
 
 template <typename T, int VEC, int MASK, bool X2>
@@ -341,7 +344,7 @@ int bn_bwd_fused_apply_launch(const stgcn_bn_bwd_desc& a, int dtype, hipStream_t
   if (!fits(a, dtype, vec) || !a.out1 || !a.sums || !a.x1 || !a.mref || (a.osum && !a.work) ||
       (a.mask != 1 && a.mask != 2))
     return STGCN_EBADSHAPE;
-  const Geo g = geo(a.M, a.C, vec);
+  const Geo g = geo(a.M, a.C, vec, STGCN_BN_APPLY_TB);
   if (dtype == 1) apply_dispatch<bf16, 8>(a, g, s);
   else apply_dispatch<float, 4>(a, g, s);
   if (a.osum)

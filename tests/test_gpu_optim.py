@@ -108,3 +108,38 @@ def test_adam_model_step(P):
         o_got.step()
     for a, p in zip(ref, params):
         torch.testing.assert_close(p.detach(), a.detach(), **TOL)
+
+
+def test_adam_graph_replay(P):
+    """optim.Adam captured in a HIP graph (as parallel.GraphedStep / bench.py --graph capture it): replaying the
+    captured step with new gradients copied into the same .grad tensors gives bit-identical parameters, moments
+    and step counts to eager steps (device step counters; gradient pointers baked into the captured launch)."""
+    ref = [p.clone().requires_grad_(True) for p in _params(2)]
+    got = [p.clone().requires_grad_(True) for p in _params(2)]
+    o_ref = P.optim.Adam(ref, lr=1e-3)
+    o_got = P.optim.Adam(got, lr=1e-3)
+    grads = [_grads(ref, 40 + it) for it in range(4)]
+    for a, b, g in zip(ref, got, grads[0]):  # first step eager on both (allocates the flat state)
+        a.grad, b.grad = g.clone(), g.clone()
+    o_ref.step()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        o_got.step()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=s):
+            o_got.step()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    # capture does not execute: one eager step so far on both
+    for it in range(1, 4):
+        for a, b, g in zip(ref, got, grads[it]):
+            a.grad.copy_(g)
+            b.grad.copy_(g)
+        o_ref.step()
+        graph.replay()
+    torch.cuda.synchronize()
+    for a, b in zip(ref, got):
+        assert torch.equal(a.detach(), b.detach())
+        assert torch.equal(o_ref.state[a]["exp_avg_sq"], o_got.state[b]["exp_avg_sq"])
+        assert float(o_ref.state[a]["step"]) == float(o_got.state[b]["step"]) == 4.0
