@@ -4,8 +4,8 @@ The reference trains with ``torch.optim.Adam(model.parameters(), lr=learning_rat
 steps it every ``batch_size`` trials (processor.py:561).  ``Adam`` here is a drop-in for that optimizer: the same
 constructor arguments, update rule, ``param_groups`` / ``state`` (``step``, ``exp_avg``, ``exp_avg_sq``) and
 state_dict, but the moments of a parameter group live in two flat fp32 buffers and the whole group is updated
-by ONE kernel launch (torch's fused multi-tensor Adam takes three launches for the config-2 model plus the
-step-counter updates).  The step counters live on the device (one slot per 2048-element block), so a step
+by ONE kernel launch per 256 tensors (torch's fused multi-tensor Adam takes three launches for the config-2
+model plus the step-counter updates).  The step counters live on the device (one slot per 2048-element block), so a step
 can be captured into a HIP graph (``parallel.GraphedStep``) without ``capturable`` bookkeeping.
 No CPU fallback: parameters must be fp32 HIP tensors.
 """
@@ -17,6 +17,16 @@ import torch
 
 from . import _lib as L
 from . import native as K
+
+MAXT = 256  # STGCN_ADAM_MAXT: tensors per launch (gradient pointers travel as kernel arguments)
+
+
+def _offsets(fs):
+    out, o = [], 0
+    for f in fs:
+        out.append(o)
+        o += f.n
+    return out
 
 
 class _Flat:
@@ -71,12 +81,14 @@ class Adam(torch.optim.Optimizer):
         self._flat = {}
 
     def _flat_of(self, gi, group):
+        """The flat states of a group: one per chunk of <= STGCN_ADAM_MAXT tensors (one launch each)."""
         params = group["params"]
-        f = self._flat.get(gi)
-        if f is None or f.key != tuple(p.data_ptr() for p in params) or f.n != len(params):
-            f = _Flat(params, self.state)
-            self._flat[gi] = f
-        return f
+        fs = self._flat.get(gi)
+        if fs is None or sum(f.n for f in fs) != len(params) or \
+                any(f.key != tuple(p.data_ptr() for p in params[o:o + f.n]) for f, o in zip(fs, _offsets(fs))):
+            fs = [_Flat(params[o:o + MAXT], self.state) for o in range(0, len(params), MAXT)]
+            self._flat[gi] = fs
+        return fs
 
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
@@ -97,22 +109,22 @@ class Adam(torch.optim.Optimizer):
             params = group["params"]
             if not params:
                 continue
-            f = self._flat_of(gi, group)
             keep = []
-            for k, p in enumerate(params):
-                g = p.grad
-                if g is None:
-                    f.grads[k] = None
-                    continue
-                if g.is_sparse or g.dtype != torch.float32 or g.shape != p.shape:
-                    raise RuntimeError("stgcn_amd.optim.Adam: dense fp32 gradients of the parameter's shape only")
-                if not g.is_contiguous():
-                    g = g.contiguous()
-                    keep.append(g)
-                f.grads[k] = g.data_ptr()
             b1, b2 = group["betas"]
-            with K.device_of(params[0]):
-                L.check(L.lib().stgcn_adam_step(f.table.data_ptr(), f.n, f.nblocks, f.grads, f.steps.data_ptr(),
-                                                float(group["lr"]), float(b1), float(b2), float(group["eps"]),
-                                                float(group["weight_decay"]), L.stream()), "adam_step")
+            for f, o in zip(self._flat_of(gi, group), _offsets(self._flat[gi])):
+                for k, p in enumerate(params[o:o + f.n]):
+                    g = p.grad
+                    if g is None:
+                        f.grads[k] = None
+                        continue
+                    if g.is_sparse or g.dtype != torch.float32 or g.shape != p.shape:
+                        raise RuntimeError("stgcn_amd.optim.Adam: dense fp32 gradients of the parameter's shape only")
+                    if not g.is_contiguous():
+                        g = g.contiguous()
+                        keep.append(g)
+                    f.grads[k] = g.data_ptr()
+                with K.device_of(params[0]):
+                    L.check(L.lib().stgcn_adam_step(f.table.data_ptr(), f.n, f.nblocks, f.grads, f.steps.data_ptr(),
+                                                    float(group["lr"]), float(b1), float(b2), float(group["eps"]),
+                                                    float(group["weight_decay"]), L.stream()), "adam_step")
         return loss

@@ -143,3 +143,23 @@ def test_adam_graph_replay(P):
         assert torch.equal(a.detach(), b.detach())
         assert torch.equal(o_ref.state[a]["exp_avg_sq"], o_got.state[b]["exp_avg_sq"])
         assert float(o_ref.state[a]["step"]) == float(o_got.state[b]["step"]) == 4.0
+
+
+def test_adam_many_tensors(P):
+    """More tensors than one launch carries (STGCN_ADAM_MAXT = 256; the AAGCN 2-stream model has more): the
+    group is split into launches, same update as torch."""
+    g0 = torch.Generator().manual_seed(11)
+    shapes = [(int(torch.randint(1, 300, (1,), generator=g0)),) for _ in range(300)]
+    base = [torch.randn(s, generator=g0).to(DEV) for s in shapes]
+    ref = [p.clone().requires_grad_(True) for p in base]
+    got = [p.clone().requires_grad_(True) for p in base]
+    o_ref, o_got = torch.optim.Adam(ref, lr=5e-4), P.optim.Adam(got, lr=5e-4)
+    for it in range(3):
+        for a, b in zip(ref, got):
+            g = torch.randn(a.shape, generator=g0).to(DEV)
+            a.grad, b.grad = g.clone(), g.clone()
+        o_ref.step()
+        o_got.step()
+    for a, b in zip(ref, got):
+        torch.testing.assert_close(b.detach(), a.detach(), **TOL)
+        assert float(o_got.state[b]["step"]) == 3.0
