@@ -192,6 +192,75 @@ def layer_roofline(pkg, dev, reps=20, norm="BatchNorm"):
                                             / BF16_DENSE_PEAK_TFLOPS, 4)}}
 
 
+RIDGE_FLOP_PER_BYTE = BF16_DENSE_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)  # ~312 flop/B
+
+
+def kernel_table(K, step, nsteps, top=4):
+    """The step's kernels by time: every launch of the instrumented wrappers (native.KTIME_HOOK: temporal and
+    1x1 convs, their weight gradients, graph conv fwd / data grad / weight grad + finish, BatchNorm apply and
+    backward passes) bracketed by HIP events on its launch stream, over ``nsteps`` eager steps run after the
+    timed region (recording ~150 event pairs per step costs host time, so not inside it).  Grouped by kernel
+    family: time per step, algorithmic work per step (flops of the reference's formula for the GEMM-shaped
+    families, bytes of the operands read + written once for the streaming ones), achieved rate and fraction of
+    the roof the family's arithmetic intensity puts it under (MFMA above the ridge, HBM below)."""
+    recs = []
+
+    def hook(tag, phase, work):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream())
+        recs.append((tag, phase, ev, work))
+
+    K.KTIME_HOOK = hook
+    try:
+        for _ in range(nsteps):
+            step()
+        torch.cuda.synchronize()
+    finally:
+        K.KTIME_HOOK = None
+    fam = {}
+    open_ = {}
+    for tag, phase, ev, work in recs:
+        if phase == "start":
+            open_[tag] = (ev, work)
+            continue
+        e0, w = open_.pop(tag)
+        _, f, shape = tag.split(":", 2)
+        d = fam.setdefault(f, {"ms": 0.0, "n": 0, "flop": 0.0, "bytes": 0.0, "shapes": {}})
+        ms = e0.elapsed_time(ev)
+        d["ms"] += ms
+        d["n"] += 1
+        d["flop"] += w["flop"] or 0.0
+        d["bytes"] += w["bytes"] or 0.0
+        s = d["shapes"].setdefault(shape, [0.0, 0, 0.0, 0.0])
+        s[0] += ms
+        s[1] += 1
+        s[2] += w["flop"] or 0.0
+        s[3] += w["bytes"] or 0.0
+
+    def rate(ms, flop, nbytes):
+        mfma = flop > 0 and flop / max(nbytes, 1.0) > RIDGE_FLOP_PER_BYTE
+        if mfma:
+            a = flop / (ms * 1e-3) / 1e12
+            return "mfma", a, BF16_DENSE_PEAK_TFLOPS, "TFLOP/s"
+        a = nbytes / (ms * 1e-3) / 1e9
+        return "hbm", a, HBM_PEAK_GBS, "GB/s"
+
+    out = []
+    for f, d in sorted(fam.items(), key=lambda kv: -kv[1]["ms"])[:top]:
+        bound, a, peak, unit = rate(d["ms"], d["flop"], d["bytes"])
+        shapes = []
+        for sh, (ms, n, fl, nb) in sorted(d["shapes"].items(), key=lambda kv: -kv[1][0]):
+            b2, a2, p2, u2 = rate(ms, fl, nb)
+            shapes.append({"shape": sh, "avg_us": round(1e3 * ms / n, 1), "launches_per_step": n / nsteps,
+                           "bound": b2, "achieved": round(a2, 1), "unit": u2, "frac": round(a2 / p2, 4)})
+        out.append({"kernel": f, "ms_per_step": round(d["ms"] / nsteps, 4), "launches_per_step": d["n"] / nsteps,
+                    "bound": bound, "work_per_step": round((d["flop"] if bound == "mfma" else d["bytes"]) / nsteps),
+                    "work_unit": "flop" if bound == "mfma" else "byte", "achieved": round(a, 1), "peak": peak,
+                    "unit": unit, "frac": round(a / peak, 4), "by_shape": shapes})
+    return {"method": f"HIP events around every instrumented launch, {nsteps} eager steps after the timed region",
+            "top": out}
+
+
 def cpu_baseline(pkg, model_cpu_sd):
     """Oracle (CPU restatement, oracle/stgcn_oracle.py) fwd+bwd on a bounded sample of the workload."""
     from oracle import stgcn_oracle as O
@@ -254,6 +323,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-layer-roofline", action="store_true", help="skip the north_star layer timing (profiling)")
     ap.add_argument("--graph", action="store_true", help="config 2: replay the step as HIP graphs")
+    ap.add_argument("--kernel-steps", type=int, default=3,
+                    help="eager steps after the timed region whose kernel-wrapper launches are timed one by one "
+                         "(the `kernels` table); 0 = off")
     args = ap.parse_args()
     if args.config == 4 and args.graph:
         sys.exit("bench.py: --graph needs fixed shapes (config 2); config 4's units have 49-65 windows")
@@ -398,6 +470,9 @@ def main():
         torch.cuda.synchronize()
     timing["on"] = False
     K.EVENT_HOOK = None
+    ktable = None
+    if args.kernel_steps > 0 and args.config == 2:
+        ktable = kernel_table(K, eager_step, args.kernel_steps)
     if world > 1:
         t = torch.tensor([elapsed, float(frames)], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t[:1], op=torch.distributed.ReduceOp.MAX)
@@ -453,6 +528,7 @@ def main():
                          "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4) if achieved else None,
                          "traffic": traffic, "avg_launch_ms": round(k_ms, 4), "launches_timed": len(kt)},
+            "kernels": ktable,
             "layer_roofline": lroof,
             "layer_roofline_ln": lroof_ln,
             "cpu_baseline": cpu,

@@ -214,13 +214,14 @@ def _stats_arena(cache, dev, dtype, shapes, route):
     write (rows past the kernel's row-block count, padded channels) must read as zero for bn_finalize — so a
     buffer kept per (device, dtype, shapes, route) in the layer's cache is zero-filled ONCE, not per forward.
     Streams: consumed by the layer's own bn_finalize right after, in stream order; the layer's next forward
-    writes it again only after that.  Without a cache (bare calls): a fresh zeroed arena."""
+    writes it again only after that.  Without a cache (bare calls): a fresh zeroed arena.  ``cache`` is the
+    layer's sub-dict of this device (StgcnLayerFunction.forward), so eviction never touches another device's."""
     if cache is None:
         return K.zeros_arena(dev, *shapes)
     key = ("bn_stats", str(dev), dtype, tuple(map(tuple, shapes)), route)
     st = cache.get(key)
     if st is None:
-        old = [k for k in cache if isinstance(k, tuple) and k[:1] == ("bn_stats",)]
+        old = [k for k in list(cache) if isinstance(k, tuple) and k[:1] == ("bn_stats",)]
         for k in old[:-3]:  # keep a few shapes (config 4 alternates 64- and 65-window units)
             del cache[k]
         st = cache[key] = K.zeros_arena(dev, *shapes)
@@ -245,6 +246,10 @@ class StgcnLayerFunction(torch.autograd.Function):
         A32 = A.detach().float().contiguous()
         res_conv = residual and not (Cin == Cout and stride == 1)
         packs = cfg[9] if len(cfg) > 9 else None  # LayerPacks of the model's PrepPlan launch, or None
+        # the layer's cache, one sub-dict per device: DataParallel replicas share the module's dict (shallow
+        # __dict__ copy) and run in one thread per device, so each thread only ever touches its own sub-dict
+        # (dict.setdefault is atomic under the GIL)
+        cache = cfg[8].setdefault(("dev", str(dev)), {}) if len(cfg) > 8 and cfg[8] is not None else None
 
         # ---- graph convolution: g = sum_p A_p-mix(x) W_p + bias2d
         sup = cfg[5] if len(cfg) > 5 else None
@@ -255,7 +260,7 @@ class StgcnLayerFunction(torch.autograd.Function):
             # LayerNorm layers: one kernel, ~3x the unfused forward; BatchNorm layers: the two-pass form,
             # 0.175 vs 0.187 ms graph-replayed (routing.fused_bn_inference off = unfused)
             return fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, sup, dtype,
-                                       cache=cfg[8] if len(cfg) > 8 else None, norm=norm)
+                                       cache=cache, norm=norm)
         tiled = gather and K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype)  # fused frame-tiled graph conv
         # gathered path: bias2d comes out of the effective-weight launch below
         bias2d = None if (gather and not tiled) else K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
@@ -265,7 +270,7 @@ class StgcnLayerFunction(torch.autograd.Function):
                 else K.row_blocks(M1, Cout)
             st_shapes = [(rb1, cpo, 4),
                          (K.row_blocks(M2, Cout), cpo, 4)] + ([(K.row_blocks(M2, Cout), cpo, 4)] if res_conv else [])
-            st_all = _stats_arena(cfg[8] if len(cfg) > 8 else None, dev, x.dtype, st_shapes, (tiled, gather))
+            st_all = _stats_arena(cache, dev, x.dtype, st_shapes, (tiled, gather))
             st1, st2 = st_all[0], st_all[1]
             str_ = st_all[2] if res_conv else None
         # ---- residual branch: independent of the graph conv -> temporal conv chain until the output norm,

@@ -64,6 +64,19 @@ def on_tensor_device(cls):
 # algorithmic flops where the wrapper knows them, else None) and after ("end", None) a tagged launch, on the
 # launching stream (bench.py records HIP events with it).  None = off.
 EVENT_HOOK = None
+# Per-kernel timing: callable(tag, phase, work) for EVERY launch of the instrumented wrappers (conv_rows,
+# conv_wgrad_w, gconv, gconv_wgrad(_finish), bn_apply, the fused BN backward), tag "k:<family>:<shape>", work
+# {"flop", "bytes"} (algorithmic).  bench.py's kernel table installs it outside its timed region.  None = off.
+KTIME_HOOK = None
+
+
+def _k_start(h, family, shape, flop=None, nbytes=None):
+    """Report a kernel-wrapper launch to the hook ``h`` (= KTIME_HOOK, checked by the caller so that the
+    uninstrumented path costs one global read): tag ``"k:<family>:<shape>"``, work ``{"flop": algorithmic
+    flops, "bytes": algorithmic HBM bytes}`` — bench.py's per-kernel table.  Returns the tag for _k_end."""
+    tag = f"k:{family}:{shape}"
+    h(tag, "start", {"flop": flop, "bytes": nbytes})
+    return tag
 
 
 def _dense(A: torch.Tensor) -> torch.Tensor:
@@ -244,7 +257,14 @@ def conv_rows(x, w3p, Cin, Cout, cp, kp, T_in, T_out, Kt=1, stride=1, pad=0, tra
     hook = EVENT_HOOK if tag is not None else None
     if hook:  # (tag, phase, algorithmic flops of the launch)
         hook(tag, "start", 2.0 * N * T_out * V * Cout * Cin * Kt)
+    h = KTIME_HOOK
+    if h:
+        fam = ("tcn_dgrad" if trans else "tcn_fwd") if Kt > 1 else "conv1x1"
+        ktag = _k_start(h, fam, f"{Cin}->{Cout} s{stride}", 2.0 * N * T_out * V * Cout * Cin * Kt,
+                        x.element_size() * N * V * (T_in * Cin + T_out * Cout))
     L.check(L.lib().stgcn_conv_rows(d, L.dtype_code(x.dtype), L.stream()), "conv_rows")
+    if h:
+        h(ktag, "end", None)
     if hook:
         hook(tag, "end", None)
     return out
@@ -290,7 +310,13 @@ def conv_wgrad_w(x, dy, Cin, Cout, T_in, T_out, Kt=1, stride=1, pad=0, pro=0, pr
     d.work, d.work_bytes = work.data_ptr(), nbytes
     dw = torch.empty((Cout, Cin, Kt), dtype=torch.float32, device=x.device)
     d.dw, d.out_mode = dw.data_ptr(), 1
+    h = KTIME_HOOK
+    if h:
+        ktag = _k_start(h, "tcn_wgrad" if Kt > 1 else "wgrad1x1", f"{Cin}->{Cout} s{stride}",
+                        2.0 * N * T_out * V * Cout * Cin * Kt, x.element_size() * N * V * (T_in * Cin + T_out * Cout))
     L.check(L.lib().stgcn_conv_wgrad(d, code, L.stream()), "conv_wgrad")
+    if h:
+        h(ktag, "end", None)
     return dw
 
 
@@ -582,12 +608,14 @@ def gconv(x, wpk, sup, Cin, Cout, trans=False, bias=None, stats=None, out=None, 
     d.NT, d.V, d.J, d.Cin, d.Cout = N * T, V, sup.J, Cin, Cout
     d.Cin_pad, d.Cout_pad = wpk.shape[3], wpk.shape[2]
     d.in_ld, d.out_ld, d.accumulate = rows_ld(x), rows_ld(out), int(accumulate)
-    hook = EVENT_HOOK if tag is not None else None
-    if hook:
-        hook(tag, "start", None)
+    h = KTIME_HOOK
+    if h:
+        ktag = _k_start(h, "gconv_dgrad" if trans else "gconv_fwd", f"{Cin}->{Cout}" if not trans else f"{Cout}->{Cin}",
+                        2.0 * N * T * sup.nnz * Cin * Cout,
+                        x.element_size() * N * T * V * (Cin + Cout * (2 if accumulate else 1)))
     L.check(L.lib().stgcn_gconv(d, L.dtype_code(x.dtype), L.stream()), "gconv")
-    if hook:
-        hook(tag, "end", None)
+    if h:
+        h(ktag, "end", None)
     return out
 
 
@@ -611,7 +639,13 @@ def gconv_wgrad(x, dy, sup, Cin, Cout, rowsum=None):
     if nbytes > 0:
         work = torch.empty(nbytes // 4, dtype=torch.float32, device=x.device)
         d.work, d.work_bytes = work.data_ptr(), nbytes
+    h = KTIME_HOOK
+    if h:
+        ktag = _k_start(h, "gconv_wgrad", f"{Cin}->{Cout}", 2.0 * N * T * sup.nnz * Cin * Cout,
+                        x.element_size() * N * T * V * (Cin + Cout))
     L.check(L.lib().stgcn_gconv_wgrad(d, code, L.stream()), "gconv_wgrad")
+    if h:
+        h(ktag, "end", None)
     return dweff
 
 
@@ -642,10 +676,15 @@ def gconv_finish_bias(dweff, A, W, sup, Cout, Cin, bconv, S):
     dA = out[P * Cout * Cin:P * Cout * Cin + P * V * V].view(P, V, V)
     db = out[P * Cout * Cin + P * V * V:]
     work = _workspace(L.lib().stgcn_gconv_wgrad_finish_workspace(P, V, sup.J, Cout, Cin), dev)
+    h = KTIME_HOOK
+    if h:
+        ktag = _k_start(h, "gconv_wgrad_finish", f"{Cin}->{Cout}", None, 4 * dweff.numel())
     L.check(L.lib().stgcn_gconv_wgrad_finish_bias(dweff.data_ptr(), A.data_ptr(), W.data_ptr(), sup.nbr.data_ptr(),
                                                   sup.deg.data_ptr(), P, V, sup.J, Cout, Cin, bconv.data_ptr(),
                                                   S.data_ptr(), dW.data_ptr(), dA.data_ptr(), db.data_ptr(),
                                                   work.data_ptr(), L.stream()), "gconv_finish_bias")
+    if h:
+        h(ktag, "end", None)
     return dW, dA, db
 
 
@@ -677,10 +716,15 @@ def bn_finalize(part, nb, ld_part, C, gamma, beta, eps=1e-5):
 def bn_apply(u, sc, sh, M, C, res_mode=0, r=None, rsc=None, rsh=None, relu=True, out=None, ldu=None, ldy=None):
     if out is None:
         out = torch.empty_like(u)
+    h = KTIME_HOOK
+    if h:
+        ktag = _k_start(h, "bn_apply", f"C{C}", None, u.element_size() * M * C * (3 if r is not None else 2))
     L.check(L.lib().stgcn_bn_apply(u.data_ptr(), ldu or rows_ld(u), sc.data_ptr(), sh.data_ptr(), res_mode, L.ptr(r),
                                    rows_ld(r) if r is not None else 0, L.ptr(rsc), L.ptr(rsh), int(relu),
                                    out.data_ptr(), ldy or rows_ld(out), M, C, L.dtype_code(u.dtype), L.stream()),
             "bn_apply")
+    if h:
+        h(ktag, "end", None)
     return out
 
 
@@ -732,9 +776,21 @@ def bn_bwd_fused(dy, M, C, mask=0, mref=None, msc=None, msh=None, x1=None, mr1=N
     d.ldo1 = rows_ld(out1) if out1 is not None else 0
     d.ldo2 = rows_ld(out2) if out2 is not None else 0
     d.acc2 = int(acc2)
+    h = KTIME_HOOK
+    es = dy.element_size()
+    n_in = sum(t is not None for t in (dy, mref, x1, x2))
+    if h:
+        ktag = _k_start(h, "bn_bwd_reduce", f"C{C}", None, es * M * C * n_in)
     L.check(L.lib().stgcn_bn_bwd_fused_reduce(d, code, L.stream()), "bn_bwd_fused_reduce")
+    if h:
+        h(ktag, "end", None)
     if out1 is not None:
+        if h:
+            n_out = 1 + (out2 is not None) * (2 if acc2 else 1)
+            ktag = _k_start(h, "bn_bwd_apply", f"C{C}", None, es * M * C * (n_in + n_out))
         L.check(L.lib().stgcn_bn_bwd_fused_apply(d, code, L.stream()), "bn_bwd_fused_apply")
+        if h:
+            h(ktag, "end", None)
     return sums[4 * C:].view(3, C), (osum[4 * C:].view(3, C) if osum is not None else None)
 
 

@@ -86,6 +86,10 @@ class Adam(torch.optim.Optimizer):
         fs = self._flat.get(gi)
         if fs is None or sum(f.n for f in fs) != len(params) or \
                 any(f.key != tuple(p.data_ptr() for p in params[o:o + f.n]) for f, o in zip(fs, _offsets(fs))):
+            dev = params[0].device
+            if any(p.device != dev for p in params):
+                # every chunk of a group launches on one device's stream (step())
+                raise RuntimeError("stgcn_amd.optim.Adam: all parameters of a group must be on one HIP device")
             fs = [_Flat(params[o:o + MAXT], self.state) for o in range(0, len(params), MAXT)]
             self._flat[gi] = fs
         return fs
@@ -109,7 +113,7 @@ class Adam(torch.optim.Optimizer):
             params = group["params"]
             if not params:
                 continue
-            keep = []
+            keep, updated = [], []
             b1, b2 = group["betas"]
             for f, o in zip(self._flat_of(gi, group), _offsets(self._flat[gi])):
                 for k, p in enumerate(params[o:o + f.n]):
@@ -117,6 +121,7 @@ class Adam(torch.optim.Optimizer):
                     if g is None:
                         f.grads[k] = None
                         continue
+                    updated.append(p)
                     if g.is_sparse or g.dtype != torch.float32 or g.shape != p.shape:
                         raise RuntimeError("stgcn_amd.optim.Adam: dense fp32 gradients of the parameter's shape only")
                     if not g.is_contiguous():
@@ -127,4 +132,8 @@ class Adam(torch.optim.Optimizer):
                     L.check(L.lib().stgcn_adam_step(f.table.data_ptr(), f.n, f.nblocks, f.grads, f.steps.data_ptr(),
                                                     float(group["lr"]), float(b1), float(b2), float(group["eps"]),
                                                     float(group["weight_decay"]), L.stream()), "adam_step")
+            # the kernel writes the parameters through raw pointers: bump their in-place version counters as
+            # an aten in-place update would, so caches keyed on (storage, _version) — the fused-inference and
+            # RT packs — see the new weights
+            torch._C._increment_version(updated)
         return loss

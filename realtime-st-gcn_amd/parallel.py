@@ -183,9 +183,12 @@ class GraphedStep:
         graph 2: [N > 1: the averaged flat gradient back into .grad] + ``opt.step()``
 
     ``fwd_loss`` must only read tensors whose storage stays put between replays (copy new batches into the
-    tensors it closes over).  The optimizer must be capturable (torch.optim.Adam(capturable=True)).  One
-    eager step runs first (on a side stream, as graph capture requires) so that every gradient and optimizer
-    state tensor exists and keeps its address."""
+    tensors it closes over).  The optimizer must be capturable: the package's ``optim.Adam`` (device-side step
+    counters; what bench.py uses) or torch.optim.Adam(capturable=True).  One eager step runs first (on a side
+    stream, as graph capture requires) so that every gradient and optimizer state tensor exists and keeps its
+    address; a parameter that got no gradient in it is given a zero gradient so the captured zeroing has a
+    buffer.  Replays do not bump the parameters' version counters (host-side bookkeeping is not captured):
+    call ``train()`` / ``eval()`` before an inference forward that should see replayed updates."""
 
     def __init__(self, fwd_loss, params, opt, world: int = 1, group=None):
         self.fwd_loss, self.params, self.opt = fwd_loss, list(params), opt
@@ -201,6 +204,9 @@ class GraphedStep:
             if self.flat is not None:
                 self._allreduce()
             self._apply()
+            for p in self.params:
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
             self.g1, self.g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g1, stream=s):
                 for p in self.params:

@@ -68,8 +68,12 @@ class Model(nn.Module):
         (native.PrepPlan, prep.hip) instead of ~50 per-layer launches; returns the plan (its ``layers`` /
         ``head`` packs) or None.  Only for the autograd path on the device: inference keeps the per-call
         packing (the fused inference route packs differently).  The packs are refilled every forward from the
-        current parameters; the plan (job table of raw pointers) is rebuilt when a storage moves."""
-        if not (ROUTING.prep_plan and torch.is_grad_enabled() and self.A.is_cuda):
+        current parameters; the plan (job table of raw pointers) is rebuilt when a storage moves.
+        nn.DataParallel replicas (the reference's multi-GPU form, processor.py:33) are rebuilt every forward
+        from freshly broadcast storages, so a plan would be rebuilt per step and never reach the parent: they
+        pack per call instead."""
+        if not (ROUTING.prep_plan and torch.is_grad_enabled() and self.A.is_cuda) or getattr(self, "_is_replica",
+                                                                                              False):
             return None
         dt = self.compute_dtype
         imp = isinstance(self.edge_importance, nn.ParameterList) and len(self.edge_importance)

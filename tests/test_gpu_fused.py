@@ -260,3 +260,30 @@ def test_fused_ln_large_bias(P):
         y = layer(x.to(DEV), A.to(DEV))
     torch.cuda.synchronize()
     assert_close(y.float().cpu(), ref, 3e-2, "fused LN layer, bias 3000")
+
+
+def test_fused_packs_follow_package_adam(P, monkeypatch):
+    """The package's Adam writes parameters through raw pointers; it bumps their version counters, so a
+    no_grad forward in train mode right after a step (no train()/eval() in between) repacks and equals the
+    unfused route on the updated weights (stale fused packs)."""
+    calls = _count_fused(P, monkeypatch)
+    A = _graph(P).to(DEV)
+    layer = _ln_layer(P, 13).to(DEV).train()
+    P.set_compute_dtype(layer, "bf16")
+    x = cl(torch.randn(4, 64, 40, 25), BF)
+    with torch.no_grad():
+        y0 = layer(x, A).float()
+    opt = P.optim.Adam(layer.parameters(), lr=0.05)
+    for p in layer.parameters():
+        p.grad = torch.randn_like(p)
+    v0 = [p._version for p in layer.parameters()]
+    opt.step()
+    assert all(p._version > v for p, v in zip(layer.parameters(), v0))
+    with torch.no_grad():
+        y1 = layer(x, A).float()
+        monkeypatch.setattr(P.routing.ROUTING, "fused_inference", False)
+        u1 = layer(x, A).float()
+    torch.cuda.synchronize()
+    assert (u1 - y0).abs().max() > 0.1
+    assert_close(y1, u1, 3e-2, "fused forward after a package-Adam step")
+    assert len(calls) == 2
