@@ -365,6 +365,16 @@ typedef struct {
   const float* ln2_g;
   const float* ln2_b;
   int ln, residual;
+  /* LayerNorm training forward (ln = 1; all four set, or all NULL for inference): what the layer's backward
+   * (StgcnLayerFunction's unfused LN backward) reads besides y — g_out: the graph-conv output incl. its bias
+   * (pre-LN1) rows [N][T][V][g_ld]; u_out: the temporal-conv output incl. its bias (pre-LN2) rows, u_ld;
+   * st1_out / st2_out: per-frame LayerNorm statistics (mean, 1/sqrt(unbiased var + 1e-5)) of g and u, float2
+   * [N*T] — stgcn_ln_stats's layout, computed here from the fp32 values before their bf16 rounding. */
+  void* g_out;
+  void* u_out;
+  float* st1_out;
+  float* st2_out;
+  int g_ld, u_ld;
 } stgcn_layer_fused_desc;
 
 int stgcn_layer_fused_fwd(const stgcn_layer_fused_desc* d, void* stream);

@@ -390,6 +390,24 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
               *reinterpret_cast<uint4*>(hrow + (e >> 3) * RSH + (e & 7) * 16) = make_uint4(0, 0, 0, 0);
             continue;
           }
+          if (a.g_out && fa >= HALO && fa < HALO + (R1 - R0)) {
+            // training forward: this run's own frames (the halo frames are some other block's) — g rows
+            // (pre-LN1, bias included) and the frame's LN1 statistics, for the unfused backward
+            const long frow = (long)n * T + (R0 - HALO + fa);
+            if (lane == 0) reinterpret_cast<float2*>(a.st1_out)[frow] = make_float2(mean[i], rstd[i]);
+            if (jv) {
+              bf16* gr = reinterpret_cast<bf16*>(a.g_out) + (frow * V + lr) * a.g_ld + 4 * lh;
+#pragma unroll
+              for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) {
+                  bf16x4 gv;
+#pragma unroll
+                  for (int e = 0; e < 4; ++e) gv[e] = (bf16)accf[i][t][4 * q4 + e];
+                  *reinterpret_cast<bf16x4*>(gr + 32 * t + 8 * q4) = gv;
+                }
+            }
+          }
           if (jv) {
             char* hr = hrow + lr * RSH;
 #pragma unroll
@@ -654,6 +672,17 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
           const float cnt = (float)(V * C), dmean = su / cnt;  // mean of z - piv
           const float2 st = make_float2(piv + dmean, 1.f / sqrtf(fmaxf(sq - su * dmean, 0.f) / (cnt - 1.f) + 1e-5f));
           const int w = jw_[i];
+          if (a.u_out) {  // training forward: u = z (pre-LN2, bias included) rows and the frame's LN2 statistics
+            bf16* ur = reinterpret_cast<bf16*>(a.u_out) + (((long)n * T + f0) * V + r) * a.u_ld + 32 * ct + 4 * lh;
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+              bf16x4 uv;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) uv[e] = (bf16)acc[i][4 * q4 + e];
+              *reinterpret_cast<bf16x4*>(ur + 8 * q4) = uv;
+            }
+            if (ct == 0 && w == 0 && lh == 0) reinterpret_cast<float2*>(a.st2_out)[(long)n * T + f0 + fo] = st;
+          }
 #pragma unroll
           for (int q4 = 0; q4 < 4; ++q4) {
             const int co = 32 * ct + 8 * q4 + 4 * lh;
@@ -774,6 +803,9 @@ long layer_fused_row_blocks(int N, int T) {
 int layer_fused_launch(const stgcn_layer_fused_desc& a, hipStream_t s) {
   if (!a.x || !a.z || !a.wg_frag || !a.A || !a.wt_frag) return STGCN_EBADSHAPE;
   if (a.ln ? (!a.ln1_g || !a.ln1_b || !a.ln2_g || !a.ln2_b || a.stats) : (!a.n1_scale || !a.n1_shift))
+    return STGCN_EBADSHAPE;
+  const int ntrain = !!a.g_out + !!a.u_out + !!a.st1_out + !!a.st2_out;
+  if (ntrain != 0 && (ntrain != 4 || !a.ln || a.g_ld < C || a.g_ld % 4 || a.u_ld < C || a.u_ld % 4))
     return STGCN_EBADSHAPE;
   if (a.N < 1 || a.T < 1 || a.V <= 16 || a.V > VMAX || a.P < 1 || a.P > 3) return STGCN_EBADSHAPE;
   if (a.x_ld < C || a.x_ld % 8 || a.z_ld < C || a.z_ld % 4) return STGCN_EBADSHAPE;

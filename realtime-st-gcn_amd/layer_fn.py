@@ -174,11 +174,12 @@ def _ln_vc(p, V, C):
 
 
 def fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, sup, dtype, tag=None, cache=None,
-                        norm=BN):
+                        norm=BN, train=False):
     """StgcnLayer.forward (stgcn.py:181-193) through layer_fused.hip.  BatchNorm: the two-pass fused form
     (SURVEY §7): pass 1 = graph conv statistics only (gcn_tile, no g stores) -> BN1 scale/shift; pass 2 =
     graph conv recomputed per tile + BN1 + ReLU + temporal conv in one kernel (z + BN2 partials); then
-    y = relu(BN2(z) + x).  LayerNorm (per-frame norms): the whole layer is the one kernel.
+    y = relu(BN2(z) + x).  LayerNorm (per-frame norms): the whole layer is the one kernel; ``train``: it also
+    writes what the unfused backward reads and this returns (y, g, u, ls1, ls2).
     x: channels-last bf16 (N, 64, T, V)."""
     N, Cin, T, V = x.shape
     P = A32.shape[0]
@@ -196,7 +197,7 @@ def fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, su
             if cache is not None:
                 cache["ln_key"], cache["ln_val"] = lkey, ln
         return K.layer_fused(x, A32, wimg, bias2d, None, None, wtp, bt.detach().float().contiguous(), tag=tag,
-                             ln=ln, residual=residual)
+                             ln=ln, residual=residual, train=train)
     rb1, rb2 = K.gcn_tile_row_blocks(N * T, V, Cout), K.layer_fused_row_blocks(N, T)
     # both kernels write every row block of their statistics: no zero fill
     st1 = torch.empty((rb1, cpg, 4), dtype=torch.float32, device=dev)
@@ -261,6 +262,20 @@ class StgcnLayerFunction(torch.autograd.Function):
             # 0.175 vs 0.187 ms graph-replayed (routing.fused_bn_inference off = unfused)
             return fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, sup, dtype,
                                        cache=cache, norm=norm)
+        if (gather and norm == LN and ROUTING.fused_ln_train and not (len(cfg) > 7 and cfg[7])
+                and K.layer_fused_ok(sup, P, Cin, Cout, V, kt, stride, dtype)):
+            # training forward of a LayerNorm 64 -> 64 stride-1 layer: the one-kernel layer (g and h on chip for
+            # the temporal conv) also writes g, u and both LN statistics — exactly what the unfused forward
+            # saves — so the backward below is unchanged (ln/ configs)
+            y, g, u, ls1, ls2 = fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, sup, dtype,
+                                                    cache=cache, norm=LN, train=True)
+            ctx.cfg = cfg
+            ctx.sup = sup
+            ctx.dims = (N, Cin, Cout, T, T_out, V, P, pad, False)
+            ctx.packs = None
+            ctx.save_for_backward(x, A32, None, g, u, y, wg, bg, wt, n1w, n1b, n2w, n2b, ls1, ls2)
+            ctx.in_dtype = A.dtype
+            return y
         tiled = gather and K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype)  # fused frame-tiled graph conv
         # gathered path: bias2d comes out of the effective-weight launch below
         bias2d = None if (gather and not tiled) else K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)

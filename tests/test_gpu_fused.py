@@ -287,3 +287,105 @@ def test_fused_packs_follow_package_adam(P, monkeypatch):
     assert (u1 - y0).abs().max() > 0.1
     assert_close(y1, u1, 3e-2, "fused forward after a package-Adam step")
     assert len(calls) == 2
+
+
+def _spy_train(P, monkeypatch):
+    calls = []
+    orig = P.native.layer_fused
+
+    def spy(*a, **k):
+        calls.append(bool(k.get("train")))
+        return orig(*a, **k)
+
+    monkeypatch.setattr(P.native, "layer_fused", spy)
+    return calls
+
+
+@pytest.mark.parametrize("N,T,residual", [(3, 37, True), (2, 20, False), (64, 300, True)])
+def test_ln_layer_fused_training(P, monkeypatch, N, T, residual):
+    """Training forward of a LayerNorm 64 -> 64 stride-1 layer through the one-kernel layer (routing
+    fused_ln_train), which also writes g, u and both LN statistics for the unfused backward: y and every
+    gradient against the fp32 oracle (layernorm.py:22-28, stgcn.py:181-193; bf16 tolerance 4e-2 as the other
+    bf16 layer tests) and against the unfused training route on the same inputs (2e-2); the fused kernel ran in
+    training mode."""
+    from conftest import assert_grad_close, grad_floor
+    calls = _spy_train(P, monkeypatch)
+    g = torch.Generator().manual_seed(21 + T)
+    A = _graph(P)
+    torch.manual_seed(21 + T)
+    layer = P.StgcnLayer(64, 64, (9, 25), 3, 25, stride=1, residual=residual, normalization="LayerNorm")
+    with torch.no_grad():  # non-trivial LayerNorm affines
+        for nm in ("tcn.0", "tcn.3"):
+            m = layer.get_submodule(nm)
+            m.weight.copy_(1 + 0.2 * torch.randn(m.weight.shape, generator=g))
+            m.bias.copy_(0.2 * torch.randn(m.bias.shape, generator=g))
+    sd = {k: v.clone().requires_grad_(True) for k, v in layer.state_dict().items()}
+    x = torch.randn(N, 64, T, 25, generator=g)
+    dy = torch.randn(N, 64, T, 25, generator=g)
+    small = N * T <= 200
+    if small:
+        xr = x.clone().requires_grad_(True)
+        Ar = A.clone().requires_grad_(True)
+        ref = O.stgcn_layer(xr, Ar, sd, "", 9, 1, residual, "LayerNorm")
+        ref.backward(dy)
+    layer = P.set_compute_dtype(layer.to(DEV), "bf16")
+    out = {}
+    for route in (True, False):
+        monkeypatch.setattr(P.routing.ROUTING, "fused_ln_train", route)
+        layer.zero_grad(set_to_none=True)
+        xg = x.to(DEV).requires_grad_(True)
+        Ag = A.to(DEV).requires_grad_(True)
+        y = layer(xg, Ag)
+        y.backward(dy.to(DEV))
+        torch.cuda.synchronize()
+        out[route] = (y.detach().float().cpu(), xg.grad.float().cpu(), Ag.grad.float().cpu(),
+                      {k: p.grad.float().cpu() for k, p in layer.named_parameters()})
+    assert calls == [True], calls  # the fused route ran once, in training mode; the unfused one not at all
+    (yf, dxf, dAf, gf), (yu, dxu, dAu, gu) = out[True], out[False]
+    assert_close(yf, yu, 2e-2, "fused vs unfused y")
+    assert_grad_close(dxf, dxu, 2e-2, "fused vs unfused dx")
+    assert_grad_close(dAf, dAu, 2e-2, "fused vs unfused dA", reduction=True)
+    for k in gu:
+        assert_grad_close(gf[k], gu[k], 2e-2, f"fused vs unfused {k}", reduction=True)
+    if small:
+        tol = 4e-2
+        assert_close(yf, ref, tol, "y")
+        assert_grad_close(dxf, xr.grad, tol, "dx")
+        assert_grad_close(dAf, Ar.grad, tol, "dA", reduction=True)
+        grads = {k: v.grad for k, v in sd.items() if v.grad is not None}
+        for k, gr in grads.items():
+            assert_grad_close(gf[k], gr, tol, k, grad_floor(grads, k), reduction=True)
+
+
+def test_ln_model_fused_training(P, monkeypatch):
+    """ln/stgcn_vsc.json-style model (LayerNorm, Kt = 9, the config-2 widths, 9 layers) fwd + loss-free bwd in
+    bf16 with the fused training route on its three 64 -> 64 layers: logits and every parameter gradient equal
+    the unfused route's (2e-2) and the logits the fp32 oracle's (3e-2)."""
+    from conftest import assert_grad_close
+    calls = _spy_train(P, monkeypatch)
+    arch = {"strategy": "spatial", "in_feat": 3, "normalization": "LayerNorm", "num_classes": 52,
+            "output_type": "logits",
+            "st-gcn": {"in_feat": 3, "layers": 9, "kernel": 9, "importance": True,
+                       "in_ch": [64, 64, 64, 64, 128, 128, 128, 256, 256],
+                       "out_ch": [64, 64, 64, 128, 128, 128, 256, 256, 256],
+                       "stride": [1, 1, 1, 2, 1, 1, 2, 1, 1], "residual": [1] * 9, "dropout": [0] * 9}}
+    torch.manual_seed(31)
+    m = P.MODELS["st-gcn"](rank=None, **dict(arch, graph=P.PKU_MMD))
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    x = torch.randn(4, 3, 48, 25, generator=torch.Generator().manual_seed(32))
+    with torch.no_grad():
+        ref = O.stgcn_model(x, sd, dict(arch, graph=P.PKU_MMD))
+    m = m.to(DEV).set_compute_dtype("bf16")
+    out = {}
+    for route in (True, False):
+        monkeypatch.setattr(P.routing.ROUTING, "fused_ln_train", route)
+        m.zero_grad(set_to_none=True)
+        y = m(x.to(DEV))
+        (y.float() ** 2).sum().backward()
+        torch.cuda.synchronize()
+        out[route] = (y.detach().float().cpu(), {k: p.grad.float().cpu() for k, p in m.named_parameters()})
+    assert calls == [True] * 3, calls
+    assert_close(out[True][0], ref, 3e-2, "fused-route logits vs oracle")
+    assert_close(out[True][0], out[False][0], 2e-2, "fused vs unfused logits")
+    for k, gu in out[False][1].items():
+        assert_grad_close(out[True][1][k], gu, 2e-2, f"fused vs unfused {k}", reduction=True)

@@ -12,7 +12,7 @@ f1:       window staging (config/pku-mmd/ln/stgcn_local.json: receptive_field 50
           order (unfold the windows, then norm_in and fcn_in on the copies — our HIP kernels on both sides),
           fwd and bwd, BatchNorm and LayerNorm, bf16.
 
-    python tools/bench_configs.py [--frames 2000] [--steps 10] [--only 3|5|f1]
+    python tools/bench_configs.py [--frames 2000] [--steps 10] [--only 3|5|ln|f1]
 Prints one JSON line per config.
 """
 import argparse
@@ -126,6 +126,51 @@ def config5(P, dev, steps, warmup):
             "ms_per_step": round(1e3 * dt / steps, 3), "steps": steps, "data": "synthetic"}
 
 
+LN_ARCH = {"strategy": "spatial", "in_feat": 3, "normalization": "LayerNorm", "num_classes": 52,
+           "output_type": "logits", "st-gcn": dict(LAYERS, importance=True, in_feat=3)}
+
+
+def ln_train(P, dev, steps, warmup, reps=3):
+    """The LayerNorm st-gcn (ln/stgcn_vsc.json-style: LN, Kt = 9, config-2 widths) training step (fwd + loss +
+    bwd + Adam, bf16, N=64 T=300) with its three 64 -> 64 layers' forward on the fused one-kernel layer
+    (routing.fused_ln_train, default) and unfused, interleaved ``reps`` times."""
+    R = P.routing.ROUTING
+    torch.manual_seed(1538574472)
+    m = P.MODELS["st-gcn"](rank=None, **dict(LN_ARCH, graph=P.PKU_MMD)).to(dev).set_compute_dtype("bf16")
+    opt = P.optim.Adam(m.parameters(), lr=5e-4)
+    gen = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(64, 3, 300, 25, device=dev, generator=gen)
+    labels = torch.randint(0, 52, (1, 64), device=dev, generator=gen)
+    crit = P.loss.Loss(dev, torch.rand(52, device=dev, generator=gen) + 0.5)
+
+    def step():
+        ce, mse = crit(0, m(x).permute(2, 1, 0), labels)
+        (ce + mse).backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+
+    out = {"config": "ln st-gcn (LayerNorm, Kt=9, 9 layers, config-2 widths) fwd+loss+bwd+Adam, bf16, N=64 T=300",
+           "metric": "ms/step"}
+    prev = R.fused_ln_train
+    try:
+        for rep in range(reps):
+            for route in (True, False):
+                R.fused_ln_train = route
+                for _ in range(warmup):
+                    step()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(steps):
+                    step()
+                torch.cuda.synchronize()
+                k = "fused_ms_per_step" if route else "unfused_ms_per_step"
+                out.setdefault(k, []).append(round(1e3 * (time.perf_counter() - t0) / steps, 3))
+    finally:
+        R.fused_ln_train = prev
+    out["fused_frames_per_s"] = round(64 * 300 / (min(out["fused_ms_per_step"]) * 1e-3), 1)
+    return out
+
+
 def staging(P, dev, reps=50):
     import torch.nn.functional as F
     W, nw, L, C, V, Cout = 50, 1000, 1000, 3, 25, 64
@@ -188,6 +233,8 @@ def main():
         print(json.dumps(config3(P, dev, args.frames)), flush=True)
     if args.only in (None, "5"):
         print(json.dumps(config5(P, dev, args.steps, args.warmup)), flush=True)
+    if args.only in (None, "ln"):
+        print(json.dumps(ln_train(P, dev, args.steps, args.warmup)), flush=True)
     if args.only in (None, "f1"):
         print(json.dumps(staging(P, dev)), flush=True)
 
