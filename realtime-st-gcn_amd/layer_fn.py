@@ -154,10 +154,12 @@ def plan_layer_packs(plan, layer, A, M, dtype):
     if sup is None or A.dim() != 3 or sup.dense(P) or K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype):
         return None
     pk = LayerPacks()
-    wg2 = layer.gcn.conv.weight.detach().reshape(P * Cout, Cin)
-    pk.gw = K.gconv_weights(A, wg2, sup, Cout, Cin, False, dtype, bias=layer.gcn.conv.bias.detach(), plan=plan, M=M)
-    if not K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype, trans=True):
-        pk.gwT = K.gconv_weights(A, wg2, sup, Cout, Cin, True, dtype, plan=plan, M=M)
+    if not layer.afirst_forced():  # the A-first graph conv packs its channel GEMM per call
+        wg2 = layer.gcn.conv.weight.detach().reshape(P * Cout, Cin)
+        pk.gw = K.gconv_weights(A, wg2, sup, Cout, Cin, False, dtype, bias=layer.gcn.conv.bias.detach(), plan=plan,
+                                M=M)
+        if not K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype, trans=True):
+            pk.gwT = K.gconv_weights(A, wg2, sup, Cout, Cin, True, dtype, plan=plan, M=M)
     wt = conv.weight.detach().squeeze(-1)
     pk.wt = K.pack_weight(wt.permute(2, 0, 1), dtype, stride=stride, plan=plan)
     pk.wtT = K.pack_weight(wt.permute(2, 1, 0), dtype, stride=stride, trans=True, plan=plan)

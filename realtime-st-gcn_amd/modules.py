@@ -140,8 +140,12 @@ class StgcnLayer(nn.Module):
             self._gsup = K.GraphSupport(A)
         self._graph_bound = self._graph_bound or masked
 
+    def afirst_forced(self):
+        """The A-first graph conv chosen by routing (gcn_afirst / gcn_afirst_min_c) for a shared graph."""
+        return ROUTING.gcn_afirst or 0 < ROUTING.gcn_afirst_min_c <= self.gcn.conv.in_channels
+
     def graph_support(self, A):
-        if A.dim() != 3 or ROUTING.gcn_afirst:
+        if A.dim() != 3 or self.afirst_forced():
             return None  # per-sample A (AAGCN) or forced A-first path
         self.bind_graph(A, masked=False)
         return self._gsup

@@ -19,6 +19,9 @@ also assign the attributes directly.
                                               unfused backward; default on)
     gcn_tile            STGCN_GCN_TILE=0|1|auto  graph conv on the two-stage MFMA kernel gcn_tile.hip (default 0)
     gcn_afirst          STGCN_GCN_AFIRST=1    force the A-first graph conv (amix + GEMM) for shared graphs
+    gcn_afirst_min_c    STGCN_GCN_AFIRST_MIN_C=<C>  ... only for layers with at least C input channels (A/B of the
+                                              A-first form where the gathered form's per-joint effective weights
+                                              outgrow L2; default 0 = off)
     prep_plan           STGCN_PREP_PLAN=0     stgcn.Model training forwards pack every weight per call instead of
                                               in the one-launch plan (native.PrepPlan; default on)
 """
@@ -34,6 +37,7 @@ class _Routing:
         self.fused_ln_train = e("STGCN_FUSED_LN_TRAIN", "1") != "0"
         self.gcn_tile = e("STGCN_GCN_TILE", "0")
         self.gcn_afirst = e("STGCN_GCN_AFIRST", "0") not in ("0", "")
+        self.gcn_afirst_min_c = int(e("STGCN_GCN_AFIRST_MIN_C", "0") or 0)
         self.prep_plan = e("STGCN_PREP_PLAN", "1") != "0"
 
 

@@ -178,3 +178,37 @@ def test_prep_plan_builds_and_validates(pkg):
     # frag images where the kernels expect them
     assert layers[0].wt[0].frag_stride == 1 and layers[3].wt[0].frag_stride == 2 and layers[3].wtT[0].frag_stride == 2
     assert head[0][0][1] == 64 and head[0][0][2] == 32
+
+
+def test_descriptor_layouts_match_header(pkg, tmp_path):
+    """Every ctypes descriptor of _lib.py has the size and field offsets the C compiler gives the struct of
+    include/stgcn_amd.h (the boundary's pointer-and-size structs; a field appended on one side only would make
+    the library read garbage).  Compiled with gcc on the host: no GPU, no HIP headers (the header is plain C)."""
+    import ctypes
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    L = pkg._lib
+    structs = {"stgcn_conv_desc": L.ConvDesc, "stgcn_wgrad_desc": L.WgradDesc, "stgcn_amix_desc": L.AmixDesc,
+               "stgcn_gconv_desc": L.GconvDesc, "stgcn_gcn_tile_desc": L.GcnTileDesc,
+               "stgcn_gconv_wgrad_desc": L.GconvWgradDesc, "stgcn_bn_bwd_desc": L.BnBwdDesc,
+               "stgcn_layer_fused_desc": L.LayerFusedDesc, "stgcn_prep_job": L.PrepJob,
+               "stgcn_adam_entry": L.AdamEntry}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{os.path.join(ROOT, "include", "stgcn_amd.h")}"',
+             'int main(void) {']
+    expect = []
+    for cname, cls in structs.items():
+        lines.append(f'  printf("%zu\\n", sizeof({cname}));')
+        expect.append(ctypes.sizeof(cls))
+        for fname, _ in cls._fields_:
+            cf = "in" if fname == "in_" else fname
+            lines.append(f'  printf("%zu\\n", offsetof({cname}, {cf}));')
+            expect.append(getattr(cls, fname).offset)
+    lines += ['  return 0;', '}']
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-o", str(exe), str(src)], check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    assert got == expect

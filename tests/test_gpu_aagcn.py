@@ -134,6 +134,29 @@ def aagcn_ref(P):
     return arch, sd0, x, dy, refs
 
 
+@pytest.fixture(scope="module")
+def aagcn_ref64(P):
+    """Config 5 at its timed size, N = 64 T = 300: the same model and seeds as aagcn_ref, the oracle's fwd + bwd in
+    fp64 (the yardstick) and fp32 (the reference's precision) on the CPU."""
+    from test_gpu_bench_config import oracle_fwd_bwd
+    torch.manual_seed(1538574472)
+    arch = dict(AAGCN_ARCH, graph=P.PKU_MMD)
+    m = P.MODELS["aa-gcn"](rank=None, **arch)
+    with torch.no_grad():
+        for name, p in m.named_parameters():
+            if name.endswith(".B"):
+                p.copy_(0.05 * torch.randn(p.shape))
+    sd0 = {k: v.clone() for k, v in m.state_dict().items()}
+    gen = torch.Generator().manual_seed(0)
+    x = torch.randn(64, 3, 300, 25, generator=gen)
+    dy = torch.randn(64, 52, 1, generator=gen)
+    far = P.Graph(**P.PKU_MMD).get_adjacency_raw()[2]
+    fn = lambda xx, sd: O.aagcn_model(xx, sd, arch, far)  # noqa: E731
+    refs = {"f64": oracle_fwd_bwd(fn, x, dy, sd0, torch.float64),
+            "f32": oracle_fwd_bwd(fn, x, dy, sd0, torch.float32)}
+    return arch, sd0, x, dy, refs
+
+
 def _aagcn_run(P, arch, sd0, x, dy, dtype):
     m = P.MODELS["aa-gcn"](rank=None, **arch)
     m.load_state_dict(sd0, strict=True)
@@ -154,10 +177,11 @@ def _mx(t, ref):
     return ((t.double() - ref).abs().max() / ref.abs().max().clamp_min(1e-300)).item()
 
 
-def test_aagcn_model_fp32_config5(P, aagcn_ref):
-    """fp32 AAGCN at config-5 widths: logits within the north_star 1e-3 of the reference's fp32, every
-    gradient as close to fp64 as the reference's fp32 (L2 within 3x + 1e-4; see test_gpu_bench_config)."""
-    arch, sd0, x, dy, refs = aagcn_ref
+def test_aagcn_model_fp32_config5(P, aagcn_ref64):
+    """fp32 AAGCN at config 5's timed size (N = 64, T = 300): logits within the north_star 1e-3 of the
+    reference's fp32, every gradient as close to fp64 as the reference's fp32 (L2 within 3x + 1e-4; see
+    test_gpu_bench_config)."""
+    arch, sd0, x, dy, refs = aagcn_ref64
     r64, r32 = refs["f64"], refs["f32"]
     got = _aagcn_run(P, arch, sd0, x, dy, "fp32")
     assert_close(got["logits"], r32["logits"], 1e-3, "aagcn fp32 logits vs reference fp32")
@@ -207,3 +231,23 @@ def test_aagcn_model_bf16_config5(P, aagcn_ref):
     med, p90 = ratios[len(ratios) // 2], ratios[int(0.9 * len(ratios))]
     print(f"[err] aagcn bf16 L2 ratio ours / reference bf16: median {med:.3f}, p90 {p90:.3f}", flush=True)
     assert not bad and med <= 1.0 and p90 <= 3.0, f"bf16 AAGCN: bad {bad}, median {med:.3f}, p90 {p90:.3f}"
+
+
+def test_aagcn_bf16_vs_fp32_per_tensor(P, aagcn_ref64):
+    """Per tensor, config 5's bf16 path against the HIP fp32 path on the same inputs at N = 64: logits and every
+    gradient point the same way (cosine >= 0.95), except gradients that are exactly 0 in exact arithmetic (the
+    conv biases feeding a batch-statistics BatchNorm, phi's bias, which cancels in the softmax)."""
+    arch, sd0, x, dy, _ = aagcn_ref64
+    g16 = _aagcn_run(P, arch, sd0, x, dy, "bf16")
+    g32 = _aagcn_run(P, arch, sd0, x, dy, "fp32")
+    bad, worst = [], (2.0, None)
+    for k, ref in g32.items():
+        if bn_fed_bias(k) or k.endswith("phi.bias"):
+            continue
+        cos = torch.nn.functional.cosine_similarity(g16[k].reshape(1, -1), ref.reshape(1, -1)).item()
+        print(f"[err] aagcn bf16 vs fp32 {k}: cos {cos:.5f} L2 {_l2(g16[k], ref):.2e}", flush=True)
+        worst = min(worst, (cos, k))
+        if not cos >= 0.95:
+            bad.append((k, round(cos, 4)))
+    print(f"[err] aagcn bf16 vs fp32 worst cosine {worst[0]:.5f} ({worst[1]})", flush=True)
+    assert not bad, f"bf16 AAGCN tensors with cosine < 0.95 to the HIP fp32 path: {bad}"

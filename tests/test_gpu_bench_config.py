@@ -296,6 +296,26 @@ def test_model_bf16_bench_config(K, pkg, model_ref):
     assert not bad, f"bf16 gradients further from fp64 than 3x the reference's bf16 (or cosine < 0.9): {bad}"
 
 
+def test_model_bf16_vs_fp32_per_tensor(K, pkg, model_ref):
+    """Per tensor, the bf16 perf path against the HIP fp32 path on the same inputs (the same kernels' schedule in
+    the two precisions): every gradient points the same way — cosine >= 0.95 — except the conv biases that feed a
+    batch-statistics BatchNorm, whose exact gradient is 0 (both values are rounding noise)."""
+    sd_model, x, dy, _ = model_ref
+    g16 = _run_model(pkg, sd_model, x, dy, "bf16")
+    g32 = _run_model(pkg, sd_model, x, dy, "fp32")
+    bad, worst = [], (2.0, None)
+    for k, ref in g32.items():
+        if bn_fed_bias(k):
+            continue
+        cos = torch.nn.functional.cosine_similarity(g16[k].reshape(1, -1), ref.reshape(1, -1)).item()
+        print(f"[err] bf16 vs fp32 {k}: cos {cos:.5f} L2 {_errs(g16[k], ref)[0]:.2e}", flush=True)
+        worst = min(worst, (cos, k))
+        if not cos >= 0.95:
+            bad.append((k, round(cos, 4)))
+    print(f"[err] bf16 vs fp32 worst cosine {worst[0]:.5f} ({worst[1]})", flush=True)
+    assert not bad, f"bf16 gradients with cosine < 0.95 to the HIP fp32 path: {bad}"
+
+
 @pytest.mark.parametrize("cin,cout,stride", [(64, 64, 1), (128, 256, 2)])
 def test_layer_bf16_per_sample_A(K, pkg, cin, cout, stride):
     """The st_gcn part of an AAGCN layer (config 5): StgcnLayer with a dense per-sample adjacency
