@@ -211,6 +211,34 @@ int stgcn_gconv_wgrad_finish_bias(const float* dweff, const float* A, const floa
 int stgcn_gconv_wgrad_finish(const float* dweff, const float* A, const float* W, const int* nbr, const int* deg, int P,
                              int V, int J, int Cout, int Cin, float* dW, float* dA, void* work, void* stream);
 
+/* Graph-conv weight, adjacency and bias gradients in one pass over (x, dy) (bf16; gconv_wgrad_frame.hip),
+ * frame by frame on MFMA (autograd of ConvTemporalGraphical.forward, tgcn.py:71-79, with a shared A):
+ *   dW[p*Cout+co][ci] = sum_i sum_v (sum_w A[p][v][w] dy[(i,w)][co]) x[(i,v)][ci]
+ *   dA[p][v][w]       = sum_i sum_co (sum_ci W[p*Cout+co][ci] x[(i,v)][ci] + bconv[p*Cout+co]) dy[(i,w)][co]
+ *                       (dense: every (v, w), also off the graph's support)
+ *   db[p*Cout+co]     = sum_i sum_w (sum_v A[p][v][w]) dy[(i,w)][co]
+ * i over the NT = N*T frames, x / dy rows (i*V + v) with row strides x_ld / dy_ld.  A [P][V][V] fp32, W fp32
+ * [P*Cout][Cin] (the Conv2d weight), bconv fp32 [P*Cout] or NULL.  Outputs fp32, OVERWRITTEN.
+ * P <= 3, 16 < V <= 32, Cin and Cout multiples of 64, ld multiples of 8.  work: the workspace's bytes
+ * (per-block partials, summed in a fixed order: deterministic).  Replaces stgcn_gconv_wgrad +
+ * stgcn_gconv_wgrad_finish_bias (bf16).  Two launches. */
+typedef struct {
+  const void* x;
+  const void* dy;
+  const float* A;
+  const float* W;
+  const float* bconv;
+  float* dW;
+  float* dA;
+  float* db;
+  void* work;
+  long work_bytes;
+  int NT, V, P, Cin, Cout, x_ld, dy_ld;
+} stgcn_gconv_wgrad_frame_desc;
+
+long stgcn_gconv_wgrad_frame_workspace(const stgcn_gconv_wgrad_frame_desc* d);
+int stgcn_gconv_wgrad_frame(const stgcn_gconv_wgrad_frame_desc* d, void* stream);
+
 /* BatchNorm with batch statistics (nn.BatchNorm2d(track_running_stats=False), stgcn.py:152,160,171;
  * BatchNorm1d input norm, models/utils/batchnorm.py:13-23 viewed as [N*T][V*C]).
  * Partials are float4 (count, mean, M2, 0) per (row block, channel); finalize merges them (fp64). */

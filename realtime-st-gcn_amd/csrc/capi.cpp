@@ -47,6 +47,8 @@ int gconv_wgrad_finish_bias_launch(const float* dweff, const float* A, const flo
                                    int P, int V, int J, int Cout, int Cin, const float* bconv, const float* S, float* dW,
                                    float* dA, float* db, void* work, hipStream_t s);
 int amix_trans_launch(const AmixArgs& a, int dtype, hipStream_t s);
+long gconv_wgrad_frame_workspace(const stgcn_gconv_wgrad_frame_desc& a);
+int gconv_wgrad_frame_launch(const stgcn_gconv_wgrad_frame_desc& a, hipStream_t s);
 int amix_dA_launch(const AmixArgs& a, const void* dw, float* dA, void* work, int dtype, hipStream_t s);
 long amix_dA_workspace(const AmixArgs& a);
 int gcn_bias_bwd_launch(const float* A, const float* b, const float* S, int P, int V, int C, float* dA, float* db,
@@ -268,6 +270,13 @@ int stgcn_gconv_wgrad_finish(const float* dweff, const float* A, const float* W,
   if (!dweff || !A || !W || !nbr || !deg || P <= 0 || V <= 0 || J <= 0 || Cout <= 0 || Cin <= 0)
     return STGCN_EBADSHAPE;
   return gconv_wgrad_finish_launch(dweff, A, W, nbr, deg, P, V, J, Cout, Cin, dW, dA, work, STREAM(stream));
+}
+long stgcn_gconv_wgrad_frame_workspace(const stgcn_gconv_wgrad_frame_desc* d) {
+  return d ? gconv_wgrad_frame_workspace(*d) : -1;
+}
+int stgcn_gconv_wgrad_frame(const stgcn_gconv_wgrad_frame_desc* d, void* stream) {
+  if (!d) return STGCN_EBADSHAPE;
+  return gconv_wgrad_frame_launch(*d, STREAM(stream));
 }
 
 int stgcn_amix_fwd(const stgcn_amix_desc* d, int dtype, void* stream) {

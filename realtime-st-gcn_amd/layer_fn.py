@@ -512,33 +512,20 @@ class StgcnLayerFunction(torch.autograd.Function):
         bgp = bg.detach().float().view(P, Cout)
         if ctx.sup is not None:
             # data grad: same gather GEMM on dg over the reverse lists with transposed effective weights;
-            # weight/adjacency grads from dWeff[w][j] = sum_i dg[(i,w)] x[(i,S(w)_j)]^T
+            # weight / adjacency / bias grads: one pass of the frame kernel (bf16), else through the per-joint
+            # dWeff[w][j] = sum_i dg[(i,w)] x[(i,S(w)_j)]^T blocks
             sup = ctx.sup
             wg2 = wg.detach().float().reshape(P * Cout, Cin).contiguous()
-            with _fork(side):
-                fuse_s = A32.dim() == 3 and K.gconv_wgrad_rowsum_ok(sup, Cin, Cout, dtype)
-                dense_dA = ctx.cfg[6] and ctx.needs_input_grad[1]
-                # row sums: overwritten by the joint-grouped wgrad kernel
-                S_rows = torch.empty((V, Cout), dtype=torch.float32, device=dev) if fuse_s else None
-                dweff = K.gconv_wgrad(x, dg, sup, Cin, Cout, rowsum=S_rows)
-                if fuse_s and not dense_dA and K.gconv_finish_bias_ok(A32, sup):
-                    # dW, dA (support + bias through A) and db in two launches, outputs overwritten
-                    dwg2, dA, grads["bg"] = K.gconv_finish_bias(dweff, A32, wg2, sup, Cout, Cin,
-                                                                bg.detach().float().contiguous(), S_rows)
-                    dA_done = True
-                else:
-                    z_dwg, z_dA, z_S = zero_targets()
-                    dwg2, dA = K.gconv_finish(dweff, A32, wg2, sup, Cout, Cin, dW=z_dwg, dA=z_dA)
-                    dA_done = False
-                grads["wg"] = dwg2.view(P * Cout, Cin, 1, 1)
-                if dense_dA:
-                    # caller-owned A: the reference's dA is dense (also off the graph's support), so take
-                    # it from the A-first factorisation dA_p[v][w] = sum x[(i,v)] . (dg W_p)[(i,w)]
-                    wgTd = wg.detach().float().view(P, Cout, Cin).permute(0, 2, 1).reshape(1, P * Cin, Cout)
-                    wgTp, cq, kq = K.pack_weight(wgTd, dtype)
-                    dA = K.amix_dA(x, K.conv_rows(dg, wgTp, Cout, P * Cin, cq, kq, T, T), A32)
-                if not dA_done:
-                    dA = _bias_through_A(dA, A32, bg, bgp, dg, S_rows, zero_targets()[2], M1, Cout, V, grads)
+            if K.gconv_wgrad_frame_ok(A32, Cin, Cout, dtype):
+                with _fork(side):
+                    # one pass over (x, dg): dW, the dense dA (bias through A included) and db (gconv_wgrad_frame.hip)
+                    dwg2, dA, grads["bg"] = K.gconv_wgrad_frame(x, dg, A32, wg2, bg)
+                    grads["wg"] = dwg2.view(P * Cout, Cin, 1, 1)
+            else:
+                with _fork(side):
+                    _gconv_wgrad_dweff(ctx, x, dg, A32, wg, wg2, bg, bgp, sup, grads, zero_targets, P, Cin, Cout, T,
+                                       V, M1, dtype, dev)
+                dA = grads.pop("dA")
             if K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype, trans=True):  # dx = sum_p A_p-mix(dg) W_p^T, fused (gcn_tile.hip)
                 wdf = wg.detach().float().view(P, Cout, Cin).permute(2, 0, 1).reshape(Cin, P * Cout)
                 wimgT, cq, kwT = K.pack_gcn_weight(wdf, dtype)
@@ -592,6 +579,37 @@ def _bias_through_A(dA, A32, bg, bgp, dg, S_fused, z_S, M1, Cout, V, grads):
         dA = dA.contiguous()
     grads["bg"] = K.gcn_bias_bwd(A32, bg.detach().float().contiguous(), S, dA, Cout)
     return dA
+
+
+def _gconv_wgrad_dweff(ctx, x, dg, A32, wg, wg2, bg, bgp, sup, grads, zero_targets, P, Cin, Cout, T, V, M1, dtype,
+                       dev):
+    """Graph-conv weight / adjacency / bias gradients through the per-joint dWeff[w][j] = sum_i dg[(i,w)]
+    x[(i,S(w)_j)]^T blocks (gconv_wgrad + finish): the fp32 path and shapes gconv_wgrad_frame does not take.
+    Sets grads["wg"], grads["bg"], grads["dA"]."""
+    fuse_s = A32.dim() == 3 and K.gconv_wgrad_rowsum_ok(sup, Cin, Cout, dtype)
+    dense_dA = ctx.cfg[6] and ctx.needs_input_grad[1]
+    # row sums: overwritten by the joint-grouped wgrad kernel
+    S_rows = torch.empty((V, Cout), dtype=torch.float32, device=dev) if fuse_s else None
+    dweff = K.gconv_wgrad(x, dg, sup, Cin, Cout, rowsum=S_rows)
+    if fuse_s and not dense_dA and K.gconv_finish_bias_ok(A32, sup):
+        # dW, dA (support + bias through A) and db in two launches, outputs overwritten
+        dwg2, dA, grads["bg"] = K.gconv_finish_bias(dweff, A32, wg2, sup, Cout, Cin, bg.detach().float().contiguous(),
+                                                    S_rows)
+        dA_done = True
+    else:
+        z_dwg, z_dA, z_S = zero_targets()
+        dwg2, dA = K.gconv_finish(dweff, A32, wg2, sup, Cout, Cin, dW=z_dwg, dA=z_dA)
+        dA_done = False
+    grads["wg"] = dwg2.view(P * Cout, Cin, 1, 1)
+    if dense_dA:
+        # caller-owned A: the reference's dA is dense (also off the graph's support), so take
+        # it from the A-first factorisation dA_p[v][w] = sum x[(i,v)] . (dg W_p)[(i,w)]
+        wgTd = wg.detach().float().view(P, Cout, Cin).permute(0, 2, 1).reshape(1, P * Cin, Cout)
+        wgTp, cq, kq = K.pack_weight(wgTd, dtype)
+        dA = K.amix_dA(x, K.conv_rows(dg, wgTp, Cout, P * Cin, cq, kq, T, T), A32)
+    if not dA_done:
+        dA = _bias_through_A(dA, A32, bg, bgp, dg, S_rows, zero_targets()[2], M1, Cout, V, grads)
+    grads["dA"] = dA
 
 
 @K.on_tensor_device

@@ -704,6 +704,46 @@ def gconv_finish_bias_ok(A, sup) -> bool:
     return A.dim() == 3 and A.shape[0] <= 4 and A.shape[-1] <= 32 and A.shape[-1] * sup.J <= 256
 
 
+def gconv_wgrad_frame_ok(A, Cin, Cout, dtype) -> bool:
+    """Whether the graph-conv weight / adjacency / bias gradients take the one-pass frame kernel
+    (gconv_wgrad_frame.hip): bf16, a batch-shared A with P <= 3 and 16 < V <= 32, 64-multiple channels."""
+    return (ROUTING.gconv_wgrad_frame and dtype == torch.bfloat16 and A.dim() == 3 and A.shape[0] <= 3
+            and 16 < A.shape[-1] <= 32 and Cin % 64 == 0 and Cout % 64 == 0)
+
+
+def gconv_wgrad_frame(x, dy, A, W, bconv):
+    """(dW [P*Cout][Cin], dA [P][V][V] dense, db [P*Cout]) fp32, overwritten (stgcn_gconv_wgrad_frame): the
+    graph conv's weight, adjacency and bias gradients from its input rows x and output gradient rows dy."""
+    N, Cin, T, V = x.shape
+    A = _dense(A)
+    P = A.shape[0]
+    Cout = dy.shape[1]
+    dev = x.device
+    out = torch.empty(P * Cout * Cin + P * V * V + P * Cout, dtype=torch.float32, device=dev)
+    dW = out[:P * Cout * Cin].view(P * Cout, Cin)
+    dA = out[P * Cout * Cin:P * Cout * Cin + P * V * V].view(P, V, V)
+    db = out[P * Cout * Cin + P * V * V:]
+    W = _f32c(W.detach())
+    b = _f32c(bconv.detach()) if bconv is not None else None
+    d = L.GconvWgradFrameDesc()
+    d.x, d.dy, d.A, d.W, d.bconv = x.data_ptr(), dy.data_ptr(), A.data_ptr(), W.data_ptr(), L.ptr(b)
+    d.dW, d.dA, d.db = dW.data_ptr(), dA.data_ptr(), db.data_ptr()
+    d.NT, d.V, d.P, d.Cin, d.Cout, d.x_ld, d.dy_ld = N * T, V, P, Cin, Cout, rows_ld(x), rows_ld(dy)
+    nbytes = L.lib().stgcn_gconv_wgrad_frame_workspace(d)
+    if nbytes < 0:
+        raise RuntimeError("stgcn_amd: gconv_wgrad_frame: unsupported shape")
+    work = _workspace(nbytes, dev)
+    d.work, d.work_bytes = work.data_ptr(), work.numel() * 4
+    h = KTIME_HOOK
+    if h:
+        ktag = _k_start(h, "gconv_wgrad_frame", f"{Cin}->{Cout}", 2.0 * N * T * V * P * Cin * Cout * 2,
+                        x.element_size() * N * T * V * (Cin + Cout))
+    L.check(L.lib().stgcn_gconv_wgrad_frame(d, L.stream()), "gconv_wgrad_frame")
+    if h:
+        h(ktag, "end", None)
+    return dW, dA, db
+
+
 # ------------------------------------------------------------------------------------ BatchNorm
 def bn_stat_blocks(M: int) -> int:
     return L.lib().stgcn_bn_stat_blocks(M)

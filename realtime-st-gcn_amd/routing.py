@@ -22,6 +22,9 @@ also assign the attributes directly.
     gcn_afirst_min_c    STGCN_GCN_AFIRST_MIN_C=<C>  ... only for layers with at least C input channels (A/B of the
                                               A-first form where the gathered form's per-joint effective weights
                                               outgrow L2; default 0 = off)
+    gconv_wgrad_frame   STGCN_GWF=0           graph-conv weight / adjacency / bias gradients (bf16, shared A) in the
+                                              one-pass frame kernel gconv_wgrad_frame.hip instead of the per-joint
+                                              dWeff kernel + finish (default on)
     prep_plan           STGCN_PREP_PLAN=0     stgcn.Model training forwards pack every weight per call instead of
                                               in the one-launch plan (native.PrepPlan; default on)
 """
@@ -39,6 +42,7 @@ class _Routing:
         self.gcn_afirst = e("STGCN_GCN_AFIRST", "0") not in ("0", "")
         self.gcn_afirst_min_c = int(e("STGCN_GCN_AFIRST_MIN_C", "0") or 0)
         self.prep_plan = e("STGCN_PREP_PLAN", "1") != "0"
+        self.gconv_wgrad_frame = e("STGCN_GWF", "1") != "0"
 
 
 ROUTING = _Routing()

@@ -105,3 +105,30 @@ def assert_grad_close(got, ref, rel=1e-3, name="", scale_floor=0.0, reduction=Fa
         print(f"[l2-path] {name}: L2 {l2:.2e} frac beyond {frac:.2e} reduction={reduction}", flush=True)
     assert l2 <= 3 * rel and (frac <= 5e-3 or reduction), \
         f"{name}: max err {err.max().item():.3e} > {rel:g}*{scale:.3e}; L2 rel {l2:.2e}, frac beyond {frac:.2e}"
+
+
+def collect_ranks(q, procs, n, timeout=300):
+    """n results from the rank processes' queue; fails fast (instead of waiting out the timeout) when a rank
+    process has died with an error."""
+    import queue
+    import time
+    t0, out = time.time(), []
+    while len(out) < n:
+        try:
+            out.append(q.get(timeout=5))
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            if dead:
+                raise AssertionError(f"rank process exited with {dead[0]}")
+            if time.time() - t0 > timeout:
+                raise AssertionError("rank processes timed out")
+    return out
+
+
+def reap_ranks(procs):
+    for p in procs:
+        p.join(timeout=60)
+    for p in procs:  # our own children only, by handle
+        if p.is_alive():
+            p.terminate()
+            p.join(timeout=10)

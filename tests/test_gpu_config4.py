@@ -26,7 +26,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import ROOT, assert_close, assert_grad_close
+from conftest import ROOT, assert_close, assert_grad_close, collect_ranks, reap_ranks
 
 pytestmark = pytest.mark.gpu
 
@@ -141,12 +141,10 @@ def _spawn(dtype):
         p.start()
     got = {}
     try:
-        for _ in range(WORLD):
-            r, us, g = q.get(timeout=300)
+        for r, us, g in collect_ranks(q, procs, WORLD):
             got[r] = (us, g)
     finally:
-        for p in procs:
-            p.join(timeout=120)
+        reap_ranks(procs)
     for p in procs:
         assert p.exitcode == 0, f"rank process exited with {p.exitcode}"
     return got

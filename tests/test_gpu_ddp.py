@@ -20,7 +20,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import ROOT, assert_grad_close
+from conftest import ROOT, assert_grad_close, collect_ranks, reap_ranks
 
 pytestmark = pytest.mark.gpu
 
@@ -112,12 +112,10 @@ def _spawn(target, *args):
         p.start()
     got = {}
     try:
-        for _ in range(WORLD):
-            r, g = q.get(timeout=240)
+        for r, g in collect_ranks(q, procs, WORLD, timeout=240):
             got[r] = g
     finally:
-        for p in procs:
-            p.join(timeout=120)
+        reap_ranks(procs)
     for p in procs:
         assert p.exitcode == 0, f"rank process exited with {p.exitcode}"
     return got

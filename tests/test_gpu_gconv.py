@@ -117,3 +117,36 @@ def test_gconv_finish_bias_merged(K, pkg, Cin, Cout):
     dW, dA, db = K.gconv_finish_bias(dweff, A, W, sup, Cout, Cin, b, S)
     torch.cuda.synchronize()
     assert torch.equal(dW, dW_ref) and torch.equal(dA, dA_ref) and torch.equal(db, db_ref)
+
+
+@pytest.mark.parametrize("Cin,Cout,N,T", [(64, 64, 4, 40), (64, 128, 3, 29), (128, 128, 2, 33), (128, 256, 2, 21),
+                                          (256, 256, 2, 13), (64, 64, 64, 300)])
+@pytest.mark.parametrize("strategy", ["spatial", "uniform", "distance"])
+def test_gconv_wgrad_frame(K, pkg, Cin, Cout, N, T, strategy):
+    """stgcn_gconv_wgrad_frame (dW, the dense dA with the bias through A, db in one pass over (x, dy), bf16
+    operands) vs autograd of the reference's conv1x1 -> einsum(A) in fp32 on the same bf16-rounded inputs
+    (tgcn.py:71-79); tolerance 2e-2 of each gradient's max (the kernel rounds A, A dy and W^T dy to bf16 as the
+    reference's bf16 autocast rounds its einsum operands).  Run twice: bit-identical (fixed-order partials)."""
+    if N * T > 4000 and (strategy != "spatial"):
+        pytest.skip("config-2 size: spatial only")
+    torch.manual_seed(7)
+    A0 = torch.tensor(pkg.Graph(**dict(pkg.PKU_MMD, strategy=strategy)).A, dtype=torch.float32)
+    A = (A0 * (torch.rand(A0.shape) + 0.5)).requires_grad_(True)
+    P, V = A.shape[0], A.shape[-1]
+    xb = torch.randn(N, Cin, T, V).to(torch.bfloat16)
+    dyb = torch.randn(N, Cout, T, V).to(torch.bfloat16)
+    x = xb.float().requires_grad_(True)
+    W = (torch.randn(P * Cout, Cin) / Cin ** 0.5).requires_grad_(True)
+    b = torch.randn(P * Cout).requires_grad_(True)
+    ref = ref_gcn(x, A, W, b)
+    ref.backward(dyb.float())
+    assert K.gconv_wgrad_frame_ok(A0, Cin, Cout, torch.bfloat16)
+    Ad = A.detach().to(DEV).contiguous()
+    args = (cl(xb, torch.bfloat16), cl(dyb, torch.bfloat16), Ad, W.detach().to(DEV), b.detach().to(DEV))
+    dW, dA, db = K.gconv_wgrad_frame(*args)
+    dW2, dA2, db2 = K.gconv_wgrad_frame(*args)
+    torch.cuda.synchronize()
+    assert_close(dW.cpu(), W.grad, 2e-2, "frame dW")
+    assert_close(dA.cpu(), A.grad, 2e-2, "frame dA (dense)")
+    assert_close(db.cpu(), b.grad, 2e-2, "frame db")
+    assert torch.equal(dW, dW2) and torch.equal(dA, dA2) and torch.equal(db, db2)
