@@ -168,6 +168,18 @@ typedef struct {
 
 int stgcn_gcn_tile(const stgcn_gcn_tile_desc* d, int dtype, void* stream);
 long stgcn_gcn_tile_row_blocks(int NT, int V, int Cout);
+/* The same graph convolution in the reference's own order, the 1x1 conv first and the joint mix after, per frame
+ * (bf16; gcn_frame.hip):
+ *   trans_a 0: out[(i,w)][co] (+)= sum_p sum_v A[p][v][w] sum_ci W'[co][p*Cin+ci] in[(i,v)][ci]  (+ bias[w][co])
+ *   trans_a 1: out[(i,v)][c]  (+)= sum_p sum_w A[p][v][w] sum_k  W'[c][p*Cin+k]   in[(i,w)][k]
+ * W' as stgcn_gcn_tile's, given as U_p[c][k] = W'[c][p*Cin+k]: w_frag = the Kt = P MFMA-fragment image of U
+ * (stgcn_pack_weight_frag with Kt = P, Co = Cout, Ci = Cin; rows padded to Cout_pad % 32 == 0, columns to Kw_pad):
+ * forward U = the conv weight viewed (P, Cout, Cin), data grad its (P, Cin, Cout) transpose.
+ * Cin = 64 or 128 (the kernel's input channels), Cout % 64 == 0, 16 < V <= 32, P <= 3, row strides % 8 == 0.
+ * Optional BN partial statistics [stgcn_gcn_frame_row_blocks(NT, Cout)][Cout_pad] float4 (count, mean, M2).
+ * Replaces: conv1x1 + einsum of ConvTemporalGraphical.forward (tgcn.py:71-79) and its input grad. */
+int stgcn_gcn_frame(const stgcn_gcn_tile_desc* d, void* stream);
+long stgcn_gcn_frame_row_blocks(int NT, int Cout);
 long stgcn_gconv_row_blocks(int NT, int V);
 int stgcn_gconv_weights(const float* A, const float* W, const int* nbr, const int* deg, int P, int V, int J, int Cout,
                         int Cin, int trans, void* out, int rows_pad, int cols_pad, int dtype, void* stream);
@@ -480,7 +492,10 @@ int stgcn_window_grad(const void* dy, int ldd, int dtype, const float* x, int Ci
  *   kind 2 (graph conv): A [P][V][V] (times the edge importance M [P][V][V] when non-NULL: the product the
  *                  model feeds the layer, formed here exactly as a rounded fp32 product), W = src
  *                  [P*Cout][Cin] (Co = Cout, Ci = Cin), nbr / deg support lists, trans, dst [V][J][R_pad]
- *                  [C_pad] (dtype), and for trans 0 with bconv non-NULL bias2d [V][Cout].
+ *                  [C_pad] (dtype), and for trans 0 with bconv non-NULL bias2d [V][Cout];
+ *   kind 3 (graph-conv bias through A alone, the frame-kernel route): A (times M when non-NULL), bconv
+ *                  [P*Cout] (Co = Cout) -> bias2d [V][Cout] = sum_p bconv[p*Cout+c] sum_v (A*M)[p][v][w]
+ *                  (src = bconv, dst = bias2d, Ci = 1).
  * stgcn_prep_check validates a host-side job array and fills each job's thread count (threads);
  * stgcn_prep_run launches the jobs from a DEVICE copy of that array with block_start [njobs + 1] (device,
  * block_start[j] = first 256-thread block of job j, block_start[njobs] = nblocks). */

@@ -48,6 +48,8 @@ int gconv_wgrad_finish_bias_launch(const float* dweff, const float* A, const flo
                                    float* dA, float* db, void* work, hipStream_t s);
 int amix_trans_launch(const AmixArgs& a, int dtype, hipStream_t s);
 long gconv_wgrad_frame_workspace(const stgcn_gconv_wgrad_frame_desc& a);
+int gcn_frame_launch(const stgcn_gcn_tile_desc& a, hipStream_t s);
+long gcn_frame_row_blocks(int NT, int Cout);
 int gconv_wgrad_frame_launch(const stgcn_gconv_wgrad_frame_desc& a, hipStream_t s);
 int amix_dA_launch(const AmixArgs& a, const void* dw, float* dA, void* work, int dtype, hipStream_t s);
 long amix_dA_workspace(const AmixArgs& a);
@@ -271,6 +273,11 @@ int stgcn_gconv_wgrad_finish(const float* dweff, const float* A, const float* W,
     return STGCN_EBADSHAPE;
   return gconv_wgrad_finish_launch(dweff, A, W, nbr, deg, P, V, J, Cout, Cin, dW, dA, work, STREAM(stream));
 }
+int stgcn_gcn_frame(const stgcn_gcn_tile_desc* d, void* stream) {
+  if (!d) return STGCN_EBADSHAPE;
+  return gcn_frame_launch(*d, STREAM(stream));
+}
+long stgcn_gcn_frame_row_blocks(int NT, int Cout) { return gcn_frame_row_blocks(NT, Cout); }
 long stgcn_gconv_wgrad_frame_workspace(const stgcn_gconv_wgrad_frame_desc* d) {
   return d ? gconv_wgrad_frame_workspace(*d) : -1;
 }

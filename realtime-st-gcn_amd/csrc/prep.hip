@@ -20,7 +20,7 @@ __global__ __launch_bounds__(256) void prep_kernel(const stgcn_prep_job* __restr
   }
   const stgcn_prep_job& j = jobs[lo];
   __shared__ float colsum[GW_COLSUM_MAX];
-  if (j.kind == 2 && j.bias2d) gconv_colsum_block(j.A, j.M, j.P, j.V, colsum);  // block-uniform: one job per block
+  if ((j.kind == 2 && j.bias2d) || j.kind == 3) gconv_colsum_block(j.A, j.M, j.P, j.V, colsum);  // block-uniform
   const long i = (b - start[lo]) * 256 + threadIdx.x;
   if (i >= j.threads) return;
   if (j.kind == 0) {
@@ -31,6 +31,12 @@ __global__ __launch_bounds__(256) void prep_kernel(const stgcn_prep_job* __restr
   } else if (j.kind == 1) {
     const int co_f = j.trans ? 2 * j.Co : j.Co, ci_f = j.trans ? j.Ci : 2 * j.Ci;
     pack_s2frag_elem(j.src, j.s0, j.s1, j.s2, j.Co, j.Ci, j.trans, co_f, ci_f, i, (bf16*)j.dst);
+  } else if (j.kind == 3) {
+    // the graph-conv bias pushed through A alone (frame-kernel route, gcn_frame.hip): thread = (joint, channel)
+    const int a = (int)(i / j.Co), r = (int)(i - (long)a * j.Co);
+    float sb = 0.f;
+    for (int p = 0; p < j.P; ++p) sb += j.bconv[p * j.Co + r] * colsum[p * j.V + a];
+    j.bias2d[(long)a * j.Co + r] = sb;
   } else {
     if (j.dtype == 1)
       gconv_weights_elem<bf16>(j.A, j.M, j.src, j.nbr, j.deg, j.P, j.V, j.J, j.Co, j.Ci, j.trans, (bf16*)j.dst,
@@ -64,6 +70,10 @@ extern "C" int stgcn_prep_check(stgcn_prep_job* jobs, int njobs) {
           (j.bias2d && (j.trans || !j.bconv || j.P * j.V > GW_COLSUM_MAX)))
         return STGCN_EBADSHAPE;
       j.threads = (long)j.V * j.R_pad * (j.C_pad / 8);
+    } else if (j.kind == 3) {
+      if (!j.A || !j.bconv || !j.bias2d || j.P <= 0 || j.P > GW_PMAX || j.V <= 0 || j.P * j.V > GW_COLSUM_MAX)
+        return STGCN_EBADSHAPE;
+      j.threads = (long)j.V * j.Co;
     } else {
       return STGCN_EBADSHAPE;
     }

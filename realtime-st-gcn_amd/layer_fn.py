@@ -135,11 +135,12 @@ class LayerPacks:
     """Packed operands of one StgcnLayer's training step, filled by the model's PrepPlan launch
     (native.PrepPlan): graph-conv effective weights + bias through A (forward), their data-gradient form,
     temporal conv (forward / data gradient) and residual 1x1 conv (forward / data gradient) packs, each as
-    the (tensor, Cout_pad, Cin_pad) triple pack_weight returns (gw: (weights, bias2d))."""
-    __slots__ = ("gw", "gwT", "wt", "wtT", "wr", "wrT")
+    the (tensor, Cout_pad, Cin_pad) triple pack_weight returns (gw: (weights, bias2d)); gf / gfT: the frame-streaming
+    graph conv's forward (image triple, bias2d) and data-gradient image triple (pack_gcn_frame), when it takes them."""
+    __slots__ = ("gw", "gwT", "gf", "gfT", "wt", "wtT", "wr", "wrT")
 
     def __init__(self):
-        self.gw = self.gwT = self.wt = self.wtT = self.wr = self.wrT = None
+        self.gw = self.gwT = self.gf = self.gfT = self.wt = self.wtT = self.wr = self.wrT = None
 
 
 def plan_layer_packs(plan, layer, A, M, dtype):
@@ -155,10 +156,17 @@ def plan_layer_packs(plan, layer, A, M, dtype):
         return None
     pk = LayerPacks()
     if not layer.afirst_forced():  # the A-first graph conv packs its channel GEMM per call
-        wg2 = layer.gcn.conv.weight.detach().reshape(P * Cout, Cin)
-        pk.gw = K.gconv_weights(A, wg2, sup, Cout, Cin, False, dtype, bias=layer.gcn.conv.bias.detach(), plan=plan,
-                                M=M)
-        if not K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype, trans=True):
+        wg = layer.gcn.conv.weight
+        wg2 = wg.detach().reshape(P * Cout, Cin)
+        if K.gcn_frame_ok(sup, P, Cin, Cout, V, dtype):
+            pk.gf = (K.pack_gcn_frame(wg, P, Cout, Cin, False, dtype, plan=plan),
+                     K.gcn_bias_plan(A, layer.gcn.conv.bias, Cout, plan, M=M))
+        else:
+            pk.gw = K.gconv_weights(A, wg2, sup, Cout, Cin, False, dtype, bias=layer.gcn.conv.bias.detach(), plan=plan,
+                                    M=M)
+        if K.gcn_frame_ok(sup, P, Cout, Cin, V, dtype) and not K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype, trans=True):
+            pk.gfT = K.pack_gcn_frame(wg, P, Cout, Cin, True, dtype, plan=plan)
+        elif not K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype, trans=True):
             pk.gwT = K.gconv_weights(A, wg2, sup, Cout, Cin, True, dtype, plan=plan, M=M)
     wt = conv.weight.detach().squeeze(-1)
     pk.wt = K.pack_weight(wt.permute(2, 0, 1), dtype, stride=stride, plan=plan)
@@ -279,15 +287,21 @@ class StgcnLayerFunction(torch.autograd.Function):
             ctx.in_dtype = A.dtype
             return y
         tiled = gather and K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype)  # fused frame-tiled graph conv
-        # gathered path: bias2d comes out of the effective-weight launch below
+        # frame-streaming graph conv (1x1 conv then joint mix per frame, gcn_frame.hip)
+        framed = gather and not tiled and K.gcn_frame_ok(sup, P, Cin, Cout, V, dtype)
+        # gathered / framed paths: bias2d comes from the weight preparation below
         bias2d = None if (gather and not tiled) else K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
         if norm == BN:  # all BatchNorm partial-statistics buffers of the layer from one zero fill
             cpo = -(-Cout // K.col_tile(Cout)) * K.col_tile(Cout)
-            rb1 = (K.gcn_tile_row_blocks(N * T, V, Cout) if tiled else K.gconv_row_blocks(N * T, V)) if gather \
-                else K.row_blocks(M1, Cout)
-            st_shapes = [(rb1, cpo, 4),
+            if framed:
+                rb1, cp1 = K.gcn_frame_row_blocks(N * T, Cout), -(-Cout // 32) * 32
+            else:
+                rb1 = (K.gcn_tile_row_blocks(N * T, V, Cout) if tiled else K.gconv_row_blocks(N * T, V)) if gather \
+                    else K.row_blocks(M1, Cout)
+                cp1 = cpo
+            st_shapes = [(rb1, cp1, 4),
                          (K.row_blocks(M2, Cout), cpo, 4)] + ([(K.row_blocks(M2, Cout), cpo, 4)] if res_conv else [])
-            st_all = _stats_arena(cache, dev, x.dtype, st_shapes, (tiled, gather))
+            st_all = _stats_arena(cache, dev, x.dtype, st_shapes, (tiled, gather, framed))
             st1, st2 = st_all[0], st_all[1]
             str_ = st_all[2] if res_conv else None
         # ---- residual branch: independent of the graph conv -> temporal conv chain until the output norm,
@@ -315,8 +329,17 @@ class StgcnLayerFunction(torch.autograd.Function):
                 assert cpg == cpo
             g = K.gcn_tile(x, A32, wimg, kwg, Cin, Cout, cpg, sup, bias=bias2d, stats=st1 if norm == BN else None)
             XA = None
+        elif framed:  # per frame: 1x1 conv then joint mix on MFMA (gcn_frame.hip), no XA in HBM
+            if packs is not None and packs.gf is not None:
+                img, bias2d = packs.gf
+            else:
+                img = K.pack_gcn_frame(wg, P, Cout, Cin, False, dtype)
+                bias2d = K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
+            cpg, kpg = img[1], img[2]
+            g = K.gcn_frame(x, A32, img, Cin, Cout, bias=bias2d, stats=st1 if norm == BN else None)
+            XA = None
         elif gather:  # joint-gathered GEMM over per-joint effective weights (gconv.hip), no XA in HBM
-            if packs is not None:
+            if packs is not None and packs.gw is not None:
                 wgp, bias2d = packs.gw
             else:
                 wg2 = wg.detach().float().reshape(P * Cout, Cin).contiguous()
@@ -526,7 +549,12 @@ class StgcnLayerFunction(torch.autograd.Function):
                     _gconv_wgrad_dweff(ctx, x, dg, A32, wg, wg2, bg, bgp, sup, grads, zero_targets, P, Cin, Cout, T,
                                        V, M1, dtype, dev)
                 dA = grads.pop("dA")
-            if K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype, trans=True):  # dx = sum_p A_p-mix(dg) W_p^T, fused (gcn_tile.hip)
+            if K.gcn_frame_ok(sup, P, Cout, Cin, V, dtype) and not K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype, trans=True):
+                # dx (+)= sum_p A_p-mix(dg W_p) per frame (gcn_frame.hip)
+                imgT = packs.gfT if packs is not None and packs.gfT is not None else \
+                    K.pack_gcn_frame(wg, P, Cout, Cin, True, dtype)
+                K.gcn_frame(dg, A32, imgT, Cout, Cin, trans_a=True, out=dx, accumulate=dx_written)
+            elif K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype, trans=True):  # dx = sum_p A_p-mix(dg) W_p^T, fused (gcn_tile.hip)
                 wdf = wg.detach().float().view(P, Cout, Cin).permute(2, 0, 1).reshape(Cin, P * Cout)
                 wimgT, cq, kwT = K.pack_gcn_weight(wdf, dtype)
                 K.gcn_tile(dg, A32, wimgT, kwT, Cout, Cin, cq, sup, trans_a=True, out=dx, accumulate=dx_written)

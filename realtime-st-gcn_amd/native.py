@@ -553,6 +553,81 @@ def gcn_tile(x, A, wimg, kw_pad, Cin, Cout, cp, sup, trans_a=False, bias=None, s
     return out
 
 
+def gcn_frame_ok(sup, P, Cin, Cout, V, dtype) -> bool:
+    """Whether a graph conv with ``Cin`` kernel-input and ``Cout`` kernel-output channels (forward: the layer's;
+    data grad: swapped) runs on the frame-streaming kernel gcn_frame.hip (bf16, shared A, P <= 3, 16 < V <= 32,
+    Cin 64 or 128, Cout % 64 == 0; routing.gcn_frame)."""
+    return (ROUTING.gcn_frame and dtype == torch.bfloat16 and sup is not None and P <= 3 and 16 < V <= 32
+            and Cin in (64, 128) and Cout % 64 == 0)
+
+
+def gcn_frame_row_blocks(NT: int, Cout: int) -> int:
+    return L.lib().stgcn_gcn_frame_row_blocks(NT, Cout)
+
+
+def pack_gcn_frame(w, P, Cout, Cin, trans, dtype, plan=None):
+    """U image of stgcn_gcn_frame from the graph-conv weight w (P*Cout, Cin, 1, 1): the Kt = P MFMA-fragment image of
+    w viewed (P, Cout, Cin) (forward) or of its (P, Cin, Cout) transpose (data grad).  Returns (image, rows_pad,
+    cols_pad).  ``plan``: record the job in a PrepPlan (the view keeps pointing at the parameter)."""
+    w3 = w.detach().view(P, Cout, Cin)
+    if trans:
+        w3 = w3.transpose(1, 2)
+    if w3.dtype != torch.float32:
+        w3 = w3.float()
+    Kt, Co, Ci = w3.shape
+    cp, kp = -(-Co // 32) * 32, -(-Ci // 16) * 16
+    n = Kt * cp * kp
+    code = L.dtype_code(dtype)
+    buf = torch.empty(2 * n, dtype=dtype, device=w.device)
+    if plan is not None:
+        plan.add(kind=0, dtype=code, src=w3, Kt=Kt, Co=Co, Ci=Ci, cp=cp, kp=kp, dst=buf[:n], dst_frag=buf[n:])
+    else:
+        s0, s1, s2 = w3.stride()
+        L.check(L.lib().stgcn_pack_weight_frag(w3.data_ptr(), s0, s1, s2, Kt, Co, Ci, buf[:n].data_ptr(),
+                                               buf[n:].data_ptr(), cp, kp, code, L.stream()), "pack_weight_frag")
+    return buf[n:], cp, kp
+
+
+def gcn_bias_plan(A, b, Cout, plan, M=None):
+    """bias2d [V][Cout] = sum_p b_p colsum_p(A * M) recorded as a PrepPlan job (kind 3)."""
+    A = _dense(A)
+    P, V = A.shape[0], A.shape[-1]
+    b2 = torch.empty((V, Cout), dtype=torch.float32, device=A.device)
+    bc = b.detach()
+    plan.add(kind=3, dtype=1, src=bc.view(1, -1), dst=b2, Co=Cout, Ci=1, A=A, M=None if M is None else _dense(M), P=P, V=V,
+             bconv=bc, bias2d=b2)
+    return b2
+
+
+def gcn_frame(x, A, img, Cin, Cout, trans_a=False, bias=None, stats=None, out=None, accumulate=False, tag=None):
+    """Graph conv on the frame-streaming kernel (stgcn_gcn_frame): out rows (N, Cout, T, V) (+)= the 1x1 conv
+    then the joint mix (trans_a: the data gradient's transposed mix) (+ bias[w][co]); img = pack_gcn_frame's
+    (image, rows_pad, cols_pad)."""
+    N, _, T, V = x.shape
+    if out is None:
+        out = cl_empty(N, Cout, T, V, x.dtype, x.device)
+    A = _dense(A)
+    wimg, cp, kp = img
+    d = L.GcnTileDesc()
+    d.in_, d.out, d.w_frag, d.A = x.data_ptr(), out.data_ptr(), wimg.data_ptr(), A.data_ptr()
+    d.bias, d.stats = L.ptr(bias), L.ptr(stats)
+    d.NT, d.V, d.P, d.Cin, d.Cout, d.Cout_pad, d.Kw_pad = N * T, V, A.shape[0], Cin, Cout, cp, kp
+    d.in_ld, d.out_ld = rows_ld(x), rows_ld(out)
+    d.trans_a, d.accumulate = int(trans_a), int(accumulate)
+    if stats is not None and stats.shape[1] != cp:
+        raise RuntimeError("stgcn_amd: gcn_frame statistics rows must be rows_pad wide")
+    h = KTIME_HOOK
+    if h:
+        P = A.shape[0]
+        ktag = _k_start(h, "gcn_frame_dgrad" if trans_a else "gcn_frame_fwd", f"{Cin}->{Cout}",
+                        2.0 * N * T * V * P * Cin * Cout,
+                        x.element_size() * N * T * V * (Cin + Cout * (2 if accumulate else 1)))
+    L.check(L.lib().stgcn_gcn_frame(d, L.stream()), "gcn_frame")
+    if h:
+        h(ktag, "end", None)
+    return out
+
+
 def layer_fused_ok(sup, P, Cin, Cout, V, kt, stride, dtype) -> bool:
     """Whether a layer's forward can run as the fused graph conv + BN1 + ReLU + temporal conv kernel
     (layer_fused.hip): bf16, 64 -> 64 channels, stride 1, Kt = 9, a batch-shared graph, 16 < V <= 25.

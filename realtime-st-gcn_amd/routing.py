@@ -25,6 +25,9 @@ also assign the attributes directly.
     gconv_wgrad_frame   STGCN_GWF=0           graph-conv weight / adjacency / bias gradients (bf16, shared A) in the
                                               one-pass frame kernel gconv_wgrad_frame.hip instead of the per-joint
                                               dWeff kernel + finish (default on)
+    gcn_frame           STGCN_GCN_FRAME=0     graph conv forward / data grad (bf16, shared A, 64 or 128 kernel-input
+                                              channels) on the frame-streaming kernel gcn_frame.hip instead of the
+                                              joint-gathered gconv.hip (default on)
     prep_plan           STGCN_PREP_PLAN=0     stgcn.Model training forwards pack every weight per call instead of
                                               in the one-launch plan (native.PrepPlan; default on)
 """
@@ -43,6 +46,7 @@ class _Routing:
         self.gcn_afirst_min_c = int(e("STGCN_GCN_AFIRST_MIN_C", "0") or 0)
         self.prep_plan = e("STGCN_PREP_PLAN", "1") != "0"
         self.gconv_wgrad_frame = e("STGCN_GWF", "1") != "0"
+        self.gcn_frame = e("STGCN_GCN_FRAME", "1") != "0"
 
 
 ROUTING = _Routing()

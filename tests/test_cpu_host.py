@@ -160,7 +160,8 @@ def test_prep_plan_builds_and_validates(pkg):
     """The one-launch weight preparation of the config-2 model (stgcn.Model._prepared -> native.PrepPlan):
     the per-layer jobs are recorded and validated on the host (stgcn_prep_check fills each job's thread
     count) — 9 layers x (graph conv fwd + data grad, temporal conv fwd + data grad) + 2 residual convs x 2 +
-    the head's 2 x 2, where the stride-2 temporal packs take two jobs each (plain + folded image)."""
+    the head's 2 x 2, where the stride-2 temporal packs take two jobs each (plain + folded image), and the frame
+    kernel's graph-conv forward two (weight image + bias through A)."""
     import bench
     m = pkg.MODELS["st-gcn"](rank=None, **dict(bench.ARCH, graph=pkg.PKU_MMD)).set_compute_dtype("bf16")
     K, LF = pkg.native, pkg.layer_fn
@@ -173,7 +174,11 @@ def test_prep_plan_builds_and_validates(pkg):
             LF.plan_conv1x1_packs(plan, m.fcn_out.weight, torch.bfloat16))
     plan.finalize()
     assert all(p is not None for p in layers)
-    assert plan.njobs == 9 * 4 + 2 * 2 + 2 * 2 + 2 * 2
+    # the frame-streaming graph conv's forward takes two jobs (U image + the bias through A, kind 3): layers with
+    # 64 or 128 input channels (0-6)
+    framed = sum(p.gf is not None for p in layers)
+    assert framed == (7 if pkg.routing.ROUTING.gcn_frame else 0)
+    assert plan.njobs == 9 * 4 + framed + 2 * 2 + 2 * 2 + 2 * 2
     assert plan.nblocks > 0
     # frag images where the kernels expect them
     assert layers[0].wt[0].frag_stride == 1 and layers[3].wt[0].frag_stride == 2 and layers[3].wtT[0].frag_stride == 2
