@@ -176,7 +176,8 @@ long stgcn_gcn_tile_row_blocks(int NT, int V, int Cout);
  * (stgcn_pack_weight_frag with Kt = P, Co = Cout, Ci = Cin; rows padded to Cout_pad % 32 == 0, columns to Kw_pad):
  * forward U = the conv weight viewed (P, Cout, Cin), data grad its (P, Cin, Cout) transpose.
  * Cin = 64 or 128 (the kernel's input channels), Cout % 64 == 0, 16 < V <= 32, P <= 3, row strides % 8 == 0.
- * Optional BN partial statistics [stgcn_gcn_frame_row_blocks(NT, Cout)][Cout_pad] float4 (count, mean, M2).
+ * Optional BN partial statistics [stgcn_gcn_frame_row_blocks(NT, Cout)][Cout_pad] float4 (count, mean, M2);
+ * out = NULL: statistics only (no stores; pass 1 of the fused BatchNorm layer).
  * Replaces: conv1x1 + einsum of ConvTemporalGraphical.forward (tgcn.py:71-79) and its input grad. */
 int stgcn_gcn_frame(const stgcn_gcn_tile_desc* d, void* stream);
 long stgcn_gcn_frame_row_blocks(int NT, int Cout);

@@ -182,6 +182,7 @@ __global__ __launch_bounds__(NW * 64, 2) void gcf_kernel(const stgcn_gcn_tile_de
     s2[r] = 0.f;
   }
   const bool stats = a.stats != nullptr;
+  const bool has_out = a.out != nullptr;  // NULL: BatchNorm statistics only (pass 1 of the fused BN layer)
 
   for (int k = 0; k < nsteps; ++k) {
     // ops issued after step k's DMA: (D - 2) DMA steps + the stores of this wave's valid frames among the
@@ -190,7 +191,7 @@ __global__ __launch_bounds__(NW * 64, 2) void gcf_kernel(const stgcn_gcn_tile_de
       const int j0 = max(0, k - D + 2);
       int nv = 0;
       for (int j = j0; j < k; ++j) nv += (f0 + 2 * j + fp < f1) ? 1 : 0;
-      wait_vm<XMAX>((D - 2) * NDMA + NST * nv);
+      wait_vm<XMAX>((D - 2) * NDMA + (has_out ? NST : 0) * nv);
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     const int f = f0 + 2 * k + fp;
@@ -231,7 +232,7 @@ __global__ __launch_bounds__(NW * 64, 2) void gcf_kernel(const stgcn_gcn_tile_de
 #pragma unroll
         for (int e = 0; e < 4; ++e) st[e] = (bf16)v[4 * q + e];
         // lanes past V store nothing; the wave's store instruction still issues (counted above)
-        if (jok) *reinterpret_cast<u32x2*>(orow + 8 * q) = __builtin_bit_cast(u32x2, st);
+        if (has_out && jok) *reinterpret_cast<u32x2*>(orow + 8 * q) = __builtin_bit_cast(u32x2, st);
       }
       if (stats && jok) {
 #pragma unroll
@@ -289,8 +290,8 @@ long gcn_frame_row_blocks(int NT, int Cout) {
 }
 
 int gcn_frame_launch(const stgcn_gcn_tile_desc& a, hipStream_t s) {
-  if (a.V <= 16 || a.V > 32 || a.P < 1 || a.P > 3 || a.NT < 1 || !a.in || !a.out || !a.w_frag || !a.A)
-    return STGCN_EBADSHAPE;
+  if (a.V <= 16 || a.V > 32 || a.P < 1 || a.P > 3 || a.NT < 1 || !a.in || !a.w_frag || !a.A) return STGCN_EBADSHAPE;
+  if (!a.out && (!a.stats || a.accumulate)) return STGCN_EBADSHAPE;  // statistics-only launches need stats
   if ((a.Cin != 64 && a.Cin != 128) || a.in_ld % 8 || a.Cout % 64 || a.Cout_pad < a.Cout || a.out_ld % 8)
     return STGCN_EBADSHAPE;
   if (a.Kw_pad < a.Cin || a.Kw_pad % 16 || a.Cout_pad % 32) return STGCN_EBADSHAPE;

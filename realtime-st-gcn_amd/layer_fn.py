@@ -125,7 +125,10 @@ def _packs(cache, wg, wt, P, Cin, Cout, dtype):
     wimg, cpg, kwg = K.pack_gcn_weight(wgf, dtype)
     wt3 = wt.detach().float().squeeze(-1).permute(2, 0, 1)  # [Kt][Cout][Cin]
     wtp, _, _ = K.pack_weight(wt3, dtype, stride=1)
-    val = (wimg, cpg, kwg, wtp)
+    # pass 1 of the BatchNorm form (graph-conv statistics) on the frame-streaming kernel where it runs
+    fimg = K.pack_gcn_frame(wg, P, Cout, Cin, False, dtype) if ROUTING.gcn_frame and dtype == torch.bfloat16 \
+        and Cin in (64, 128) and Cout % 64 == 0 else None
+    val = (wimg, cpg, kwg, wtp, fimg)
     if cache is not None:
         cache["key"], cache["val"] = key, val
     return val
@@ -196,7 +199,7 @@ def fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, su
     Cout = wt.shape[0]
     dev = x.device
     bias2d = K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
-    wimg, cpg, kwg, wtp = _packs(cache, wg, wt, P, Cin, Cout, dtype)
+    wimg, cpg, kwg, wtp, fimg = _packs(cache, wg, wt, P, Cin, Cout, dtype)
     if norm == LN:
         # the [V][64] parameter rows, re-laid-out only when a LayerNorm parameter changed (4 copy launches)
         lkey = tuple((t.data_ptr(), t._version) for t in (n1w, n1b, n2w, n2b))
@@ -208,11 +211,17 @@ def fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, su
                 cache["ln_key"], cache["ln_val"] = lkey, ln
         return K.layer_fused(x, A32, wimg, bias2d, None, None, wtp, bt.detach().float().contiguous(), tag=tag,
                              ln=ln, residual=residual, train=train)
-    rb1, rb2 = K.gcn_tile_row_blocks(N * T, V, Cout), K.layer_fused_row_blocks(N, T)
-    # both kernels write every row block of their statistics: no zero fill
-    st1 = torch.empty((rb1, cpg, 4), dtype=torch.float32, device=dev)
+    rb2 = K.layer_fused_row_blocks(N, T)
     st2 = torch.empty((rb2, Cout, 4), dtype=torch.float32, device=dev)
-    K.gcn_tile(x, A32, wimg, kwg, Cin, Cout, cpg, sup, bias=bias2d, stats=st1, stats_only=True)
+    # both kernels write every row block of their statistics: no zero fill
+    if fimg is not None and fimg[1] == cpg:  # pass 1: graph-conv statistics only (gcn_frame.hip)
+        rb1 = K.gcn_frame_row_blocks(N * T, Cout)
+        st1 = torch.empty((rb1, cpg, 4), dtype=torch.float32, device=dev)
+        K.gcn_frame(x, A32, fimg, Cin, Cout, bias=bias2d, stats=st1, stats_only=True)
+    else:
+        rb1 = K.gcn_tile_row_blocks(N * T, V, Cout)
+        st1 = torch.empty((rb1, cpg, 4), dtype=torch.float32, device=dev)
+        K.gcn_tile(x, A32, wimg, kwg, Cin, Cout, cpg, sup, bias=bias2d, stats=st1, stats_only=True)
     _, sc1, sh1 = K.bn_finalize(st1, rb1, cpg, Cout, n1w.detach().float(), n1b.detach().float())
     z = K.layer_fused(x, A32, wimg, bias2d, sc1, sh1, wtp, bt.detach().float().contiguous(), stats=st2, tag=tag)
     _, sc2, sh2 = K.bn_finalize(st2, rb2, Cout, Cout, n2w.detach().float(), n2b.detach().float())

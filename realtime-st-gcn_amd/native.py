@@ -599,20 +599,24 @@ def gcn_bias_plan(A, b, Cout, plan, M=None):
     return b2
 
 
-def gcn_frame(x, A, img, Cin, Cout, trans_a=False, bias=None, stats=None, out=None, accumulate=False, tag=None):
+def gcn_frame(x, A, img, Cin, Cout, trans_a=False, bias=None, stats=None, out=None, accumulate=False, tag=None,
+              stats_only=False):
     """Graph conv on the frame-streaming kernel (stgcn_gcn_frame): out rows (N, Cout, T, V) (+)= the 1x1 conv
     then the joint mix (trans_a: the data gradient's transposed mix) (+ bias[w][co]); img = pack_gcn_frame's
-    (image, rows_pad, cols_pad)."""
+    (image, rows_pad, cols_pad).  stats_only: no output, the BatchNorm partial statistics only (returns None)."""
     N, _, T, V = x.shape
-    if out is None:
+    if stats_only:
+        if stats is None or out is not None or accumulate:
+            raise RuntimeError("stgcn_amd: gcn_frame stats_only needs a stats buffer and no output")
+    elif out is None:
         out = cl_empty(N, Cout, T, V, x.dtype, x.device)
     A = _dense(A)
     wimg, cp, kp = img
     d = L.GcnTileDesc()
-    d.in_, d.out, d.w_frag, d.A = x.data_ptr(), out.data_ptr(), wimg.data_ptr(), A.data_ptr()
+    d.in_, d.out, d.w_frag, d.A = x.data_ptr(), L.ptr(out), wimg.data_ptr(), A.data_ptr()
     d.bias, d.stats = L.ptr(bias), L.ptr(stats)
     d.NT, d.V, d.P, d.Cin, d.Cout, d.Cout_pad, d.Kw_pad = N * T, V, A.shape[0], Cin, Cout, cp, kp
-    d.in_ld, d.out_ld = rows_ld(x), rows_ld(out)
+    d.in_ld, d.out_ld = rows_ld(x), (rows_ld(out) if out is not None else Cout)
     d.trans_a, d.accumulate = int(trans_a), int(accumulate)
     if stats is not None and stats.shape[1] != cp:
         raise RuntimeError("stgcn_amd: gcn_frame statistics rows must be rows_pad wide")
