@@ -48,6 +48,13 @@ typedef struct {
 } stgcn_conv_desc;
 
 int stgcn_conv_rows(const stgcn_conv_desc* d, int dtype, void* stream);
+/* The 64-channel Kt = 9 stride-1 temporal conv (stgcn.py:151-159) forward (trans 0, pro 0 or 1: BN1 scale /
+ * shift + ReLU on the input, bias_mode 0/1, optional BN partial statistics [stgcn_tconv_frame_row_blocks(N, T)]
+ * [Cout_pad]) and data gradient (trans 1, pro 0), bf16, on the frame-streaming kernel (tconv_frame.hip): the same
+ * arithmetic as stgcn_conv_rows for these shapes; w_frag = the MFMA-fragment image of the packed weight
+ * (stgcn_pack_weight_frag, Kt = 9), Cin = Cout = 64, pad = 4, 16 < V <= 32, no accumulate. */
+int stgcn_tconv_frame(const stgcn_conv_desc* d, void* stream);
+long stgcn_tconv_frame_row_blocks(int N, int T);
 /* Pack an fp32 weight given as any strided [Kt][Cout][Cin] view (element (k,co,ci) at src[k*s0+co*s1+ci*s2])
  * into the zero-padded contiguous [Kt][Cout_pad][Cin_pad] dtype image stgcn_conv_rows reads. */
 int stgcn_pack_weight(const float* src, long s0, long s1, long s2, int Kt, int Cout, int Cin, void* dst, int Cout_pad,

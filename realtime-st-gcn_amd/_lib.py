@@ -126,6 +126,8 @@ _SIGS = {
     "stgcn_gcn_tile": (c_int, [ctypes.POINTER(GcnTileDesc), c_int, c_void_p]),
     "stgcn_gcn_tile_row_blocks": (ctypes.c_long, [c_int, c_int, c_int]),
     "stgcn_gcn_frame": (c_int, [ctypes.POINTER(GcnTileDesc), c_void_p]),
+    "stgcn_tconv_frame": (c_int, [ctypes.POINTER(ConvDesc), c_void_p]),
+    "stgcn_tconv_frame_row_blocks": (ctypes.c_long, [c_int, c_int]),
     "stgcn_gcn_frame_row_blocks": (ctypes.c_long, [c_int, c_int]),
     "stgcn_pack_weight_s2frag": (c_int, [c_void_p, ctypes.c_long, ctypes.c_long, ctypes.c_long, c_int, c_int,
                                          c_void_p, c_int, c_int, c_void_p]),

@@ -49,6 +49,8 @@ int gconv_wgrad_finish_bias_launch(const float* dweff, const float* A, const flo
 int amix_trans_launch(const AmixArgs& a, int dtype, hipStream_t s);
 long gconv_wgrad_frame_workspace(const stgcn_gconv_wgrad_frame_desc& a);
 int gcn_frame_launch(const stgcn_gcn_tile_desc& a, hipStream_t s);
+int tconv_frame_launch(const stgcn_conv_desc& a, hipStream_t s);
+long tconv_frame_row_blocks(int N, int T);
 long gcn_frame_row_blocks(int NT, int Cout);
 int gconv_wgrad_frame_launch(const stgcn_gconv_wgrad_frame_desc& a, hipStream_t s);
 int amix_dA_launch(const AmixArgs& a, const void* dw, float* dA, void* work, int dtype, hipStream_t s);
@@ -273,6 +275,11 @@ int stgcn_gconv_wgrad_finish(const float* dweff, const float* A, const float* W,
     return STGCN_EBADSHAPE;
   return gconv_wgrad_finish_launch(dweff, A, W, nbr, deg, P, V, J, Cout, Cin, dW, dA, work, STREAM(stream));
 }
+int stgcn_tconv_frame(const stgcn_conv_desc* d, void* stream) {
+  if (!d) return STGCN_EBADSHAPE;
+  return tconv_frame_launch(*d, STREAM(stream));
+}
+long stgcn_tconv_frame_row_blocks(int N, int T) { return tconv_frame_row_blocks(N, T); }
 int stgcn_gcn_frame(const stgcn_gcn_tile_desc* d, void* stream) {
   if (!d) return STGCN_EBADSHAPE;
   return gcn_frame_launch(*d, STREAM(stream));

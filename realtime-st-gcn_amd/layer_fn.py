@@ -300,6 +300,8 @@ class StgcnLayerFunction(torch.autograd.Function):
         framed = gather and not tiled and K.gcn_frame_ok(sup, P, Cin, Cout, V, dtype)
         # gathered / framed paths: bias2d comes from the weight preparation below
         bias2d = None if (gather and not tiled) else K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
+        # the 64-channel temporal conv on the frame-streaming kernel (tconv_frame.hip; BN1 prologue)
+        tframe = norm == BN and K.tconv_frame_ok(Cout, kt, stride, V, dtype)
         if norm == BN:  # all BatchNorm partial-statistics buffers of the layer from one zero fill
             cpo = -(-Cout // K.col_tile(Cout)) * K.col_tile(Cout)
             if framed:
@@ -308,9 +310,9 @@ class StgcnLayerFunction(torch.autograd.Function):
                 rb1 = (K.gcn_tile_row_blocks(N * T, V, Cout) if tiled else K.gconv_row_blocks(N * T, V)) if gather \
                     else K.row_blocks(M1, Cout)
                 cp1 = cpo
-            st_shapes = [(rb1, cp1, 4),
-                         (K.row_blocks(M2, Cout), cpo, 4)] + ([(K.row_blocks(M2, Cout), cpo, 4)] if res_conv else [])
-            st_all = _stats_arena(cache, dev, x.dtype, st_shapes, (tiled, gather, framed))
+            rb2 = K.tconv_frame_row_blocks(N, T_out) if tframe else K.row_blocks(M2, Cout)
+            st_shapes = [(rb1, cp1, 4), (rb2, cpo, 4)] + ([(K.row_blocks(M2, Cout), cpo, 4)] if res_conv else [])
+            st_all = _stats_arena(cache, dev, x.dtype, st_shapes, (tiled, gather, framed, tframe))
             st1, st2 = st_all[0], st_all[1]
             str_ = st_all[2] if res_conv else None
         # ---- residual branch: independent of the graph conv -> temporal conv chain until the output norm,
@@ -378,9 +380,13 @@ class StgcnLayerFunction(torch.autograd.Function):
         wtp, cpt, kpt = packs.wt if packs is not None else \
             K.pack_weight(wt.detach().float().squeeze(-1).permute(2, 0, 1), dtype, stride=stride)  # [Kt][Cout][Cin]
 
-        u = K.conv_rows(g, wtp, Cout, Cout, cpt, kpt, T, T_out, Kt=kt, stride=stride, pad=pad,
-                        bias=bt.detach().float().contiguous(), stats=st2 if norm == BN else None,
-                        tag=f"tcn_fwd_c{Cout}" if stride == 1 else None, **pro1)
+        if tframe:
+            u = K.tconv_frame(g, wtp, cpt, kpt, bias=bt.detach().float().contiguous(), pro_a=sc1, pro_b=sh1, stats=st2,
+                              tag=f"tcn_fwd_c{Cout}")
+        else:
+            u = K.conv_rows(g, wtp, Cout, Cout, cpt, kpt, T, T_out, Kt=kt, stride=stride, pad=pad,
+                            bias=bt.detach().float().contiguous(), stats=st2 if norm == BN else None,
+                            tag=f"tcn_fwd_c{Cout}" if stride == 1 else None, **pro1)
         if side is not None:  # join the residual branch
             main = torch.cuda.current_stream(dev)
             main.wait_stream(side)
@@ -520,7 +526,10 @@ class StgcnLayerFunction(torch.autograd.Function):
         with _fork(side):
             grads["wt"] = K.conv_wgrad_w(g, du, Cout, Cout, T, T_out, Kt=kt, stride=stride, pad=pad,
                                          **pro1).unsqueeze(-1)  # (co, ci, Kt, 1)
-        dh = K.conv_rows(du, wtTp, Cout, Cout, cq, kq, T_out, T, Kt=kt, stride=stride, pad=pad, trans=True)
+        if K.tconv_frame_ok(Cout, kt, stride, V, dtype) and getattr(wtTp, "frag_stride", None) == 1:
+            dh = K.tconv_frame(du, wtTp, cq, kq, trans=True)
+        else:
+            dh = K.conv_rows(du, wtTp, Cout, Cout, cq, kq, T_out, T, Kt=kt, stride=stride, pad=pad, trans=True)
         if not bt_done:
             grads["bt"] = K.bn_bwd_reduce(du, M2, Cout)[:, 0].clone()
 

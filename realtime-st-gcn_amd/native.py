@@ -270,6 +270,47 @@ def conv_rows(x, w3p, Cin, Cout, cp, kp, T_in, T_out, Kt=1, stride=1, pad=0, tra
     return out
 
 
+def tconv_frame_ok(C, kt, stride, V, dtype) -> bool:
+    """Whether a layer's temporal conv (C -> C channels) runs on the frame-streaming kernel tconv_frame.hip: bf16,
+    C = 64, Kt = 9, stride 1, 16 < V <= 32 (routing.tconv_frame)."""
+    return ROUTING.tconv_frame and dtype == torch.bfloat16 and C == 64 and kt == 9 and stride == 1 and 16 < V <= 32
+
+
+def tconv_frame_row_blocks(N: int, T: int) -> int:
+    return L.lib().stgcn_tconv_frame_row_blocks(N, T)
+
+
+def tconv_frame(x, w3p, cp, kp, trans=False, bias=None, pro_a=None, pro_b=None, stats=None, tag=None):
+    """The 64-channel Kt = 9 stride-1 temporal conv (forward: BN1 scale / shift + ReLU prologue when pro_a is given,
+    bias, BN partials; trans: the data gradient) on the frame-streaming kernel (stgcn_tconv_frame); w3p a
+    pack_weight result carrying its stride-1 fragment image.  Returns the (N, 64, T, V) channels-last output."""
+    N, C, T, V = x.shape
+    if getattr(w3p, "frag_stride", None) != 1:
+        raise RuntimeError("stgcn_amd: tconv_frame needs the stride-1 fragment image of the weight")
+    out = cl_empty(N, C, T, V, x.dtype, x.device)
+    d = L.ConvDesc()
+    d.in_, d.out, d.w, d.w_frag = x.data_ptr(), out.data_ptr(), w3p.data_ptr(), w3p.frag_ptr
+    d.bias, d.pro_a, d.pro_b, d.stats = L.ptr(bias), L.ptr(pro_a), L.ptr(pro_b), L.ptr(stats)
+    d.N, d.T_in, d.T_out, d.V, d.Cin, d.Cout, d.Cin_pad, d.Cout_pad = N, T, T, V, C, C, kp, cp
+    d.Kt, d.stride, d.pad, d.trans, d.pro = 9, 1, 4, int(trans), 1 if pro_a is not None else 0
+    d.bias_mode, d.accumulate = 0 if bias is None else 1, 0
+    d.in_ld, d.out_ld = rows_ld(x), rows_ld(out)
+    hook = EVENT_HOOK if tag is not None else None
+    flop = 2.0 * N * T * V * C * C * 9
+    if hook:
+        hook(tag, "start", flop)
+    h = KTIME_HOOK
+    if h:
+        ktag = _k_start(h, "tconv_frame_dgrad" if trans else "tconv_frame_fwd", f"{C}->{C} s1", flop,
+                        x.element_size() * N * V * T * 2 * C)
+    L.check(L.lib().stgcn_tconv_frame(d, L.stream()), "tconv_frame")
+    if h:
+        h(ktag, "end", None)
+    if hook:
+        hook(tag, "end", None)
+    return out
+
+
 def conv_wgrad(x, dy, Cin, Cout, T_in, T_out, Kt=1, stride=1, pad=0, pro=0, pro_a=None, pro_b=None, pro_stats=None,
                dw=None):
     """dw[Kt][Cout][Cin] (fp32) += weight gradient (stgcn_conv_wgrad)."""

@@ -22,12 +22,17 @@ also assign the attributes directly.
     gcn_afirst_min_c    STGCN_GCN_AFIRST_MIN_C=<C>  ... only for layers with at least C input channels (A/B of the
                                               A-first form where the gathered form's per-joint effective weights
                                               outgrow L2; default 0 = off)
-    gconv_wgrad_frame   STGCN_GWF=0           graph-conv weight / adjacency / bias gradients (bf16, shared A) in the
+    gconv_wgrad_frame   STGCN_GWF=1           graph-conv weight / adjacency / bias gradients (bf16, shared A) in the
                                               one-pass frame kernel gconv_wgrad_frame.hip instead of the per-joint
-                                              dWeff kernel + finish (default on)
-    gcn_frame           STGCN_GCN_FRAME=0     graph conv forward / data grad (bf16, shared A, 64 or 128 kernel-input
+                                              dWeff kernel + finish (default off: 115 vs 72 us at C = 64, 242 vs 133
+                                              at C = 256 in isolation, r04c)
+    gcn_frame           STGCN_GCN_FRAME=1     graph conv forward / data grad (bf16, shared A, 64 or 128 kernel-input
                                               channels) on the frame-streaming kernel gcn_frame.hip instead of the
-                                              joint-gathered gconv.hip (default on)
+                                              joint-gathered gconv.hip (default off: equal forward, slower data
+                                              grad in isolation, r04c)
+    tconv_frame         STGCN_TCONV_FRAME=1   64-channel Kt = 9 stride-1 temporal conv forward (BatchNorm layers) and data
+                                              grad on the frame-streaming kernel tconv_frame.hip instead of
+                                              conv_wide / conv_persist (default off until measured)
     prep_plan           STGCN_PREP_PLAN=0     stgcn.Model training forwards pack every weight per call instead of
                                               in the one-launch plan (native.PrepPlan; default on)
 """
@@ -45,8 +50,9 @@ class _Routing:
         self.gcn_afirst = e("STGCN_GCN_AFIRST", "0") not in ("0", "")
         self.gcn_afirst_min_c = int(e("STGCN_GCN_AFIRST_MIN_C", "0") or 0)
         self.prep_plan = e("STGCN_PREP_PLAN", "1") != "0"
-        self.gconv_wgrad_frame = e("STGCN_GWF", "1") != "0"
-        self.gcn_frame = e("STGCN_GCN_FRAME", "1") != "0"
+        self.gconv_wgrad_frame = e("STGCN_GWF", "0") == "1"
+        self.gcn_frame = e("STGCN_GCN_FRAME", "0") == "1"
+        self.tconv_frame = e("STGCN_TCONV_FRAME", "0") == "1"
 
 
 ROUTING = _Routing()

@@ -122,13 +122,14 @@ def test_gconv_finish_bias_merged(K, pkg, Cin, Cout):
 @pytest.mark.parametrize("Cin,Cout,N,T", [(64, 64, 4, 40), (64, 128, 3, 29), (128, 128, 2, 33), (128, 256, 2, 21),
                                           (256, 256, 2, 13), (64, 64, 64, 300)])
 @pytest.mark.parametrize("strategy", ["spatial", "uniform", "distance"])
-def test_gconv_wgrad_frame(K, pkg, Cin, Cout, N, T, strategy):
+def test_gconv_wgrad_frame(K, pkg, Cin, Cout, N, T, strategy, monkeypatch):
     """stgcn_gconv_wgrad_frame (dW, the dense dA with the bias through A, db in one pass over (x, dy), bf16
     operands) vs autograd of the reference's conv1x1 -> einsum(A) in fp32 on the same bf16-rounded inputs
     (tgcn.py:71-79); tolerance 2e-2 of each gradient's max (the kernel rounds A, A dy and W^T dy to bf16 as the
     reference's bf16 autocast rounds its einsum operands).  Run twice: bit-identical (fixed-order partials)."""
     if N * T > 4000 and (strategy != "spatial"):
         pytest.skip("config-2 size: spatial only")
+    monkeypatch.setattr(pkg.routing.ROUTING, "gconv_wgrad_frame", True)
     torch.manual_seed(7)
     A0 = torch.tensor(pkg.Graph(**dict(pkg.PKU_MMD, strategy=strategy)).A, dtype=torch.float32)
     A = (A0 * (torch.rand(A0.shape) + 0.5)).requires_grad_(True)
@@ -155,12 +156,13 @@ def test_gconv_wgrad_frame(K, pkg, Cin, Cout, N, T, strategy):
 @pytest.mark.parametrize("Cin,Cout,N,T", [(64, 64, 3, 37), (64, 128, 2, 29), (128, 128, 2, 33), (128, 256, 1, 21),
                                           (64, 64, 64, 300), (128, 128, 64, 150)])
 @pytest.mark.parametrize("strategy", ["spatial", "uniform", "distance"])
-def test_gcn_frame_fwd_dgrad(K, pkg, Cin, Cout, N, T, strategy):
+def test_gcn_frame_fwd_dgrad(K, pkg, Cin, Cout, N, T, strategy, monkeypatch):
     """stgcn_gcn_frame (the 1x1 conv then the joint mix per frame, bf16) vs the reference's conv1x1 -> einsum(A)
     in fp32 on the same bf16-rounded inputs (tgcn.py:71-79): forward with the bias through A and the BatchNorm
     partial statistics, data grad accumulating onto existing rows (the residual branch's dx), at 2e-2 of max."""
     if N * T > 4000 and strategy != "spatial":
         pytest.skip("config-2 size: spatial only")
+    monkeypatch.setattr(pkg.routing.ROUTING, "gcn_frame", True)
     torch.manual_seed(8)
     A0 = torch.tensor(pkg.Graph(**dict(pkg.PKU_MMD, strategy=strategy)).A, dtype=torch.float32)
     A = A0 * (torch.rand(A0.shape) + 0.5)

@@ -1,7 +1,7 @@
 """Micro-benchmark of the graph-conv kernels at the config-2 shapes (HIP-event timing, bf16, N = 64, V = 25):
 forward / data grad on the joint-gathered gconv.hip vs the frame-streaming gcn_frame.hip, weight / adjacency / bias
 gradients on gconv_wgrad + finish vs gconv_wgrad_frame.hip.  Prints one JSON line per shape.
-Usage: python tools/bench_gframe.py [reps]"""
+Usage: python tools/bench_gframe.py [reps] [shape, e.g. 64->64]"""
 import json
 import os
 import sys
@@ -13,6 +13,7 @@ import __graft_entry__ as ge  # noqa: E402
 
 PKG = ge.load_package()
 K = PKG.native
+PKG.routing.ROUTING.gcn_frame = PKG.routing.ROUTING.gconv_wgrad_frame = True  # the opt-in kernels are timed too
 dev = "cuda:0"
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 dt = torch.bfloat16
@@ -35,7 +36,10 @@ A = (A0 * (torch.rand(A0.shape) + 0.5)).to(dev).contiguous()
 P, V = A.shape[0], A.shape[-1]
 sup = K.GraphSupport(A)
 N = 64
+only = sys.argv[2] if len(sys.argv) > 2 else None
 for Cin, Cout, T in [(64, 64, 300), (64, 128, 300), (128, 128, 150), (128, 256, 150), (256, 256, 75)]:
+    if only and only != f"{Cin}->{Cout}":
+        continue
     x = torch.randn(N, Cin, T, V, device=dev).to(dt).contiguous(memory_format=torch.channels_last)
     dg = torch.randn(N, Cout, T, V, device=dev).to(dt).contiguous(memory_format=torch.channels_last)
     dx = torch.empty_like(x)
@@ -62,4 +66,22 @@ for Cin, Cout, T in [(64, 64, 300), (64, 128, 300), (128, 128, 150), (128, 256, 
         K.gconv_finish_bias(dweff, A, W, sup, Cout, Cin, b, S)
     out["wgrad_dweff_finish_us"] = timeit(old_wgrad)
     out["wgrad_frame_us"] = timeit(lambda: K.gconv_wgrad_frame(x, dg, A, W, b))
+    print(json.dumps(out), flush=True)
+
+# the 64-channel Kt = 9 temporal conv: conv_rows (conv_wide fwd / conv_persist dgrad) vs tconv_frame.hip
+if not only or only == "tcn":
+    T = 300
+    g = torch.randn(N, 64, T, V, device=dev).to(dt).contiguous(memory_format=torch.channels_last)
+    wt = torch.randn(64, 64, 9, device=dev) * 0.05
+    wtp, cp, kp = K.pack_weight(wt.permute(2, 0, 1), dt, stride=1)
+    wtT, cq, kq = K.pack_weight(wt.permute(2, 1, 0), dt, stride=1, trans=True)
+    sc, sh, bt = torch.rand(64, device=dev) + 0.5, torch.randn(64, device=dev), torch.randn(64, device=dev)
+    st0 = torch.zeros((K.row_blocks(N * T * V, 64), cp, 4), device=dev)
+    st1 = torch.zeros((K.tconv_frame_row_blocks(N, T), cp, 4), device=dev)
+    out = {"shape": "tcn 64->64 T=300"}
+    out["conv_rows_fwd_us"] = timeit(lambda: K.conv_rows(g, wtp, 64, 64, cp, kp, T, T, Kt=9, pad=4, bias=bt, stats=st0,
+                                                          pro=1, pro_a=sc, pro_b=sh))
+    out["tconv_frame_fwd_us"] = timeit(lambda: K.tconv_frame(g, wtp, cp, kp, bias=bt, pro_a=sc, pro_b=sh, stats=st1))
+    out["conv_rows_dgrad_us"] = timeit(lambda: K.conv_rows(g, wtT, 64, 64, cq, kq, T, T, Kt=9, pad=4, trans=True))
+    out["tconv_frame_dgrad_us"] = timeit(lambda: K.tconv_frame(g, wtT, cq, kq, trans=True))
     print(json.dumps(out), flush=True)
