@@ -526,7 +526,7 @@ class StgcnLayerFunction(torch.autograd.Function):
         with _fork(side):
             grads["wt"] = K.conv_wgrad_w(g, du, Cout, Cout, T, T_out, Kt=kt, stride=stride, pad=pad,
                                          **pro1).unsqueeze(-1)  # (co, ci, Kt, 1)
-        if K.tconv_frame_ok(Cout, kt, stride, V, dtype) and getattr(wtTp, "frag_stride", None) == 1:
+        if K.tconv_frame_ok(Cout, kt, stride, V, dtype, trans=True) and getattr(wtTp, "frag_stride", None) == 1:
             dh = K.tconv_frame(du, wtTp, cq, kq, trans=True)
         else:
             dh = K.conv_rows(du, wtTp, Cout, Cout, cq, kq, T_out, T, Kt=kt, stride=stride, pad=pad, trans=True)

@@ -270,10 +270,11 @@ def conv_rows(x, w3p, Cin, Cout, cp, kp, T_in, T_out, Kt=1, stride=1, pad=0, tra
     return out
 
 
-def tconv_frame_ok(C, kt, stride, V, dtype) -> bool:
+def tconv_frame_ok(C, kt, stride, V, dtype, trans=False) -> bool:
     """Whether a layer's temporal conv (C -> C channels) runs on the frame-streaming kernel tconv_frame.hip: bf16,
-    C = 64, Kt = 9, stride 1, 16 < V <= 32 (routing.tconv_frame)."""
-    return ROUTING.tconv_frame and dtype == torch.bfloat16 and C == 64 and kt == 9 and stride == 1 and 16 < V <= 32
+    C = 64, Kt = 9, stride 1, 16 < V <= 32; forward (routing.tconv_frame) or data grad (routing.tconv_frame_dgrad)."""
+    on = ROUTING.tconv_frame_dgrad if trans else ROUTING.tconv_frame
+    return on and dtype == torch.bfloat16 and C == 64 and kt == 9 and stride == 1 and 16 < V <= 32
 
 
 def tconv_frame_row_blocks(N: int, T: int) -> int:

@@ -30,9 +30,11 @@ also assign the attributes directly.
                                               channels) on the frame-streaming kernel gcn_frame.hip instead of the
                                               joint-gathered gconv.hip (default off: equal forward, slower data
                                               grad in isolation, r04c)
-    tconv_frame         STGCN_TCONV_FRAME=1   64-channel Kt = 9 stride-1 temporal conv forward (BatchNorm layers) and data
-                                              grad on the frame-streaming kernel tconv_frame.hip instead of
-                                              conv_wide / conv_persist (default off until measured)
+    tconv_frame         STGCN_TCONV_FRAME=1   64-channel Kt = 9 stride-1 temporal conv forward (BatchNorm layers) on the
+                                              frame-streaming kernel tconv_frame.hip instead of conv_wide (default off:
+                                              67.1 vs 64.1 us in isolation, r04d)
+    tconv_frame_dgrad   STGCN_TCONV_FRAME_DGRAD=0  its data grad on tconv_frame.hip instead of conv_persist (default on:
+                                              52.0 vs 65.0 us in isolation, r04d)
     prep_plan           STGCN_PREP_PLAN=0     stgcn.Model training forwards pack every weight per call instead of
                                               in the one-launch plan (native.PrepPlan; default on)
 """
@@ -53,6 +55,7 @@ class _Routing:
         self.gconv_wgrad_frame = e("STGCN_GWF", "0") == "1"
         self.gcn_frame = e("STGCN_GCN_FRAME", "0") == "1"
         self.tconv_frame = e("STGCN_TCONV_FRAME", "0") == "1"
+        self.tconv_frame_dgrad = e("STGCN_TCONV_FRAME_DGRAD", "1") != "0"
 
 
 ROUTING = _Routing()
