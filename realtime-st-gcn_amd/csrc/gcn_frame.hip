@@ -31,6 +31,11 @@ namespace {
 constexpr int NW = 4;
 constexpr int PAN = 32 * 64;  // [32 rows][32 ch] bf16
 constexpr int BLOCKS = 512;   // 2 per CU
+// timing ablations (results wrong; tools builds only, -DGCF_DBG=<mask>): 1 skip the LDS reads and MFMAs, 2 skip the
+// output stores, 4 skip the DMA, 8 skip the per-step barrier
+#ifndef GCF_DBG
+#define GCF_DBG 0
+#endif
 
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
@@ -172,7 +177,8 @@ __global__ __launch_bounds__(NW * 64, 2) void gcf_kernel(const stgcn_gcn_tile_de
     }
   };
 #pragma unroll
-  for (int k = 0; k < D - 1; ++k) issue(k);
+  for (int k = 0; k < D - 1; ++k)
+    if constexpr (!(GCF_DBG & 4)) issue(k);
 
   const f32x16 zero = {};
   float s1[16], s2[16];
@@ -193,7 +199,7 @@ __global__ __launch_bounds__(NW * 64, 2) void gcf_kernel(const stgcn_gcn_tile_de
       for (int j = j0; j < k; ++j) nv += (f0 + 2 * j + fp < f1) ? 1 : 0;
       wait_vm<XMAX>((D - 2) * NDMA + (has_out ? NST : 0) * nv);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if constexpr (!(GCF_DBG & 8)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     const int f = f0 + 2 * k + fp;
     if (f < f1) {
       const char* slot = ring + (k % D) * SLOT;
@@ -201,6 +207,7 @@ __global__ __launch_bounds__(NW * 64, 2) void gcf_kernel(const stgcn_gcn_tile_de
       f32x16 acc = zero;
 #pragma unroll
       for (int p = 0; p < P; ++p) {
+        if constexpr ((GCF_DBG & 1) != 0) break;
         f32x16 y = zero;
 #pragma unroll
         for (int kk = 0; kk < 2 * G; ++kk) {
@@ -232,7 +239,7 @@ __global__ __launch_bounds__(NW * 64, 2) void gcf_kernel(const stgcn_gcn_tile_de
 #pragma unroll
         for (int e = 0; e < 4; ++e) st[e] = (bf16)v[4 * q + e];
         // lanes past V store nothing; the wave's store instruction still issues (counted above)
-        if (has_out && jok) *reinterpret_cast<u32x2*>(orow + 8 * q) = __builtin_bit_cast(u32x2, st);
+        if (!(GCF_DBG & 2) && has_out && jok) *reinterpret_cast<u32x2*>(orow + 8 * q) = __builtin_bit_cast(u32x2, st);
       }
       if (stats && jok) {
 #pragma unroll
@@ -242,7 +249,7 @@ __global__ __launch_bounds__(NW * 64, 2) void gcf_kernel(const stgcn_gcn_tile_de
         }
       }
     }
-    issue(k + D - 1);  // into the slot read in step k - 1 (every wave is past this step's barrier)
+    if constexpr (!(GCF_DBG & 4)) issue(k + D - 1);  // into the slot read in step k - 1 (every wave is past this step's barrier)
   }
   asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   if (!stats) return;

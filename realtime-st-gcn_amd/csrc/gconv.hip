@@ -1068,7 +1068,7 @@ __global__ void gconv_dA_kernel(const float* __restrict__ dweff, const float* __
 
 constexpr int PMAX = 4;
 // dW[p][e] += sum_{pairs} A[p][v][w] dWeff[pair][e] for all p in one pass (dWeff read once).
-// Block = 64 e-columns x 4 groups over the used (w, j) pairs (pair list and coefficients A[p][S(w)_j][w]
+// Block = 256 e-columns (4 per lane) x 4 groups over the used (w, j) pairs (pair list and coefficients A[p][S(w)_j][w]
 // staged in LDS first: the per-pair deg -> nbr -> A chain of dependent global loads was this kernel's
 // cost); fixed-order LDS combine.
 constexpr int DW_PAIRS = 32 * 8;  // V * J upper bound for the LDS tables
@@ -1094,17 +1094,23 @@ DEV void gconv_dw_all_body(const float* __restrict__ dweff, const float* __restr
   }
   __syncthreads();
   const int g = threadIdx.x >> 6;
-  const long e = bb * 64 + (threadIdx.x & 63);
-  float acc[PMAX] = {0.f, 0.f, 0.f, 0.f};
+  // 4 consecutive e per lane (16-B loads of dWeff): a block covers 256 columns of E (E % 4 == 0)
+  const long e = (bb * 64 + (threadIdx.x & 63)) * 4;
+  float4 acc[PMAX];
+#pragma unroll
+  for (int p = 0; p < PMAX; ++p) acc[p] = make_float4(0.f, 0.f, 0.f, 0.f);
   if (e < E) {
 #pragma unroll 4
     for (int k = g; k < np; k += 4) {
-      const float d = dweff[(long)spair[k] * E + e];
+      const float4 d = *reinterpret_cast<const float4*>(dweff + (long)spair[k] * E + e);
 #pragma unroll
-      for (int p = 0; p < PMAX; ++p) acc[p] += scoef[k][p] * d;
+      for (int p = 0; p < PMAX; ++p) {
+        const float c = scoef[k][p];
+        acc[p].x += c * d.x; acc[p].y += c * d.y; acc[p].z += c * d.z; acc[p].w += c * d.w;
+      }
     }
   }
-  __shared__ float part[4][PMAX][64];
+  __shared__ float4 part[4][PMAX][64];
 #pragma unroll
   for (int p = 0; p < PMAX; ++p) part[g][p][threadIdx.x & 63] = acc[p];
   __syncthreads();
@@ -1113,8 +1119,15 @@ DEV void gconv_dw_all_body(const float* __restrict__ dweff, const float* __restr
 #pragma unroll
     for (int p = 0; p < PMAX; ++p)
       if (p < P) {
-        const float t = ((part[0][p][l] + part[1][p][l]) + part[2][p][l]) + part[3][p][l];
-        dW[(long)p * E + e] = acc_out ? dW[(long)p * E + e] + t : t;
+        const float4 a0 = part[0][p][l], a1 = part[1][p][l], a2 = part[2][p][l], a3 = part[3][p][l];
+        float4 t = make_float4(((a0.x + a1.x) + a2.x) + a3.x, ((a0.y + a1.y) + a2.y) + a3.y,
+                               ((a0.z + a1.z) + a2.z) + a3.z, ((a0.w + a1.w) + a2.w) + a3.w);
+        float4* o = reinterpret_cast<float4*>(dW + (long)p * E + e);
+        if (acc_out) {
+          const float4 q = *o;
+          t.x += q.x; t.y += q.y; t.z += q.z; t.w += q.w;
+        }
+        *o = t;
       }
   }
 }
@@ -1134,11 +1147,14 @@ DEV void gconv_dA_part_body(const float* __restrict__ dweff, const float* __rest
   const float* d = dweff + (long)pair * E;
   float acc[PMAX] = {0.f, 0.f, 0.f, 0.f};
   const long e1 = min(E, (long)(c + 1) * DA_CHUNK);
-  for (long e = (long)c * DA_CHUNK + threadIdx.x; e < e1; e += 256) {
-    const float dv = d[e];
+  for (long e = (long)c * DA_CHUNK + threadIdx.x * 4; e < e1; e += 1024) {  // 16-B loads (E % 4 == 0)
+    const float4 dv = *reinterpret_cast<const float4*>(d + e);
 #pragma unroll
     for (int p = 0; p < PMAX; ++p)
-      if (p < P) acc[p] += W[(long)p * E + e] * dv;
+      if (p < P) {
+        const float4 w = *reinterpret_cast<const float4*>(W + (long)p * E + e);
+        acc[p] += ((w.x * dv.x + w.y * dv.y) + w.z * dv.z) + w.w * dv.w;
+      }
   }
   __shared__ float red[4][PMAX];
 #pragma unroll
@@ -1404,14 +1420,15 @@ long gconv_wgrad_finish_workspace(int P, int V, int J, int Cout, int Cin) {
 }
 
 bool gconv_finish_bias_ok(int P, int V, int J) { return P <= PMAX && V <= FV_MAX && V * J <= DW_PAIRS; }
+// the one-pass dW and the chunked dA read dWeff / W as float4 (Cout * Cin % 4 == 0)
 
 int gconv_wgrad_finish_bias_launch(const float* dweff, const float* A, const float* W, const int* nbr, const int* deg,
                                    int P, int V, int J, int Cout, int Cin, const float* bconv, const float* S, float* dW,
                                    float* dA, float* db, void* work, hipStream_t s) {
-  if (!gconv_finish_bias_ok(P, V, J) || !work) return STGCN_EBADSHAPE;
+  if (!gconv_finish_bias_ok(P, V, J) || !work || ((long)Cout * Cin) % 4) return STGCN_EBADSHAPE;
   const long E = (long)Cout * Cin;
   const int nch = (int)((E + DA_CHUNK - 1) / DA_CHUNK);
-  const int nb_dw = (int)((E + 63) / 64);
+  const int nb_dw = (int)((E + 255) / 256);  // 256 columns per dW block
   float* part = reinterpret_cast<float*>(work);
   hipLaunchKernelGGL(gconv_finish1_kernel, dim3((unsigned)(nb_dw + V * J * nch)), dim3(256), 0, s, dweff, A, W, nbr,
                      deg, P, V, J, E, dW, nb_dw, nch, part);
@@ -1423,7 +1440,7 @@ int gconv_wgrad_finish_bias_launch(const float* dweff, const float* A, const flo
 int gconv_wgrad_finish_launch(const float* dweff, const float* A, const float* W, const int* nbr, const int* deg,
                               int P, int V, int J, int Cout, int Cin, float* dW, float* dA, void* work, hipStream_t s) {
   const long E = (long)Cout * Cin;
-  if (P > PMAX || (dA && !work) || V * J > DW_PAIRS) {  // generic per-partition path (dA via per-(pair,p) blocks)
+  if (P > PMAX || (dA && !work) || V * J > DW_PAIRS || E % 4) {  // generic per-partition path (dA per (pair,p) block)
     const long n = (long)P * E;
     if (dW)
       hipLaunchKernelGGL(gconv_dw_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dweff, A, nbr, deg, P,
@@ -1433,7 +1450,7 @@ int gconv_wgrad_finish_launch(const float* dweff, const float* A, const float* W
                          P, V, J, Cout, Cin, dA);
   } else {  // one pass over dWeff per output, all partitions at once
     if (dW)
-      hipLaunchKernelGGL(gconv_dw_all_kernel, dim3((unsigned)((E + 63) / 64)), dim3(256), 0, s, dweff, A, nbr, deg,
+      hipLaunchKernelGGL(gconv_dw_all_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, dweff, A, nbr, deg,
                          P, V, J, E, dW);
     if (dA) {
       const int nch = (int)((E + DA_CHUNK - 1) / DA_CHUNK);

@@ -33,6 +33,11 @@ constexpr int PAN = 32 * 64;          // one panel: 32 rows x 64 B
 constexpr int SLOT = 4 * PAN;         // one frame: dg q0, dg q1, x h0, x h1
 constexpr int DR = 8;                 // frame slots in the ring
 constexpr int BLOCKS = 512;           // target blocks per launch (2 per CU)
+// timing ablations (results wrong; tools builds only, -DGWF_DBG=<mask>): 1 skip the per-frame LDS reads and MFMAs,
+// 2 skip the per-frame barrier, 4 skip the DMA
+#ifndef GWF_DBG
+#define GWF_DBG 0
+#endif
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -173,7 +178,7 @@ __global__ __launch_bounds__(NW * 64, 2) void gwf_kernel(const stgcn_gconv_wgrad
   };
 #pragma unroll
   for (int k = 0; k < DR - 1; ++k)
-    if (f0 + k < f1) issue(f0 + k);
+    if (!(GWF_DBG & 4) && f0 + k < f1) issue(f0 + k);
 
   const f32x16 zero = {};
   f32x16 accW[P], accA[P], accS = zero;
@@ -189,8 +194,9 @@ __global__ __launch_bounds__(NW * 64, 2) void gwf_kernel(const stgcn_gconv_wgrad
     sfor<DR - 1>([&]<int m>() {
       if (after == m) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * m) : "memory");
     });
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (f + DR - 1 < f1) issue(f + DR - 1);  // into the slot of frame f - 1, free after the barrier
+    if constexpr (!(GWF_DBG & 2)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (!(GWF_DBG & 4) && f + DR - 1 < f1) issue(f + DR - 1);  // into the slot of frame f - 1, free after the barrier
+    if constexpr ((GWF_DBG & 1) != 0) continue;
     const char* slot = ring + ((f - f0) % DR) * SLOT;
     const char* pdy = slot + cq * PAN;
     const char* px = slot + (2 + ch) * PAN;
