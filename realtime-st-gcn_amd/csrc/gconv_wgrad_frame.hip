@@ -284,14 +284,14 @@ __global__ __launch_bounds__(NW * 64, 2) void gwf_kernel(const stgcn_gconv_wgrad
   }
 }
 
-// out = fixed-order sums of the partials: dW[e] = sum_r part_w[r][e]; dA[p][v][w] = sum_{r,tile} part_a;
-// db[e] = sum_r part_b[r][e].  Block = 64 consecutive outputs x 4 groups of partial rows, summed in LDS.
+// dA[p][v][w] = sum_{r,tile} part_a; db[e] = sum_r part_b[r][e] in a fixed order (dW goes through the float4
+// slab reduction).  Block = 64 consecutive outputs x 4 groups of partial rows, summed in LDS.
 __global__ __launch_bounds__(256) void gwf_reduce_kernel(const GWF g, int P, int V, int Cout, int Cin, float* dW,
                                                          float* dA, float* db) {
   __shared__ float red[4][64];
   const int tid = threadIdx.x, el = tid & 63, grp = tid >> 6;
   const long Ew = (long)P * Cout * Cin, Ea = (long)P * V * V, Eb = (long)P * Cout;
-  const long nbw = (Ew + 63) / 64, nba = (Ea + 63) / 64;
+  const long nbw = 0, nba = (Ea + 63) / 64;  // dW: slab_reduce_launch
   long b = blockIdx.x;
   float s = 0.f;
   float* out;
@@ -342,10 +342,15 @@ bool shape_ok(const stgcn_gconv_wgrad_frame_desc& a) {
 
 }  // namespace
 
+// deterministic two-level float4 sum of R fp32 slabs (wgrad_tile.hip); part holds 16 * E floats
+int slab_reduce_launch(const float* slab, int R, long E, float* part, float* dw, hipStream_t s, int mode, int Kt,
+                       long CoCi);
+
 long gconv_wgrad_frame_workspace(const stgcn_gconv_wgrad_frame_desc& a) {
   if (!shape_ok(a)) return -1;
   const GWF g = plan(a);
-  return 4L * ((long)g.R * a.P * a.Cout * a.Cin + (long)g.R * g.ntiles * a.P * 1024 + (long)g.R * a.P * a.Cout);
+  const long Ew = (long)a.P * a.Cout * a.Cin;
+  return 4L * ((long)g.R * Ew + (long)g.R * g.ntiles * a.P * 1024 + (long)g.R * a.P * a.Cout + 16 * Ew);
 }
 
 int gconv_wgrad_frame_launch(const stgcn_gconv_wgrad_frame_desc& a, hipStream_t s) {
@@ -364,7 +369,11 @@ int gconv_wgrad_frame_launch(const stgcn_gconv_wgrad_frame_desc& a, hipStream_t 
   if (stgcn_lds_attr((const void*)k, lds, s)) return STGCN_EHIP;
   hipLaunchKernelGGL(k, dim3((unsigned)(g.R * g.ntiles)), dim3(NW * 64), lds, s, a, g);
   if (hipGetLastError() != hipSuccess) return STGCN_EHIP;
-  const long nb = ((long)a.P * a.Cout * a.Cin + 63) / 64 + ((long)a.P * a.V * a.V + 63) / 64 + ((long)a.P * a.Cout + 63) / 64;
+  // dW: the float4 two-level slab reduction (16 row groups in parallel, then their fixed-order sum); dA, db here
+  const long Ew = (long)a.P * a.Cout * a.Cin;
+  float* part = g.part_b + (long)g.R * a.P * a.Cout;
+  if (slab_reduce_launch(g.part_w, g.R, Ew, part, a.dW, s, 1, 1, Ew) != STGCN_OK) return STGCN_EHIP;
+  const long nb = ((long)a.P * a.V * a.V + 63) / 64 + ((long)a.P * a.Cout + 63) / 64;
   hipLaunchKernelGGL(gwf_reduce_kernel, dim3((unsigned)nb), dim3(256), 0, s, g, a.P, a.V, a.Cout, a.Cin, a.dW, a.dA,
                      a.db);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;

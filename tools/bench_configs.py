@@ -130,7 +130,7 @@ LN_ARCH = {"strategy": "spatial", "in_feat": 3, "normalization": "LayerNorm", "n
            "output_type": "logits", "st-gcn": dict(LAYERS, importance=True, in_feat=3)}
 
 
-def ln_train(P, dev, steps, warmup, reps=3):
+def ln_train(P, dev, steps, warmup, reps=3, routes=(True, False)):
     """The LayerNorm st-gcn (ln/stgcn_vsc.json-style: LN, Kt = 9, config-2 widths) training step (fwd + loss +
     bwd + Adam, bf16, N=64 T=300) with its three 64 -> 64 layers' forward on the fused one-kernel layer
     (routing.fused_ln_train, default) and unfused, interleaved ``reps`` times."""
@@ -154,7 +154,7 @@ def ln_train(P, dev, steps, warmup, reps=3):
     prev = R.fused_ln_train
     try:
         for rep in range(reps):
-            for route in (True, False):
+            for route in routes:
                 R.fused_ln_train = route
                 for _ in range(warmup):
                     step()
@@ -167,7 +167,8 @@ def ln_train(P, dev, steps, warmup, reps=3):
                 out.setdefault(k, []).append(round(1e3 * (time.perf_counter() - t0) / steps, 3))
     finally:
         R.fused_ln_train = prev
-    out["fused_frames_per_s"] = round(64 * 300 / (min(out["fused_ms_per_step"]) * 1e-3), 1)
+    if "fused_ms_per_step" in out:
+        out["fused_frames_per_s"] = round(64 * 300 / (min(out["fused_ms_per_step"]) * 1e-3), 1)
     return out
 
 
@@ -226,6 +227,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--only", default=None)
+    ap.add_argument("--ln-reps", type=int, default=3)
+    ap.add_argument("--ln-route", choices=("both", "fused", "unfused"), default="both")
     args = ap.parse_args()
     P = ge.load_package()
     dev = torch.device("cuda", 0)
@@ -234,7 +237,8 @@ def main():
     if args.only in (None, "5"):
         print(json.dumps(config5(P, dev, args.steps, args.warmup)), flush=True)
     if args.only in (None, "ln"):
-        print(json.dumps(ln_train(P, dev, args.steps, args.warmup)), flush=True)
+        print(json.dumps(ln_train(P, dev, args.steps, args.warmup, args.ln_reps,
+                                    {"both": (True, False), "fused": (True,), "unfused": (False,)}[args.ln_route])), flush=True)
     if args.only in (None, "f1"):
         print(json.dumps(staging(P, dev)), flush=True)
 
