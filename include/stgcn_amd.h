@@ -324,9 +324,13 @@ int stgcn_ln_stats(const void* x, int ld, long frames, int V, int C, float eps, 
 int stgcn_ln_apply(const void* u, int ldu, const void* st_f2, const float* g, const float* b, int res_mode,
                    const void* r, int ldr, const void* rst_f2, const float* rg, const float* rb, int relu, void* y,
                    int ldy, long M, int V, int C, int dtype, void* stream);
+/* dx (+)= rstd*(gz - mean(gz) - xhat*sum(gz*xhat)/(E-1)), gz = dz*g, dz = dy*mask (0 none | 1 mref > 0 |
+ * 2 relu(LN(x)) > 0); dgb (optional, [2][C*V]) += (sum dz*xhat, sum dz) over all frames, reduced in a fixed
+ * order through `work` (stgcn_ln_bwd_workspace bytes; unused when dgb is NULL). */
 int stgcn_ln_bwd(const void* dy, int lddy, int mask, const void* mref, int ldm, const void* x, int ldx,
                  const void* st_f2, const float* g, const float* b, long frames, int V, int C, void* dx, int lddx,
-                 int accumulate, float* dgb, int dtype, void* stream);
+                 int accumulate, float* dgb, void* work, long work_bytes, int dtype, void* stream);
+long stgcn_ln_bwd_workspace(long frames, int V, int C, int dtype);
 
 /* Head: F.avg_pool2d over (T,V) (stgcn.py:92) and its gradient. */
 int stgcn_pool_rows(const void* x, int ld, int N, int R, int C, void* out, int ldo, int dtype, void* stream);

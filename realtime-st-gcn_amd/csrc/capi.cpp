@@ -80,9 +80,10 @@ int ln_stats_launch(const void* x, int ld, long F, int V, int C, float eps, floa
 int ln_apply_launch(const void* u, int ldu, const float2* st, const float* g, const float* b, int res_mode,
                     const void* r, int ldr, const float2* rst, const float* rg, const float* rb, int relu, void* y,
                     int ldy, long M, int V, int C, int dtype, hipStream_t s);
+long ln_bwd_workspace(long F, int V, int C, int dtype);
 int ln_bwd_launch(const void* dy, int lddy, int mask, const void* mref, int ldm, const void* x, int ldx,
                   const float2* st, const float* g, const float* b, long F, int V, int C, void* dx, int lddx,
-                  int accumulate, float* dgb, int dtype, hipStream_t s);
+                  int accumulate, float* dgb, void* work, long work_bytes, int dtype, hipStream_t s);
 int pool_rows_launch(const void* x, int ld, int N, int R, int C, void* out, int ldo, int dtype, hipStream_t s);
 int unpool_rows_launch(const void* dp, int ldp, int R, int C, long M, void* dx, int ldx, int dtype, hipStream_t s);
 int box_sum_launch(const void* x, int ldx, void* y, int ldy, int N, int T_, int V, int C, int K, int S, int trans,
@@ -374,11 +375,12 @@ int stgcn_ln_apply(const void* u, int ldu, const void* st, const float* g, const
 }
 int stgcn_ln_bwd(const void* dy, int lddy, int mask, const void* mref, int ldm, const void* x, int ldx,
                  const void* st, const float* g, const float* b, long frames, int V, int C, void* dx, int lddx,
-                 int accumulate, float* dgb, int dtype, void* stream) {
+                 int accumulate, float* dgb, void* work, long work_bytes, int dtype, void* stream) {
   CHECK_DTYPE(dtype);
   return ln_bwd_launch(dy, lddy, mask, mref, ldm, x, ldx, (const float2*)st, g, b, frames, V, C, dx, lddx,
-                       accumulate, dgb, dtype, STREAM(stream));
+                       accumulate, dgb, work, work_bytes, dtype, STREAM(stream));
 }
+long stgcn_ln_bwd_workspace(long frames, int V, int C, int dtype) { return ln_bwd_workspace(frames, V, C, dtype); }
 int stgcn_pool_rows(const void* x, int ld, int N, int R, int C, void* out, int ldo, int dtype, void* stream) {
   CHECK_DTYPE(dtype);
   return pool_rows_launch(x, ld, N, R, C, out, ldo, dtype, STREAM(stream));

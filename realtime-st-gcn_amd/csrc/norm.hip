@@ -383,112 +383,7 @@ __global__ __launch_bounds__(256) void rowgroup_sum_kernel(const T* __restrict__
 }
 
 
-// ------------------------------------------------------------------ LayerNorm([C,1,V])
-// one wave per frame: frame = V rows x C channels (row stride ld)
-template <typename T>
-__global__ __launch_bounds__(256) void ln_stats_kernel(const T* __restrict__ x, int ld, long F, int V, int C,
-                                                       float eps, float2* stats) {
-  const int lane = threadIdx.x & 63;
-  const long f = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (f >= F) return;
-  const int E = V * C;
-  const T* base = x + f * V * (long)ld;
-  float s = 0.f;
-  for (int e = lane; e < E; e += 64) s += Tr<T>::to_f(base[(e / C) * (long)ld + e % C]);
-  s = wave_sum(s);
-  const float mean = s / (float)E;
-  float q = 0.f;
-  for (int e = lane; e < E; e += 64) {
-    const float d = Tr<T>::to_f(base[(e / C) * (long)ld + e % C]) - mean;
-    q += d * d;
-  }
-  q = wave_sum(q);
-  const float var = q / (float)(E - 1);  // unbiased (torch.var default, layernorm.py:24)
-  if (lane == 0) stats[f] = make_float2(mean, 1.f / sqrtf(var + eps));
-}
-
-// y = act((u-mu)*rs*g[c*V+v] + b[c*V+v] + res); res: 0 none | 1 r | 2 LN(r) with its own stats/affine
-template <typename T>
-__global__ __launch_bounds__(256) void ln_apply_kernel(const T* __restrict__ u, int ldu, const float2* st,
-                                                       const float* g, const float* b, int res_mode,
-                                                       const T* __restrict__ r, int ldr, const float2* rst,
-                                                       const float* rg, const float* rb, int relu,
-                                                       T* __restrict__ y, int ldy, long M, int V, int C) {
-  const long total = M * C;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const long m = i / C;
-    const int c = (int)(i % C);
-    const int v = (int)(m % V);
-    const long f = m / V;
-    const int gi = c * V + v;
-    const float2 s = st[f];
-    float o = (Tr<T>::to_f(u[m * ldu + c]) - s.x) * s.y * g[gi] + b[gi];
-    if (relu & 2) o = fmaxf(o, 0.f);
-    if (res_mode == 1) o += Tr<T>::to_f(r[m * ldr + c]);
-    if (res_mode == 2) {
-      const float2 q = rst[f];
-      o += (Tr<T>::to_f(r[m * ldr + c]) - q.x) * q.y * rg[gi] + rb[gi];
-    }
-    if (relu & 1) o = fmaxf(o, 0.f);
-    y[m * ldy + c] = Tr<T>::from_f(o);
-  }
-}
-
-// LN backward, one wave per frame.  mask: 0 none | 1 (mref > 0) | 2 (LN-output of x > 0, i.e. relu(LN(x)))
-// dgb: optional [2][C*V] accumulators for dgamma (sum dz*xhat) and dbeta (sum dz)
-template <typename T>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, int lddy, int mask,
-                                                     const T* __restrict__ mref, int ldm, const T* __restrict__ x,
-                                                     int ldx, const float2* st, const float* g, const float* b,
-                                                     long F, int V, int C, T* __restrict__ dx, int lddx,
-                                                     int accumulate, float* dgb) {
-  extern __shared__ float sg[];  // [2][C*V] per block
-  const int E = V * C;
-  for (int i = threadIdx.x; i < 2 * E; i += 256) sg[i] = 0.f;
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const long f = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (f < F) {
-    const float2 s = st[f];
-    float a1 = 0.f, a2 = 0.f;
-    for (int e = lane; e < E; e += 64) {
-      const int v = e / C, c = e % C;
-      const long m = f * V + v;
-      float dz = Tr<T>::to_f(dy[m * lddy + c]);
-      const float xh = (Tr<T>::to_f(x[m * ldx + c]) - s.x) * s.y;
-      const int gi = c * V + v;
-      if (mask == 1 && !(Tr<T>::to_f(mref[m * ldm + c]) > 0.f)) dz = 0.f;
-      if (mask == 2 && !(xh * g[gi] + b[gi] > 0.f)) dz = 0.f;
-      const float gz = dz * g[gi];
-      a1 += gz;
-      a2 += gz * xh;
-      if (dgb) {
-        atomicAdd(&sg[gi], dz * xh);
-        atomicAdd(&sg[E + gi], dz);
-      }
-    }
-    a1 = wave_sum(a1);
-    a2 = wave_sum(a2);
-    const float k1 = a1 / (float)E, k2 = a2 / (float)(E - 1);
-    for (int e = lane; e < E; e += 64) {
-      const int v = e / C, c = e % C;
-      const long m = f * V + v;
-      float dz = Tr<T>::to_f(dy[m * lddy + c]);
-      const float xh = (Tr<T>::to_f(x[m * ldx + c]) - s.x) * s.y;
-      const int gi = c * V + v;
-      if (mask == 1 && !(Tr<T>::to_f(mref[m * ldm + c]) > 0.f)) dz = 0.f;
-      if (mask == 2 && !(xh * g[gi] + b[gi] > 0.f)) dz = 0.f;
-      float o = s.y * (dz * g[gi] - k1 - xh * k2);
-      T* p = dx + m * lddx + c;
-      if (accumulate) o += Tr<T>::to_f(*p);
-      *p = Tr<T>::from_f(o);
-    }
-  }
-  if (dgb) {
-    __syncthreads();
-    for (int i = threadIdx.x; i < 2 * E; i += 256) atomicAdd(dgb + i, sg[i]);
-  }
-}
+// LayerNorm([C,1,V]): ln.hip
 
 // ------------------------------------------------------------------ head: global average pool
 // out[n][c] = mean_{r < R} x[(n*R + r)][c].  Block = (sample n, 64 channels); 256 threads = 8 units of
@@ -704,33 +599,6 @@ int rowgroup_sum_launch(const void* x, int ld, long M, int C, int G, long period
                                             (const T*)x, ld, F, C, G, fpb, fps, work));
   const long E = (long)G * C;
   slab_sum_launch(work, nsamp, nb, E, work + (long)nb * nsamp * E, S, 1, s);  // fixed-order, two levels
-  RET_HIP;
-}
-
-int ln_stats_launch(const void* x, int ld, long F, int V, int C, float eps, float2* stats, int dtype, hipStream_t s) {
-  DISPATCH_T(dtype, hipLaunchKernelGGL(ln_stats_kernel<T>, dim3((unsigned)((F + 3) / 4)), dim3(256), 0, s,
-                                       (const T*)x, ld, F, V, C, eps, stats));
-  RET_HIP;
-}
-
-int ln_apply_launch(const void* u, int ldu, const float2* st, const float* g, const float* b, int res_mode,
-                    const void* r, int ldr, const float2* rst, const float* rg, const float* rb, int relu, void* y,
-                    int ldy, long M, int V, int C, int dtype, hipStream_t s) {
-  DISPATCH_T(dtype, hipLaunchKernelGGL(ln_apply_kernel<T>, dim3(grid_for(M * C)), dim3(256), 0, s, (const T*)u, ldu,
-                                       st, g, b, res_mode, (const T*)r, ldr, rst, rg, rb, relu, (T*)y, ldy, M, V, C));
-  RET_HIP;
-}
-
-int ln_bwd_launch(const void* dy, int lddy, int mask, const void* mref, int ldm, const void* x, int ldx,
-                  const float2* st, const float* g, const float* b, long F, int V, int C, void* dx, int lddx,
-                  int accumulate, float* dgb, int dtype, hipStream_t s) {
-  const size_t lds = dgb ? (size_t)2 * V * C * 4 : 0;
-  if (lds > 150 * 1024) return STGCN_EBADSHAPE;
-  DISPATCH_T(dtype, {
-    if (lds > 64 * 1024 && stgcn_lds_attr((const void*)ln_bwd_kernel<T>, (int)lds, s)) return STGCN_EHIP;
-    hipLaunchKernelGGL(ln_bwd_kernel<T>, dim3((unsigned)((F + 3) / 4)), dim3(256), lds, s, (const T*)dy, lddy, mask,
-                       (const T*)mref, ldm, (const T*)x, ldx, st, g, b, F, V, C, (T*)dx, lddx, accumulate, dgb);
-  });
   RET_HIP;
 }
 

@@ -292,7 +292,7 @@ class StgcnLayerFunction(torch.autograd.Function):
             ctx.sup = sup
             ctx.dims = (N, Cin, Cout, T, T_out, V, P, pad, False)
             ctx.packs = None
-            ctx.save_for_backward(x, A32, None, g, u, y, wg, bg, wt, n1w, n1b, n2w, n2b, ls1, ls2)
+            ctx.save_for_backward(x, A32, None, g, u, y, wg, bg, wt, n1w, n1b, n2w, n2b, ls1, ls2, None)
             ctx.in_dtype = A.dtype
             return y
         tiled = gather and K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype)  # fused frame-tiled graph conv
@@ -372,9 +372,13 @@ class StgcnLayerFunction(torch.autograd.Function):
             mr1, sc1, sh1 = K.bn_finalize(st1, st1.shape[0], cpg, Cout, n1w.detach().float(), n1b.detach().float())
             pro1 = dict(pro=1, pro_a=sc1, pro_b=sh1)
         else:
+            # LayerNorm: h = relu(LN1(g)) is materialised (one HBM-bound pass, ln.hip) and the temporal conv runs
+            # without a prologue on the persistent kernels; a per-frame-statistics, per-(c,v)-affine prologue
+            # in the conv tiles measured 304 us vs ~85 us for this pass + conv_wide at 64 -> 64.  h is kept for
+            # the weight gradient.
             ls1 = K.ln_stats(g, N * T, V, Cout)
-            g1, b1 = _flat_ln(n1w), _flat_ln(n1b)
-            pro1 = dict(pro=2, pro_a=g1, pro_b=b1, pro_stats=ls1)
+            h = K.ln_apply(g, ls1, _flat_ln(n1w), _flat_ln(n1b), M1, V, Cout, relu=True)
+            pro1 = {}
 
         # ---- temporal conv on relu(norm1(g)) (norm applied in the prologue)
         wtp, cpt, kpt = packs.wt if packs is not None else \
@@ -384,7 +388,7 @@ class StgcnLayerFunction(torch.autograd.Function):
             u = K.tconv_frame(g, wtp, cpt, kpt, bias=bt.detach().float().contiguous(), pro_a=sc1, pro_b=sh1, stats=st2,
                               tag=f"tcn_fwd_c{Cout}")
         else:
-            u = K.conv_rows(g, wtp, Cout, Cout, cpt, kpt, T, T_out, Kt=kt, stride=stride, pad=pad,
+            u = K.conv_rows(g if norm == BN else h, wtp, Cout, Cout, cpt, kpt, T, T_out, Kt=kt, stride=stride, pad=pad,
                             bias=bt.detach().float().contiguous(), stats=st2 if norm == BN else None,
                             tag=f"tcn_fwd_c{Cout}" if stride == 1 else None, **pro1)
         if side is not None:  # join the residual branch
@@ -418,7 +422,7 @@ class StgcnLayerFunction(torch.autograd.Function):
         if norm == BN:
             saved += [mr1, sc1, sh1, mr2]
         else:
-            saved += [ls1, ls2]
+            saved += [ls1, ls2, h]
         if res_conv:
             saved += [r, wr, nrw, nrb] + ([mrr] if norm == BN else [lsr])
         ctx.save_for_backward(*saved)
@@ -436,8 +440,8 @@ class StgcnLayerFunction(torch.autograd.Function):
             mr1, sc1, sh1, mr2 = rest[:4]
             rest = rest[4:]
         else:
-            ls1, ls2 = rest[:2]
-            rest = rest[2:]
+            ls1, ls2, h = rest[:3]
+            rest = rest[3:]
         if res_conv:
             r, wr, nrw, nrb, strr = rest
         dev = x.device
@@ -520,11 +524,12 @@ class StgcnLayerFunction(torch.autograd.Function):
         wtTp, cq, kq = packs.wtT if packs is not None else \
             K.pack_weight(wt.detach().float().squeeze(-1).permute(2, 1, 0), dtype, stride=stride, trans=True)
         if norm == BN:
-            pro1 = dict(pro=1, pro_a=sc1, pro_b=sh1)
-        else:
-            pro1 = dict(pro=2, pro_a=_flat_ln(n1w), pro_b=_flat_ln(n1b), pro_stats=ls1)
+            pro1, hin = dict(pro=1, pro_a=sc1, pro_b=sh1), g
+        else:  # the forward's h = relu(LN1(g)), recomputed when the forward did not keep it (fused route)
+            pro1 = {}
+            hin = h if h is not None else K.ln_apply(g, ls1, _flat_ln(n1w), _flat_ln(n1b), M1, V, Cout, relu=True)
         with _fork(side):
-            grads["wt"] = K.conv_wgrad_w(g, du, Cout, Cout, T, T_out, Kt=kt, stride=stride, pad=pad,
+            grads["wt"] = K.conv_wgrad_w(hin, du, Cout, Cout, T, T_out, Kt=kt, stride=stride, pad=pad,
                                          **pro1).unsqueeze(-1)  # (co, ci, Kt, 1)
         if K.tconv_frame_ok(Cout, kt, stride, V, dtype, trans=True) and getattr(wtTp, "frag_stride", None) == 1:
             dh = K.tconv_frame(du, wtTp, cq, kq, trans=True)

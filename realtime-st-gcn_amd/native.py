@@ -998,10 +998,17 @@ def ln_apply(u, st, g, b, M, V, C, res_mode=0, r=None, rst=None, rg=None, rb=Non
 
 
 def ln_bwd(dy, x, st, g, b, frames, V, C, out, mask=0, mref=None, accumulate=False, dgb=None):
+    """out (+)= the LayerNorm input gradient; dgb ([2][C*V] fp32, optional) += (dgamma, dbeta), reduced over the
+    frames in a fixed order through a per-call workspace (stgcn_ln_bwd, ln.hip)."""
+    work, nbytes = None, 0
+    if dgb is not None:
+        nbytes = L.lib().stgcn_ln_bwd_workspace(frames, V, C, L.dtype_code(dy.dtype))
+        work = torch.empty(max(nbytes, 4) // 4, dtype=torch.float32, device=dy.device)
     L.check(L.lib().stgcn_ln_bwd(dy.data_ptr(), rows_ld(dy), mask, L.ptr(mref),
                                  rows_ld(mref) if mref is not None else 0, x.data_ptr(), rows_ld(x), st.data_ptr(),
                                  g.data_ptr(), b.data_ptr(), frames, V, C, out.data_ptr(), rows_ld(out),
-                                 int(accumulate), L.ptr(dgb), L.dtype_code(dy.dtype), L.stream()), "ln_bwd")
+                                 int(accumulate), L.ptr(dgb), L.ptr(work), nbytes, L.dtype_code(dy.dtype),
+                                 L.stream()), "ln_bwd")
     return out
 
 

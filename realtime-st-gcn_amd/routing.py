@@ -14,9 +14,10 @@ also assign the attributes directly.
     fused_bn_inference  STGCN_FUSED_BN=0      BatchNorm layers too (default on since the fused kernel reached 78-82 us:
                                               the two-pass fused forward measured 0.175 vs 0.187 ms graph-replayed,
                                               0.178 vs 0.179 eager)
-    fused_ln_train      STGCN_FUSED_LN_TRAIN=0  training forward of LayerNorm 64->64 stride-1 layers through the same
+    fused_ln_train      STGCN_FUSED_LN_TRAIN=1  training forward of LayerNorm 64->64 stride-1 layers through the same
                                               one-kernel layer (it also writes g, u and both LN statistics for the
-                                              unfused backward; default on)
+                                              unfused backward).  Default off since the LayerNorm kernels of ln.hip:
+                                              the LN training step measured 8.77 ms unfused vs 8.86 fused (r04k)
     gcn_tile            STGCN_GCN_TILE=0|1|auto  graph conv on the two-stage MFMA kernel gcn_tile.hip (default 0)
     gcn_afirst          STGCN_GCN_AFIRST=1    force the A-first graph conv (amix + GEMM) for shared graphs
     gcn_afirst_min_c    STGCN_GCN_AFIRST_MIN_C=<C>  ... only for layers with at least C input channels (A/B of the
@@ -47,7 +48,7 @@ class _Routing:
         self.side_stream = e("STGCN_SIDE_STREAM", "0") == "1"
         self.fused_inference = e("STGCN_FUSED", "1") != "0"
         self.fused_bn_inference = e("STGCN_FUSED_BN", "1") != "0"
-        self.fused_ln_train = e("STGCN_FUSED_LN_TRAIN", "1") != "0"
+        self.fused_ln_train = e("STGCN_FUSED_LN_TRAIN", "0") == "1"
         self.gcn_tile = e("STGCN_GCN_TILE", "0")
         self.gcn_afirst = e("STGCN_GCN_AFIRST", "0") not in ("0", "")
         self.gcn_afirst_min_c = int(e("STGCN_GCN_AFIRST_MIN_C", "0") or 0)

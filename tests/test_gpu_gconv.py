@@ -120,7 +120,7 @@ def test_gconv_finish_bias_merged(K, pkg, Cin, Cout):
 
 
 @pytest.mark.parametrize("Cin,Cout,N,T", [(64, 64, 4, 40), (64, 128, 3, 29), (128, 128, 2, 33), (128, 256, 2, 21),
-                                          (256, 256, 2, 13), (64, 64, 64, 300)])
+                                          (256, 256, 2, 13), (64, 64, 64, 300), (64, 64, 65, 300)])
 @pytest.mark.parametrize("strategy", ["spatial", "uniform", "distance"])
 def test_gconv_wgrad_frame(K, pkg, Cin, Cout, N, T, strategy, monkeypatch):
     """stgcn_gconv_wgrad_frame (dW, the dense dA with the bias through A, db in one pass over (x, dy), bf16
@@ -154,7 +154,7 @@ def test_gconv_wgrad_frame(K, pkg, Cin, Cout, N, T, strategy, monkeypatch):
 
 
 @pytest.mark.parametrize("Cin,Cout,N,T", [(64, 64, 3, 37), (64, 128, 2, 29), (128, 128, 2, 33), (128, 256, 1, 21),
-                                          (64, 64, 64, 300), (128, 128, 64, 150)])
+                                          (64, 64, 64, 300), (128, 128, 64, 150), (64, 64, 65, 300)])
 @pytest.mark.parametrize("strategy", ["spatial", "uniform", "distance"])
 def test_gcn_frame_fwd_dgrad(K, pkg, Cin, Cout, N, T, strategy, monkeypatch):
     """stgcn_gcn_frame (the 1x1 conv then the joint mix per frame, bf16) vs the reference's conv1x1 -> einsum(A)

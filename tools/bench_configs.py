@@ -133,7 +133,7 @@ LN_ARCH = {"strategy": "spatial", "in_feat": 3, "normalization": "LayerNorm", "n
 def ln_train(P, dev, steps, warmup, reps=3, routes=(True, False)):
     """The LayerNorm st-gcn (ln/stgcn_vsc.json-style: LN, Kt = 9, config-2 widths) training step (fwd + loss +
     bwd + Adam, bf16, N=64 T=300) with its three 64 -> 64 layers' forward on the fused one-kernel layer
-    (routing.fused_ln_train, default) and unfused, interleaved ``reps`` times."""
+    (routing.fused_ln_train) and unfused (default), interleaved ``reps`` times."""
     R = P.routing.ROUTING
     torch.manual_seed(1538574472)
     m = P.MODELS["st-gcn"](rank=None, **dict(LN_ARCH, graph=P.PKU_MMD)).to(dev).set_compute_dtype("bf16")
