@@ -332,6 +332,13 @@ int stgcn_ln_bwd(const void* dy, int lddy, int mask, const void* mref, int ldm, 
                  int accumulate, float* dgb, void* work, long work_bytes, int dtype, void* stream);
 long stgcn_ln_bwd_workspace(long frames, int V, int C, int dtype);
 
+/* out_bf16[m][c] = bf16(x[m][c]) and colsum[c] = sum_m x[m][c] (fp32, fixed order) from one read of the fp32
+ * rows: the attention projections' backward (models/aagcn/aagcn.py:139-141 autograd; the bf16 GEMM operand
+ * and the bias gradients).  C % 4 == 0, C <= 1024; work: stgcn_cast_colsum_workspace floats. */
+int stgcn_cast_colsum(const float* x, int ldx, long M, int C, void* out_bf16, int ldo, float* colsum, float* work,
+                      void* stream);
+long stgcn_cast_colsum_workspace(long M, int C);
+
 /* Head: F.avg_pool2d over (T,V) (stgcn.py:92) and its gradient. */
 int stgcn_pool_rows(const void* x, int ld, int N, int R, int C, void* out, int ldo, int dtype, void* stream);
 int stgcn_unpool_rows(const void* dp, int ldp, int R, int C, long M, void* dx, int ldx, int dtype, void* stream);

@@ -157,6 +157,8 @@ _SIGS = {
                              c_long, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_long, c_int,
                              c_void_p]),
     "stgcn_ln_bwd_workspace": (c_long, [c_long, c_int, c_int, c_int]),
+    "stgcn_cast_colsum": (c_int, [c_void_p, c_int, c_long, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "stgcn_cast_colsum_workspace": (c_long, [c_long, c_int]),
     "stgcn_pool_rows": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p]),
     "stgcn_unpool_rows": (c_int, [c_void_p, c_int, c_int, c_int, c_long, c_void_p, c_int, c_int, c_void_p]),
     "stgcn_box_sum": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,

@@ -81,6 +81,9 @@ int ln_apply_launch(const void* u, int ldu, const float2* st, const float* g, co
                     const void* r, int ldr, const float2* rst, const float* rg, const float* rb, int relu, void* y,
                     int ldy, long M, int V, int C, int dtype, hipStream_t s);
 long ln_bwd_workspace(long F, int V, int C, int dtype);
+long cast_colsum_workspace(long M, int C);
+int cast_colsum_launch(const float* x, int ldx, long M, int C, void* out16, int ldo, float* colsum, float* work,
+                       hipStream_t s);
 int ln_bwd_launch(const void* dy, int lddy, int mask, const void* mref, int ldm, const void* x, int ldx,
                   const float2* st, const float* g, const float* b, long F, int V, int C, void* dx, int lddx,
                   int accumulate, float* dgb, void* work, long work_bytes, int dtype, hipStream_t s);
@@ -381,6 +384,12 @@ int stgcn_ln_bwd(const void* dy, int lddy, int mask, const void* mref, int ldm, 
                        accumulate, dgb, work, work_bytes, dtype, STREAM(stream));
 }
 long stgcn_ln_bwd_workspace(long frames, int V, int C, int dtype) { return ln_bwd_workspace(frames, V, C, dtype); }
+int stgcn_cast_colsum(const float* x, int ldx, long M, int C, void* out_bf16, int ldo, float* colsum, float* work,
+                      void* stream) {
+  if (!x || !out_bf16 || !colsum || (!work && M > 0)) return STGCN_EBADSHAPE;
+  return cast_colsum_launch(x, ldx, M, C, out_bf16, ldo, colsum, work, STREAM(stream));
+}
+long stgcn_cast_colsum_workspace(long M, int C) { return cast_colsum_workspace(M, C); }
 int stgcn_pool_rows(const void* x, int ld, int N, int R, int C, void* out, int ldo, int dtype, void* stream) {
   CHECK_DTYPE(dtype);
   return pool_rows_launch(x, ld, N, R, C, out, ldo, dtype, STREAM(stream));

@@ -107,6 +107,17 @@ __global__ __launch_bounds__(NT, 2) void conv1x1_kernel(const stgcn_conv_desc a,
   __syncthreads();  // every wave is done reading the staged rows
   constexpr int OS = BN * 2 + 16;  // padded output row in LDS
   float4* red = reinterpret_cast<float4*>(smem + BM * OS);  // [2 row halves][BN]
+  // ROWB: each row's bias row index, once per tile (a 64-bit division per accumulator element cost 3x the kernel)
+  int* const sbi = reinterpret_cast<int*>(smem + BM * OS + 2 * BN * 16);
+  if (ROWB) {
+    for (int t = tid; t < BM; t += NT) {
+      const long m = m0 + (t < rows_valid ? t : 0);
+      const long fr = m / V;
+      const int v = (int)(m - fr * V);
+      sbi[t] = a.bias_mode == 2 ? v : (int)((fr / a.T_out) * V + v);
+    }
+    __syncthreads();
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int cl = (wn * TN + j) * 32 + lr;  // column within the tile
@@ -122,13 +133,7 @@ __global__ __launch_bounds__(NT, 2) void conv1x1_kernel(const stgcn_conv_desc a,
       for (int r = 0; r < 16; ++r) {
         const int row = (wm * TM + i) * 32 + acc_row(r, lane);
         float bb = b;
-        if (ROWB) {
-          const long m = m0 + (row < rows_valid ? row : 0);
-          const long fr = m / V;
-          const int v = (int)(m - fr * V);
-          const long bi = a.bias_mode == 2 ? v : (fr / a.T_out) * V + v;
-          bb = a.bias[bi * a.Cout + col];
-        }
+        if (ROWB) bb = a.bias[(long)sbi[row] * a.Cout + col];
         const float v = acc[i][j][r] + bb;
         acc[i][j][r] = v;
         *reinterpret_cast<bf16*>(smem + row * OS + cl * 2) = (bf16)v;
@@ -306,7 +311,7 @@ template <int KS, int BN, bool ROWB = false>
 int launch1(const stgcn_conv_desc& a, const XGeom& g, hipStream_t s) {
   constexpr int RS = KS * 16 * 2 + 16, OS = BN * 2 + 16;
   size_t lds = (size_t)BM * RS;
-  const size_t lout = (size_t)BM * OS + 2 * BN * 16;
+  const size_t lout = (size_t)BM * OS + 2 * BN * 16 + (ROWB ? BM * sizeof(int) : 0);
   if (lout > lds) lds = lout;
   constexpr bool RB = ROWB;
   if (stgcn_lds_attr((const void*)conv1x1_kernel<KS, BN, RB>, 160 * 1024, s)) return STGCN_EHIP;

@@ -231,6 +231,90 @@ __global__ __launch_bounds__(256) void amix_dA_kernel(const AmixArgs a, const vo
   }
 }
 
+// The same products with 16-B rows (Cin % 8 == 0): x's fragment is loaded once for all P partitions
+// (P accumulators), and KC k-steps' fragments of x and of the P DW blocks are issued before their MFMAs — the
+// generic kernel above re-read x per partition and waited for every 16-channel step's two loads.
+template <typename T>
+__global__ __launch_bounds__(256) void amix_dA_vec_kernel(const AmixArgs a, const void* dwp, float* dA, float* work,
+                                                          int frames_per_block) {
+  constexpr int VEC = 16 / sizeof(T);
+  constexpr int NU = 8 / VEC;                 // 16-B units per 8-channel fragment
+  constexpr int KC = sizeof(T) == 2 ? 4 : 2;  // k-steps per load batch
+  constexpr int PM = 4;
+  __shared__ float red[4][VMAX * VMAX];
+  const int n = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
+  const T* __restrict__ dw = reinterpret_cast<const T*>(dwp);
+  const int ld_dw = a.P * a.Cin;
+  const int t0 = blockIdx.x * frames_per_block;
+  const int t1 = min(a.T, t0 + frames_per_block);
+  const bool rok = r < a.V;
+  f32x16 acc[PM];
+#pragma unroll
+  for (int p = 0; p < PM; ++p)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[p][i] = 0.f;
+  for (int t = t0 + wave; t < t1; t += 4) {
+    const long row = ((long)n * a.T + t) * a.V + (rok ? r : 0);
+    const T* px = x + row * a.x_ld + 8 * h;
+    const T* pd = dw + row * ld_dw + 8 * h;
+    for (int k0 = 0; k0 < a.Cin; k0 += 16 * KC) {
+      uint4 ux[KC][NU], ud[KC][PM][NU];
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        const int ci = k0 + 16 * kc;
+        const bool ok = rok && ci < a.Cin;
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          ux[kc][u] = ok ? *reinterpret_cast<const uint4*>(px + ci + u * VEC) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+          for (int p = 0; p < PM; ++p)
+            ud[kc][p][u] = ok && p < a.P ? *reinterpret_cast<const uint4*>(pd + p * a.Cin + ci + u * VEC)
+                                         : make_uint4(0, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        if (k0 + 16 * kc >= a.Cin) break;  // wave-uniform
+        float fx[8];
+        typename Tr<T>::frag fa;
+#pragma unroll
+        for (int u = 0; u < NU; ++u) unpack16(ux[kc][u], fx + u * VEC, (T*)nullptr);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) fa[j] = Tr<T>::from_f(fx[j]);
+#pragma unroll
+        for (int p = 0; p < PM; ++p) {
+          if (p >= a.P) break;
+          float fd[8];
+          typename Tr<T>::frag fb;
+#pragma unroll
+          for (int u = 0; u < NU; ++u) unpack16(ud[kc][p][u], fd + u * VEC, (T*)nullptr);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) fb[j] = Tr<T>::from_f(fd[j]);
+          Tr<T>::mma(acc[p], fa, fb);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < PM; ++p) {
+    if (p >= a.P) break;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) red[wave][acc_row(i, lane) * VMAX + r] = acc[p][i];
+    __syncthreads();
+    float* dst = work ? work + ((long)n * gridDim.x + blockIdx.x) * a.P * a.V * a.V + (long)p * a.V * a.V
+                      : dA + ((a.per_sample ? (long)n * a.P : 0) + p) * a.V * a.V;
+    for (int i = threadIdx.x; i < a.V * a.V; i += 256) {
+      const int v = i / a.V, w = i % a.V;
+      const float s = red[0][v * VMAX + w] + red[1][v * VMAX + w] + red[2][v * VMAX + w] + red[3][v * VMAX + w];
+      if (work) dst[i] = s; else atomicAdd(dst + i, s);
+    }
+    __syncthreads();
+  }
+}
+
 // out[b][r2][e] (+)= sum_{r in group r2} in[b][r][e], rows summed in a fixed order (deterministic).
 // Block: 64 columns x 4 row-interleaved waves, LDS combine in wave order.
 __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ in, long R, long E, int rpb,
@@ -407,10 +491,15 @@ int amix_dA_launch(const AmixArgs& a, const void* dw, float* dA, void* work, int
   const int chunks = amix_dA_chunks(a, &fpb);
   dim3 grid(chunks, a.N);
   float* w = reinterpret_cast<float*>(work);
-  if (dtype)
-    hipLaunchKernelGGL(amix_dA_kernel<bf16>, grid, dim3(256), 0, s, a, dw, dA, w, fpb);
-  else
-    hipLaunchKernelGGL(amix_dA_kernel<float>, grid, dim3(256), 0, s, a, dw, dA, w, fpb);
+  const bool vec = a.Cin % 8 == 0 && a.x_ld % 8 == 0 && (a.P * a.Cin) % 8 == 0 && ((size_t)a.x & 15) == 0 &&
+                   ((size_t)dw & 15) == 0;
+  if (dtype) {
+    if (vec) hipLaunchKernelGGL(amix_dA_vec_kernel<bf16>, grid, dim3(256), 0, s, a, dw, dA, w, fpb);
+    else hipLaunchKernelGGL(amix_dA_kernel<bf16>, grid, dim3(256), 0, s, a, dw, dA, w, fpb);
+  } else {
+    if (vec) hipLaunchKernelGGL(amix_dA_vec_kernel<float>, grid, dim3(256), 0, s, a, dw, dA, w, fpb);
+    else hipLaunchKernelGGL(amix_dA_kernel<float>, grid, dim3(256), 0, s, a, dw, dA, w, fpb);
+  }
   if (w) {
     const long E = (long)a.P * a.V * a.V;
     const long B = a.per_sample ? a.N : 1, R = a.per_sample ? chunks : (long)a.N * chunks;

@@ -64,6 +64,21 @@ DEV void dma16(const void* src, unsigned lds_off) {
 }
 DEV unsigned lds_u32(const void* p) { return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p; }
 
+// s_waitcnt vmcnt(n) for a wave-uniform run-time n (clamped to 63; waiting for fewer is always safe)
+template <int N>
+DEV void wait_vm_upto(int n) {
+  if constexpr (N < 63) {
+    if (n <= N) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+      return;
+    }
+    wait_vm_upto<N + 1>(n);
+  } else {
+    asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+  }
+}
+DEV void wait_vm(int n) { wait_vm_upto<0>(n < 0 ? 0 : n); }
+
 struct JmixArgs {
   const void* in;
   void* out;
@@ -88,7 +103,7 @@ __global__ __launch_bounds__(NWJ * 64) void jmix_kernel(const JmixArgs a) {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lr = lane & 31, lh = lane >> 5;
   const int V = a.V;
-  constexpr int NBUF = 3;  // items in flight: the current one and the next two
+  constexpr int NBUF = NP == 1 ? 5 : 3;  // panel slots per wave: the current item and the ones in flight
   char* const buf = smem + wave * NBUF * NP * PANEL;  // [NBUF][NP] panels
   // rows V..31 stay zero (the DMA never writes them)
   for (int e = lane; e < NBUF * NP * PANEL / 16; e += 64) reinterpret_cast<uint4*>(buf)[e] = make_uint4(0, 0, 0, 0);
@@ -112,9 +127,7 @@ __global__ __launch_bounds__(NWJ * 64) void jmix_kernel(const JmixArgs a) {
   // lanes past the frame's V rows or past a partial last channel block (mode 2) copy the frame's first
   // unit instead — finite data, multiplied by zero coefficients (rows >= V) or masked (channels).
   constexpr int DMA_OPS = NP * (32 / RPI);
-  auto issue = [&](long it, int slot) {
-    const long i = it / a.nob;
-    const int ob = (int)(it - i * a.nob);
+  auto issue_io = [&](long i, int ob, int slot) {
     const T* src0 = in + i * V * (long)a.in_ld;
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
@@ -128,6 +141,10 @@ __global__ __launch_bounds__(NWJ * 64) void jmix_kernel(const JmixArgs a) {
         dma16(ok ? src0 + (long)row * a.in_ld + cb + lunit * (16 / ELT) : src0, pan + rr * 32 * ELT);
       }
     }
+  };
+  auto issue = [&](long it, int slot) {
+    const long i = it / a.nob;
+    issue_io(i, (int)(it - i * a.nob), slot);
   };
 
   // coefficients of one sample as B operands: B[k = in joint b][n = out joint a] = coef(a, b, p)
@@ -200,6 +217,115 @@ __global__ __launch_bounds__(NWJ * 64) void jmix_kernel(const JmixArgs a) {
     }
   };
 
+  // store instructions of an item: the 8-channel quarters with any channel below cout (an instruction whose
+  // lanes are all masked is branched over and does not count on vmcnt)
+  auto nstores = [&](int ob) {
+    int n = 0;
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) n += 32 * ob + 8 * q4 < a.cout ? 1 : 0;
+    return n;
+  };
+  if (!a.accumulate) {
+    // Order per item j: [wait: panels(j)] [mix(j)] [DMA(j+AH)] [stores(j)], AH = NBUF - 1 items in flight.
+    // vmcnt completes in order, so the wait before item j counts exactly the ops issued after DMA(j): the DMAs
+    // of the next items already issued and the stores of the last AH items — a store is waited for only AH
+    // items after it (waiting for the previous item's stores had serialised the items behind the write
+    // latency).  Item -> (frame, block) and the sample advance by counters: no 64-bit division per item.
+    constexpr int AH = NBUF - 1;
+    constexpr int DOPS = NP * (32 / RPI);
+    long ci = it0 / a.nob;  // item j's frame and block
+    int cob = (int)(it0 - ci * a.nob);
+    long ii = ci;  // next item to issue
+    int iob = cob;
+    auto adv = [&](long& f, int& o) {
+      if (++o == a.nob) {
+        o = 0;
+        ++f;
+      }
+    };
+    long oi = ci;  // item j - AH (its stores leave the wait count once j passes it)
+    int oob = cob;
+    for (int k = 0; k < AH && it0 + k < it1; ++k) {
+      issue_io(ii, iob, k);
+      adv(ii, iob);
+    }
+    int nsum = 0;  // store instructions of items max(it0, j-AH) .. j-1
+    int slot = 0, islot = AH;
+    long nt = ci / a.T, tt = ci - nt * a.T;  // sample and frame-in-sample of item j's frame
+    for (long it = it0; it < it1; ++it) {
+      const long i = ci;
+      const int ob = cob;
+      const long ndma = it1 - 1 - it < AH - 1 ? it1 - 1 - it : AH - 1;
+      wait_vm((int)ndma * DOPS + nsum);
+      const long n = nt;
+      if (n != cur_n) {
+        load_coef(n);
+        cur_n = n;
+      }
+    f32x16 acc = zero;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const char* pan = buf + (slot * NP + k) * PANEL;
+      // partitions feeding this (block, panel) and the channel rows each one owns (mode 2: groups of C)
+      int p0, p1;
+      if (a.mode == 0) p0 = p1 = (32 * ob) / a.C;
+      else if (a.mode == 1) p0 = p1 = k;
+      else {
+        p0 = (32 * ob) / a.C;
+        p1 = min(a.P - 1, (32 * ob + 31) / a.C);
+      }
+#pragma unroll
+      for (int p = 0; p < PMAXJ; ++p) {  // compile-time p: the coefficient registers are never indexed at run time
+        if (p < p0 || p > p1) continue;
+        bool mok = true;  // this lane's A row (channel m = lr) belongs to partition p
+        if (a.mode == 2) {
+          const int ch = 32 * ob + lr;
+          mok = ch >= p * a.C && ch < (p + 1) * a.C;
+        }
+        if constexpr (sizeof(T) == 2) {
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) {
+            bf16x8 af = trfrag16(pan, 16 * ks, lane);
+            if (!mok) af = bf16x8{};
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bh[p][ks], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bl[p][ks], acc, 0, 0, 0);
+          }
+        } else {
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) {
+            if (2 * ks >= V) break;
+            float av = *reinterpret_cast<const float*>(pan + ((2 * ks + lh) * 32 + lr) * 4);
+            av = mok ? av : 0.f;
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bh[p][ks], acc, 0, 0, 0);
+          }
+        }
+      }
+    }
+    // D: lane = output joint lr, acc[r] = channel 32*ob + 8*(r>>2) + 4*lh + (r&3); stored next item
+    pend = acc;
+    pend_i = i;
+    pend_ob = ob;
+      if (it + AH < it1) {
+        issue_io(ii, iob, islot);
+        adv(ii, iob);
+        islot = islot + 1 == NBUF ? 0 : islot + 1;
+      }
+      flush();
+      nsum += nstores(ob);
+      if (it - it0 >= AH) {  // item j-AH leaves the window of item j+1
+        nsum -= nstores(oob);
+        adv(oi, oob);
+      }
+      slot = slot + 1 == NBUF ? 0 : slot + 1;
+      adv(ci, cob);
+      if (cob == 0 && ++tt == a.T) {
+        tt = 0;
+        ++nt;
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
   // Order per item j: [stores(j-1)] [accumulate loads(j)] [DMA(j+2)] [mix(j)] [wait].  The youngest ops at
   // the wait are DMA(j+2)'s DMA_OPS; waiting until at most DMA_OPS are outstanding (in-order completion)
   // retires DMA(j+1), the loads(j) and everything older, and leaves j+2's panels in flight.
@@ -308,13 +434,14 @@ int jmix_launch(const void* in, int in_ld, void* out, int out_ld, const float* M
   a.items = (long)N * T * nob;
   const int ncu = stgcn_cu_count(s);
   long waves = a.items / ITEMS_PER_WAVE;
-  const long wmax = (long)(ncu > 0 ? ncu : 256) * 8 * NWJ;
+  // one round of resident waves (2 per SIMD at the kernel's ~210 VGPRs): more waves only queue behind them
+  const long wmax = (long)(ncu > 0 ? ncu : 256) * 2 * NWJ;
   if (waves > wmax) waves = wmax;
   if (waves < 1) waves = 1;
   a.ipw = (a.items + waves - 1) / waves;
   const long blocks = (a.items + a.ipw * NWJ - 1) / (a.ipw * NWJ);
   const int panel = dtype ? JT<bf16>::PANEL : JT<float>::PANEL;
-  const size_t lds = (size_t)NWJ * 3 * a.npan * panel;
+  const size_t lds = (size_t)NWJ * (a.npan == 1 ? 5 : 3) * a.npan * panel;  // NBUF slots per wave
 #define JM_LAUNCH(TT, NPV)                                                                                   \
   do {                                                                                                       \
     if (stgcn_lds_attr((const void*)jmix_kernel<TT, NPV>, (int)lds, s)) return STGCN_EHIP;                    \

@@ -383,6 +383,48 @@ __global__ __launch_bounds__(256) void rowgroup_sum_kernel(const T* __restrict__
 }
 
 
+// ------------------------------------------------------------------ fp32 -> bf16 rows + column sums
+// out16[m][c] = bf16(x[m][c]); part[b][c] = sum over block b's rows of x[m][c] (fp32, before the rounding).
+// The attention projections' backward (aagcn.py:139-141 autograd): the bf16 operand of the data / weight
+// gradient GEMMs and the bias gradient from one read of the fp32 gradient.  Thread = one 16-B unit (4
+// channels) of a row, rows strided by the block's row groups; four rows' loads issued before their use.
+__global__ __launch_bounds__(256) void cast_colsum_kernel(const float* __restrict__ x, int ldx, long M, int C,
+                                                          bf16* __restrict__ out, int ldo, long rpb,
+                                                          float* __restrict__ part) {
+  __shared__ float red[256 * 4];
+  const int cun = C / 4, rpi = 256 / cun;
+  const int tid = threadIdx.x, cu = tid % cun, rs = tid / cun;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  if (rs < rpi) {
+    const long mb = (long)blockIdx.x * rpb, me = min(M, mb + rpb);
+    for (long m0 = mb + rs; m0 < me; m0 += 4L * rpi) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long m = m0 + (long)u * rpi;
+        v[u] = m < me ? *reinterpret_cast<const float4*>(x + m * ldx + cu * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long m = m0 + (long)u * rpi;
+        if (m >= me) continue;
+        s[0] += v[u].x; s[1] += v[u].y; s[2] += v[u].z; s[3] += v[u].w;
+        bf16x4 r;
+        r[0] = (bf16)v[u].x; r[1] = (bf16)v[u].y; r[2] = (bf16)v[u].z; r[3] = (bf16)v[u].w;
+        *reinterpret_cast<bf16x4*>(out + m * ldo + cu * 4) = r;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[rs * C + cu * 4 + j] = s[j];
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    float t = 0.f;
+    for (int r = 0; r < rpi; ++r) t += red[r * C + c];  // fixed order
+    part[(long)blockIdx.x * C + c] = t;
+  }
+}
+
 // LayerNorm([C,1,V]): ln.hip
 
 // ------------------------------------------------------------------ head: global average pool
@@ -599,6 +641,25 @@ int rowgroup_sum_launch(const void* x, int ld, long M, int C, int G, long period
                                             (const T*)x, ld, F, C, G, fpb, fps, work));
   const long E = (long)G * C;
   slab_sum_launch(work, nsamp, nb, E, work + (long)nb * nsamp * E, S, 1, s);  // fixed-order, two levels
+  RET_HIP;
+}
+
+static long cast_colsum_rpb(long M) {
+  long rpb = (M + 1023) / 1024;
+  return rpb < 64 ? 64 : rpb;
+}
+long cast_colsum_workspace(long M, int C) {
+  const long nb = (M + cast_colsum_rpb(M) - 1) / cast_colsum_rpb(M);
+  return nb * C + slab_sum_tmp_floats(1, nb, C);
+}
+int cast_colsum_launch(const float* x, int ldx, long M, int C, void* out16, int ldo, float* colsum, float* work,
+                       hipStream_t s) {
+  if (M <= 0) return STGCN_OK;
+  if (C % 4 || C / 4 > 256 || ldx % 4 || ldo % 4 || ((size_t)x & 15) || ((size_t)out16 & 7)) return STGCN_EBADSHAPE;
+  const long rpb = cast_colsum_rpb(M), nb = (M + rpb - 1) / rpb;
+  hipLaunchKernelGGL(cast_colsum_kernel, dim3((unsigned)nb), dim3(256), 0, s, x, ldx, M, C, (bf16*)out16, ldo, rpb,
+                     work);
+  slab_sum_launch(work, 1, nb, C, work + nb * C, colsum, 0, s);
   RET_HIP;
 }
 

@@ -4,8 +4,9 @@
 // so this is a split-K reduction bound by reading x and dy once:
 //   * a block owns a contiguous chunk of 32-row steps and a group of <= 2 x 12 (co, ci) 32x32 output tiles,
 //     spread over its 4 waves (<= 6 accumulator tiles per wave);
-//   * per step the group's dy and x row panels ([32 rows][32 ch] bf16) are DMA'd into LDS, three steps in
-//     flight (every wave issues a fixed number of DMAs per step, so the waits are counted vmcnt waits);
+//   * per step the group's dy and x row panels ([32 rows][32 ch] bf16) are DMA'd into LDS, a ring of 3-6
+//     stages (~64 KB per block, sized to the group's panels) with all but one in flight (every wave issues a
+//     fixed number of DMAs per step, so the waits are counted vmcnt waits);
 //   * both MFMA operands are transposed reads of the panels (ds_read_tr16_b64: m = co / n = ci, k = rows);
 //   * per-block fp32 partials go to a slab, summed over the chunks in a fixed order (deterministic).
 // Served: bf16, M % 32 == 0, Cin and Cout multiples of 32, 16-B aligned rows; else the frame-tiled kernel.
@@ -18,7 +19,7 @@ constexpr int NT1 = 256;
 constexpr int PANEL = 32 * 64;  // [32 rows][32 ch] bf16
 constexpr int GCO = 2, GCI = 12;  // co / ci blocks per group
 constexpr int TPW = GCO * GCI / 4;  // tiles per wave (<= 6)
-constexpr int NSTAGE = 3;
+constexpr int NSTAGE = 3;  // minimum ring depth
 constexpr int TARGET_BLOCKS = 512;
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -46,27 +47,21 @@ DEV void dma16(const void* src, unsigned lds_off) {
 }
 DEV unsigned lds_u32(const void* p) { return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p; }
 
-// s_waitcnt vmcnt(n) for a wave-uniform run-time n <= 15
-DEV void wait_vm(int n) {
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
-    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+// s_waitcnt vmcnt(n) for a wave-uniform run-time n (clamped to 63, the counter's range: waiting for fewer
+// outstanding operations is always safe)
+template <int N>
+DEV void wait_vm_upto(int n) {
+  if constexpr (N < 63) {
+    if (n <= N) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+      return;
+    }
+    wait_vm_upto<N + 1>(n);
+  } else {
+    asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
   }
 }
+DEV void wait_vm(int n) { wait_vm_upto<0>(n < 0 ? 0 : n); }
 
 struct W1Geom {
   long steps;    // M / 32
@@ -74,6 +69,8 @@ struct W1Geom {
   int nchunk;
   int ncog, ncig;  // groups along co / ci
   int ncob, ncib;  // 32-channel blocks
+  int pstage;      // panels per ring stage: the largest group's (LDS sized to it, not to GCO + GCI)
+  int nstage;      // ring depth (3..6: ~64 KB of LDS per block)
 };
 
 __global__ __launch_bounds__(NT1) void wgrad1x1_kernel(const stgcn_wgrad_desc a, const W1Geom g, float* __restrict__ slab) {
@@ -94,7 +91,7 @@ __global__ __launch_bounds__(NT1) void wgrad1x1_kernel(const stgcn_wgrad_desc a,
   const int my_pan = (npan - wave + 3) / 4;  // panels of this wave
   const int ops = 2 * my_pan;                 // DMA instructions per step of this wave
   auto issue = [&](long st, int stage) {
-    char* base = smem + stage * (GCO + GCI) * PANEL;
+    char* base = smem + stage * g.pstage * PANEL;
     for (int p = wave; p < npan; p += 4) {
       const bf16* src;
       int ld;
@@ -118,17 +115,21 @@ __global__ __launch_bounds__(NT1) void wgrad1x1_kernel(const stgcn_wgrad_desc a,
 #pragma unroll
   for (int k = 0; k < TPW; ++k) acc[k] = f32x16{};
 
-  const long nst = s1 - s0;
-  issue(s0, 0);
-  if (nst > 1) issue(s0 + 1, 1);
-  for (long si = 0; si < nst; ++si) {
-    // this step's panels: own DMAs of the (up to) one younger step may stay in flight
-    wait_vm(si + 1 < nst ? ops : 0);
+  const int nst = (int)(s1 - s0);
+  const int ahead = g.nstage - 1;  // steps in flight
+  for (int k = 0; k < ahead && k < nst; ++k) issue(s0 + k, k);
+  int cur = 0, nxt = ahead;  // ring stages of step si and of step si + ahead (no run-time modulo)
+  for (int si = 0; si < nst; ++si) {
+    // this step's panels: own DMAs of the younger steps already issued may stay in flight
+    const int left = nst - 1 - si;
+    wait_vm((left < ahead - 1 ? left : ahead - 1) * ops);
     // LDS-only barrier (no vmcnt drain): every wave's DMAs of this step landed; the stage refilled below
     // was last read in the previous step
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (si + 2 < nst) issue(s0 + si + 2, (int)((si + 2) % NSTAGE));
-    const char* base = smem + (int)(si % NSTAGE) * (GCO + GCI) * PANEL;
+    if (si + ahead < nst) issue(s0 + si + ahead, nxt);
+    nxt = nxt + 1 == g.nstage ? 0 : nxt + 1;
+    const char* base = smem + cur * g.pstage * PANEL;
+    cur = cur + 1 == g.nstage ? 0 : cur + 1;
 #pragma unroll
     for (int k = 0; k < TPW; ++k) {
       const int t = wave + 4 * k;
@@ -193,6 +194,9 @@ W1Geom w1_plan(const stgcn_wgrad_desc& a) {
   g.ncib = a.Cin / 32;
   g.ncog = (g.ncob + GCO - 1) / GCO;
   g.ncig = (g.ncib + GCI - 1) / GCI;
+  g.pstage = (g.ncob < GCO ? g.ncob : GCO) + (g.ncib < GCI ? g.ncib : GCI);
+  g.nstage = (64 * 1024) / (g.pstage * PANEL);
+  g.nstage = g.nstage < NSTAGE ? NSTAGE : (g.nstage > 6 ? 6 : g.nstage);
   const int groups = g.ncog * g.ncig;
   long nch = TARGET_BLOCKS / groups;
   if (nch < 1) nch = 1;
@@ -216,7 +220,9 @@ int wgrad1x1_launch(const stgcn_wgrad_desc& a, int dtype, hipStream_t s) {
   const W1Geom g = w1_plan(a);
   if (a.work_bytes < (long)g.nchunk * a.Cout * a.Cin * (long)sizeof(float)) return -1;
   float* slab = reinterpret_cast<float*>(a.work);
-  const size_t lds = (size_t)NSTAGE * (GCO + GCI) * PANEL;
+  // LDS of the actual group (the 14-panel maximum took 84 KB: one block per CU at the A-first graph conv's
+  // 64 x 192 groups, whose 8 panels need 48 KB — three blocks, three times the DMAs in flight)
+  const size_t lds = (size_t)g.nstage * g.pstage * PANEL;
   if (stgcn_lds_attr((const void*)wgrad1x1_kernel, (int)lds, s)) return STGCN_EHIP;
   hipLaunchKernelGGL(wgrad1x1_kernel, dim3((unsigned)g.nchunk, (unsigned)(g.ncog * g.ncig)), dim3(NT1), lds, s, a, g,
                      slab);

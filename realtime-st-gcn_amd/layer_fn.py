@@ -980,11 +980,11 @@ class AttnProjFunction(torch.autograd.Function):
         else:
             D = torch.cat([dth, dph], 1).contiguous(memory_format=torch.channels_last)
         D = D.float()
-        D16 = D.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        # the bf16 GEMM operand and the bias gradients (column sums of the fp32 values) from one read of D
+        D16, db = K.cast_colsum(D, N * T * V, Nout)
         wT, cq, kq = K.pack_weight(W.t().reshape(1, Cin, Nout), torch.bfloat16)
         dx = K.conv_rows(D16, wT, Nout, Cin, cq, kq, T, T, trans=True)
         dW = K.conv_wgrad(x, D16, Cin, Nout, T, T).view(Nout, Cin)
-        db = K.bn_bwd_reduce(D, N * T * V, Nout)[:, 0]
         wts, wps, wdt = ctx.shapes
         return (dx, dW[:Nt].reshape(wts).to(wdt), db[:Nt].to(wdt), dW[Nt:].reshape(wps).to(wdt),
                 db[Nt:].to(wdt))

@@ -120,12 +120,14 @@ def test_conv_prologue_bn_relu_and_stats(K, dtype):
     assert_close(mr[:, 1].cpu(), 1 / torch.sqrt(var + 1e-5), stol, "bn rstd")
 
 
-@pytest.mark.parametrize("C", [16, 64, 256, 4])
+@pytest.mark.parametrize("C,N,T", [(16, 2, 7), (64, 2, 7), (256, 2, 7), (4, 2, 7), (64, 6, 131), (16, 5, 97)])
 @pytest.mark.parametrize("per_sample", [False, True])
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 2e-2)])
-def test_amix(K, per_sample, dtype, tol, C):
+def test_amix(K, per_sample, dtype, tol, C, N, T):
+    """A-mix forward / transposed / dA (jmix.hip, gcn_amix.hip) vs einsum; the larger cases give every wave
+    of the jmix grid dozens of items across sample boundaries (its counted DMA/store waits)."""
     torch.manual_seed(3)
-    N, T, V, P = 2, 7, 25, 3
+    V, P = 25, 3
     x = torch.randn(N, C, T, V)
     A = torch.randn((N, P, V, V) if per_sample else (P, V, V))
     xa = torch.einsum("nctv,npvw->npctw", x, A) if per_sample else torch.einsum("nctv,pvw->npctw", x, A)
@@ -142,6 +144,20 @@ def test_amix(K, per_sample, dtype, tol, C):
     if not per_sample:
         ref_dA = ref_dA.sum(0)
     assert_close(dA.cpu(), ref_dA, tol, "amix dA")
+
+
+@pytest.mark.parametrize("N,C,T,V", [(2, 96, 7, 25), (3, 48, 41, 25), (1, 4, 5, 3)])
+def test_cast_colsum(K, N, C, T, V):
+    """stgcn_cast_colsum: the bf16 copy of fp32 rows and their fp32 column sums (attention projections' backward,
+    aagcn.py:139-141 autograd), against torch; run twice, bit-identical sums (fixed order)."""
+    torch.manual_seed(11)
+    x = torch.randn(N, C, T, V) * 3 + 1
+    xd = x.to(DEV).contiguous(memory_format=torch.channels_last)
+    out, cs = K.cast_colsum(xd, N * T * V, C)
+    _, cs2 = K.cast_colsum(xd, N * T * V, C)
+    assert torch.equal(out.cpu(), x.to(torch.bfloat16))
+    assert_close(cs.cpu(), x.sum(dim=(0, 2, 3)), 1e-5, "column sums")
+    assert torch.equal(cs, cs2)
 
 
 def test_bn_kernels(K):
