@@ -41,7 +41,12 @@ __global__ __launch_bounds__(NT, 2) void conv1x1_kernel(const stgcn_conv_desc a,
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int lr = lane & 31, lh = lane >> 5;
-  const int ct = blockIdx.x % g.ncol, rt = blockIdx.x / g.ncol;
+  // the column tiles of one row tile are consecutive rounds on ONE XCD (block ids are dealt round-robin over the
+  // 8 XCDs): the staged input rows come from HBM once and from that XCD's L2 for the other column tiles
+  // (with the row tile's ncol blocks spread over ncol XCDs the input was fetched ncol times)
+  const int L = blockIdx.x, k = L >> 3;
+  const int ct = k % g.ncol, rt = (k / g.ncol) * 8 + (L & 7);
+  if (rt >= g.nrow) return;  // block-uniform, before any barrier
   const long m0 = (long)rt * BM;
   const int n0 = ct * BN;
   const int V = a.V, S = a.stride;
@@ -315,7 +320,8 @@ int launch1(const stgcn_conv_desc& a, const XGeom& g, hipStream_t s) {
   if (lout > lds) lds = lout;
   constexpr bool RB = ROWB;
   if (stgcn_lds_attr((const void*)conv1x1_kernel<KS, BN, RB>, 160 * 1024, s)) return STGCN_EHIP;
-  hipLaunchKernelGGL((conv1x1_kernel<KS, BN, RB>), dim3((unsigned)((long)g.nrow * g.ncol)), dim3(NT), lds, s, a, g);
+  const long rounds = ((long)g.nrow + 7) / 8;  // row tiles in whole rounds of the 8 XCDs (kernel mapping)
+  hipLaunchKernelGGL((conv1x1_kernel<KS, BN, RB>), dim3((unsigned)(rounds * 8 * g.ncol)), dim3(NT), lds, s, a, g);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
 
@@ -355,7 +361,7 @@ int conv1x1_launch(const stgcn_conv_desc& a, int dtype, hipStream_t s) {
   const int BN = a.Cout % 128 == 0 && !rowb ? 128 : 64;
   g.ncol = a.Cout / BN;
   const long nrow = (g.M + BM - 1) / BM;
-  if (nrow * g.ncol > 0x7fffffffL) return -1;
+  if ((nrow + 7) / 8 * 8 * g.ncol > 0x7fffffffL) return -1;
   g.nrow = (int)nrow;
   g.k16n = a.Cin_pad / 16;
   if (a.stats && nrow > conv_rows_num_row_blocks(g.M, a.Cout)) return -1;

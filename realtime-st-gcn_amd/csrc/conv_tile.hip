@@ -444,16 +444,29 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stg
     for (int i = 0; i < TM; ++i) {
       const int lb = (wm * TM + i) * 32 + 4 * lh;
       T* pb = out + (row0 + lb) * ld + col;
+      // per-row bias (bias_mode 2 / 3): joint and sample of the lane's first row once (two 64-bit divisions
+      // per element had cost more than the tile's MFMAs); rows lb + ro advance by < 2V
+      int vb = 0, tb = 0;
+      long nb = 0;
+      if (a.bias_mode >= 2) {
+        const long mb = row0 + lb, ntb = mb / V;
+        vb = (int)(mb - ntb * V);
+        nb = a.bias_mode == 3 ? ntb / a.T_out : 0;
+        tb = (int)(ntb - nb * a.T_out);
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int ro = (r & 3) + 8 * (r >> 2);
         const bool ok = cok && lb + ro < rows_valid;
         float v = acc[i][j][r] + b1;
         if (a.bias_mode >= 2 && ok) {
-          const long m = row0 + lb + ro;
-          const long nt = m / V;
-          long bi = m - nt * V;
-          if (a.bias_mode == 3) bi += (nt / a.T_out) * V;
+          int vv = vb + ro, dt = 0;
+          while (vv >= V) {
+            vv -= V;
+            ++dt;
+          }
+          long bi = vv;
+          if (a.bias_mode == 3) bi += (nb + (tb + dt) / a.T_out) * V;
           v += a.bias[bi * a.Cout + col];
         }
         if (ok) {

@@ -15,14 +15,22 @@
 //         alone would add 2^-9 relative error per coefficient);
 //   fp32: 32x32x2 fp32 MFMAs (exact fp32 products), one LDS read per fragment.
 // Work item = (frame, 32-channel output block); a wave walks a contiguous run of items (the coefficients
-// are reloaded only when the sample changes), double-buffered: the next item's panels are in flight while
-// the current one is mixed.  Output: lane = output joint, 4 consecutive channels per store.
+// are reloaded only when the sample changes), through a ring of 2-5 item slots: the next items' panels (and,
+// accumulating, the old output block, DMA'd like an input panel) are in flight while the current one is mixed,
+// and the counted vmcnt wait before an item never waits for the stores of the last slots' items (vmcnt
+// completes in order: waiting behind a store's write latency per item had serialised the waves).
+// Output: lane = output joint, 4 consecutive channels per store.
 #include "common.h"
 #include <type_traits>
 
 namespace {
 
 constexpr int NWJ = 4;             // waves per block
+// item slots per wave: 2..5, as many as keep a block's ring within 80 KB of LDS (two blocks per CU)
+constexpr int jmix_nbuf(int panel, int ns) {
+  const int n = (80 * 1024) / (NWJ * ns * panel);
+  return n < 2 ? 2 : (n > 5 ? 5 : n);
+}
 constexpr int PMAXJ = 3;
 constexpr int ITEMS_PER_WAVE = 16;  // target work items per wave (sizes the grid)
 
@@ -94,7 +102,7 @@ struct JmixArgs {
   int cin;      // input channels per row (mode 0: C, else P*C)
 };
 
-template <typename T, int NP>
+template <typename T, int NP, bool ACC>
 __global__ __launch_bounds__(NWJ * 64) void jmix_kernel(const JmixArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int PANEL = JT<T>::PANEL, KS = JT<T>::KS;
@@ -103,10 +111,11 @@ __global__ __launch_bounds__(NWJ * 64) void jmix_kernel(const JmixArgs a) {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lr = lane & 31, lh = lane >> 5;
   const int V = a.V;
-  constexpr int NBUF = NP == 1 ? 5 : 3;  // panel slots per wave: the current item and the ones in flight
-  char* const buf = smem + wave * NBUF * NP * PANEL;  // [NBUF][NP] panels
+  constexpr int NS = NP + (ACC ? 1 : 0);  // panels per slot: the inputs, then (accumulating) the old output block
+  constexpr int NBUF = jmix_nbuf(PANEL, NS);  // item slots per wave: the current item and the ones in flight
+  char* const buf = smem + wave * NBUF * NS * PANEL;  // [NBUF][NS] panels
   // rows V..31 stay zero (the DMA never writes them)
-  for (int e = lane; e < NBUF * NP * PANEL / 16; e += 64) reinterpret_cast<uint4*>(buf)[e] = make_uint4(0, 0, 0, 0);
+  for (int e = lane; e < NBUF * NS * PANEL / 16; e += 64) reinterpret_cast<uint4*>(buf)[e] = make_uint4(0, 0, 0, 0);
   __builtin_amdgcn_s_waitcnt(0);
 
   const long gw = (long)blockIdx.x * NWJ + wave;
@@ -123,15 +132,14 @@ __global__ __launch_bounds__(NWJ * 64) void jmix_kernel(const JmixArgs a) {
   };
   const int lrow = lane / UPR, lunit = lane % UPR;
   constexpr int RPI = 64 / UPR;  // panel rows per DMA instruction
-  // Every lane issues every DMA instruction (a fixed count per item, DMA_OPS, for the counted waits below):
+  // Every lane issues every DMA instruction (a fixed count per item, DOPS, for the counted waits below):
   // lanes past the frame's V rows or past a partial last channel block (mode 2) copy the frame's first
   // unit instead — finite data, multiplied by zero coefficients (rows >= V) or masked (channels).
-  constexpr int DMA_OPS = NP * (32 / RPI);
   auto issue_io = [&](long i, int ob, int slot) {
     const T* src0 = in + i * V * (long)a.in_ld;
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
-      const unsigned pan = lds_u32(buf + (slot * NP + k) * PANEL);
+      const unsigned pan = lds_u32(buf + (slot * NS + k) * PANEL);
       const int cb = panel_col(ob, k);
       const bool uok = cb + lunit * (16 / ELT) < a.cin;
 #pragma unroll
@@ -141,12 +149,18 @@ __global__ __launch_bounds__(NWJ * 64) void jmix_kernel(const JmixArgs a) {
         dma16(ok ? src0 + (long)row * a.in_ld + cb + lunit * (16 / ELT) : src0, pan + rr * 32 * ELT);
       }
     }
+    if constexpr (ACC) {  // the old output block [V rows][32 channels], read back in the flush from LDS
+      const T* o0 = out + i * V * (long)a.out_ld + 32 * ob;
+      const unsigned pan = lds_u32(buf + (slot * NS + NP) * PANEL);
+      const bool uok = 32 * ob + lunit * (16 / ELT) < a.cout;
+#pragma unroll
+      for (int rr = 0; rr < 32; rr += RPI) {
+        const int row = rr + lrow;
+        const bool ok = row < V && uok;
+        dma16(ok ? o0 + (long)row * a.out_ld + lunit * (16 / ELT) : o0, pan + rr * 32 * ELT);
+      }
+    }
   };
-  auto issue = [&](long it, int slot) {
-    const long i = it / a.nob;
-    issue_io(i, (int)(it - i * a.nob), slot);
-  };
-
   // coefficients of one sample as B operands: B[k = in joint b][n = out joint a] = coef(a, b, p)
   //   mode 0: M[p][b][a]; mode 1: M[p][a][b]; mode 2: bt ? M[p][a][b] : M[p][b][a]
   const bool ab = a.mode == 1 || (a.mode == 2 && a.bt);
@@ -180,15 +194,11 @@ __global__ __launch_bounds__(NWJ * 64) void jmix_kernel(const JmixArgs a) {
     }
   };
 
-  // Pipeline per item j: [wait: panels(j), the accumulate loads(j-1) and the stores(j-2) are all a whole
-  // item old] [stores(j-1)] [DMA panels(j+1)] [accumulate loads(j)] [mix(j) -> registers].  Every global
-  // access of an item is thus covered by the next item's MFMAs instead of a wait right behind it.
   typedef std::conditional_t<sizeof(T) == 2, bf16x4, float4> OVec;
   const f32x16 zero = {};
-  f32x16 pend = zero;                     // the previous item's results
-  OVec pold[4];                           // its accumulate operands
+  f32x16 pend = zero;  // the item's results
   long pend_i = -1;
-  int pend_ob = 0;
+  int pend_ob = 0, pend_slot = 0;
   auto out_ptr = [&](long i, int ob, int q4) {
     return out + (i * V + lr) * (long)a.out_ld + 32 * ob + 8 * q4 + 4 * lh;
   };
@@ -199,19 +209,22 @@ __global__ __launch_bounds__(NWJ * 64) void jmix_kernel(const JmixArgs a) {
     for (int q4 = 0; q4 < 4; ++q4) {
       if (!ch_ok(pend_ob, q4)) continue;
       float v[4] = {pend[4 * q4], pend[4 * q4 + 1], pend[4 * q4 + 2], pend[4 * q4 + 3]};
-      if constexpr (sizeof(T) == 2) {
-        if (a.accumulate) {
+      if constexpr (ACC) {  // old output: row lr, channels 8*q4 + 4*lh .. +3 of the slot's output panel
+        const OVec o = *reinterpret_cast<const OVec*>(buf + (pend_slot * NS + NP) * PANEL + lr * 32 * ELT +
+                                                      (8 * q4 + 4 * lh) * ELT);
+        if constexpr (sizeof(T) == 2) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += (float)pold[q4][e];
+          for (int e = 0; e < 4; ++e) v[e] += (float)o[e];
+        } else {
+          v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
         }
+      }
+      if constexpr (sizeof(T) == 2) {
         bf16x4 r;
 #pragma unroll
         for (int e = 0; e < 4; ++e) r[e] = (bf16)v[e];
         *reinterpret_cast<bf16x4*>(out_ptr(pend_i, pend_ob, q4)) = r;
       } else {
-        if (a.accumulate) {
-          v[0] += pold[q4].x; v[1] += pold[q4].y; v[2] += pold[q4].z; v[3] += pold[q4].w;
-        }
         *reinterpret_cast<float4*>(out_ptr(pend_i, pend_ob, q4)) = make_float4(v[0], v[1], v[2], v[3]);
       }
     }
@@ -225,14 +238,14 @@ __global__ __launch_bounds__(NWJ * 64) void jmix_kernel(const JmixArgs a) {
     for (int q4 = 0; q4 < 4; ++q4) n += 32 * ob + 8 * q4 < a.cout ? 1 : 0;
     return n;
   };
-  if (!a.accumulate) {
+  {
     // Order per item j: [wait: panels(j)] [mix(j)] [DMA(j+AH)] [stores(j)], AH = NBUF - 1 items in flight.
     // vmcnt completes in order, so the wait before item j counts exactly the ops issued after DMA(j): the DMAs
     // of the next items already issued and the stores of the last AH items — a store is waited for only AH
     // items after it (waiting for the previous item's stores had serialised the items behind the write
     // latency).  Item -> (frame, block) and the sample advance by counters: no 64-bit division per item.
     constexpr int AH = NBUF - 1;
-    constexpr int DOPS = NP * (32 / RPI);
+    constexpr int DOPS = NS * (32 / RPI);
     long ci = it0 / a.nob;  // item j's frame and block
     int cob = (int)(it0 - ci * a.nob);
     long ii = ci;  // next item to issue
@@ -265,7 +278,7 @@ __global__ __launch_bounds__(NWJ * 64) void jmix_kernel(const JmixArgs a) {
     f32x16 acc = zero;
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
-      const char* pan = buf + (slot * NP + k) * PANEL;
+      const char* pan = buf + (slot * NS + k) * PANEL;
       // partitions feeding this (block, panel) and the channel rows each one owns (mode 2: groups of C)
       int p0, p1;
       if (a.mode == 0) p0 = p1 = (32 * ob) / a.C;
@@ -305,6 +318,7 @@ __global__ __launch_bounds__(NWJ * 64) void jmix_kernel(const JmixArgs a) {
     pend = acc;
     pend_i = i;
     pend_ob = ob;
+    pend_slot = slot;
       if (it + AH < it1) {
         issue_io(ii, iob, islot);
         adv(ii, iob);
@@ -326,85 +340,6 @@ __global__ __launch_bounds__(NWJ * 64) void jmix_kernel(const JmixArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     return;
   }
-  // Order per item j: [stores(j-1)] [accumulate loads(j)] [DMA(j+2)] [mix(j)] [wait].  The youngest ops at
-  // the wait are DMA(j+2)'s DMA_OPS; waiting until at most DMA_OPS are outstanding (in-order completion)
-  // retires DMA(j+1), the loads(j) and everything older, and leaves j+2's panels in flight.
-  issue(it0, 0);
-  if (it0 + 1 < it1) {
-    issue(it0 + 1, 1);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA_OPS) : "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  for (long it = it0; it < it1; ++it) {
-    const int slot = (int)((it - it0) % NBUF);
-    flush();
-    const long i = it / a.nob;
-    const int ob = (int)(it - i * a.nob);
-    if (a.accumulate) {
-#pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4)
-        if (ch_ok(ob, q4)) pold[q4] = *reinterpret_cast<const OVec*>(out_ptr(i, ob, q4));
-    }
-    if (it + 2 < it1) {
-      int s2 = slot + 2;
-      s2 = s2 >= NBUF ? s2 - NBUF : s2;
-      issue(it + 2, s2);  // two items ahead: their panels fly under this item's and the next one's MFMAs
-    }
-    const long n = i / a.T;
-    if (n != cur_n) {
-      load_coef(n);
-      cur_n = n;
-    }
-    f32x16 acc = zero;
-#pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      const char* pan = buf + (slot * NP + k) * PANEL;
-      // partitions feeding this (block, panel) and the channel rows each one owns (mode 2: groups of C)
-      int p0, p1;
-      if (a.mode == 0) p0 = p1 = (32 * ob) / a.C;
-      else if (a.mode == 1) p0 = p1 = k;
-      else {
-        p0 = (32 * ob) / a.C;
-        p1 = min(a.P - 1, (32 * ob + 31) / a.C);
-      }
-#pragma unroll
-      for (int p = 0; p < PMAXJ; ++p) {  // compile-time p: the coefficient registers are never indexed at run time
-        if (p < p0 || p > p1) continue;
-        bool mok = true;  // this lane's A row (channel m = lr) belongs to partition p
-        if (a.mode == 2) {
-          const int ch = 32 * ob + lr;
-          mok = ch >= p * a.C && ch < (p + 1) * a.C;
-        }
-        if constexpr (sizeof(T) == 2) {
-#pragma unroll
-          for (int ks = 0; ks < KS; ++ks) {
-            bf16x8 af = trfrag16(pan, 16 * ks, lane);
-            if (!mok) af = bf16x8{};
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bh[p][ks], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bl[p][ks], acc, 0, 0, 0);
-          }
-        } else {
-#pragma unroll
-          for (int ks = 0; ks < KS; ++ks) {
-            if (2 * ks >= V) break;
-            float av = *reinterpret_cast<const float*>(pan + ((2 * ks + lh) * 32 + lr) * 4);
-            av = mok ? av : 0.f;
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bh[p][ks], acc, 0, 0, 0);
-          }
-        }
-      }
-    }
-    // D: lane = output joint lr, acc[r] = channel 32*ob + 8*(r>>2) + 4*lh + (r&3); stored next item
-    pend = acc;
-    pend_i = i;
-    pend_ob = ob;
-    // next item's panels (DMA(j+1)) and this item's accumulate loads: all but the youngest DMA_OPS ops
-    if (it + 2 < it1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMA_OPS) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  flush();
 }
 
 }  // namespace
@@ -441,11 +376,17 @@ int jmix_launch(const void* in, int in_ld, void* out, int out_ld, const float* M
   a.ipw = (a.items + waves - 1) / waves;
   const long blocks = (a.items + a.ipw * NWJ - 1) / (a.ipw * NWJ);
   const int panel = dtype ? JT<bf16>::PANEL : JT<float>::PANEL;
-  const size_t lds = (size_t)NWJ * (a.npan == 1 ? 5 : 3) * a.npan * panel;  // NBUF slots per wave
-#define JM_LAUNCH(TT, NPV)                                                                                   \
+  const int ns = a.npan + (accumulate ? 1 : 0);
+  const size_t lds = (size_t)NWJ * jmix_nbuf(panel, ns) * ns * panel;
+#define JM_LAUNCH1(TT, NPV, AC)                                                                               \
   do {                                                                                                       \
-    if (stgcn_lds_attr((const void*)jmix_kernel<TT, NPV>, (int)lds, s)) return STGCN_EHIP;                    \
-    hipLaunchKernelGGL((jmix_kernel<TT, NPV>), dim3((unsigned)blocks), dim3(NWJ * 64), lds, s, a);            \
+    if (stgcn_lds_attr((const void*)jmix_kernel<TT, NPV, AC>, (int)lds, s)) return STGCN_EHIP;                \
+    hipLaunchKernelGGL((jmix_kernel<TT, NPV, AC>), dim3((unsigned)blocks), dim3(NWJ * 64), lds, s, a);        \
+  } while (0)
+#define JM_LAUNCH(TT, NPV)                   \
+  do {                                       \
+    if (accumulate) JM_LAUNCH1(TT, NPV, true); \
+    else JM_LAUNCH1(TT, NPV, false);         \
   } while (0)
   if (dtype) {
     if (a.npan == 1) JM_LAUNCH(bf16, 1);
@@ -457,5 +398,6 @@ int jmix_launch(const void* in, int in_ld, void* out, int out_ld, const float* M
     else JM_LAUNCH(float, 3);
   }
 #undef JM_LAUNCH
+#undef JM_LAUNCH1
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
