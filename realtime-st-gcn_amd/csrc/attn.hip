@@ -30,55 +30,45 @@ __global__ __launch_bounds__(256) void attn_scores_kernel(const T* __restrict__ 
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
   const long K = (long)(t1 - t0) * ce;
-  // k = (t - t0)*ce + c ; each wave takes k-steps of 16 round-robin, UNR of them per iteration with all their
-  // loads issued before the first MFMA (one load round trip per UNR steps instead of per step)
-  constexpr int UNR = 4;
-  for (long kb = (long)wave * 16; kb < K; kb += 64 * UNR) {
-    float fx[UNR][8], fy[UNR][8];
+  // k = (t - t0)*ce + c ; each wave takes k-steps of 16 round-robin
+  for (long k0 = (long)wave * 16; k0 < K; k0 += 64) {
+    typename Tr<T>::frag fa, fb;
+    float fx[8], fy[8];
+    if (vec && r < V) {
+      const long k = k0 + 8 * h;
+      const int t = t0 + (int)(k / ce), c = (int)(k % ce);
+      if (k < K) {
+        const long base = ((long)n * T_ + t) * V;
+        const T* pa = th + (base + r) * ld + p * ce + c;
+        const T* pb = ph + (base + r) * ld + p * ce + c;
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const long k0 = kb + 64L * u;
-      if (vec && r < V) {
-        const long k = k0 + 8 * h;
-        if (k < K) {
-          const int t = t0 + (int)(k / ce), c = (int)(k % ce);
-          const long base = ((long)n * T_ + t) * V;
-          const T* pa = th + (base + r) * ld + p * ce + c;
-          const T* pb = ph + (base + r) * ld + p * ce + c;
-#pragma unroll
-          for (int q = 0; q < 8; q += VEC) {
-            unpack16(*reinterpret_cast<const uint4*>(pa + q), fx[u] + q, (T*)nullptr);
-            unpack16(*reinterpret_cast<const uint4*>(pb + q), fy[u] + q, (T*)nullptr);
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) fx[u][j] = fy[u][j] = 0.f;
+        for (int u = 0; u < 8; u += VEC) {
+          unpack16(*reinterpret_cast<const uint4*>(pa + u), fx + u, (T*)nullptr);
+          unpack16(*reinterpret_cast<const uint4*>(pb + u), fy + u, (T*)nullptr);
         }
       } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const long k = k0 + 8 * h + j;
-          fx[u][j] = fy[u][j] = 0.f;
-          if (r < V && k < K) {
-            const int t = t0 + (int)(k / ce), c = (int)(k % ce);
-            const long row = ((long)n * T_ + t) * V + r;
-            fx[u][j] = Tr<T>::to_f(th[row * ld + p * ce + c]);
-            fy[u][j] = Tr<T>::to_f(ph[row * ld + p * ce + c]);
-          }
+        for (int j = 0; j < 8; ++j) fx[j] = fy[j] = 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const long k = k0 + 8 * h + j;
+        fx[j] = fy[j] = 0.f;
+        if (r < V && k < K) {
+          const int t = t0 + (int)(k / ce), c = (int)(k % ce);
+          const long row = ((long)n * T_ + t) * V + r;
+          fx[j] = Tr<T>::to_f(th[row * ld + p * ce + c]);
+          fy[j] = Tr<T>::to_f(ph[row * ld + p * ce + c]);
         }
       }
     }
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      if (kb + 64L * u >= K) break;  // wave-uniform
-      typename Tr<T>::frag fa, fb;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        fa[j] = Tr<T>::from_f(fx[u][j]);
-        fb[j] = Tr<T>::from_f(fy[u][j]);
-      }
-      Tr<T>::mma(acc, fa, fb);  // rows v (theta), cols w (phi)
+    for (int j = 0; j < 8; ++j) {
+      fa[j] = Tr<T>::from_f(fx[j]);
+      fb[j] = Tr<T>::from_f(fy[j]);
     }
+    Tr<T>::mma(acc, fa, fb);  // rows v (theta), cols w (phi)
   }
 #pragma unroll
   for (int i = 0; i < 16; ++i) red[wave][acc_row(i, lane) * VMAX + r] = acc[i];
@@ -220,25 +210,18 @@ int attn_bwd_launch(const void* th, const void* ph, int ld, int N, int T_, int V
 // must not be rounded to bf16 (aagcn.py:142-145), but they need no fp32 MFMA either.
 // D^T = W x^T on 32x32x16 MFMAs: A = W rows (m = output channel) from LDS (hi/lo staged once per block for
 // its group of <= 128 output channels), B = x rows (n = row) straight from global as 16-B fragments held
-// in registers for all channel tiles, the next row tile's loaded while this one is multiplied and stored;
-// D lane = row, 4 consecutive channels per float4 store.
+// in registers for all channel tiles; D lane = row, 4 consecutive channels per float4 store.
 namespace {
 constexpr int PJ_CG = 128;  // output channels per block group
 template <int KSN>
 __global__ __launch_bounds__(256) void attn_proj_kernel(const bf16* __restrict__ x, int ldx, long M, int Cin,
                                                         const float* __restrict__ W, const float* __restrict__ bias,
-                                                        int Nout, float* __restrict__ out, int ldo, int rt_per_block,
-                                                        int groups) {
+                                                        int Nout, float* __restrict__ out, int ldo, int rt_per_block) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int RS = Cin * 2 + 16;  // padded LDS row bytes
   char* const sHi = smem;
   char* const sLo = smem + PJ_CG * RS;
-  // (row chunk, channel group) from the linear id so that the groups of one row chunk are consecutive rounds on
-  // ONE XCD (ids are dealt round-robin over the 8 XCDs): x is fetched from HBM once and read from that L2 by
-  // the other groups (speed only)
-  const int L = blockIdx.x, xcd = L & 7, k = L >> 3;
-  const int g = k % groups;
-  const long rchunk = (long)(k / groups) * 8 + xcd;
+  const int g = blockIdx.y;
   const int o0 = g * PJ_CG, og = min(PJ_CG, Nout - o0);
   for (int e = threadIdx.x; e < PJ_CG * Cin; e += 256) {  // stage W_hi / W_lo (rows >= og: zeros)
     const int o = e / Cin, c = e - o * Cin;
@@ -251,23 +234,16 @@ __global__ __launch_bounds__(256) void attn_proj_kernel(const bf16* __restrict__
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, lr = lane & 31, lh = lane >> 5;
   const int ntile = (og + 31) / 32;
   const long rt_total = (M + 31) / 32;
-  const long rt0 = rchunk * rt_per_block, rt1 = min(rt_total, rt0 + rt_per_block);
-  auto load = [&](long rt, bf16x8* xf) {
+  const long rt0 = (long)blockIdx.x * rt_per_block, rt1 = min(rt_total, rt0 + rt_per_block);
+  for (long rt = rt0 + wave; rt < rt1; rt += 4) {
     const long row = rt * 32 + lr;
-    const bool rok = rt < rt1 && row < M;
+    const bool rok = row < M;
+    bf16x8 xf[KSN];
 #pragma unroll
     for (int ks = 0; ks < KSN; ++ks) {
       const uint4 u = rok ? *reinterpret_cast<const uint4*>(x + row * ldx + 16 * ks + 8 * lh) : make_uint4(0, 0, 0, 0);
       xf[ks] = __builtin_bit_cast(bf16x8, u);
     }
-  };
-  bf16x8 xf[KSN], xn[KSN];
-  long rt = rt0 + wave;
-  if (rt < rt1) load(rt, xf);
-  for (; rt < rt1; rt += 4) {
-    load(rt + 4, xn);  // the next tile's rows in flight under this tile's MFMAs and stores
-    const long row = rt * 32 + lr;
-    const bool rok = row < M;
     for (int ct = 0; ct < ntile; ++ct) {
       f32x16 acc = {};
       const char* ah = sHi + (ct * 32 + lr) * RS + lh * 16;
@@ -293,8 +269,6 @@ __global__ __launch_bounds__(256) void attn_proj_kernel(const bf16* __restrict__
         }
       }
     }
-#pragma unroll
-    for (int ks = 0; ks < KSN; ++ks) xf[ks] = xn[ks];
   }
 }
 }  // namespace
@@ -308,20 +282,19 @@ int attn_proj_launch(const void* x, int ldx, long M, int Cin, const float* W, co
   const long rt_total = (M + 31) / 32;
   const int groups = (Nout + PJ_CG - 1) / PJ_CG;
   const int ncu = stgcn_cu_count(s);
-  long chunks = (long)(ncu > 0 ? ncu : 256) * 4 / groups;
-  if (chunks < 1) chunks = 1;
-  long rpb = (rt_total + chunks - 1) / chunks;
+  long blocks = (long)(ncu > 0 ? ncu : 256) * 4 / groups;
+  if (blocks < 1) blocks = 1;
+  long rpb = (rt_total + blocks - 1) / blocks;
   if (rpb < 4) rpb = 4;
-  chunks = (rt_total + rpb - 1) / rpb;
-  chunks = (chunks + 7) / 8 * 8;  // whole rounds of the 8 XCDs (chunks past the rows exit at once)
+  blocks = (rt_total + rpb - 1) / rpb;
   const size_t lds = (size_t)2 * PJ_CG * (Cin * 2 + 16);
-  const dim3 grid((unsigned)(chunks * groups));
+  const dim3 grid((unsigned)blocks, (unsigned)groups);
   switch (KSN) {
 #define PJ_CASE(K)                                                                                            \
   case K:                                                                                                     \
     if (stgcn_lds_attr((const void*)attn_proj_kernel<K>, (int)lds, s)) return STGCN_EHIP;                      \
     hipLaunchKernelGGL(attn_proj_kernel<K>, grid, dim3(256), lds, s, (const bf16*)x, ldx, M, Cin, W, bias, Nout, \
-                       out, ldo, (int)rpb, groups);                                                           \
+                       out, ldo, (int)rpb);                                                                   \
     break;
     PJ_CASE(1) PJ_CASE(2) PJ_CASE(3) PJ_CASE(4) PJ_CASE(5) PJ_CASE(6) PJ_CASE(7) PJ_CASE(8)
     PJ_CASE(9) PJ_CASE(10) PJ_CASE(11) PJ_CASE(12) PJ_CASE(13) PJ_CASE(14) PJ_CASE(15) PJ_CASE(16)

@@ -265,7 +265,7 @@ __global__ __launch_bounds__(256) void amix_dA_vec_kernel(const AmixArgs a, cons
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
         const int ci = k0 + 16 * kc;
-        const bool ok = rok && ci < a.Cin;
+        const bool ok = rok && ci + 8 * h < a.Cin;  // this lane's 8 channels (Cin % 8 == 0: all or none)
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
           ux[kc][u] = ok ? *reinterpret_cast<const uint4*>(px + ci + u * VEC) : make_uint4(0, 0, 0, 0);

@@ -397,13 +397,19 @@ __global__ __launch_bounds__(256) void cast_colsum_kernel(const float* __restric
   float s[4] = {0.f, 0.f, 0.f, 0.f};
   if (rs < rpi) {
     const long mb = (long)blockIdx.x * rpb, me = min(M, mb + rpb);
-    for (long m0 = mb + rs; m0 < me; m0 += 4L * rpi) {
-      float4 v[4];
+    // four rows per thread per iteration; the next iteration's loads are issued before this one's stores
+    // (vmcnt completes in order: loads issued after a store wait for its write to finish)
+    auto ld4 = [&](long m0, float4* v) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const long m = m0 + (long)u * rpi;
         v[u] = m < me ? *reinterpret_cast<const float4*>(x + m * ldx + cu * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
+    };
+    float4 v[4], nv[4];
+    ld4(mb + rs, v);
+    for (long m0 = mb + rs; m0 < me; m0 += 4L * rpi) {
+      ld4(m0 + 4L * rpi, nv);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const long m = m0 + (long)u * rpi;
@@ -413,6 +419,8 @@ __global__ __launch_bounds__(256) void cast_colsum_kernel(const float* __restric
         r[0] = (bf16)v[u].x; r[1] = (bf16)v[u].y; r[2] = (bf16)v[u].z; r[3] = (bf16)v[u].w;
         *reinterpret_cast<bf16x4*>(out + m * ldo + cu * 4) = r;
       }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = nv[u];
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) red[rs * C + cu * 4 + j] = s[j];
@@ -645,7 +653,7 @@ int rowgroup_sum_launch(const void* x, int ld, long M, int C, int G, long period
 }
 
 static long cast_colsum_rpb(long M) {
-  long rpb = (M + 1023) / 1024;
+  long rpb = (M + 2047) / 2048;  // ~2048 blocks
   return rpb < 64 ? 64 : rpb;
 }
 long cast_colsum_workspace(long M, int C) {

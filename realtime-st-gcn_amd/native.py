@@ -981,7 +981,7 @@ def rowgroup_sum(x, M, C, G, per_sample=False, out=None):
 
 def cast_colsum(x, M, C):
     """(bf16 channels-last copy of the fp32 rows x, fp32 column sums [C]) from one pass (stgcn_cast_colsum)."""
-    out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device).contiguous(memory_format=torch.channels_last)
+    out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
     cs = torch.empty(C, dtype=torch.float32, device=x.device)
     work = torch.empty(max(L.lib().stgcn_cast_colsum_workspace(M, C), 1), dtype=torch.float32, device=x.device)
     L.check(L.lib().stgcn_cast_colsum(x.data_ptr(), rows_ld(x), M, C, out.data_ptr(), rows_ld(out), cs.data_ptr(),

@@ -120,7 +120,8 @@ def test_conv_prologue_bn_relu_and_stats(K, dtype):
     assert_close(mr[:, 1].cpu(), 1 / torch.sqrt(var + 1e-5), stol, "bn rstd")
 
 
-@pytest.mark.parametrize("C,N,T", [(16, 2, 7), (64, 2, 7), (256, 2, 7), (4, 2, 7), (64, 6, 131), (16, 5, 97)])
+@pytest.mark.parametrize("C,N,T", [(16, 2, 7), (64, 2, 7), (256, 2, 7), (4, 2, 7), (24, 3, 11), (8, 2, 9), (64, 6, 131),
+                                   (16, 5, 97)])
 @pytest.mark.parametrize("per_sample", [False, True])
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 2e-2)])
 def test_amix(K, per_sample, dtype, tol, C, N, T):
