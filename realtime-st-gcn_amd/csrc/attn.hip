@@ -223,12 +223,18 @@ __global__ __launch_bounds__(256) void attn_proj_kernel(const bf16* __restrict__
   char* const sLo = smem + PJ_CG * RS;
   const int g = blockIdx.y;
   const int o0 = g * PJ_CG, og = min(PJ_CG, Nout - o0);
-  for (int e = threadIdx.x; e < PJ_CG * Cin; e += 256) {  // stage W_hi / W_lo (rows >= og: zeros)
-    const int o = e / Cin, c = e - o * Cin;
-    const float w = o < og ? W[(long)(o0 + o) * Cin + c] : 0.f;
-    const bf16 h = (bf16)w;
-    *reinterpret_cast<bf16*>(sHi + o * RS + c * 2) = h;
-    *reinterpret_cast<bf16*>(sLo + o * RS + c * 2) = (bf16)(w - (float)h);
+  for (int e = threadIdx.x; e < PJ_CG * Cin / 4; e += 256) {  // stage W_hi / W_lo, 4 weights per thread (rows >= og: 0)
+    const int o = (4 * e) / Cin, c = 4 * e - o * Cin;
+    const float4 w = o < og ? *reinterpret_cast<const float4*>(W + (long)(o0 + o) * Cin + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float wv[4] = {w.x, w.y, w.z, w.w};
+    bf16x4 h, l;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      h[j] = (bf16)wv[j];
+      l[j] = (bf16)(wv[j] - (float)h[j]);
+    }
+    *reinterpret_cast<bf16x4*>(sHi + o * RS + c * 2) = h;
+    *reinterpret_cast<bf16x4*>(sLo + o * RS + c * 2) = l;
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, lr = lane & 31, lh = lane >> 5;
@@ -276,13 +282,16 @@ __global__ __launch_bounds__(256) void attn_proj_kernel(const bf16* __restrict__
 int attn_proj_launch(const void* x, int ldx, long M, int Cin, const float* W, const float* bias, int Nout, float* out,
                      int ldo, hipStream_t s) {
   if (!x || !W || !out || M < 1 || Nout < 1 || Nout % 4 || ldo < Nout || ldo % 4 || Cin % 16 || Cin < 16 ||
-      Cin > 256 || ldx < Cin || ldx % 8)
+      Cin > 256 || ldx < Cin || ldx % 8 || ((size_t)W & 15))
     return STGCN_EBADSHAPE;
   const int KSN = Cin / 16;
   const long rt_total = (M + 31) / 32;
   const int groups = (Nout + PJ_CG - 1) / PJ_CG;
   const int ncu = stgcn_cu_count(s);
-  long blocks = (long)(ncu > 0 ? ncu : 256) * 4 / groups;
+  // one round of resident blocks (each stages its group's W_hi / W_lo, up to 132 KB: more blocks only repeat that)
+  const size_t lds0 = (size_t)2 * PJ_CG * (Cin * 2 + 16);
+  const long bpc = lds0 > 80 * 1024 ? 1 : (lds0 > 53 * 1024 ? 2 : 4);
+  long blocks = (long)(ncu > 0 ? ncu : 256) * bpc / groups;
   if (blocks < 1) blocks = 1;
   long rpb = (rt_total + blocks - 1) / blocks;
   if (rpb < 4) rpb = 4;
