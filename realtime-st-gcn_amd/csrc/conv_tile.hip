@@ -337,6 +337,33 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stg
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // per-row bias (bias_mode 2 / 3: the graph-conv bias through A, per joint / per sample and joint) as the
+  // accumulators' initial value: its loads complete under the K loop instead of stalling the epilogue (+55 us
+  // per launch at K = 384 / 768 when added there)
+  if (!PAR && a.bias_mode >= 2) {
+    // the tile's bias row of every local row, once per block (one division per row, not per element)
+    int* const sRb = reinterpret_cast<int*>(sPro + (a.pro == 1 ? 2 * a.Cin_pad : 0));  // [BM]
+    for (int t = tid; t < BM; t += NT) {
+      const long m = row0 + (t < rows_valid ? t : 0), fr = m / V;
+      const int v = (int)(m - fr * V);
+      sRb[t] = a.bias_mode == 2 ? v : (int)((fr / a.T_out) * V + v);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + (wn * TN + j) * 32 + lr;
+      if (col >= a.Cout) continue;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int lb = (wm * TM + i) * 32 + 4 * lh;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ro = (r & 3) + 8 * (r >> 2);
+          if (lb + ro < rows_valid) acc[i][j][r] = a.bias[(long)sRb[lb + ro] * a.Cout + col];
+        }
+      }
+    }
+  }
 
   const int tap_stride = V * L::RS;
   constexpr int NSTEP = KT * KS;  // k-steps of 16 per chunk
@@ -444,11 +471,11 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stg
     for (int i = 0; i < TM; ++i) {
       const int lb = (wm * TM + i) * 32 + 4 * lh;
       T* pb = out + (row0 + lb) * ld + col;
-      // per-row bias (bias_mode 2 / 3): joint and sample of the lane's first row once (two 64-bit divisions
-      // per element had cost more than the tile's MFMAs); rows lb + ro advance by < 2V
+      // per-row bias of the parity tiles (bias_mode 2 / 3; the other tiles start from it in the accumulators):
+      // joint and sample of the lane's first row once, rows lb + ro advance by < 2V
       int vb = 0, tb = 0;
       long nb = 0;
-      if (a.bias_mode >= 2) {
+      if (PAR && a.bias_mode >= 2) {
         const long mb = row0 + lb, ntb = mb / V;
         vb = (int)(mb - ntb * V);
         nb = a.bias_mode == 3 ? ntb / a.T_out : 0;
@@ -459,7 +486,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stg
         const int ro = (r & 3) + 8 * (r >> 2);
         const bool ok = cok && lb + ro < rows_valid;
         float v = acc[i][j][r] + b1;
-        if (a.bias_mode >= 2 && ok) {
+        if (PAR && a.bias_mode >= 2 && ok) {
           int vv = vb + ro, dt = 0;
           while (vv >= V) {
             vv -= V;
@@ -576,7 +603,8 @@ int launch_tile(const stgcn_conv_desc& a, long max_row_blocks, hipStream_t s) {
   const size_t red = a.stats ? (size_t)WM * BN * 16 : 0;
   // two B stages: a 3-stage pipeline (prefetch distance 2) measured no gain on the config-2 shapes (the
   // chunk barriers, not load latency, bound this kernel) and was removed
-  size_t lds = 2 * ((size_t)A_BYTES + B_BYTES) + pro_bytes;
+  const size_t rb_bytes = a.bias_mode >= 2 ? (size_t)BM * sizeof(int) : 0;  // per-row bias indices
+  size_t lds = 2 * ((size_t)A_BYTES + B_BYTES) + pro_bytes + rb_bytes;
   if (red > lds) lds = red;
   if (lds > 160 * 1024) return -1;
   if (stgcn_lds_attr((const void*)conv_tile_kernel<T, WM, WN, TM, TN, KC, KT, S, MINW, false, 2>, 160 * 1024, s) ||
