@@ -17,8 +17,10 @@ namespace {
 
 constexpr int NT1 = 256;
 constexpr int PANEL = 32 * 64;  // [32 rows][32 ch] bf16
-constexpr int GCO = 2, GCI = 12;  // co / ci blocks per group
-constexpr int TPW = GCO * GCI / 4;  // tiles per wave (<= 6)
+// co / ci blocks per group: GCO x gci with gci = all ci blocks up to 8, else 6 (a group of 14 panels took 84 KB
+// of LDS at its 3-stage minimum: one block per CU; 8 panels make a 4-stage ring in 64 KB, two blocks per CU)
+constexpr int GCO = 2, GCI_MAX = 8;
+constexpr int TPW = GCO * GCI_MAX / 4;  // tiles per wave (<= 4)
 constexpr int NSTAGE = 3;  // minimum ring depth
 constexpr int TARGET_BLOCKS = 512;
 
@@ -69,7 +71,8 @@ struct W1Geom {
   int nchunk;
   int ncog, ncig;  // groups along co / ci
   int ncob, ncib;  // 32-channel blocks
-  int pstage;      // panels per ring stage: the largest group's (LDS sized to it, not to GCO + GCI)
+  int gci;         // ci blocks per group
+  int pstage;      // panels per ring stage: the largest group's (LDS sized to it)
   int nstage;      // ring depth (3..6: ~64 KB of LDS per block)
 };
 
@@ -78,8 +81,8 @@ __global__ __launch_bounds__(NT1) void wgrad1x1_kernel(const stgcn_wgrad_desc a,
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int chunk = blockIdx.x, grp = blockIdx.y;
   const int gco = grp / g.ncig, gci = grp - gco * g.ncig;
-  const int cob0 = gco * GCO, cib0 = gci * GCI;
-  const int nco = min(GCO, g.ncob - cob0), nci = min(GCI, g.ncib - cib0);
+  const int cob0 = gco * GCO, cib0 = gci * g.gci;
+  const int nco = min(GCO, g.ncob - cob0), nci = min(g.gci, g.ncib - cib0);
   const int npan = nco + nci;  // panels per step: the dy blocks first, then the x blocks
   const long s0 = (long)chunk * g.spb, s1 = min(g.steps, s0 + g.spb);
   if (s0 >= s1) return;  // block-uniform, before any barrier
@@ -192,9 +195,10 @@ W1Geom w1_plan(const stgcn_wgrad_desc& a) {
   g.steps = (long)a.N * a.T_out * a.V / 32;
   g.ncob = a.Cout / 32;
   g.ncib = a.Cin / 32;
+  g.gci = g.ncib <= GCI_MAX ? g.ncib : 6;
   g.ncog = (g.ncob + GCO - 1) / GCO;
-  g.ncig = (g.ncib + GCI - 1) / GCI;
-  g.pstage = (g.ncob < GCO ? g.ncob : GCO) + (g.ncib < GCI ? g.ncib : GCI);
+  g.ncig = (g.ncib + g.gci - 1) / g.gci;
+  g.pstage = (g.ncob < GCO ? g.ncob : GCO) + g.gci;
   g.nstage = (64 * 1024) / (g.pstage * PANEL);
   g.nstage = g.nstage < NSTAGE ? NSTAGE : (g.nstage > 6 ? 6 : g.nstage);
   const int groups = g.ncog * g.ncig;
