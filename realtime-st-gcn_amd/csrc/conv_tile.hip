@@ -235,11 +235,13 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void conv_tile_kernel(const stg
   // BatchNorm prologue (pro 1) scale/shift for all input channels staged once in LDS
   const bool pro_lds = a.pro == 1 && fast_ld;
   float* const sPro = reinterpret_cast<float*>(Bbase + NBS * B_BYTES);  // [2][Cin_pad]
-  if (pro_lds)
+  if (pro_lds) {
     for (int i = tid; i < a.Cin_pad; i += NT) {
       sPro[i] = i < a.Cin ? a.pro_a[i] : 0.f;
       sPro[a.Cin_pad + i] = i < a.Cin ? a.pro_b[i] : 0.f;
     }
+    __syncthreads();  // the first halo store reads the table from every wave (block-uniform condition)
+  }
   uint4 ra[2][A_MAX];
   float sc[VEC], sh[VEC];  // pro 1 without pro_lds (ragged channels)
 

@@ -104,6 +104,10 @@ __global__ __launch_bounds__(256, LN ? 1 : 2) void wgrad_tile_kernel(const stgcn
     sScSh[tid] = c < a.Cin ? a.pro_a[c] : 0.f;
     sScSh[32 * NB + tid] = c < a.Cin ? a.pro_b[c] : 0.f;
   }
+  // the first tile's halo store below reads the table from every wave: without this barrier the waves past
+  // the writers read whatever the CU's previous workgroup left in that LDS (intermittent garbage gradients,
+  // seen when two processes share the GPU: config-4 DDP test)
+  __syncthreads();
 
   // tile-invariant part of each halo unit: frame offset from the tile's first halo frame (fo, -1 = unused unit)
   // and joint (v < 32), packed as fo * 32 + v (registers: two staged sets are live in the tile loop)
