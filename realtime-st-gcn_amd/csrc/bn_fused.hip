@@ -185,20 +185,28 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(const stgcn_bn_
       msh[j] = MASK == 2 ? a.msh[c0 + j] : 0.f;
     }
     const long mb = (long)blockIdx.x * g.rpb, me = min(a.M, mb + g.rpb);
-    for (long m0 = mb + rs; m0 < me; m0 += (long)g.RPI * UNR) {
-      uint4 Udz[UNR], Umr[UNR], Uxa[UNR], Uxb[UNR], Upa[UNR];
-      bool ok[UNR];
+    // the next iteration's loads are issued before this iteration's stores (vmcnt completes in order: loads
+    // issued after the stores would wait for their writes)
+    uint4 Udz[UNR], Umr[UNR], Uxa[UNR], Uxb[UNR], Upa[UNR];
+    uint4 Ndz[UNR], Nmr[UNR], Nxa[UNR], Nxb[UNR], Npa[UNR];
+    bool ok[UNR], nok[UNR];
+    auto load = [&](long m0, uint4* Ldz, uint4* Lmr, uint4* Lxa, uint4* Lxb, uint4* Lpa, bool* lok) {
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
         const long m = m0 + (long)u * g.RPI;
-        ok[u] = m < me;
-        const long mm = ok[u] ? m : mb;
-        Udz[u] = *reinterpret_cast<const uint4*>(dy + mm * a.lddy + c0);
-        Umr[u] = *reinterpret_cast<const uint4*>(mref + mm * a.ldm + c0);
-        if (!same_x) Uxa[u] = *reinterpret_cast<const uint4*>(x1 + mm * a.ldx1 + c0);
-        if (O2 == 1) Uxb[u] = *reinterpret_cast<const uint4*>(x2 + mm * a.ldx2 + c0);
-        if (O2 && a.acc2) Upa[u] = *reinterpret_cast<const uint4*>(o2 + mm * a.ldo2 + c0);
+        lok[u] = m < me;
+        const long mm = lok[u] ? m : mb;
+        Ldz[u] = *reinterpret_cast<const uint4*>(dy + mm * a.lddy + c0);
+        Lmr[u] = *reinterpret_cast<const uint4*>(mref + mm * a.ldm + c0);
+        if (!same_x) Lxa[u] = *reinterpret_cast<const uint4*>(x1 + mm * a.ldx1 + c0);
+        if (O2 == 1) Lxb[u] = *reinterpret_cast<const uint4*>(x2 + mm * a.ldx2 + c0);
+        if (O2 && a.acc2) Lpa[u] = *reinterpret_cast<const uint4*>(o2 + mm * a.ldo2 + c0);
       }
+    };
+    if (mb + rs < me) load(mb + rs, Udz, Umr, Uxa, Uxb, Upa, ok);
+    for (long m0 = mb + rs; m0 < me; m0 += (long)g.RPI * UNR) {
+      const bool more = m0 + (long)g.RPI * UNR < me;
+      if (more) load(m0 + (long)g.RPI * UNR, Ndz, Nmr, Nxa, Nxb, Npa, nok);
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
         if (!ok[u]) continue;
@@ -230,6 +238,17 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(const stgcn_bn_
             q1[j] += r1[j];
             q2[j] += r2[j];
           }
+        }
+      }
+      if (more) {
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          Udz[u] = Ndz[u];
+          Umr[u] = Nmr[u];
+          Uxa[u] = Nxa[u];
+          Uxb[u] = Nxb[u];
+          Upa[u] = Npa[u];
+          ok[u] = nok[u];
         }
       }
     }

@@ -12,6 +12,7 @@
 //  Backward: dz = dy * relu-mask; BN: dx = g*rstd*(dz - E[dz] - xhat*E[dz*xhat]);
 //    LN: dx = rstd*(gz - mean(gz) - xhat*sum(gz*xhat)/(F-1)), gz = dz*gamma.
 #include "common.h"
+#include <type_traits>
 
 namespace {
 
@@ -168,35 +169,60 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ u, 
   }
   const long mb = blockIdx.x * rpb, me = min(M, mb + rpb);
   // AU rows per thread and iteration, all loads issued before any use (a one-row loop kept two 16-B loads in
-  // flight per thread: 4.5 TB/s at config 2)
+  // flight per thread: 4.5 TB/s at config 2); the next iteration's loads (raw 16-B units) are issued before this
+  // iteration's stores — vmcnt completes in order, so loads issued after the stores would wait for their writes
   constexpr int AU = VEC == 1 ? 1 : 4;
-  for (long m0 = mb + rs; m0 < me; m0 += (long)RPI * AU) {
-    float f[AU][VEC], g[AU][VEC];
+  typedef typename std::conditional<VEC == 1, T, uint4>::type Raw;
+  auto ld_raw = [&](const T* p) -> Raw {
+    if constexpr (VEC == 1) return *p;
+    else return *reinterpret_cast<const uint4*>(p);
+  };
+  auto unraw = [&](const Raw& v, float* f) {
+    if constexpr (VEC == 1) f[0] = Tr<T>::to_f(v);
+    else unpack16(v, f, (T*)nullptr);
+  };
+  Raw fu[AU], gu[AU], fn[AU], gn[AU];
+  auto load = [&](long m0, Raw* fr, Raw* gr) {
 #pragma unroll
     for (int k = 0; k < AU; ++k) {
       const long m = min(m0 + (long)k * RPI, me - 1);  // rows past the block's end re-read its last row
-      ldv<T, VEC>(u + m * ldu + c0, f[k]);
-      if (res_mode) ldv<T, VEC>(r + m * ldr + c0, g[k]);
+      fr[k] = ld_raw(u + m * ldu + c0);
+      if (res_mode) gr[k] = ld_raw(r + m * ldr + c0);
     }
+  };
+  if (mb + rs < me) load(mb + rs, fu, gu);
+  for (long m0 = mb + rs; m0 < me; m0 += (long)RPI * AU) {
+    const bool more = m0 + (long)RPI * AU < me;
+    if (more) load(m0 + (long)RPI * AU, fn, gn);
 #pragma unroll
     for (int k = 0; k < AU; ++k) {
       const long m = m0 + (long)k * RPI;
       if (m >= me) break;
+      float f[VEC], g[VEC];
+      unraw(fu[k], f);
+      if (res_mode) unraw(gu[k], g);
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) f[k][j] = f[k][j] * a[j] + b[j];
+      for (int j = 0; j < VEC; ++j) f[j] = f[j] * a[j] + b[j];
       if (relu & 2) {  // inner ReLU on the normalised branch (RT-ST-GCN bn_relu, rtstgcn.py:319-321)
 #pragma unroll
-        for (int j = 0; j < VEC; ++j) f[k][j] = fmaxf(f[k][j], 0.f);
+        for (int j = 0; j < VEC; ++j) f[j] = fmaxf(f[j], 0.f);
       }
       if (res_mode) {
 #pragma unroll
-        for (int j = 0; j < VEC; ++j) f[k][j] += g[k][j] * ra[j] + rb[j];
+        for (int j = 0; j < VEC; ++j) f[j] += g[j] * ra[j] + rb[j];
       }
       if (relu & 1) {
 #pragma unroll
-        for (int j = 0; j < VEC; ++j) f[k][j] = fmaxf(f[k][j], 0.f);
+        for (int j = 0; j < VEC; ++j) f[j] = fmaxf(f[j], 0.f);
       }
-      stv<T, VEC>(y + m * ldy + c0, f[k]);
+      stv<T, VEC>(y + m * ldy + c0, f);
+    }
+    if (more) {
+#pragma unroll
+      for (int k = 0; k < AU; ++k) {
+        fu[k] = fn[k];
+        gu[k] = gn[k];
+      }
     }
   }
 }
