@@ -134,35 +134,23 @@ __global__ __launch_bounds__(256) void ln_apply_kernel(const LnApplyArgs a) {
   const T* u = reinterpret_cast<const T*>(a.u);
   const T* r = reinterpret_cast<const T*>(a.r);
   const long ou = (long)v * a.ldu + c0, orr = (long)v * a.ldr + c0;
-  // two frames per iteration; the next iteration's loads are issued before this iteration's stores (vmcnt
-  // completes in order: loads issued after the stores would wait for their writes)
-  float u0[VEC], u1[VEC], r0[VEC], r1[VEC], nu0[VEC], nu1[VEC], nr0[VEC], nr1[VEC];
-  auto load2 = [&](long f, float* x0, float* x1, float* y0, float* y1) {
-    if (f < a.F) {
-      ldu<T, VEC>(u + f * a.V * (long)a.ldu + ou, x0);
-      if (a.res_mode) ldu<T, VEC>(r + f * a.V * (long)a.ldr + orr, y0);
-    }
-    if (f + fstep < a.F) {
-      ldu<T, VEC>(u + (f + fstep) * a.V * (long)a.ldu + ou, x1);
-      if (a.res_mode) ldu<T, VEC>(r + (f + fstep) * a.V * (long)a.ldr + orr, y1);
-    }
-  };
   long f = i0 / U;
-  load2(f, u0, u1, r0, r1);
-  for (; f < a.F; f += 2 * fstep) {
-    const bool more = f + 2 * fstep < a.F;
-    if (more) load2(f + 2 * fstep, nu0, nu1, nr0, nr1);
-    apply_unit<T, VEC>(a, f, v, c0, ga, ba, rga, rba, u0, r0);
-    if (f + fstep < a.F) apply_unit<T, VEC>(a, f + fstep, v, c0, ga, ba, rga, rba, u1, r1);
-    if (more) {
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) {
-        u0[j] = nu0[j];
-        u1[j] = nu1[j];
-        r0[j] = nr0[j];
-        r1[j] = nr1[j];
-      }
+  for (; f + fstep < a.F; f += 2 * fstep) {  // two frames' loads in flight
+    float u0[VEC], u1[VEC], r0[VEC], r1[VEC];
+    ldu<T, VEC>(u + f * a.V * (long)a.ldu + ou, u0);
+    ldu<T, VEC>(u + (f + fstep) * a.V * (long)a.ldu + ou, u1);
+    if (a.res_mode) {
+      ldu<T, VEC>(r + f * a.V * (long)a.ldr + orr, r0);
+      ldu<T, VEC>(r + (f + fstep) * a.V * (long)a.ldr + orr, r1);
     }
+    apply_unit<T, VEC>(a, f, v, c0, ga, ba, rga, rba, u0, r0);
+    apply_unit<T, VEC>(a, f + fstep, v, c0, ga, ba, rga, rba, u1, r1);
+  }
+  if (f < a.F) {
+    float u0[VEC], r0[VEC];
+    ldu<T, VEC>(u + f * a.V * (long)a.ldu + ou, u0);
+    if (a.res_mode) ldu<T, VEC>(r + f * a.V * (long)a.ldr + orr, r0);
+    apply_unit<T, VEC>(a, f, v, c0, ga, ba, rga, rba, u0, r0);
   }
 }
 
