@@ -114,25 +114,40 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_fused_kernel(const stgcn_bn
 // The same values also go planar to ((float*)(out + C))[k*C + c], k < 3, so per-channel parameter
 // gradients are contiguous views (no gather copies on the host side).
 __global__ __launch_bounds__(256) void sum4_kernel(const float4* part, int nb, int C, float4* out) {
-  __shared__ double sx[256], sy[256], sz[256];
+  // the partials of a thread are loaded together, then a wave reduction and one LDS step (an 8-level LDS
+  // tree with a barrier per level was most of this ~5 us launch, 27 of them per config-2 step)
+  __shared__ double sred[3][4];
   const int c = xcd_channel(blockIdx.x, C);
   double x = 0, y = 0, z = 0;
-  for (int i = threadIdx.x; i < nb; i += 256) {
-    const float4 v = part[(long)i * C + c];
-    x += v.x; y += v.y; z += v.z;
-  }
-  sx[threadIdx.x] = x; sy[threadIdx.x] = y; sz[threadIdx.x] = z;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) {
-      sx[threadIdx.x] += sx[threadIdx.x + s];
-      sy[threadIdx.x] += sy[threadIdx.x + s];
-      sz[threadIdx.x] += sz[threadIdx.x + s];
+  for (int i0 = 0; i0 < nb; i0 += 256 * 4) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + threadIdx.x + 256 * u;
+      v[u] = i < nb ? part[(long)i * C + c] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      x += v[u].x; y += v[u].y; z += v[u].z;
+    }
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    x += __shfl_xor(x, o);
+    y += __shfl_xor(y, o);
+    z += __shfl_xor(z, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    sred[0][threadIdx.x >> 6] = x;
+    sred[1][threadIdx.x >> 6] = y;
+    sred[2][threadIdx.x >> 6] = z;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
-    const float4 r = make_float4((float)sx[0], (float)sy[0], (float)sz[0], 0.f);
+    const double sx0 = ((sred[0][0] + sred[0][1]) + sred[0][2]) + sred[0][3];
+    const double sy0 = ((sred[1][0] + sred[1][1]) + sred[1][2]) + sred[1][3];
+    const double sz0 = ((sred[2][0] + sred[2][1]) + sred[2][2]) + sred[2][3];
+    const float4 r = make_float4((float)sx0, (float)sy0, (float)sz0, 0.f);
     out[c] = r;
     float* pl = reinterpret_cast<float*>(out + C);
     pl[c] = r.x;

@@ -79,7 +79,8 @@ DEV void pack_s2frag_elem(const float* __restrict__ src, long s0, long s1, long 
 // C = 256 launch).  Slots j >= deg[a] are never read by gconv and are skipped; padding rows / columns are
 // written as zeros (they meet zero-filled operands).
 constexpr int GW_PMAX = 4;
-constexpr int GW_JMAX = 8;  // neighbour slots per joint whose loads are issued together
+constexpr int GW_JMAX = 1;  // neighbour slots per joint whose loads are issued together (8 and 4 held 138 / 98
+                            // VGPRs: 3 / 4 waves per SIMD for the batched prep launch, 93 / 61 us vs 51 us at 1)
 // M (optional, the layer's edge importance [P][V][V]): coefficients are A * M, the same fp32 product the
 // model forms for the layer (stgcn.py:89), so a model can prepare every layer before that product exists.
 // Column sums of A * M for the bias through A, colsum[p * V + a] = sum_v (A * M)[p][v][a] (summed in v order),
@@ -119,7 +120,8 @@ DEV void gconv_weights_elem(const float* __restrict__ A, const float* __restrict
                             const float* colsum, long idx) {
   const int C8 = C_pad / 8;
   // forward: c (ci) fastest across lanes, so W rows are read as float4 runs; trans: r (ci) fastest, so
-  // the 8 scalar reads of W[co][r] per thread are coalesced across lanes
+  // the 8 scalar reads of W[co][r] per thread are coalesced across lanes (c fastest for trans too, for
+  // contiguous stores, measured 1.6x slower: its W reads are 8 rows per lane)
   int c0, r, a;
   if (!trans) {
     c0 = (int)(idx % C8) * 8;

@@ -9,19 +9,33 @@
 
 namespace {
 
+constexpr int PREP_LDS_STARTS = 512;  // job starts searched in LDS (larger tables: the search reads global memory)
+
 __global__ __launch_bounds__(256) void prep_kernel(const stgcn_prep_job* __restrict__ jobs,
                                                    const long* __restrict__ start, int njobs) {
+  // Every block pays this prologue before its job's own loads: the starts are fetched by one load per thread
+  // into LDS and searched there (a binary search over global memory was ~6 dependent load latencies per
+  // block, with ~8 k blocks in the config-2 step's launch), and the job index is made wave-uniform so the
+  // job's fields come through scalar loads.
   const long b = blockIdx.x;
+  __shared__ long sst[PREP_LDS_STARTS];
+  const bool lds = njobs <= PREP_LDS_STARTS;
+  if (lds) {
+    for (int t = threadIdx.x; t < njobs; t += blockDim.x) sst[t] = start[t];
+    __syncthreads();
+  }
   int lo = 0, hi = njobs - 1;  // last job with start[j] <= b
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    if (start[mid] <= b) lo = mid;
+    if ((lds ? sst[mid] : start[mid]) <= b) lo = mid;
     else hi = mid - 1;
   }
+  lo = __builtin_amdgcn_readfirstlane(lo);
   const stgcn_prep_job& j = jobs[lo];
+  const long j0 = lds ? sst[lo] : start[lo];
   __shared__ float colsum[GW_COLSUM_MAX];
   if ((j.kind == 2 && j.bias2d) || j.kind == 3) gconv_colsum_block(j.A, j.M, j.P, j.V, colsum);  // block-uniform
-  const long i = (b - start[lo]) * 256 + threadIdx.x;
+  const long i = (b - j0) * 256 + threadIdx.x;
   if (i >= j.threads) return;
   if (j.kind == 0) {
     if (j.dtype == 1)

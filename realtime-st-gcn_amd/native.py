@@ -496,11 +496,11 @@ def gconv_weights(A, W, sup, Cout, Cin, trans, dtype, bias=None, plan=None, M=No
     out = torch.empty((V, sup.J, rp, cpad), dtype=dtype, device=A.device)
     if plan is not None:
         nbr, deg = (sup.rnbr, sup.rdeg) if trans else (sup.nbr, sup.deg)
-        b2 = torch.empty((V, Cout), dtype=torch.float32, device=A.device) if bias is not None else None
         plan.add(kind=2, dtype=L.dtype_code(dtype), src=W, dst=out, Co=Cout, Ci=Cin, trans=int(trans), A=A,
-                 M=None if M is None else _dense(M), nbr=nbr, deg=deg, P=P, V=V, J=sup.J, R_pad=rp, C_pad=cpad,
-                 bconv=bias, bias2d=b2)
-        return (out, b2) if bias is not None else out
+                 M=None if M is None else _dense(M), nbr=nbr, deg=deg, P=P, V=V, J=sup.J, R_pad=rp, C_pad=cpad)
+        # the bias through A as its own job (kind 3, the same per-output sum): a kind-2 job carrying it had every
+        # one of its blocks compute the column sums of A * M before its first weight load
+        return (out, gcn_bias_plan(A, bias, Cout, plan, M)) if bias is not None else out
     if bias is not None:
         assert not trans
         b2 = torch.empty((V, Cout), dtype=torch.float32, device=A.device)

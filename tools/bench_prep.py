@@ -30,7 +30,7 @@ if __name__ == "__main__":
     m = P.MODELS["st-gcn"](rank=None, **dict(bench.ARCH, graph=P.PKU_MMD)).to(dev).set_compute_dtype("bf16")
     plan = m._prepared()
     print("whole plan: %d jobs, %d blocks, %.1f us" % (plan.njobs, plan.nblocks, timed(plan.run)))
-    kinds = {0: "pack", 1: "s2frag", 2: "gconv"}
+    kinds = {0: "pack", 1: "s2frag", 2: "gconv", 3: "gbias"}
     for i, j in enumerate(plan._jobs):
         sub = K.PrepPlan(dev)
         sub._jobs = [j]
@@ -38,3 +38,13 @@ if __name__ == "__main__":
         sub.finalize()
         print("job %2d %-6s trans %d Co %4d Ci %4d Kt %d threads %8d: %.1f us" %
               (i, kinds[j.kind], j.trans, j.Co, j.Ci, j.Kt, j.threads, timed(sub.run)))
+    # every job of one kind (and direction) in one launch: which group bounds the batched launch
+    groups = {}
+    for j in plan._jobs:
+        groups.setdefault((kinds[j.kind], j.trans), []).append(j)
+    for (kn, tr), js in groups.items():
+        sub = K.PrepPlan(dev)
+        sub._jobs = js
+        sub._keep = plan._keep
+        sub.finalize()
+        print("group %-6s trans %d: %2d jobs %5d blocks %.1f us" % (kn, tr, len(js), sub.nblocks, timed(sub.run)))
