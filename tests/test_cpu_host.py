@@ -178,7 +178,8 @@ def test_prep_plan_builds_and_validates(pkg):
     # 64 or 128 input channels (0-6)
     framed = sum(p.gf is not None for p in layers)
     assert framed == (7 if pkg.routing.ROUTING.gcn_frame else 0)
-    assert plan.njobs == 9 * 4 + framed + 2 * 2 + 2 * 2 + 2 * 2
+    # per layer: effective weights both ways, the bias through A (kind 3), temporal packs both ways
+    assert plan.njobs == 9 * 5 + framed + 2 * 2 + 2 * 2 + 2 * 2
     assert plan.nblocks > 0
     # frag images where the kernels expect them
     assert layers[0].wt[0].frag_stride == 1 and layers[3].wt[0].frag_stride == 2 and layers[3].wtT[0].frag_stride == 2
