@@ -97,10 +97,22 @@ __global__ __launch_bounds__(1024) void seg_loss_kernel(LossArgs a) {
   // D: every block sums the label weights itself (L loads; no cross-block dependency)
   float den = a.den ? *a.den : 0.f;
   if (!a.den) {
+    // eight labels, then their eight weights, requested together per batch (same per-thread order as one
+    // window at a time, which was a chain of ~19 dependent label -> weight loads ahead of everything: the
+    // 36 us of this launch in the config-2 step)
     float d = 0.f;
-    for (int w = a.first + threadIdx.x; w < a.L; w += blockDim.x) {
-      const long y = a.labels[w - a.first];
-      d += (y >= 0 && y < C) ? a.wt[y] : 0.f;  // out-of-range labels are ignored (weight 0)
+    for (int w0 = a.first + threadIdx.x; w0 < a.L; w0 += 8 * blockDim.x) {
+      long y[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int w = w0 + u * blockDim.x;
+        y[u] = w < a.L ? a.labels[w - a.first] : -1;
+      }
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = (y[u] >= 0 && y[u] < C) ? a.wt[y[u]] : 0.f;  // out-of-range: weight 0
+#pragma unroll
+      for (int u = 0; u < 8; ++u) d += v[u];
     }
     d = wave_sum(d);
     if (lane == 0) red[wave][0] = d;
@@ -224,13 +236,15 @@ __global__ __launch_bounds__(1024) void seg_loss_kernel(LossArgs a) {
 }
 
 // multi-block: fixed-order sum of the block partials
-__global__ void seg_loss_finish_kernel(const float* __restrict__ partial, int nblk, float* out) {
-  const int i = threadIdx.x;
-  if (i < kPartials) {
-    float t = 0.f;
-    for (int b = 0; b < nblk; ++b) t += partial[b * kPartials + i];
-    out[i] = t;
-  }
+__global__ __launch_bounds__(64) void seg_loss_finish_kernel(const float* __restrict__ partial, int nblk, float* out) {
+  // lane = (block group g, partial k): eight independent strided sums per partial, then two shuffle steps
+  // (one lane walking every block's partial was a chain of nblk dependent load-adds)
+  const int k = threadIdx.x & (kPartials - 1), g = threadIdx.x / kPartials;
+  float t = 0.f;
+  for (int b = g; b < nblk; b += 64 / kPartials) t += partial[b * kPartials + k];
+#pragma unroll
+  for (int o = kPartials; o < 64; o <<= 1) t += __shfl_xor(t, o);
+  if (threadIdx.x < kPartials) out[k] = t;
 }
 
 // d loss / d p = g_ce * dce + g_mse * dmse, the upstream scalars read on the device (no host sync)
@@ -243,8 +257,11 @@ __global__ __launch_bounds__(256) void seg_loss_bwd_kernel(const float* __restri
 }
 
 int seg_loss_blocks(int L) {
-  int nb = (L + 255) / 256;  // >= 16 windows per wave before a second block pays
-  return nb < 1 ? 1 : (nb > 64 ? 64 : nb);
+  // a window per wave: the per-window work is a chain of ~30 dependent wave reductions (softmax, 5 argmax
+  // rounds, MSE), so one 16-wave block walking the config-2 step's 64 windows 4 per wave took 36 us on one
+  // CU; up to 256 blocks
+  int nb = (L + kWaves - 1) / kWaves;
+  return nb < 1 ? 1 : (nb > 256 ? 256 : nb);
 }
 
 }  // namespace
