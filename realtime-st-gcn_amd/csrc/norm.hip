@@ -92,20 +92,21 @@ __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const T* __restri
 }
 
 // one block per channel: merge nb (count, mean, M2) partials in fp64
-__global__ __launch_bounds__(256) void bn_finalize_kernel(const float4* part, int nb, int ldp, int C,
+__global__ __launch_bounds__(1024) void bn_finalize_kernel(const float4* part, int nb, int ldp, int C,
                                                           const float* gamma, const float* beta, float eps,
                                                           float2* mean_rstd, float* scale, float* shift) {
   // fp64 power sums (n, sum n*mean, sum M2 + n*mean^2) instead of pairwise Chan merges: adds only (no
   // division chain), a wave reduction and one LDS step; at fp64 the final var = S2/n - mean^2 loses
   // ~1e-16 * mean^2/var, far below the fp32 result
-  __shared__ double sred[3][4];
+  __shared__ double sred[3][16];
+  const int nt = blockDim.x;  // 256, or 1024 for long partial lists (the C = 64 layers' conv-epilogue partials)
   const int c = xcd_channel(blockIdx.x, C);
   double n = 0, s1 = 0, s2 = 0;
-  for (int b0 = 0; b0 < nb; b0 += 256 * 8) {
+  for (int b0 = 0; b0 < nb; b0 += nt * 8) {
     float4 gv[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int b = b0 + threadIdx.x + 256 * u;
+      const int b = b0 + threadIdx.x + nt * u;
       gv[u] = b < nb ? part[(long)b * ldp + c] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
@@ -129,9 +130,12 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float4* part, in
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const double tn = ((sred[0][0] + sred[0][1]) + sred[0][2]) + sred[0][3];
-    const double t1 = ((sred[1][0] + sred[1][1]) + sred[1][2]) + sred[1][3];
-    const double t2 = ((sred[2][0] + sred[2][1]) + sred[2][2]) + sred[2][3];
+    double tn = 0, t1 = 0, t2 = 0;
+    for (int w = 0; w < nt / 64; ++w) {
+      tn += sred[0][w];
+      t1 += sred[1][w];
+      t2 += sred[2][w];
+    }
     const double m = tn > 0 ? t1 / tn : 0.0;
     double var = tn > 0 ? t2 / tn - m * m : 0.0;  // biased (BatchNorm)
     if (var < 0) var = 0;
@@ -601,7 +605,8 @@ int bn_stats_partial_launch(const void* x, int ld, long M, int C, float4* part, 
 
 int bn_finalize_launch(const float4* part, int nb, int ldp, int C, const float* gamma, const float* beta, float eps,
                        float2* mean_rstd, float* scale, float* shift, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, s, part, nb, ldp, C, gamma, beta, eps, mean_rstd,
+  const int nt = nb > 2048 ? 1024 : 256;  // one 8-load batch per thread where the list allows
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(nt), 0, s, part, nb, ldp, C, gamma, beta, eps, mean_rstd,
                      scale, shift);
   RET_HIP;
 }
