@@ -12,7 +12,7 @@ N > 1: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) the ra
 (before anything touches the GPU) and exits with its status.  Each rank trains on its own trial's
 64-window subsegment (weak scaling; the subsegment's loss is self-contained, processor.py:377-392, so the
 data path has no collective); gradients are averaged over ranks by DistributedDataParallel (RCCL
-all-reduce in 16 MB buckets overlapped with backward) or, with --graph, by one all-reduce of the flat
+all-reduce in 4 MB buckets, ~4 for the 12.2 MB gradient, overlapped with backward) or, with --graph, by one all-reduce of the flat
 gradient between the two graphs — the reference's accumulation of ``loss / batch_size`` over trials.
 
 Config 4 (--config 4): the long-trial DDP workload of SURVEY 8(d): synthetic trials of U[4000, 8000]
@@ -358,7 +358,7 @@ def main():
     params = [p for p in model.parameters() if p.requires_grad]
     train_model = model
     if world > 1 and not args.graph:
-        train_model = par.ddp(model, dev, bucket_cap_mb=16)  # RCCL all-reduce overlapped with bwd
+        train_model = par.ddp(model, dev)  # RCCL all-reduce in 4 MB buckets, overlapped with bwd
     elif world > 1:  # identical replicas (DistributedDataParallel's broadcast from rank 0)
         for p in params:
             torch.distributed.broadcast(p.data, 0)

@@ -175,19 +175,6 @@ typedef struct {
 
 int stgcn_gcn_tile(const stgcn_gcn_tile_desc* d, int dtype, void* stream);
 long stgcn_gcn_tile_row_blocks(int NT, int V, int Cout);
-/* The same graph convolution in the reference's own order, the 1x1 conv first and the joint mix after, per frame
- * (bf16; gcn_frame.hip):
- *   trans_a 0: out[(i,w)][co] (+)= sum_p sum_v A[p][v][w] sum_ci W'[co][p*Cin+ci] in[(i,v)][ci]  (+ bias[w][co])
- *   trans_a 1: out[(i,v)][c]  (+)= sum_p sum_w A[p][v][w] sum_k  W'[c][p*Cin+k]   in[(i,w)][k]
- * W' as stgcn_gcn_tile's, given as U_p[c][k] = W'[c][p*Cin+k]: w_frag = the Kt = P MFMA-fragment image of U
- * (stgcn_pack_weight_frag with Kt = P, Co = Cout, Ci = Cin; rows padded to Cout_pad % 32 == 0, columns to Kw_pad):
- * forward U = the conv weight viewed (P, Cout, Cin), data grad its (P, Cin, Cout) transpose.
- * Cin = 64 or 128 (the kernel's input channels), Cout % 64 == 0, 16 < V <= 32, P <= 3, row strides % 8 == 0.
- * Optional BN partial statistics [stgcn_gcn_frame_row_blocks(NT, Cout)][Cout_pad] float4 (count, mean, M2);
- * out = NULL: statistics only (no stores; pass 1 of the fused BatchNorm layer).
- * Replaces: conv1x1 + einsum of ConvTemporalGraphical.forward (tgcn.py:71-79) and its input grad. */
-int stgcn_gcn_frame(const stgcn_gcn_tile_desc* d, void* stream);
-long stgcn_gcn_frame_row_blocks(int NT, int Cout);
 long stgcn_gconv_row_blocks(int NT, int V);
 int stgcn_gconv_weights(const float* A, const float* W, const int* nbr, const int* deg, int P, int V, int J, int Cout,
                         int Cin, int trans, void* out, int rows_pad, int cols_pad, int dtype, void* stream);
@@ -230,34 +217,6 @@ int stgcn_gconv_wgrad_finish_bias(const float* dweff, const float* A, const floa
                                   float* dA, float* db, void* work, void* stream);
 int stgcn_gconv_wgrad_finish(const float* dweff, const float* A, const float* W, const int* nbr, const int* deg, int P,
                              int V, int J, int Cout, int Cin, float* dW, float* dA, void* work, void* stream);
-
-/* Graph-conv weight, adjacency and bias gradients in one pass over (x, dy) (bf16; gconv_wgrad_frame.hip),
- * frame by frame on MFMA (autograd of ConvTemporalGraphical.forward, tgcn.py:71-79, with a shared A):
- *   dW[p*Cout+co][ci] = sum_i sum_v (sum_w A[p][v][w] dy[(i,w)][co]) x[(i,v)][ci]
- *   dA[p][v][w]       = sum_i sum_co (sum_ci W[p*Cout+co][ci] x[(i,v)][ci] + bconv[p*Cout+co]) dy[(i,w)][co]
- *                       (dense: every (v, w), also off the graph's support)
- *   db[p*Cout+co]     = sum_i sum_w (sum_v A[p][v][w]) dy[(i,w)][co]
- * i over the NT = N*T frames, x / dy rows (i*V + v) with row strides x_ld / dy_ld.  A [P][V][V] fp32, W fp32
- * [P*Cout][Cin] (the Conv2d weight), bconv fp32 [P*Cout] or NULL.  Outputs fp32, OVERWRITTEN.
- * P <= 3, 16 < V <= 32, Cin and Cout multiples of 64, ld multiples of 8.  work: the workspace's bytes
- * (per-block partials, summed in a fixed order: deterministic).  Replaces stgcn_gconv_wgrad +
- * stgcn_gconv_wgrad_finish_bias (bf16).  Two launches. */
-typedef struct {
-  const void* x;
-  const void* dy;
-  const float* A;
-  const float* W;
-  const float* bconv;
-  float* dW;
-  float* dA;
-  float* db;
-  void* work;
-  long work_bytes;
-  int NT, V, P, Cin, Cout, x_ld, dy_ld;
-} stgcn_gconv_wgrad_frame_desc;
-
-long stgcn_gconv_wgrad_frame_workspace(const stgcn_gconv_wgrad_frame_desc* d);
-int stgcn_gconv_wgrad_frame(const stgcn_gconv_wgrad_frame_desc* d, void* stream);
 
 /* BatchNorm with batch statistics (nn.BatchNorm2d(track_running_stats=False), stgcn.py:152,160,171;
  * BatchNorm1d input norm, models/utils/batchnorm.py:13-23 viewed as [N*T][V*C]).

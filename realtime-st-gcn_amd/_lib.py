@@ -67,11 +67,6 @@ class GconvWgradDesc(ctypes.Structure):
                [("work", c_void_p), ("work_bytes", c_long), ("rowsum", c_void_p)]
 
 
-class GconvWgradFrameDesc(ctypes.Structure):
-    _fields_ = [(n, c_void_p) for n in ("x", "dy", "A", "W", "bconv", "dW", "dA", "db", "work")] + \
-               [("work_bytes", c_long)] + [(n, c_int) for n in ("NT", "V", "P", "Cin", "Cout", "x_ld", "dy_ld")]
-
-
 class LayerFusedDesc(ctypes.Structure):
     _fields_ = [(n, c_void_p) for n in ("x", "z", "wg_frag", "A", "gbias", "n1_scale", "n1_shift", "wt_frag", "tbias",
                                         "stats")] + [(n, c_int) for n in ("N", "T", "V", "P", "x_ld", "z_ld")] + \
@@ -116,8 +111,6 @@ _SIGS = {
     "stgcn_gconv_wgrad_finish_workspace": (ctypes.c_long, [c_int] * 5),
     "stgcn_gconv_wgrad_finish": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_void_p, c_void_p, c_void_p, c_void_p]),
     "stgcn_gconv_wgrad_finish_bias": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_void_p] * 7),
-    "stgcn_gconv_wgrad_frame_workspace": (c_long, [ctypes.POINTER(GconvWgradFrameDesc)]),
-    "stgcn_gconv_wgrad_frame": (c_int, [ctypes.POINTER(GconvWgradFrameDesc), c_void_p]),
     "stgcn_amix_fwd": (c_int, [ctypes.POINTER(AmixDesc), c_int, c_void_p]),
     "stgcn_amix_trans": (c_int, [ctypes.POINTER(AmixDesc), c_int, c_void_p]),
     "stgcn_gcn_bias_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
@@ -125,10 +118,8 @@ _SIGS = {
                                   c_void_p, c_int, c_int, c_int, c_void_p]),
     "stgcn_gcn_tile": (c_int, [ctypes.POINTER(GcnTileDesc), c_int, c_void_p]),
     "stgcn_gcn_tile_row_blocks": (ctypes.c_long, [c_int, c_int, c_int]),
-    "stgcn_gcn_frame": (c_int, [ctypes.POINTER(GcnTileDesc), c_void_p]),
     "stgcn_tconv_frame": (c_int, [ctypes.POINTER(ConvDesc), c_void_p]),
     "stgcn_tconv_frame_row_blocks": (ctypes.c_long, [c_int, c_int]),
-    "stgcn_gcn_frame_row_blocks": (ctypes.c_long, [c_int, c_int]),
     "stgcn_pack_weight_s2frag": (c_int, [c_void_p, ctypes.c_long, ctypes.c_long, ctypes.c_long, c_int, c_int,
                                          c_void_p, c_int, c_int, c_void_p]),
     "stgcn_pack_weight_frag": (c_int, [c_void_p, ctypes.c_long, ctypes.c_long, ctypes.c_long, c_int, c_int, c_int,

@@ -47,12 +47,8 @@ int gconv_wgrad_finish_bias_launch(const float* dweff, const float* A, const flo
                                    int P, int V, int J, int Cout, int Cin, const float* bconv, const float* S, float* dW,
                                    float* dA, float* db, void* work, hipStream_t s);
 int amix_trans_launch(const AmixArgs& a, int dtype, hipStream_t s);
-long gconv_wgrad_frame_workspace(const stgcn_gconv_wgrad_frame_desc& a);
-int gcn_frame_launch(const stgcn_gcn_tile_desc& a, hipStream_t s);
 int tconv_frame_launch(const stgcn_conv_desc& a, hipStream_t s);
 long tconv_frame_row_blocks(int N, int T);
-long gcn_frame_row_blocks(int NT, int Cout);
-int gconv_wgrad_frame_launch(const stgcn_gconv_wgrad_frame_desc& a, hipStream_t s);
 int amix_dA_launch(const AmixArgs& a, const void* dw, float* dA, void* work, int dtype, hipStream_t s);
 long amix_dA_workspace(const AmixArgs& a);
 int gcn_bias_bwd_launch(const float* A, const float* b, const float* S, int P, int V, int C, float* dA, float* db,
@@ -284,18 +280,6 @@ int stgcn_tconv_frame(const stgcn_conv_desc* d, void* stream) {
   return tconv_frame_launch(*d, STREAM(stream));
 }
 long stgcn_tconv_frame_row_blocks(int N, int T) { return tconv_frame_row_blocks(N, T); }
-int stgcn_gcn_frame(const stgcn_gcn_tile_desc* d, void* stream) {
-  if (!d) return STGCN_EBADSHAPE;
-  return gcn_frame_launch(*d, STREAM(stream));
-}
-long stgcn_gcn_frame_row_blocks(int NT, int Cout) { return gcn_frame_row_blocks(NT, Cout); }
-long stgcn_gconv_wgrad_frame_workspace(const stgcn_gconv_wgrad_frame_desc* d) {
-  return d ? gconv_wgrad_frame_workspace(*d) : -1;
-}
-int stgcn_gconv_wgrad_frame(const stgcn_gconv_wgrad_frame_desc* d, void* stream) {
-  if (!d) return STGCN_EBADSHAPE;
-  return gconv_wgrad_frame_launch(*d, STREAM(stream));
-}
 
 int stgcn_amix_fwd(const stgcn_amix_desc* d, int dtype, void* stream) {
   CHECK_DTYPE(dtype);

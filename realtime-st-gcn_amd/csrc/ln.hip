@@ -315,10 +315,11 @@ int bwd_threads(int U) {  // threads per block of ln_bwd (one per unit): 256, 51
   return n <= 256 ? 256 : (n <= 512 ? 512 : (n <= 1024 ? 1024 : 0));
 }
 
-// vectors per ln_bwd unit (1, 2, 4; 16-B vectors: 1, 2): the fewest that bring a frame to <= 512 units (the
-// 1024-thread blocks' 128-VGPR cap spills the prefetch ring), else to <= 1024; 0 = none
+// vectors per ln_bwd unit (1, 2, 4, 8; 16-B vectors: 1, 2): the fewest that bring a frame to <= 512 units (the
+// 1024-thread blocks' 128-VGPR cap spills the prefetch ring), else to <= 1024; 0 = none (the scalar path's 8
+// elements per unit cover every C that is a multiple of 8 up to 1024 / V * 8: C = 256 at V = 25 on a misaligned view)
 int bwd_r(int V, int C, int vec) {
-  const int rmax = vec > 1 ? 2 : 4;
+  const int rmax = vec > 1 ? 2 : 8;
   for (int lim = 512; lim <= 1024; lim *= 2)
     for (int r = 1; r <= rmax; r *= 2)
       if ((C / vec) % r == 0 && V * (C / vec / r) <= lim) return r;
@@ -426,7 +427,8 @@ int ln_bwd_launch(const void* dy, int lddy, int mask, const void* mref, int ldm,
     if (R == 1) LN_BWD_NT(1, 4);
     else if constexpr (VEC > 1) LN_BWD_NT(2, 2);
     else if (R == 2) LN_BWD_NT(2, 2);
-    else LN_BWD_NT(4, 1);
+    else if (R == 4) LN_BWD_NT(4, 1);
+    else LN_BWD_NT(8, 1);
   });
 #undef LN_BWD_NT
 #undef LN_BWD_GO

@@ -24,46 +24,12 @@ re-packing (tiny tensors) and the (P x V)-sized reshuffles of the A/bias gradien
 """
 from __future__ import annotations
 
-import contextlib
-
 import torch
 
 from . import native as K
 from .routing import ROUTING
 
 BN, LN = "BatchNorm", "LayerNorm"
-
-_SIDE = {}
-
-
-def _side_stream(dev):
-    """Per-device side stream for the weight-gradient branch of a layer backward (None: run in order).
-
-    The data-gradient chain (BN backward -> transposed temporal conv -> BN1 backward -> transposed graph
-    conv) is the critical path from dy to dx; the weight gradients (temporal-conv wgrad, residual wgrad,
-    graph-conv wgrad + dW/dA finish + bias through A) branch off it.  They are issued on this stream after
-    a fork event and joined before the backward returns, so the latency-bound reduction kernels of the
-    branch fill the gaps and tails of the data-gradient kernels.  Under stream capture (parallel.GraphedStep)
-    the fork/join events pull the side stream into the capture: the branch becomes a parallel branch of the
-    HIP graph.  Off with routing.ROUTING.side_stream off."""
-    if not ROUTING.side_stream:
-        return None
-    s = _SIDE.get(dev.index)
-    if s is None:
-        s = _SIDE[dev.index] = torch.cuda.Stream(device=dev)
-    return s
-
-
-@contextlib.contextmanager
-def _fork(side):
-    """Run the body on ``side`` after everything already queued on the current stream."""
-    if side is None:
-        yield
-        return
-    side.wait_stream(torch.cuda.current_stream(side.device))
-    with torch.cuda.stream(side):
-        yield
-
 
 def _flat_ln(p):
     """LayerNorm([C,1,V]) parameter (C,1,V) -> flat fp32 [C*V] indexed c*V+v (kernel convention)."""
@@ -125,10 +91,7 @@ def _packs(cache, wg, wt, P, Cin, Cout, dtype):
     wimg, cpg, kwg = K.pack_gcn_weight(wgf, dtype)
     wt3 = wt.detach().float().squeeze(-1).permute(2, 0, 1)  # [Kt][Cout][Cin]
     wtp, _, _ = K.pack_weight(wt3, dtype, stride=1)
-    # pass 1 of the BatchNorm form (graph-conv statistics) on the frame-streaming kernel where it runs
-    fimg = K.pack_gcn_frame(wg, P, Cout, Cin, False, dtype) if ROUTING.gcn_frame and dtype == torch.bfloat16 \
-        and Cin in (64, 128) and Cout % 64 == 0 else None
-    val = (wimg, cpg, kwg, wtp, fimg)
+    val = (wimg, cpg, kwg, wtp)
     if cache is not None:
         cache["key"], cache["val"] = key, val
     return val
@@ -138,39 +101,28 @@ class LayerPacks:
     """Packed operands of one StgcnLayer's training step, filled by the model's PrepPlan launch
     (native.PrepPlan): graph-conv effective weights + bias through A (forward), their data-gradient form,
     temporal conv (forward / data gradient) and residual 1x1 conv (forward / data gradient) packs, each as
-    the (tensor, Cout_pad, Cin_pad) triple pack_weight returns (gw: (weights, bias2d)); gf / gfT: the frame-streaming
-    graph conv's forward (image triple, bias2d) and data-gradient image triple (pack_gcn_frame), when it takes them."""
-    __slots__ = ("gw", "gwT", "gf", "gfT", "wt", "wtT", "wr", "wrT")
+    the (tensor, Cout_pad, Cin_pad) triple pack_weight returns (gw: (weights, bias2d))."""
+    __slots__ = ("gw", "gwT", "wt", "wtT", "wr", "wrT")
 
     def __init__(self):
-        self.gw = self.gwT = self.gf = self.gfT = self.wt = self.wtT = self.wr = self.wrT = None
+        self.gw = self.gwT = self.wt = self.wtT = self.wr = self.wrT = None
 
 
 def plan_layer_packs(plan, layer, A, M, dtype):
     """Record in ``plan`` every pack StgcnLayerFunction builds per call for ``layer`` fed ``A * M`` (the
     model's graph and the layer's edge importance, M None without importance); None when the layer takes a
-    route that packs differently (per-sample or dense A, the opt-in gcn_tile kernel)."""
+    route that packs differently (per-sample or dense A: the A-first graph conv)."""
     sup = layer._gsup
     P, V = A.shape[0], A.shape[-1]
     conv = layer.tcn[2]
     Cout, Cin = conv.out_channels, layer.gcn.conv.in_channels
     kt, stride = layer.kernel_size[0], layer.stride
-    if sup is None or A.dim() != 3 or sup.dense(P) or K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype):
+    if sup is None or A.dim() != 3 or sup.dense(P):
         return None
     pk = LayerPacks()
-    if not layer.afirst_forced():  # the A-first graph conv packs its channel GEMM per call
-        wg = layer.gcn.conv.weight
-        wg2 = wg.detach().reshape(P * Cout, Cin)
-        if K.gcn_frame_ok(sup, P, Cin, Cout, V, dtype):
-            pk.gf = (K.pack_gcn_frame(wg, P, Cout, Cin, False, dtype, plan=plan),
-                     K.gcn_bias_plan(A, layer.gcn.conv.bias, Cout, plan, M=M))
-        else:
-            pk.gw = K.gconv_weights(A, wg2, sup, Cout, Cin, False, dtype, bias=layer.gcn.conv.bias.detach(), plan=plan,
-                                    M=M)
-        if K.gcn_frame_ok(sup, P, Cout, Cin, V, dtype) and not K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype, trans=True):
-            pk.gfT = K.pack_gcn_frame(wg, P, Cout, Cin, True, dtype, plan=plan)
-        elif not K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype, trans=True):
-            pk.gwT = K.gconv_weights(A, wg2, sup, Cout, Cin, True, dtype, plan=plan, M=M)
+    wg2 = layer.gcn.conv.weight.detach().reshape(P * Cout, Cin)
+    pk.gw = K.gconv_weights(A, wg2, sup, Cout, Cin, False, dtype, bias=layer.gcn.conv.bias.detach(), plan=plan, M=M)
+    pk.gwT = K.gconv_weights(A, wg2, sup, Cout, Cin, True, dtype, plan=plan, M=M)
     wt = conv.weight.detach().squeeze(-1)
     pk.wt = K.pack_weight(wt.permute(2, 0, 1), dtype, stride=stride, plan=plan)
     pk.wtT = K.pack_weight(wt.permute(2, 1, 0), dtype, stride=stride, trans=True, plan=plan)
@@ -199,7 +151,7 @@ def fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, su
     Cout = wt.shape[0]
     dev = x.device
     bias2d = K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
-    wimg, cpg, kwg, wtp, fimg = _packs(cache, wg, wt, P, Cin, Cout, dtype)
+    wimg, cpg, kwg, wtp = _packs(cache, wg, wt, P, Cin, Cout, dtype)
     if norm == LN:
         # the [V][64] parameter rows, re-laid-out only when a LayerNorm parameter changed (4 copy launches)
         lkey = tuple((t.data_ptr(), t._version) for t in (n1w, n1b, n2w, n2b))
@@ -214,14 +166,9 @@ def fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, su
     rb2 = K.layer_fused_row_blocks(N, T)
     st2 = torch.empty((rb2, Cout, 4), dtype=torch.float32, device=dev)
     # both kernels write every row block of their statistics: no zero fill
-    if fimg is not None and fimg[1] == cpg:  # pass 1: graph-conv statistics only (gcn_frame.hip)
-        rb1 = K.gcn_frame_row_blocks(N * T, Cout)
-        st1 = torch.empty((rb1, cpg, 4), dtype=torch.float32, device=dev)
-        K.gcn_frame(x, A32, fimg, Cin, Cout, bias=bias2d, stats=st1, stats_only=True)
-    else:
-        rb1 = K.gcn_tile_row_blocks(N * T, V, Cout)
-        st1 = torch.empty((rb1, cpg, 4), dtype=torch.float32, device=dev)
-        K.gcn_tile(x, A32, wimg, kwg, Cin, Cout, cpg, sup, bias=bias2d, stats=st1, stats_only=True)
+    rb1 = K.gcn_tile_row_blocks(N * T, V, Cout)
+    st1 = torch.empty((rb1, cpg, 4), dtype=torch.float32, device=dev)
+    K.gcn_tile(x, A32, wimg, kwg, Cin, Cout, cpg, sup, bias=bias2d, stats=st1, stats_only=True)
     _, sc1, sh1 = K.bn_finalize(st1, rb1, cpg, Cout, n1w.detach().float(), n1b.detach().float())
     z = K.layer_fused(x, A32, wimg, bias2d, sc1, sh1, wtp, bt.detach().float().contiguous(), stats=st2, tag=tag)
     _, sc2, sh2 = K.bn_finalize(st2, rb2, Cout, Cout, n2w.detach().float(), n2b.detach().float())
@@ -277,8 +224,8 @@ class StgcnLayerFunction(torch.autograd.Function):
         if (gather and len(cfg) > 7 and cfg[7] and (norm == LN or ROUTING.fused_bn_inference)
                 and K.layer_fused_ok(sup, P, Cin, Cout, V, kt, stride, dtype)):
             # inference: the fused layer kernel (g never leaves the chip; nothing saved for backward).
-            # LayerNorm layers: one kernel, ~3x the unfused forward; BatchNorm layers: the two-pass form,
-            # 0.175 vs 0.187 ms graph-replayed (routing.fused_bn_inference off = unfused)
+            # LayerNorm layers: one kernel, 0.14 vs 0.20 ms unfused; BatchNorm layers (routing.fused_bn_inference,
+            # opt-in): the two-pass form, 0.176 vs 0.166 ms unfused on the r05a box
             return fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, sup, dtype,
                                        cache=cache, norm=norm)
         if (gather and norm == LN and ROUTING.fused_ln_train and not (len(cfg) > 7 and cfg[7])
@@ -295,61 +242,29 @@ class StgcnLayerFunction(torch.autograd.Function):
             ctx.save_for_backward(x, A32, None, g, u, y, wg, bg, wt, n1w, n1b, n2w, n2b, ls1, ls2, None)
             ctx.in_dtype = A.dtype
             return y
-        tiled = gather and K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype)  # fused frame-tiled graph conv
-        # frame-streaming graph conv (1x1 conv then joint mix per frame, gcn_frame.hip)
-        framed = gather and not tiled and K.gcn_frame_ok(sup, P, Cin, Cout, V, dtype)
-        # gathered / framed paths: bias2d comes from the weight preparation below
-        bias2d = None if (gather and not tiled) else K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
-        # the 64-channel temporal conv on the frame-streaming kernel (tconv_frame.hip; BN1 prologue)
-        tframe = norm == BN and K.tconv_frame_ok(Cout, kt, stride, V, dtype)
+        # gathered path: bias2d comes from the weight preparation below
+        bias2d = None if gather else K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
         if norm == BN:  # all BatchNorm partial-statistics buffers of the layer from one zero fill
             cpo = -(-Cout // K.col_tile(Cout)) * K.col_tile(Cout)
-            if framed:
-                rb1, cp1 = K.gcn_frame_row_blocks(N * T, Cout), -(-Cout // 32) * 32
-            else:
-                rb1 = (K.gcn_tile_row_blocks(N * T, V, Cout) if tiled else K.gconv_row_blocks(N * T, V)) if gather \
-                    else K.row_blocks(M1, Cout)
-                cp1 = cpo
-            rb2 = K.tconv_frame_row_blocks(N, T_out) if tframe else K.row_blocks(M2, Cout)
-            st_shapes = [(rb1, cp1, 4), (rb2, cpo, 4)] + ([(K.row_blocks(M2, Cout), cpo, 4)] if res_conv else [])
-            st_all = _stats_arena(cache, dev, x.dtype, st_shapes, (tiled, gather, framed, tframe))
+            rb1 = K.gconv_row_blocks(N * T, V) if gather else K.row_blocks(M1, Cout)
+            rb2 = K.row_blocks(M2, Cout)
+            st_shapes = [(rb1, cpo, 4), (rb2, cpo, 4)] + ([(K.row_blocks(M2, Cout), cpo, 4)] if res_conv else [])
+            st_all = _stats_arena(cache, dev, x.dtype, st_shapes, gather)
             st1, st2 = st_all[0], st_all[1]
             str_ = st_all[2] if res_conv else None
-        # ---- residual branch: independent of the graph conv -> temporal conv chain until the output norm,
-        # so on the side stream (x is ready at entry; joined before the norm that adds it)
+        # ---- residual branch: independent of the graph conv -> temporal conv chain until the output norm
         r = None
-        side = _side_stream(dev) if res_conv else None
         if res_conv:
-            with _fork(side):
-                wrp, cpr, kpr = packs.wr if packs is not None else \
-                    K.pack_weight(wr.detach().float().view(1, Cout, Cin), dtype)
-                r = K.conv_rows(x, wrp, Cin, Cout, cpr, kpr, T, T_out, Kt=1, stride=stride, pad=0,
-                                bias=br.detach().float().contiguous(), stats=str_ if norm == BN else None)
-                if norm == BN:
-                    mrr, scr, shr = K.bn_finalize(str_, str_.shape[0], cpr, Cout, nrw.detach().float(),
-                                                  nrb.detach().float())
-                else:
-                    lsr = K.ln_stats(r, N * T_out, V, Cout)
-                side_made = [r] + ([mrr, scr, shr] if norm == BN else [lsr])
-
-        if tiled:  # A-mix on the fly into the MFMA operand of whole-frame tiles (gcn_tile.hip)
-            wgf = wg.detach().float().view(P, Cout, Cin).permute(1, 0, 2).reshape(Cout, P * Cin)  # W'[co][p*Cin+ci]
-            wimg, cpg, kwg = K.pack_gcn_weight(wgf, dtype)
-            kpg = kwg
+            wrp, cpr, kpr = packs.wr if packs is not None else \
+                K.pack_weight(wr.detach().float().view(1, Cout, Cin), dtype)
+            r = K.conv_rows(x, wrp, Cin, Cout, cpr, kpr, T, T_out, Kt=1, stride=stride, pad=0,
+                            bias=br.detach().float().contiguous(), stats=str_ if norm == BN else None)
             if norm == BN:
-                assert cpg == cpo
-            g = K.gcn_tile(x, A32, wimg, kwg, Cin, Cout, cpg, sup, bias=bias2d, stats=st1 if norm == BN else None)
-            XA = None
-        elif framed:  # per frame: 1x1 conv then joint mix on MFMA (gcn_frame.hip), no XA in HBM
-            if packs is not None and packs.gf is not None:
-                img, bias2d = packs.gf
+                mrr, scr, shr = K.bn_finalize(str_, str_.shape[0], cpr, Cout, nrw.detach().float(), nrb.detach().float())
             else:
-                img = K.pack_gcn_frame(wg, P, Cout, Cin, False, dtype)
-                bias2d = K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
-            cpg, kpg = img[1], img[2]
-            g = K.gcn_frame(x, A32, img, Cin, Cout, bias=bias2d, stats=st1 if norm == BN else None)
-            XA = None
-        elif gather:  # joint-gathered GEMM over per-joint effective weights (gconv.hip), no XA in HBM
+                lsr = K.ln_stats(r, N * T_out, V, Cout)
+
+        if gather:  # joint-gathered GEMM over per-joint effective weights (gconv.hip), no XA in HBM
             if packs is not None and packs.gw is not None:
                 wgp, bias2d = packs.gw
             else:
@@ -384,18 +299,9 @@ class StgcnLayerFunction(torch.autograd.Function):
         wtp, cpt, kpt = packs.wt if packs is not None else \
             K.pack_weight(wt.detach().float().squeeze(-1).permute(2, 0, 1), dtype, stride=stride)  # [Kt][Cout][Cin]
 
-        if tframe:
-            u = K.tconv_frame(g, wtp, cpt, kpt, bias=bt.detach().float().contiguous(), pro_a=sc1, pro_b=sh1, stats=st2,
-                              tag=f"tcn_fwd_c{Cout}")
-        else:
-            u = K.conv_rows(g if norm == BN else h, wtp, Cout, Cout, cpt, kpt, T, T_out, Kt=kt, stride=stride, pad=pad,
-                            bias=bt.detach().float().contiguous(), stats=st2 if norm == BN else None,
-                            tag=f"tcn_fwd_c{Cout}" if stride == 1 else None, **pro1)
-        if side is not None:  # join the residual branch
-            main = torch.cuda.current_stream(dev)
-            main.wait_stream(side)
-            for t_ in side_made:
-                t_.record_stream(main)
+        u = K.conv_rows(g if norm == BN else h, wtp, Cout, Cout, cpt, kpt, T, T_out, Kt=kt, stride=stride, pad=pad,
+                        bias=bt.detach().float().contiguous(), stats=st2 if norm == BN else None,
+                        tag=f"tcn_fwd_c{Cout}" if stride == 1 else None, **pro1)
 
         # ---- y = relu(norm2(u) + res)
         if norm == BN:
@@ -459,7 +365,6 @@ class StgcnLayerFunction(torch.autograd.Function):
                 zl["t"] = K.zeros_arena(dev, (P * Cout, Cin), (P, V, V),
                                         (N, V, Cout) if A32.dim() == 4 else (V, Cout))
             return zl["t"]
-        side = _side_stream(dev)  # weight-gradient branch (joined before returning)
 
         # ---- through relu(norm2(u) + res): dz = dy * [y > 0]
         du = K.cl_empty(N, Cout, T_out, V, dtype, dev)
@@ -510,9 +415,7 @@ class StgcnLayerFunction(torch.autograd.Function):
             # residual conv (1x1, stride s, bias): data grad (transposed), weight grad
             wrTp, cq, kq = packs.wrT if packs is not None else \
                 K.pack_weight(wr.detach().float().view(Cout, Cin).t().unsqueeze(0), dtype)
-            with _fork(side):
-                grads["wr"] = K.conv_wgrad_w(x, dr, Cin, Cout, T, T_out, Kt=1, stride=stride,
-                                             pad=0).view(Cout, Cin, 1, 1)
+            grads["wr"] = K.conv_wgrad_w(x, dr, Cin, Cout, T, T_out, Kt=1, stride=stride, pad=0).view(Cout, Cin, 1, 1)
             K.conv_rows(dr, wrTp, Cout, Cin, cq, kq, T_out, T, Kt=1, stride=stride, pad=0, trans=True, out=dx)
             dx_written = True
         elif residual and not fused:
@@ -528,10 +431,9 @@ class StgcnLayerFunction(torch.autograd.Function):
         else:  # the forward's h = relu(LN1(g)), recomputed when the forward did not keep it (fused route)
             pro1 = {}
             hin = h if h is not None else K.ln_apply(g, ls1, _flat_ln(n1w), _flat_ln(n1b), M1, V, Cout, relu=True)
-        with _fork(side):
-            grads["wt"] = K.conv_wgrad_w(hin, du, Cout, Cout, T, T_out, Kt=kt, stride=stride, pad=pad,
-                                         **pro1).unsqueeze(-1)  # (co, ci, Kt, 1)
-        if K.tconv_frame_ok(Cout, kt, stride, V, dtype, trans=True) and getattr(wtTp, "frag_stride", None) == 1:
+        grads["wt"] = K.conv_wgrad_w(hin, du, Cout, Cout, T, T_out, Kt=kt, stride=stride, pad=pad,
+                                     **pro1).unsqueeze(-1)  # (co, ci, Kt, 1)
+        if K.tconv_frame_ok(Cout, kt, stride, V, dtype) and getattr(wtTp, "frag_stride", None) == 1:
             dh = K.tconv_frame(du, wtTp, cq, kq, trans=True)
         else:
             dh = K.conv_rows(du, wtTp, Cout, Cout, cq, kq, T_out, T, Kt=kt, stride=stride, pad=pad, trans=True)
@@ -558,33 +460,15 @@ class StgcnLayerFunction(torch.autograd.Function):
         bgp = bg.detach().float().view(P, Cout)
         if ctx.sup is not None:
             # data grad: same gather GEMM on dg over the reverse lists with transposed effective weights;
-            # weight / adjacency / bias grads: one pass of the frame kernel (bf16), else through the per-joint
-            # dWeff[w][j] = sum_i dg[(i,w)] x[(i,S(w)_j)]^T blocks
+            # weight / adjacency / bias grads through the per-joint dWeff[w][j] = sum_i dg[(i,w)] x[(i,S(w)_j)]^T blocks
             sup = ctx.sup
             wg2 = wg.detach().float().reshape(P * Cout, Cin).contiguous()
-            if K.gconv_wgrad_frame_ok(A32, Cin, Cout, dtype):
-                with _fork(side):
-                    # one pass over (x, dg): dW, the dense dA (bias through A included) and db (gconv_wgrad_frame.hip)
-                    dwg2, dA, grads["bg"] = K.gconv_wgrad_frame(x, dg, A32, wg2, bg)
-                    grads["wg"] = dwg2.view(P * Cout, Cin, 1, 1)
-            else:
-                with _fork(side):
-                    _gconv_wgrad_dweff(ctx, x, dg, A32, wg, wg2, bg, bgp, sup, grads, zero_targets, P, Cin, Cout, T,
-                                       V, M1, dtype, dev)
-                dA = grads.pop("dA")
-            if K.gcn_frame_ok(sup, P, Cout, Cin, V, dtype) and not K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype, trans=True):
-                # dx (+)= sum_p A_p-mix(dg W_p) per frame (gcn_frame.hip)
-                imgT = packs.gfT if packs is not None and packs.gfT is not None else \
-                    K.pack_gcn_frame(wg, P, Cout, Cin, True, dtype)
-                K.gcn_frame(dg, A32, imgT, Cout, Cin, trans_a=True, out=dx, accumulate=dx_written)
-            elif K.gcn_tile_ok(sup, P, Cin, Cout, V, dtype, trans=True):  # dx = sum_p A_p-mix(dg) W_p^T, fused (gcn_tile.hip)
-                wdf = wg.detach().float().view(P, Cout, Cin).permute(2, 0, 1).reshape(Cin, P * Cout)
-                wimgT, cq, kwT = K.pack_gcn_weight(wdf, dtype)
-                K.gcn_tile(dg, A32, wimgT, kwT, Cout, Cin, cq, sup, trans_a=True, out=dx, accumulate=dx_written)
-            else:
-                wgT = packs.gwT if packs is not None and packs.gwT is not None else \
-                    K.gconv_weights(A32, wg2, sup, Cout, Cin, True, dtype)
-                K.gconv(dg, wgT, sup, Cout, Cin, trans=True, out=dx, accumulate=dx_written)
+            _gconv_wgrad_dweff(ctx, x, dg, A32, wg, wg2, bg, bgp, sup, grads, zero_targets, P, Cin, Cout, T, V, M1,
+                               dtype, dev)
+            dA = grads.pop("dA")
+            wgT = packs.gwT if packs is not None and packs.gwT is not None else \
+                K.gconv_weights(A32, wg2, sup, Cout, Cin, True, dtype)
+            K.gconv(dg, wgT, sup, Cout, Cin, trans=True, out=dx, accumulate=dx_written)
         else:
             # DW[(n,t,w)][p*Cin+ci] = sum_c dg[(n,t,w)][c] Wg[p*Cout+c][ci]
             wgT = wg.detach().float().view(P, Cout, Cin).permute(0, 2, 1).reshape(1, P * Cin, Cout)
@@ -595,13 +479,6 @@ class StgcnLayerFunction(torch.autograd.Function):
             dwg = K.conv_wgrad(XA, dg, P * Cin, Cout, T, T, Kt=1)              # [1][Cout][P*Cin]
             grads["wg"] = dwg.view(Cout, P, Cin).permute(1, 0, 2).reshape(P * Cout, Cin, 1, 1)
             dA = _bias_through_A(dA, A32, bg, bgp, dg, None, zero_targets()[2], M1, Cout, V, grads)
-        if side is not None:  # join the weight-gradient branch
-            main = torch.cuda.current_stream(dev)
-            main.wait_stream(side)
-            # tensors allocated on the side stream and used on the main one
-            for t in (grads.get("bg"), grads.get("wg"), grads.get("wt"), grads.get("wr"), dA):
-                if t is not None:
-                    t.record_stream(main)
 
         def gr(name, like):
             v = grads.get(name)
@@ -635,7 +512,7 @@ def _bias_through_A(dA, A32, bg, bgp, dg, S_fused, z_S, M1, Cout, V, grads):
 def _gconv_wgrad_dweff(ctx, x, dg, A32, wg, wg2, bg, bgp, sup, grads, zero_targets, P, Cin, Cout, T, V, M1, dtype,
                        dev):
     """Graph-conv weight / adjacency / bias gradients through the per-joint dWeff[w][j] = sum_i dg[(i,w)]
-    x[(i,S(w)_j)]^T blocks (gconv_wgrad + finish): the fp32 path and shapes gconv_wgrad_frame does not take.
+    x[(i,S(w)_j)]^T blocks (gconv_wgrad + finish).
     Sets grads["wg"], grads["bg"], grads["dA"]."""
     fuse_s = A32.dim() == 3 and K.gconv_wgrad_rowsum_ok(sup, Cin, Cout, dtype)
     dense_dA = ctx.cfg[6] and ctx.needs_input_grad[1]

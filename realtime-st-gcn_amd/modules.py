@@ -16,7 +16,6 @@ import torch.nn as nn
 
 from . import layer_fn as F_
 from . import native as K
-from .routing import ROUTING
 
 _DTYPES = {"fp32": torch.float32, "bf16": torch.bfloat16, torch.float32: torch.float32,
            torch.bfloat16: torch.bfloat16}
@@ -140,13 +139,9 @@ class StgcnLayer(nn.Module):
             self._gsup = K.GraphSupport(A)
         self._graph_bound = self._graph_bound or masked
 
-    def afirst_forced(self):
-        """The A-first graph conv chosen by routing (gcn_afirst / gcn_afirst_min_c) for a shared graph."""
-        return ROUTING.gcn_afirst or 0 < ROUTING.gcn_afirst_min_c <= self.gcn.conv.in_channels
-
     def graph_support(self, A):
-        if A.dim() != 3 or self.afirst_forced():
-            return None  # per-sample A (AAGCN) or forced A-first path
+        if A.dim() != 3:
+            return None  # per-sample A (AAGCN): the A-first path
         self.bind_graph(A, masked=False)
         return self._gsup
 

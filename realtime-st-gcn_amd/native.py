@@ -270,11 +270,10 @@ def conv_rows(x, w3p, Cin, Cout, cp, kp, T_in, T_out, Kt=1, stride=1, pad=0, tra
     return out
 
 
-def tconv_frame_ok(C, kt, stride, V, dtype, trans=False) -> bool:
-    """Whether a layer's temporal conv (C -> C channels) runs on the frame-streaming kernel tconv_frame.hip: bf16,
-    C = 64, Kt = 9, stride 1, 16 < V <= 32; forward (routing.tconv_frame) or data grad (routing.tconv_frame_dgrad)."""
-    on = ROUTING.tconv_frame_dgrad if trans else ROUTING.tconv_frame
-    return on and dtype == torch.bfloat16 and C == 64 and kt == 9 and stride == 1 and 16 < V <= 32
+def tconv_frame_ok(C, kt, stride, V, dtype) -> bool:
+    """Whether a layer's temporal-conv data gradient (C -> C channels) runs on the frame-streaming kernel
+    tconv_frame.hip: bf16, C = 64, Kt = 9, stride 1, 16 < V <= 32 (52 vs 65 us for conv_persist, r04d)."""
+    return dtype == torch.bfloat16 and C == 64 and kt == 9 and stride == 1 and 16 < V <= 32
 
 
 def tconv_frame_row_blocks(N: int, T: int) -> int:
@@ -534,21 +533,6 @@ def pack_frag1(w2: torch.Tensor, dtype) -> tuple:
     return buf[cp * kp:], cp, kp
 
 
-def gcn_tile_ok(sup, P, Cin, Cout, V, dtype, trans=False) -> bool:
-    """Whether the graph conv of a layer (Cin -> Cout) runs on the fused kernel (gcn_tile.hip: joint mix
-    + 1x1 conv as two chained MFMA products) in the forward (trans False) or data-grad direction.
-    "auto" takes it where it measured faster than the joint-gathered gconv.hip in isolation (DESIGN.md
-    section 4): when the kernel writes 64 channels.  Beyond that the two-stage form executes ~2x the
-    MFMA work of the gathered one (stage-1 mix per 64-channel column tile, joints padded 25 -> 32) and
-    loses.  Default "0": inside the training step (cold HBM inputs) "auto" measured equal to gconv.hip
-    (0.46 ms/step either way), so the gathered path stays the default."""
-    if ROUTING.gcn_tile == "0" or dtype != torch.bfloat16 or sup is None or P > 3 or not 16 < V <= 32:
-        return False
-    if Cin not in (64, 128, 256) or Cout not in (64, 128, 256):
-        return False
-    return ROUTING.gcn_tile == "1" or (Cin if trans else Cout) == 64
-
-
 def gcn_tile_row_blocks(NT: int, V: int, Cout: int) -> int:
     return L.lib().stgcn_gcn_tile_row_blocks(NT, V, Cout)
 
@@ -595,41 +579,6 @@ def gcn_tile(x, A, wimg, kw_pad, Cin, Cout, cp, sup, trans_a=False, bias=None, s
     return out
 
 
-def gcn_frame_ok(sup, P, Cin, Cout, V, dtype) -> bool:
-    """Whether a graph conv with ``Cin`` kernel-input and ``Cout`` kernel-output channels (forward: the layer's;
-    data grad: swapped) runs on the frame-streaming kernel gcn_frame.hip (bf16, shared A, P <= 3, 16 < V <= 32,
-    Cin 64 or 128, Cout % 64 == 0; routing.gcn_frame)."""
-    return (ROUTING.gcn_frame and dtype == torch.bfloat16 and sup is not None and P <= 3 and 16 < V <= 32
-            and Cin in (64, 128) and Cout % 64 == 0)
-
-
-def gcn_frame_row_blocks(NT: int, Cout: int) -> int:
-    return L.lib().stgcn_gcn_frame_row_blocks(NT, Cout)
-
-
-def pack_gcn_frame(w, P, Cout, Cin, trans, dtype, plan=None):
-    """U image of stgcn_gcn_frame from the graph-conv weight w (P*Cout, Cin, 1, 1): the Kt = P MFMA-fragment image of
-    w viewed (P, Cout, Cin) (forward) or of its (P, Cin, Cout) transpose (data grad).  Returns (image, rows_pad,
-    cols_pad).  ``plan``: record the job in a PrepPlan (the view keeps pointing at the parameter)."""
-    w3 = w.detach().view(P, Cout, Cin)
-    if trans:
-        w3 = w3.transpose(1, 2)
-    if w3.dtype != torch.float32:
-        w3 = w3.float()
-    Kt, Co, Ci = w3.shape
-    cp, kp = -(-Co // 32) * 32, -(-Ci // 16) * 16
-    n = Kt * cp * kp
-    code = L.dtype_code(dtype)
-    buf = torch.empty(2 * n, dtype=dtype, device=w.device)
-    if plan is not None:
-        plan.add(kind=0, dtype=code, src=w3, Kt=Kt, Co=Co, Ci=Ci, cp=cp, kp=kp, dst=buf[:n], dst_frag=buf[n:])
-    else:
-        s0, s1, s2 = w3.stride()
-        L.check(L.lib().stgcn_pack_weight_frag(w3.data_ptr(), s0, s1, s2, Kt, Co, Ci, buf[:n].data_ptr(),
-                                               buf[n:].data_ptr(), cp, kp, code, L.stream()), "pack_weight_frag")
-    return buf[n:], cp, kp
-
-
 def gcn_bias_plan(A, b, Cout, plan, M=None):
     """bias2d [V][Cout] = sum_p b_p colsum_p(A * M) recorded as a PrepPlan job (kind 3)."""
     A = _dense(A)
@@ -639,39 +588,6 @@ def gcn_bias_plan(A, b, Cout, plan, M=None):
     plan.add(kind=3, dtype=1, src=bc.view(1, -1), dst=b2, Co=Cout, Ci=1, A=A, M=None if M is None else _dense(M), P=P, V=V,
              bconv=bc, bias2d=b2)
     return b2
-
-
-def gcn_frame(x, A, img, Cin, Cout, trans_a=False, bias=None, stats=None, out=None, accumulate=False, tag=None,
-              stats_only=False):
-    """Graph conv on the frame-streaming kernel (stgcn_gcn_frame): out rows (N, Cout, T, V) (+)= the 1x1 conv
-    then the joint mix (trans_a: the data gradient's transposed mix) (+ bias[w][co]); img = pack_gcn_frame's
-    (image, rows_pad, cols_pad).  stats_only: no output, the BatchNorm partial statistics only (returns None)."""
-    N, _, T, V = x.shape
-    if stats_only:
-        if stats is None or out is not None or accumulate:
-            raise RuntimeError("stgcn_amd: gcn_frame stats_only needs a stats buffer and no output")
-    elif out is None:
-        out = cl_empty(N, Cout, T, V, x.dtype, x.device)
-    A = _dense(A)
-    wimg, cp, kp = img
-    d = L.GcnTileDesc()
-    d.in_, d.out, d.w_frag, d.A = x.data_ptr(), L.ptr(out), wimg.data_ptr(), A.data_ptr()
-    d.bias, d.stats = L.ptr(bias), L.ptr(stats)
-    d.NT, d.V, d.P, d.Cin, d.Cout, d.Cout_pad, d.Kw_pad = N * T, V, A.shape[0], Cin, Cout, cp, kp
-    d.in_ld, d.out_ld = rows_ld(x), (rows_ld(out) if out is not None else Cout)
-    d.trans_a, d.accumulate = int(trans_a), int(accumulate)
-    if stats is not None and stats.shape[1] != cp:
-        raise RuntimeError("stgcn_amd: gcn_frame statistics rows must be rows_pad wide")
-    h = KTIME_HOOK
-    if h:
-        P = A.shape[0]
-        ktag = _k_start(h, "gcn_frame_dgrad" if trans_a else "gcn_frame_fwd", f"{Cin}->{Cout}",
-                        2.0 * N * T * V * P * Cin * Cout,
-                        x.element_size() * N * T * V * (Cin + Cout * (2 if accumulate else 1)))
-    L.check(L.lib().stgcn_gcn_frame(d, L.stream()), "gcn_frame")
-    if h:
-        h(ktag, "end", None)
-    return out
 
 
 def layer_fused_ok(sup, P, Cin, Cout, V, kt, stride, dtype) -> bool:
@@ -825,47 +741,6 @@ def gconv_finish_bias_ok(A, sup) -> bool:
     return A.dim() == 3 and A.shape[0] <= 4 and A.shape[-1] <= 32 and A.shape[-1] * sup.J <= 256
 
 
-def gconv_wgrad_frame_ok(A, Cin, Cout, dtype) -> bool:
-    """Whether the graph-conv weight / adjacency / bias gradients take the one-pass frame kernel
-    (gconv_wgrad_frame.hip): bf16, a batch-shared A with P <= 3 and 16 < V <= 32, 64-multiple channels."""
-    return (ROUTING.gconv_wgrad_frame and dtype == torch.bfloat16 and A.dim() == 3 and A.shape[0] <= 3
-            and 16 < A.shape[-1] <= 32 and Cin % 64 == 0 and Cout % 64 == 0)
-
-
-def gconv_wgrad_frame(x, dy, A, W, bconv):
-    """(dW [P*Cout][Cin], dA [P][V][V] dense, db [P*Cout]) fp32, overwritten (stgcn_gconv_wgrad_frame): the
-    graph conv's weight, adjacency and bias gradients from its input rows x and output gradient rows dy."""
-    N, Cin, T, V = x.shape
-    A = _dense(A)
-    P = A.shape[0]
-    Cout = dy.shape[1]
-    dev = x.device
-    out = torch.empty(P * Cout * Cin + P * V * V + P * Cout, dtype=torch.float32, device=dev)
-    dW = out[:P * Cout * Cin].view(P * Cout, Cin)
-    dA = out[P * Cout * Cin:P * Cout * Cin + P * V * V].view(P, V, V)
-    db = out[P * Cout * Cin + P * V * V:]
-    W = _f32c(W.detach())
-    b = _f32c(bconv.detach()) if bconv is not None else None
-    d = L.GconvWgradFrameDesc()
-    d.x, d.dy, d.A, d.W, d.bconv = x.data_ptr(), dy.data_ptr(), A.data_ptr(), W.data_ptr(), L.ptr(b)
-    d.dW, d.dA, d.db = dW.data_ptr(), dA.data_ptr(), db.data_ptr()
-    d.NT, d.V, d.P, d.Cin, d.Cout, d.x_ld, d.dy_ld = N * T, V, P, Cin, Cout, rows_ld(x), rows_ld(dy)
-    nbytes = L.lib().stgcn_gconv_wgrad_frame_workspace(d)
-    if nbytes < 0:
-        raise RuntimeError("stgcn_amd: gconv_wgrad_frame: unsupported shape")
-    work = _workspace(nbytes, dev)
-    d.work, d.work_bytes = work.data_ptr(), work.numel() * 4
-    h = KTIME_HOOK
-    if h:
-        ktag = _k_start(h, "gconv_wgrad_frame", f"{Cin}->{Cout}", 2.0 * N * T * V * P * Cin * Cout * 2,
-                        x.element_size() * N * T * V * (Cin + Cout))
-    L.check(L.lib().stgcn_gconv_wgrad_frame(d, L.stream()), "gconv_wgrad_frame")
-    if h:
-        h(ktag, "end", None)
-    return dW, dA, db
-
-
-# ------------------------------------------------------------------------------------ BatchNorm
 def bn_stat_blocks(M: int) -> int:
     return L.lib().stgcn_bn_stat_blocks(M)
 

@@ -116,8 +116,11 @@ def sharded_loss(crit, i, pred_local, labels_local, shard: SegmentShard, world: 
     return ce * world, mse * world
 
 
-def ddp(model: torch.nn.Module, device: torch.device, bucket_cap_mb: int = 16):
-    """DistributedDataParallel over the initialised process group (RCCL on the GPU box, gloo in tests)."""
+def ddp(model: torch.nn.Module, device: torch.device, bucket_cap_mb: int = 4):
+    """DistributedDataParallel over the initialised process group (RCCL on the GPU box, gloo in tests).  4 MB
+    buckets: the config-2 gradient (12.2 MB fp32) goes out in ~4 all-reduces, the first as soon as the last
+    (256-channel, ~3 MB each) layers' backward is done, so the ring transfers overlap the rest of the backward
+    (16 MB buckets held the whole gradient until the backward ended)."""
     from torch.nn.parallel import DistributedDataParallel as DDP
     ids = [device.index] if device.type == "cuda" else None
     return DDP(model, device_ids=ids, bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True)
@@ -186,30 +189,32 @@ class GraphedStep:
     tensors it closes over).  The optimizer must be capturable: the package's ``optim.Adam`` (device-side step
     counters; what bench.py uses) or torch.optim.Adam(capturable=True).  One eager step runs first (on a side
     stream, as graph capture requires) so that every gradient and optimizer state tensor exists and keeps its
-    address; a parameter that got no gradient in it is given a zero gradient so the captured zeroing has a
-    buffer.  Replays do not bump the parameters' version counters (host-side bookkeeping is not captured):
+    address.  A parameter that got no gradient in it keeps ``grad = None`` and is left out of the captured zeroing,
+    the flat all-reduce and the update (the optimizers skip ``None`` gradients, as an eager step would: its Adam
+    moments and, with weight decay, its value stay put).  Replays do not bump the parameters' version counters (host-side bookkeeping is not captured):
     call ``train()`` / ``eval()`` before an inference forward that should see replayed updates."""
 
     def __init__(self, fwd_loss, params, opt, world: int = 1, group=None):
         self.fwd_loss, self.params, self.opt = fwd_loss, list(params), opt
         self.world, self.group = world, group
-        self.numels = [p.numel() for p in self.params]
+        self.flat = None
         dev = self.params[0].device
-        self.flat = torch.zeros(sum(self.numels), device=dev) if world > 1 else None
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
             self.opt.zero_grad(set_to_none=False)
-            self._fwd_bwd()
-            if self.flat is not None:
+            self.fwd_loss().backward()
+            # the parameters this step trains: the ones that received a gradient in the eager step
+            self.used = [p for p in self.params if p.grad is not None]
+            self.numels = [p.numel() for p in self.used]
+            if world > 1:
+                self.flat = torch.zeros(sum(self.numels), device=dev)
+                torch.cat([p.grad.reshape(-1) for p in self.used], out=self.flat)
                 self._allreduce()
             self._apply()
-            for p in self.params:
-                if p.grad is None:
-                    p.grad = torch.zeros_like(p)
             self.g1, self.g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g1, stream=s):
-                for p in self.params:
+                for p in self.used:
                     p.grad.zero_()
                 self.loss = self._fwd_bwd()
             with torch.cuda.graph(self.g2, stream=s):
@@ -220,7 +225,7 @@ class GraphedStep:
         loss = self.fwd_loss()
         loss.backward()
         if self.flat is not None:
-            torch.cat([p.grad.reshape(-1) for p in self.params], out=self.flat)
+            torch.cat([p.grad.reshape(-1) for p in self.used], out=self.flat)
         return loss.detach()
 
     def _allreduce(self):
@@ -229,7 +234,7 @@ class GraphedStep:
 
     def _apply(self):
         if self.flat is not None:
-            for p, g in zip(self.params, torch.split(self.flat, self.numels)):
+            for p, g in zip(self.used, torch.split(self.flat, self.numels)):
                 p.grad.copy_(g.view_as(p.grad)).div_(self.world)
         self.opt.step()
 

@@ -309,7 +309,17 @@ def loss_case():
     save("loss", d)
 
 
+def config1_cases():
+    # BASELINE config 1 at its exact shape: 1-layer st-gcn, x (2, 3, 64, 25), as_is (BatchNorm) and ln (LayerNorm)
+    model_case("stgcn_bn_1layer_t64", "as_is/stgcn_local.json", 1, False, T=64)
+    model_case("stgcn_ln_1layer_t64", "ln/stgcn_local.json", 1, False, T=64)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["config1"]:  # only the config-1 fixtures (the others are unchanged)
+        config1_cases()
+        sys.exit(0)
+    config1_cases()
     make_graphs()
     norms_case()
     stgcn_layer_case("bn_s1", 16, 16, 1, 9, "BatchNorm")

@@ -45,7 +45,8 @@ def test_graph_golden(pkg, key, name):
                                    g["A_%s/%s" % (strat, key)], rtol=0, atol=1e-12)
 
 
-@pytest.mark.parametrize("case", ["stgcn_bn_1layer", "stgcn_bn_9layer_narrow", "stgcn_ln_9layer_narrow_k69"])
+@pytest.mark.parametrize("case", ["stgcn_bn_1layer", "stgcn_bn_1layer_t64", "stgcn_ln_1layer_t64", "stgcn_bn_9layer_narrow",
+                                  "stgcn_ln_9layer_narrow_k69"])
 def test_model_state_dict_layout(pkg, case):
     d = load_golden("model_" + case)
     m = pkg.MODELS["st-gcn"](rank=None, **d["arch"])
@@ -174,12 +175,8 @@ def test_prep_plan_builds_and_validates(pkg):
             LF.plan_conv1x1_packs(plan, m.fcn_out.weight, torch.bfloat16))
     plan.finalize()
     assert all(p is not None for p in layers)
-    # the frame-streaming graph conv's forward takes two jobs (U image + the bias through A, kind 3): layers with
-    # 64 or 128 input channels (0-6)
-    framed = sum(p.gf is not None for p in layers)
-    assert framed == (7 if pkg.routing.ROUTING.gcn_frame else 0)
     # per layer: effective weights both ways, the bias through A (kind 3), temporal packs both ways
-    assert plan.njobs == 9 * 5 + framed + 2 * 2 + 2 * 2 + 2 * 2
+    assert plan.njobs == 9 * 5 + 2 * 2 + 2 * 2 + 2 * 2
     assert plan.nblocks > 0
     # frag images where the kernels expect them
     assert layers[0].wt[0].frag_stride == 1 and layers[3].wt[0].frag_stride == 2 and layers[3].wtT[0].frag_stride == 2
@@ -199,7 +196,6 @@ def test_descriptor_layouts_match_header(pkg, tmp_path):
     structs = {"stgcn_conv_desc": L.ConvDesc, "stgcn_wgrad_desc": L.WgradDesc, "stgcn_amix_desc": L.AmixDesc,
                "stgcn_gconv_desc": L.GconvDesc, "stgcn_gcn_tile_desc": L.GcnTileDesc,
                "stgcn_gconv_wgrad_desc": L.GconvWgradDesc, "stgcn_bn_bwd_desc": L.BnBwdDesc,
-               "stgcn_gconv_wgrad_frame_desc": L.GconvWgradFrameDesc,
                "stgcn_layer_fused_desc": L.LayerFusedDesc, "stgcn_prep_job": L.PrepJob,
                "stgcn_adam_entry": L.AdamEntry}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{os.path.join(ROOT, "include", "stgcn_amd.h")}"',

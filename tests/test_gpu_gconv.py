@@ -117,82 +117,3 @@ def test_gconv_finish_bias_merged(K, pkg, Cin, Cout):
     dW, dA, db = K.gconv_finish_bias(dweff, A, W, sup, Cout, Cin, b, S)
     torch.cuda.synchronize()
     assert torch.equal(dW, dW_ref) and torch.equal(dA, dA_ref) and torch.equal(db, db_ref)
-
-
-@pytest.mark.parametrize("Cin,Cout,N,T", [(64, 64, 4, 40), (64, 128, 3, 29), (128, 128, 2, 33), (128, 256, 2, 21),
-                                          (256, 256, 2, 13), (64, 64, 64, 300), (64, 64, 65, 300)])
-@pytest.mark.parametrize("strategy", ["spatial", "uniform", "distance"])
-def test_gconv_wgrad_frame(K, pkg, Cin, Cout, N, T, strategy, monkeypatch):
-    """stgcn_gconv_wgrad_frame (dW, the dense dA with the bias through A, db in one pass over (x, dy), bf16
-    operands) vs autograd of the reference's conv1x1 -> einsum(A) in fp32 on the same bf16-rounded inputs
-    (tgcn.py:71-79); tolerance 2e-2 of each gradient's max (the kernel rounds A, A dy and W^T dy to bf16 as the
-    reference's bf16 autocast rounds its einsum operands).  Run twice: bit-identical (fixed-order partials)."""
-    if N * T > 4000 and (strategy != "spatial"):
-        pytest.skip("config-2 size: spatial only")
-    monkeypatch.setattr(pkg.routing.ROUTING, "gconv_wgrad_frame", True)
-    torch.manual_seed(7)
-    A0 = torch.tensor(pkg.Graph(**dict(pkg.PKU_MMD, strategy=strategy)).A, dtype=torch.float32)
-    A = (A0 * (torch.rand(A0.shape) + 0.5)).requires_grad_(True)
-    P, V = A.shape[0], A.shape[-1]
-    xb = torch.randn(N, Cin, T, V).to(torch.bfloat16)
-    dyb = torch.randn(N, Cout, T, V).to(torch.bfloat16)
-    x = xb.float().requires_grad_(True)
-    W = (torch.randn(P * Cout, Cin) / Cin ** 0.5).requires_grad_(True)
-    b = torch.randn(P * Cout).requires_grad_(True)
-    ref = ref_gcn(x, A, W, b)
-    ref.backward(dyb.float())
-    assert K.gconv_wgrad_frame_ok(A0, Cin, Cout, torch.bfloat16)
-    Ad = A.detach().to(DEV).contiguous()
-    args = (cl(xb, torch.bfloat16), cl(dyb, torch.bfloat16), Ad, W.detach().to(DEV), b.detach().to(DEV))
-    dW, dA, db = K.gconv_wgrad_frame(*args)
-    dW2, dA2, db2 = K.gconv_wgrad_frame(*args)
-    torch.cuda.synchronize()
-    assert_close(dW.cpu(), W.grad, 2e-2, "frame dW")
-    assert_close(dA.cpu(), A.grad, 2e-2, "frame dA (dense)")
-    assert_close(db.cpu(), b.grad, 2e-2, "frame db")
-    assert torch.equal(dW, dW2) and torch.equal(dA, dA2) and torch.equal(db, db2)
-
-
-@pytest.mark.parametrize("Cin,Cout,N,T", [(64, 64, 3, 37), (64, 128, 2, 29), (128, 128, 2, 33), (128, 256, 1, 21),
-                                          (64, 64, 64, 300), (128, 128, 64, 150), (64, 64, 65, 300)])
-@pytest.mark.parametrize("strategy", ["spatial", "uniform", "distance"])
-def test_gcn_frame_fwd_dgrad(K, pkg, Cin, Cout, N, T, strategy, monkeypatch):
-    """stgcn_gcn_frame (the 1x1 conv then the joint mix per frame, bf16) vs the reference's conv1x1 -> einsum(A)
-    in fp32 on the same bf16-rounded inputs (tgcn.py:71-79): forward with the bias through A and the BatchNorm
-    partial statistics, data grad accumulating onto existing rows (the residual branch's dx), at 2e-2 of max."""
-    if N * T > 4000 and strategy != "spatial":
-        pytest.skip("config-2 size: spatial only")
-    monkeypatch.setattr(pkg.routing.ROUTING, "gcn_frame", True)
-    torch.manual_seed(8)
-    A0 = torch.tensor(pkg.Graph(**dict(pkg.PKU_MMD, strategy=strategy)).A, dtype=torch.float32)
-    A = A0 * (torch.rand(A0.shape) + 0.5)
-    P, V = A.shape[0], A.shape[-1]
-    x = torch.randn(N, Cin, T, V).to(torch.bfloat16).float().requires_grad_(True)
-    W = torch.randn(P * Cout, Cin) / Cin ** 0.5
-    b = torch.randn(P * Cout)
-    ref = ref_gcn(x, A, W, b)
-    dy = torch.randn(ref.shape).to(torch.bfloat16).float()
-    ref.backward(dy)
-    sup = K.GraphSupport(A0.to(DEV))
-    assert K.gcn_frame_ok(sup, P, Cin, Cout, V, torch.bfloat16) and K.gcn_frame_ok(sup, P, Cout, Cin, V, torch.bfloat16) \
-        == (Cout in (64, 128))
-    Ad, Wd = A.to(DEV).contiguous(), W.to(DEV)
-    img = K.pack_gcn_frame(Wd, P, Cout, Cin, False, torch.bfloat16)
-    bias2d = K.gcn_bias(Ad, b.to(DEV), N, Cout)
-    rb = K.gcn_frame_row_blocks(N * T, Cout)
-    st = torch.zeros((rb, img[1], 4), device=DEV)
-    g = K.gcn_frame(cl(x.detach(), torch.bfloat16), Ad, img, Cin, Cout, bias=bias2d, stats=st)
-    assert_close(g.float(), ref, 2e-2, "gcn_frame fwd")
-    mr, _, _ = K.bn_finalize(st, rb, img[1], Cout, None, None)
-    assert_close(mr[:, 0].cpu(), ref.detach().mean(dim=(0, 2, 3)), 3e-3, "gcn_frame stats mean")
-    assert_close(mr[:, 1].cpu(), 1.0 / (ref.detach().var(dim=(0, 2, 3), unbiased=False) + 1e-5).sqrt(), 2e-2,
-                 "gcn_frame stats rstd")
-    if Cout not in (64, 128):
-        return
-    imgT = K.pack_gcn_frame(Wd, P, Cout, Cin, True, torch.bfloat16)
-    base = torch.randn(N, Cin, T, V).to(torch.bfloat16)
-    dx = cl(base, torch.bfloat16)
-    K.gcn_frame(cl(dy, torch.bfloat16), Ad, imgT, Cout, Cin, trans_a=True, out=dx, accumulate=True)
-    assert_close(dx.float(), x.grad + base.float(), 2e-2, "gcn_frame dgrad (accumulate)")
-    dx2 = K.gcn_frame(cl(dy, torch.bfloat16), Ad, imgT, Cout, Cin, trans_a=True)
-    assert_close(dx2.float(), x.grad, 2e-2, "gcn_frame dgrad")

@@ -180,9 +180,22 @@ def test_bn_kernels(K):
     assert_close(dx.cpu(), ur.grad, 1e-4, "bn bwd")
 
 
-def test_ln_kernels(K):
+def _padded_rows(t, dtype=torch.float32):
+    """(N,C,T,V) channels-last view whose rows have one element of padding: an odd row stride, so the LayerNorm
+    kernels take their scalar (unvectorised) path."""
+    N, C, T, V = t.shape
+    buf = torch.zeros(N, T, V, C + 1, dtype=dtype, device=DEV)
+    buf[..., :C] = t.permute(0, 2, 3, 1).to(DEV, dtype)
+    return buf[..., :C].permute(0, 3, 1, 2)
+
+
+@pytest.mark.parametrize("C,padded", [(16, False), (256, True)])
+def test_ln_kernels(K, C, padded):
+    """LayerNorm stats / apply / backward (ln.hip) vs torch; C = 256 on rows with an odd stride is the scalar path
+    at 1600 elements per frame (8 per thread of a 1024-thread block)."""
     torch.manual_seed(5)
-    N, C, T, V = 3, 16, 9, 25
+    N, T, V = 3, 9, 25
+    mk = _padded_rows if padded else cl
     x = torch.randn(N, C, T, V) * 2 - 1
     w, b = torch.rand(C, 1, V) + 0.5, torch.randn(C, 1, V) * 0.1
     xr = x.clone().requires_grad_(True)
@@ -192,12 +205,12 @@ def test_ln_kernels(K):
     y = torch.relu(wr * (xr - mean) / torch.sqrt(var + 1e-5) + br)
     dy = torch.randn(y.shape)
     y.backward(dy)
-    st = K.ln_stats(cl(x), N * T, V, C)
-    yg = K.ln_apply(cl(x), st, w.reshape(-1).to(DEV), b.reshape(-1).to(DEV), N * T * V, V, C, relu=True)
+    st = K.ln_stats(mk(x), N * T, V, C)
+    yg = K.ln_apply(mk(x), st, w.reshape(-1).to(DEV), b.reshape(-1).to(DEV), N * T * V, V, C, relu=True)
     assert_close(yg.cpu(), y, 1e-5, "ln fwd")
-    dx = K.cl_empty(N, C, T, V, torch.float32, DEV)
+    dx = mk(torch.zeros(N, C, T, V))
     dgb = torch.zeros(2, C * V, device=DEV)
-    K.ln_bwd(cl(dy), cl(x), st, w.reshape(-1).to(DEV), b.reshape(-1).to(DEV), N * T, V, C, dx, mask=2, dgb=dgb)
+    K.ln_bwd(mk(dy), mk(x), st, w.reshape(-1).to(DEV), b.reshape(-1).to(DEV), N * T, V, C, dx, mask=2, dgb=dgb)
     assert_close(dx.cpu(), xr.grad, 1e-4, "ln dx")
     assert_close(dgb[0].cpu().view(C, 1, V), wr.grad, 1e-4, "ln dgamma")
     assert_close(dgb[1].cpu().view(C, 1, V), br.grad, 1e-4, "ln dbeta")

@@ -163,3 +163,35 @@ def test_adam_many_tensors(P):
     for a, b in zip(ref, got):
         torch.testing.assert_close(b.detach(), a.detach(), **TOL)
         assert float(o_got.state[b]["step"]) == 3.0
+
+
+def test_graphed_step_skips_unused_params(P):
+    """parallel.GraphedStep with a parameter that gets no gradient (weight decay on): replays leave it and its
+    Adam state untouched, as eager torch.optim.Adam steps do, and train the others exactly like eager steps."""
+    g0 = torch.Generator().manual_seed(5)
+    w0 = torch.randn(16, 8, generator=g0).to(DEV)
+    u0 = torch.randn(8, generator=g0).to(DEV)
+    xs = [torch.randn(4, 16, generator=g0).to(DEV) for _ in range(4)]
+
+    def make():
+        w = w0.clone().requires_grad_(True)
+        unused = u0.clone().requires_grad_(True)
+        return w, unused
+
+    w_ref, u_ref = make()
+    o_ref = torch.optim.Adam([w_ref, u_ref], lr=1e-2, weight_decay=0.1)
+    for x in xs:
+        o_ref.zero_grad()
+        (x @ w_ref).square().sum().backward()
+        o_ref.step()
+    w, u = make()
+    o = P.optim.Adam([w, u], lr=1e-2, weight_decay=0.1)
+    xin = xs[0].clone()
+    gstep = P.parallel.GraphedStep(lambda: (xin @ w).square().sum(), [w, u], o)  # runs xs[0] eagerly
+    for x in xs[1:]:
+        xin.copy_(x)
+        gstep()
+    torch.cuda.synchronize()
+    assert u.grad is None and torch.equal(u.detach(), u0)
+    assert u not in o.state or float(o.state[u]["step"]) == 0.0
+    torch.testing.assert_close(w.detach(), w_ref.detach(), **TOL)

@@ -50,20 +50,11 @@ def test_plan_packs_equal_single_launches(P, dtype):
         sup = gcn._gsup
         P_, Cout, Cin = Ai.shape[0], gcn.tcn[2].out_channels, gcn.gcn.conv.in_channels
         wg2 = gcn.gcn.conv.weight.detach().reshape(P_ * Cout, Cin).contiguous()
-        wgt = gcn.gcn.conv.weight
-        if pk.gf is not None:  # frame-streaming graph conv: its weight image and the bias through A (kind 3)
-            img = K.pack_gcn_frame(wgt, P_, Cout, Cin, False, dt)
-            assert torch.equal(pk.gf[0][0], img[0]) and pk.gf[0][1:] == img[1:], f"layer {i} frame image"
-            assert torch.equal(pk.gf[1], K.gcn_bias(Ai, gcn.gcn.conv.bias.detach(), 1, Cout)), f"layer {i} bias2d"
-        else:
-            w, b2 = K.gconv_weights(Ai, wg2, sup, Cout, Cin, False, dt, bias=gcn.gcn.conv.bias.detach())
-            # slots j >= deg[joint] are never written (nor read by gconv): compare the used ones
-            used = (torch.arange(sup.J, device=DEV)[None, :] < sup.deg[:, None])
-            assert torch.equal(pk.gw[0][used], w[used]) and torch.equal(pk.gw[1], b2), f"layer {i} graph-conv weights"
-        if pk.gfT is not None:
-            img = K.pack_gcn_frame(wgt, P_, Cout, Cin, True, dt)
-            assert torch.equal(pk.gfT[0], img[0]) and pk.gfT[1:] == img[1:], f"layer {i} frame image (data grad)"
-        elif pk.gwT is not None:
+        w, b2 = K.gconv_weights(Ai, wg2, sup, Cout, Cin, False, dt, bias=gcn.gcn.conv.bias.detach())
+        # slots j >= deg[joint] are never written (nor read by gconv): compare the used ones
+        used = (torch.arange(sup.J, device=DEV)[None, :] < sup.deg[:, None])
+        assert torch.equal(pk.gw[0][used], w[used]) and torch.equal(pk.gw[1], b2), f"layer {i} graph-conv weights"
+        if pk.gwT is not None:
             usedT = (torch.arange(sup.J, device=DEV)[None, :] < sup.rdeg[:, None])
             wT = K.gconv_weights(Ai, wg2, sup, Cout, Cin, True, dt)
             assert torch.equal(pk.gwT[usedT], wT[usedT]), f"layer {i} transposed"

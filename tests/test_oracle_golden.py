@@ -96,7 +96,8 @@ def test_tgcn_batched_and_shared():
         assert_close(b.grad, d[gp + "conv.bias"], 1e-5, "db" + suffix)
 
 
-@pytest.mark.parametrize("case", ["stgcn_bn_1layer", "stgcn_bn_9layer_narrow", "stgcn_ln_9layer_narrow_k69"])
+@pytest.mark.parametrize("case", ["stgcn_bn_1layer", "stgcn_bn_1layer_t64", "stgcn_ln_1layer_t64", "stgcn_bn_9layer_narrow",
+                                  "stgcn_ln_9layer_narrow_k69"])
 def test_stgcn_model(case):
     d = load_golden("model_" + case)
     sd = {k: v.clone().requires_grad_(True) for k, v in sub(d, "sd/").items()}
