@@ -25,6 +25,8 @@ int gcn_tile_launch(const stgcn_gcn_tile_desc& a, hipStream_t s);
 long gcn_tile_row_blocks(int NT, int V, int Cout);
 long wgrad_tile_workspace(const WgradArgs& a, int dtype);
 long wgrad_wide_workspace(const WgradArgs& a, int dtype);
+long wgrad_ring_workspace(const WgradArgs& a, int dtype);
+int wgrad_ring_launch(const WgradArgs& a, int dtype, hipStream_t s);
 int wgrad_wide_launch(const WgradArgs& a, int dtype, hipStream_t s);
 int wgrad_tile_launch(const WgradArgs& a, int dtype, hipStream_t s);
 long wgrad1x1_workspace(const WgradArgs& a, int dtype);
@@ -178,7 +180,9 @@ long stgcn_conv_rows_row_blocks(long M, int cout) { return conv_rows_num_row_blo
 
 long stgcn_conv_wgrad_workspace(const stgcn_wgrad_desc* d, int dtype) {
   if (!d || (dtype != 0 && dtype != 1)) return 0;
-  const long w = wgrad_wide_workspace(*d, dtype);  // >= 128-channel Kt=9 stride-1 path first
+  const long wr = wgrad_ring_workspace(*d, dtype);  // 64 / 128-channel Kt=9 stride-1 DMA-ring path first
+  if (wr > 0) return wr;
+  const long w = wgrad_wide_workspace(*d, dtype);  // >= 128-channel Kt=9 stride-1 path
   if (w > 0) return w;
   const long w1 = wgrad1x1_workspace(*d, dtype);   // 1x1 split-K path
   return w1 > 0 ? w1 : wgrad_tile_workspace(*d, dtype);
@@ -189,6 +193,8 @@ int stgcn_conv_wgrad(const stgcn_wgrad_desc* d, int dtype, void* stream) {
   if (!d || !d->in || !d->dy || !d->dw || d->N <= 0 || d->Kt <= 0 || d->stride <= 0) return STGCN_EBADSHAPE;
   if (d->pro && (!d->pro_a || !d->pro_b || (d->pro == 2 && !d->pro_stats))) return STGCN_EBADSHAPE;
   if (d->out_mode != 0 && d->out_mode != 1) return STGCN_EBADSHAPE;
+  const int rr = wgrad_ring_launch(*d, dtype, STREAM(stream));  // bf16 64 / 128-channel DMA-ring path (needs work)
+  if (rr >= 0) return rr;
   const int rw = wgrad_wide_launch(*d, dtype, STREAM(stream));  // bf16 >= 128-channel ring path (needs work)
   if (rw >= 0) return rw;
   const int r1 = wgrad1x1_launch(*d, dtype, STREAM(stream));  // bf16 1x1 split-K row reduction (needs work)

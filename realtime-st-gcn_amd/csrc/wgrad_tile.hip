@@ -303,6 +303,8 @@ __global__ __launch_bounds__(256, LN ? 1 : 2) void wgrad_tile_kernel(const stgcn
   }
 }
 
+constexpr int RS_MAX = 16;
+
 // Deterministic two-level reduction of the per-block partials:
 //   level 1: part[s][e] = sum_{r = s, s+RS, ...} slab[r][e]     grid (E/1024, RS)
 //   level 2: dw[e]     += sum_s part[s][e]
@@ -311,7 +313,19 @@ __global__ void slab_reduce1_kernel(const float* __restrict__ slab, int R, int R
   const int sidx = blockIdx.y;
   if (e4 >= E) return;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int r = sidx; r < R; r += RS) {
+  int r = sidx;
+  // eight slabs' loads in flight before their (sequential, unchanged-order) adds: one load at a time per thread
+  // left the pass latency-bound (37.7 MB in 12 us at C = 64)
+  for (; r + 7 * RS < R; r += 8 * RS) {
+    float4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(slab + (long)(r + k * RS) * E + e4);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      acc.x += v[k].x; acc.y += v[k].y; acc.z += v[k].z; acc.w += v[k].w;
+    }
+  }
+  for (; r < R; r += RS) {
     const float4 v = *reinterpret_cast<const float4*>(slab + (long)r * E + e4);
     acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
   }
@@ -325,10 +339,15 @@ __global__ void slab_reduce2_kernel(const float* __restrict__ part, int RS, long
   const long e4 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (e4 >= E) return;
   float4 s = mode ? make_float4(0.f, 0.f, 0.f, 0.f) : *reinterpret_cast<const float4*>(dw + e4);
-  for (int r = 0; r < RS; ++r) {
-    const float4 v = *reinterpret_cast<const float4*>(part + (long)r * E + e4);
-    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-  }
+  float4 v[RS_MAX];  // every partial's load in flight first (RS <= RS_MAX), then the adds in the fixed order
+#pragma unroll
+  for (int r = 0; r < RS_MAX; ++r)
+    if (r < RS) v[r] = *reinterpret_cast<const float4*>(part + (long)r * E + e4);
+#pragma unroll
+  for (int r = 0; r < RS_MAX; ++r)
+    if (r < RS) {
+      s.x += v[r].x; s.y += v[r].y; s.z += v[r].z; s.w += v[r].w;
+    }
   if (mode == 0 || Kt == 1) {
     *reinterpret_cast<float4*>(dw + e4) = s;
   } else {  // e = k * CoCi + (co * Cin + ci) -> (co * Cin + ci) * Kt + k; 4 consecutive ci never cross a co row
@@ -340,8 +359,6 @@ __global__ void slab_reduce2_kernel(const float* __restrict__ part, int RS, long
     d[3 * Kt] = s.w;
   }
 }
-
-constexpr int RS_MAX = 16;
 
 struct Plan {
   bool ok;
@@ -434,7 +451,9 @@ int slab_reduce_launch(const float* slab, int R, long E, float* part, float* dw,
   const int RS = R < RS_MAX ? R : RS_MAX;
   const unsigned blocks = (unsigned)((E / 4 + 255) / 256);
   hipLaunchKernelGGL(slab_reduce1_kernel, dim3(blocks, RS), dim3(256), 0, s, slab, R, RS, E, part);
-  hipLaunchKernelGGL(slab_reduce2_kernel, dim3(blocks), dim3(256), 0, s, (const float*)part, RS, E, dw, mode, Kt, CoCi);
+  // level 2 reads RS * E floats: 64-thread blocks, four times as many CUs as 256-thread ones at E = 36 864
+  hipLaunchKernelGGL(slab_reduce2_kernel, dim3((unsigned)((E / 4 + 63) / 64)), dim3(64), 0, s, (const float*)part, RS, E,
+                     dw, mode, Kt, CoCi);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
 
@@ -466,7 +485,7 @@ int wgrad_tile_launch(const stgcn_wgrad_desc& a, int dtype, hipStream_t s) {
   const unsigned blocks = (unsigned)((E / 4 + 255) / 256);
   hipLaunchKernelGGL(slab_reduce1_kernel, dim3(blocks, RS), dim3(256), 0, s, (const float*)p.g.slab, p.g.R, RS, E,
                      part);
-  hipLaunchKernelGGL(slab_reduce2_kernel, dim3(blocks), dim3(256), 0, s, (const float*)part, RS, E, a.dw, a.out_mode,
-                     a.Kt, (long)a.Cout * a.Cin);
+  hipLaunchKernelGGL(slab_reduce2_kernel, dim3((unsigned)((E / 4 + 63) / 64)), dim3(64), 0, s, (const float*)part, RS, E,
+                     a.dw, a.out_mode, a.Kt, (long)a.Cout * a.Cin);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }

@@ -286,7 +286,7 @@ def test_aagcn_bf16_vs_fp32_per_tensor(P, aagcn_ref64):
 @pytest.mark.parametrize("cin,cout,stride,T", [(64, 64, 1, 300), (128, 256, 2, 150)])
 def test_agcn_layer_bf16_vs_fp32_per_tensor(P, cin, cout, stride, T):
     """Per tensor where bf16 IS stable: one AgcnLayer at config-5 widths (N = 8), the bf16 path against the HIP fp32
-    path on the same inputs, every gradient with cosine >= 0.95 (except the exact zeros: BN-fed conv biases, phi's
+    path on the same inputs, every gradient with cosine >= 0.98 (except the exact zeros: BN-fed conv biases, phi's
     bias).  A single layer does not amplify rounding the way the 9-layer 2-stream model does (fp64 with 2^-9 input
     noise: every gradient cosine >= 0.99 here, vs a median of 0.13 for the whole model,
     test_aagcn_sensitivity.py), so this pins the bf16 attention and per-sample-A kernels per tensor."""
@@ -317,6 +317,6 @@ def test_agcn_layer_bf16_vs_fp32_per_tensor(P, cin, cout, stride, T):
         cos = torch.nn.functional.cosine_similarity(got["bf16"][k].reshape(1, -1), ref.reshape(1, -1)).item()
         print(f"[err] agcn layer {cin}->{cout} bf16 vs fp32 {k}: cos {cos:.5f} L2 {_l2(got['bf16'][k], ref):.2e}",
               flush=True)
-        if not cos >= 0.95:
+        if not cos >= 0.98:  # r05a: worst 0.9917 (phi.weight at 128 -> 256)
             bad.append((k, round(cos, 4)))
     assert not bad, f"bf16 AgcnLayer vs the HIP fp32 path: {bad}"
