@@ -1279,7 +1279,10 @@ WGG wplan2(const stgcn_gconv_wgrad_desc& a, int cob) {
   const long target = cob == 64 ? 512 : 256;  // COB 64: 3 register-staged / 2 DMA-ring blocks fit a CU
   // DMA ring: block target by the group count, measured per layer (targets 512 / 1024 / 2048): C = 64
   // (25 groups) 49 / 40 / 56 us, C = 128 64 / 81 / 75 us, C = 256 108 / 113 / 130 us
-  const long t3 = groups <= 32 ? 1024 : groups < 200 ? 512 : STGCN_W3_WIDE_TARGET;
+#ifndef STGCN_W3_NARROW_TARGET
+#define STGCN_W3_NARROW_TARGET 1024
+#endif
+  const long t3 = groups <= 32 ? STGCN_W3_NARROW_TARGET : groups < 200 ? 512 : STGCN_W3_WIDE_TARGET;
   long R = (cob == 64 && w3_ok(a)) ? (t3 + groups - 1) / groups : (target + groups - 1) / groups;
   if (R > g.ntile) R = g.ntile;
   if (R < 1) R = 1;
@@ -1382,7 +1385,7 @@ int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s
       g.slab = reinterpret_cast<float*>(a.work);
       g.rowpart = a.rowsum ? g.slab + (long)g.R * E : nullptr;
     }
-    const bool deep = direct && STGCN_W3_DEEP;  // one block per CU, deeper ring
+    const bool deep = (direct || STGCN_W3_DEEP > 1) && STGCN_W3_DEEP;  // one block per CU, deeper ring
     const size_t lds = ring ? (size_t)(deep ? 160 : 80) * 1024 : 2 * (size_t)(cob / 32 + 2 * J2) * w2m(cob) * WPR;
     auto* k = ring ? (deep ? gconv_wgrad3_kernel<160 * 1024> : gconv_wgrad3_kernel<80 * 1024>) : gconv_wgrad2_kernel<64>;
     if (stgcn_lds_attr((const void*)k, 160 * 1024, s)) return STGCN_EHIP;
