@@ -72,7 +72,7 @@ constexpr int RSH = 2 * C + 16;        // h row bytes (144: conflict-free ds_rea
 // per-joint LDS tables read by 32 lanes of 32 different joints at once: row strides padded off the 256-B
 // bank period (16 B further per joint), or every lane of a ds_read_b128 group hits the same four banks
 constexpr int CBP = C + 4;             // BN: bias2d * scale + shift row, floats
-constexpr int CG2 = C + 2;             // LN: (gamma2, beta2) row, float2
+constexpr int CGP = C + 4;             // LN: gamma2 / beta2 row, floats (two planes)
 constexpr int ZSB = 32 * 16;  // BN: per temporal-conv wave, 32 float4 BN2 partials
 constexpr int PANEL = 32 * 64;         // [32 joint rows][32 ch] bf16
 constexpr int SLOTS = FPW * G;         // panel slots per GCN wave (one step's panels)
@@ -91,6 +91,7 @@ DEV void static_for(F&& f) {
 }
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x2n __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
@@ -172,12 +173,12 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
   float* const sSc = reinterpret_cast<float*>(smem + g.off_tab);  // [64] BN1 scale
   float* const sBp = sSc + C;                                     // [V][CBP] bias2d * scale + shift
   char* const sH = smem + g.off_h;                                // [RF * V][RSH]
-  float2* const sRed = reinterpret_cast<float2*>(smem + g.off_red);  // BN: [2][64] (sum, sum of squares);
-  // LN: [row tile][frame slot k < 3][channel half] (sum, sum of squares) of the step's output rows
-  float2* const sG2 = reinterpret_cast<float2*>(smem + g.off_tab);     // LN: [V][CG2] (gamma2, beta2)
-  unsigned* const sCnt = reinterpret_cast<unsigned*>(smem + g.off_red + 2 * RT * 3 * 2 * 8);  // LN arrivals
+  float* const sGam = reinterpret_cast<float*>(smem + g.off_tab);  // LN: [V][CGP] gamma2, then [V][CGP] beta2
+  float* const sBet = sGam + V * CGP;
+  float2* const sPart = reinterpret_cast<float2*>(smem + g.off_red);  // LN: [TCN wave][4 frames] (sum, sum of squares)
+  unsigned* const sCnt = reinterpret_cast<unsigned*>(smem + g.off_red + NWT * 4 * 8);  // LN: per TCN wave, last step posted
   const int vrs = V * RSH;  // bytes per h frame
-  float* const sTb = reinterpret_cast<float*>(smem + g.off_tab + (LN ? V * CG2 * 8 : (C + V * CBP) * 4));  // [64] tcn bias
+  float* const sTb = reinterpret_cast<float*>(smem + g.off_tab + (LN ? 2 * V * CGP * 4 : (C + V * CBP) * 4));  // [64] tcn bias
 
   // ---- per block: W' slice, BN1 tables, zeroed panel rings (rows V..31 stay zero)
   {
@@ -185,8 +186,11 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
     uint4* wdst = reinterpret_cast<uint4*>(sW);
     for (int e = tid; e < 2 * K16 * 64; e += NW * 64) wdst[e] = wsrc[e];
     if (LN) {
-      for (int e = tid; e < V * C; e += NW * 64) sG2[(e / C) * CG2 + e % C] = make_float2(a.ln2_g[e], a.ln2_b[e]);
-      if (tid == 0) *sCnt = 0u;
+      for (int e = tid; e < V * C; e += NW * 64) {
+        sGam[(e / C) * CGP + e % C] = a.ln2_g[e];
+        sBet[(e / C) * CGP + e % C] = a.ln2_b[e];
+      }
+      if (tid < NWT) sCnt[tid] = 0u;
     } else {
       for (int c = tid; c < C; c += NW * 64) sSc[c] = a.n1_scale[c];
       for (int e = tid; e < V * C; e += NW * 64) {
@@ -351,31 +355,32 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
           }
         const float cnt = (float)(V * C);
         float mean[FPW], rstd[FPW];
-        {
+        {  // two-pass statistics on channel pairs (packed adds / FMAs)
           float sum[FPW];
 #pragma unroll
           for (int i = 0; i < FPW; ++i) {
-            sum[i] = 0.f;
+            f32x2 s2 = {0.f, 0.f};
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
-              for (int r = 0; r < 16; ++r) sum[i] += accf[i][t][r];
-            sum[i] = jv ? sum[i] : 0.f;
+              for (int r = 0; r < 16; r += 2) s2 += f32x2{accf[i][t][r], accf[i][t][r + 1]};
+            sum[i] = jv ? s2.x + s2.y : 0.f;
           }
 #pragma unroll
           for (int i = 0; i < FPW; ++i) mean[i] = wave_total(sum[i]) / cnt;
           float sq[FPW];
 #pragma unroll
           for (int i = 0; i < FPW; ++i) {
-            sq[i] = 0.f;
+            const f32x2 m2 = {mean[i], mean[i]};
+            f32x2 q2 = {0.f, 0.f};
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
-              for (int r = 0; r < 16; ++r) {
-                const float d = accf[i][t][r] - mean[i];
-                sq[i] = fmaf(d, d, sq[i]);
+              for (int r = 0; r < 16; r += 2) {
+                const f32x2 d = f32x2{accf[i][t][r], accf[i][t][r + 1]} - m2;
+                q2 = __builtin_elementwise_fma(d, d, q2);
               }
-            sq[i] = jv ? sq[i] : 0.f;
+            sq[i] = jv ? q2.x + q2.y : 0.f;
           }
 #pragma unroll
           for (int i = 0; i < FPW; ++i) rstd[i] = 1.f / sqrtf(wave_total(sq[i]) / (cnt - 1.f) + 1e-5f);
@@ -409,19 +414,25 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
             }
           }
           if (jv) {
+            // h = relu(fma(fma(g, A, B), gamma, beta)), A = rstd, B = -mean * rstd, on channel pairs
             char* hr = hrow + lr * RSH;
+            const f32x2 A2 = {rstd[i], rstd[i]}, B2 = {-mean[i] * rstd[i], -mean[i] * rstd[i]};
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
               for (int q4 = 0; q4 < 4; ++q4) {
                 const float4 gg = g4[t][q4], bb = b4[t][q4];
-                const float v[4] = {accf[i][t][4 * q4], accf[i][t][4 * q4 + 1], accf[i][t][4 * q4 + 2],
-                                    accf[i][t][4 * q4 + 3]};
+                const f32x2 v01 = {accf[i][t][4 * q4], accf[i][t][4 * q4 + 1]};
+                const f32x2 v23 = {accf[i][t][4 * q4 + 2], accf[i][t][4 * q4 + 3]};
+                const f32x2 h01 = __builtin_elementwise_fma(__builtin_elementwise_fma(v01, A2, B2), f32x2{gg.x, gg.y},
+                                                            f32x2{bb.x, bb.y});
+                const f32x2 h23 = __builtin_elementwise_fma(__builtin_elementwise_fma(v23, A2, B2), f32x2{gg.z, gg.w},
+                                                            f32x2{bb.z, bb.w});
                 bf16x4 hv;
-                hv[0] = (bf16)fmaxf(fmaf((v[0] - mean[i]) * rstd[i], gg.x, bb.x), 0.f);
-                hv[1] = (bf16)fmaxf(fmaf((v[1] - mean[i]) * rstd[i], gg.y, bb.y), 0.f);
-                hv[2] = (bf16)fmaxf(fmaf((v[2] - mean[i]) * rstd[i], gg.z, bb.z), 0.f);
-                hv[3] = (bf16)fmaxf(fmaf((v[3] - mean[i]) * rstd[i], gg.w, bb.w), 0.f);
+                hv[0] = (bf16)fmaxf(h01.x, 0.f);
+                hv[1] = (bf16)fmaxf(h01.y, 0.f);
+                hv[2] = (bf16)fmaxf(h23.x, 0.f);
+                hv[3] = (bf16)fmaxf(h23.y, 0.f);
                 *reinterpret_cast<bf16x4*>(hr + (32 * t + 8 * q4 + 4 * lh) * 2) = hv;
               }
           }
@@ -482,295 +493,391 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
   // =============================== TCN waves: temporal conv ===============================
   const bf16* __restrict__ wt = reinterpret_cast<const bf16*>(a.wt_frag);
   bf16* __restrict__ zg = reinterpret_cast<bf16*>(a.z);
-  const int ct = wave & 1, rh = wave >> 1;
-  // this lane's output rows (step-relative frame fo, joint w) per row tile; rows past CF*V clamp to row 0
-  int fo_[RT], hw_[RT], jw_[RT];
-  bool rok[RT];
+  if constexpr (LN) {
+    // LayerNorm: frame-aligned row tiles.  TCN wave w = (channel half ct = w & 1, frame group fg = w >> 1) owns
+    // row tile i = frame 4fg + i of every step (lane = joint, lanes >= V pad) for its 32 output channels, so a
+    // frame's LN2 statistics are one wave reduction per (frame, channel half) plus ONE exchange with the partner
+    // wave w ^ 1 (same frames, other channels) through LDS: no 4-wave hand-off and no partials of frames cut by
+    // 32-row tiles (the BatchNorm layout's tiles straddle frames: its LN form needed per-tile partials of <= 3
+    // frames, a 4-wave arrival counter and a combine, ~40 % of the role's cycles).  256 MFMA rows per 200 output
+    // rows instead of 224; one weight fragment per k-step as in the BatchNorm layout (both channel halves per
+    // wave doubled the per-CU vector-memory traffic of the weight stream and measured slower).
+    const int ct = wave & 1, fg = wave >> 1;
+    const int jw = min(lr, V - 1);
+    const bool jv = lr < V;
+    const int hw = jw * RSH + lh * 16;
+    const int wl = ct * 4 * 512 + lane * 8;  // 1-KiB block [dt][ct][ks] of the [9][2][4] image
+    int wcur = wl;
+    auto load_w = [&](int k) {
+      const int dt = k >> 2, ks = k & 3;
+      int o = wcur + dt * 8 * 512;
+      asm volatile("" : "+v"(o));
+      return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(wt + o + ks * 512));
+    };
+    static_assert(KSTEPS % NB == 0, "the weight ring runs on across steps");
+    bf16x8 fw[NB];
 #pragma unroll
-  for (int i = 0; i < RT; ++i) {
-    const int r = (rh * RT + i) * 32 + lr;
-    rok[i] = r < CF * V;
-    const int rr = rok[i] ? r : 0;
-    fo_[i] = rr / V;
-    jw_[i] = rr - fo_[i] * V;
-    hw_[i] = jw_[i] * RSH + lh * 16;
-  }
-  const int wlane = ct * 4 * 512 + lane * 8;  // 1-KiB block [dt][ct][ks] of the [9][2][4] image
-  int wcur = wlane;  // element offset re-materialised per step (opaque): LICM would otherwise hoist all 36
-                     // weight fragments of the step out of the step loop and spill them.  An integer, not the
-                     // pointer: a pointer laundered through asm loses its address space, and the loads become
-                     // flat loads that also count on lgkmcnt (every LDS wait then drained the weight ring)
-  auto load_w = [&](int s) {
-    const int dt = s >> 2, ks = s & 3;
-    int o = wcur + dt * 8 * 512;  // per-load opaque tap base (ks offsets fit the instruction's immediate)
-    asm volatile("" : "+v"(o));
-    return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(wt + o + ks * 512));
-  };
-  // row tiles of this wave: CF*V rows = nrt tiles of 32, the first RT to row half 0
-  const int nrt = (CF * V + 31) / 32;
-  const int rtn = rh == 0 ? min(RT, nrt) : nrt - RT;
-  static_assert(KSTEPS % NB == 0, "the weight ring runs on across steps");
-  bf16x8 fw[NB];  // k-step k's fragment in slot k % NB, the same every step
-#pragma unroll
-  for (int k = 0; k < NB - 1; ++k) fw[k] = load_w(k);
-  if (DBG & 32) fw[NB - 1] = load_w(NB - 1);
-  // BN2 partials: per row half, the (count, mean, M2) of the run's rows of each channel (row block * 2 + rh of
-  // stats): per-lane sums over the whole run in registers, reduced across the lanes once at the run's end (a
-  // per-step reduction measured 28.6 K of the role's 147 K cycles)
-  float4* const st_out = a.stats ? reinterpret_cast<float4*>(a.stats) + ((long)blockIdx.x * 2 + rh) * C : nullptr;
-  const f32x16 zero = {};
-  unsigned arrivals = 0;  // LN: TCN-wave arrivals expected at the counter so far
-  // LN: statistics shifted by the pivot mean_c(bias) (the same constant in every wave), so a large common
-  // bias does not cancel catastrophically in sum(z^2) - sum(z) * mean
-  const float piv = LN ? wave_total(sTb[lane]) * (1.f / C) : 0.f;
-  char* const zs = smem + g.off_zs + wave * ZSB;  // BN: this wave's partials scratch
-  lds_barrier();  // S_0
-  // the step loop per row-tile count (compile-time: no per-k-step branches in the MFMA stream)
-  auto tcn_run = [&]<int RTN>() {
-    float s1[16], s2[16];  // BN: per-lane (sum, sum of squares) of z - bias over the run's rows
-#pragma unroll
-    for (int r = 0; r < 16; ++r) s1[r] = s2[r] = 0.f;
-    int cnt_run = 0;
+    for (int k = 0; k < (DBG & 32 ? NB : NB - 1); ++k) fw[k] = load_w(k);
+    const f32x16 zero = {};
+    // statistics shifted by the pivot mean_c(bias) (the same constant in every wave), so a large common bias
+    // does not cancel catastrophically in sum(z^2) - sum(z) * mean
+    const float piv = wave_total(sTb[lane]) * (1.f / C);
+    const float cnt = (float)(V * C);
+    float2* const myPart = sPart + wave * 4;
+    const float2* const pePart = sPart + (wave ^ 1) * 4;
+    lds_barrier();  // S_0
     for (int s = 1; s <= nsteps; ++s) {
-      if (DBG & 2) {
-        lds_barrier();
-        continue;
-      }
-      wcur = wlane;
+      wcur = wl;
       asm volatile("" : "+v"(wcur));
-      const int f0 = R0 + CF * (s - 1);           // first output frame of the step
-      const int base = (CF * (s - 1)) % RF;       // ring slot of run frame 8(s-1) (= output frame f0 - 4)
-      // byte offset of h row (frame f0 + fo + dt - 4, joint w) = slot(base + fo + dt) * vrs + w * RSH
-      int q_[RT];
+      const int f0 = R0 + CF * (s - 1);      // first output frame of the step
+      const int base = (CF * (s - 1)) % RF;  // ring slot of run frame 8(s-1) (= output frame f0 - 4)
+      int q_[4];
 #pragma unroll
-      for (int i = 0; i < RT; ++i) q_[i] = base + fo_[i];
+      for (int i = 0; i < 4; ++i) q_[i] = base + 4 * fg + i;
       auto hoff = [&](int i, int dt) {
         const int sl = q_[i] + dt;
-        return (sl >= RF ? sl - RF : sl) * vrs + hw_[i];
+        return (sl >= RF ? sl - RF : sl) * vrs + hw;
       };
-      f32x16 acc[RT];
+      f32x16 acc[4];
 #pragma unroll
-      for (int i = 0; i < RT; ++i) acc[i] = zero;
-      bf16x8 fb[3][RT];  // h fragments two k-steps ahead (LDS latency under eight waves' traffic)
-      int ad[RT];  // h byte offsets of the current tap (recomputed per tap, opaque to LICM: hoisting all 36
-                   // k-steps' addresses out of the unrolled loop would spill)
+      for (int i = 0; i < 4; ++i) acc[i] = zero;
+      bf16x8 fb[3][4];
+      int ad[4];
 #pragma unroll
-      for (int i = 0; i < RT; ++i) {
+      for (int i = 0; i < 4; ++i) {
         ad[i] = hoff(i, 0);
         asm volatile("" : "+v"(ad[i]));
-        if (i < RTN) {
-          fb[0][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sH + ad[i]));
-          fb[1][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sH + ad[i] + 32));
-          if (DBG & 64) fb[2][i] = fb[0][i];
-        }
+        fb[0][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sH + ad[i]));
+        fb[1][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sH + ad[i] + 32));
+        if (DBG & 64) fb[2][i] = fb[0][i];
       }
       const long long pk0 = ptime();
       static_for<KSTEPS>([&]<int k>() {
-        if constexpr (!(DBG & 32)) fw[(k + NB - 1) % NB] = load_w((k + NB - 1) % KSTEPS);  // runs into the next step's first k-steps
+        if constexpr (!(DBG & 32)) fw[(k + NB - 1) % NB] = load_w((k + NB - 1) % KSTEPS);  // runs into the next step
         if constexpr (k + 2 < KSTEPS && !(DBG & 64)) {
           constexpr int dt2 = (k + 2) >> 2, ks2 = (k + 2) & 3;
           if constexpr (ks2 == 0) {
 #pragma unroll
-            for (int i = 0; i < RT; ++i) {
+            for (int i = 0; i < 4; ++i) {
               ad[i] = hoff(i, dt2);
               asm volatile("" : "+v"(ad[i]));
             }
           }
 #pragma unroll
-          for (int i = 0; i < RT; ++i)
-            if (i < RTN)
-              fb[(k + 2) % 3][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sH + ad[i] + ks2 * 32));
+          for (int i = 0; i < 4; ++i)
+            fb[(k + 2) % 3][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sH + ad[i] + ks2 * 32));
         }
 #pragma unroll
-        for (int i = 0; i < RT; ++i)
-          if (i < RTN) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[k % NB], fb[k % 3][i], acc[i], 0, 0, 0);
+        for (int i = 0; i < 4; ++i)
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[k % NB], fb[k % 3][i], acc[i], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
       });
       const long long pk1 = ptime();
       pa[0] += pk1 - pk0;
-      // epilogue: acc[i][r] = out^T[co = 32ct + 8(r>>2) + 4lh + (r&3)][row (rh*RT + i)*32 + lr]
-      const int vrows = min(CF, R1 - f0) * V;
+      // epilogue: acc[i][q] = out^T[co = 32ct + 8(q>>2) + 4lh + (q&3)][frame 4fg+i, joint lr]
+      const int nfv = min(CF, R1 - f0);  // frames of the step inside the run
       bf16* zt = zg + ((long)n * T + f0) * V * a.z_ld;
-      // the temporal-conv bias from LDS: a global load here would sit behind the weight-fragment prefetch and,
-      // on gfx9's single in-order vmcnt, behind the z stores of the row tiles before it (each tile's stores
-      // were waited out by the next: measured 60 of the 84 us of the temporal-conv role)
+      // the residual rows first: their L2 latency runs under the statistics
+      const bf16* xres = reinterpret_cast<const bf16*>(a.x) + ((long)n * T + f0) * V * a.x_ld;
+      bf16x4 rv[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int fo = 4 * fg + i;
+        const bool ok = jv && fo < nfv && a.residual && !(DBG & 4);
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+          const bf16x4 zr = {};
+          rv[i][q4] = ok ? *reinterpret_cast<const bf16x4*>(xres + (long)(fo * V + lr) * a.x_ld + 32 * ct + 8 * q4 + 4 * lh)
+                         : zr;
+        }
+      }
+      // d = z - piv (bias added); each frame's (sum, sum of squares) of d over this wave's 32 x V values
       float tb[16];
 #pragma unroll
       for (int q4 = 0; q4 < 4; ++q4) {
         const float4 b4 = *reinterpret_cast<const float4*>(sTb + 32 * ct + 8 * q4 + 4 * lh);
-        tb[4 * q4] = b4.x;
-        tb[4 * q4 + 1] = b4.y;
-        tb[4 * q4 + 2] = b4.z;
-        tb[4 * q4 + 3] = b4.w;
+        tb[4 * q4] = b4.x - piv;
+        tb[4 * q4 + 1] = b4.y - piv;
+        tb[4 * q4 + 2] = b4.z - piv;
+        tb[4 * q4 + 3] = b4.w - piv;
       }
-      if constexpr (LN) {
-        // the residual rows first: their L2 latency runs under the statistics phase
-        const bf16* xres = reinterpret_cast<const bf16*>(a.x) + ((long)n * T + f0) * V * a.x_ld;
-        bf16x4 rv_[RT][4];
+      // (vector forms: the fp32 adds / FMAs issue as packed 2-wide VALU ops)
+      f32x16 tbv;
 #pragma unroll
-        for (int i = 0; i < RT; ++i) {
-          const int r = (rh * RT + i) * 32 + lr;
-          const bool ok = i < RTN && rok[i] && r < vrows && a.residual && !(DBG & 4);
+      for (int q = 0; q < 16; ++q) tbv[q] = tb[q];
+      float ts[4], tq[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        acc[i] += tbv;
+        f32x2 su = {0.f, 0.f}, sq = {0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < 16; q += 2) {
+          const f32x2 d = {acc[i][q], acc[i][q + 1]};
+          su += d;
+          sq = __builtin_elementwise_fma(d, d, sq);
+        }
+        const bool ok = jv && 4 * fg + i < nfv;
+        ts[i] = ok ? su.x + su.y : 0.f;
+        tq[i] = ok ? sq.x + sq.y : 0.f;
+      }
+      if (!(DBG & 8)) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          ts[i] = wave_total(ts[i]);
+          tq[i] = wave_total(tq[i]);
+        }
+      }
+      // exchange with the partner wave (same frames, other 32 channels): post, then wait for its post of this
+      // step.  The partner's slot is rewritten only after the step's closing barrier, which follows this read.
+      if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) myPart[i] = make_float2(ts[i], tq[i]);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const long long pl0 = ptime();
+      pa[1] += pl0 - pk1;
+      if (lane == 0) __hip_atomic_store(sCnt + wave, (unsigned)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      while (__hip_atomic_load(sCnt + (wave ^ 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < (unsigned)s)
+        __builtin_amdgcn_s_sleep(1);
+      const long long pl1 = ptime();
+      pa[5] += pl1 - pl0;
+      float dmean[4], rstd[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float2 p = pePart[i];
+        const float su = ts[i] + p.x, sq = tq[i] + p.y;  // a + b == b + a: both waves get identical totals
+        dmean[i] = su / cnt;
+        rstd[i] = 1.f / sqrtf(fmaxf(sq - su * dmean[i], 0.f) / (cnt - 1.f) + 1e-5f);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int fo = 4 * fg + i;
+        if (fo >= nfv || !jv) continue;
+        const int r = fo * V + lr;
+        if (a.u_out) {  // training forward: u = z (pre-LN2, bias included) rows and the frame's LN2 statistics
+          bf16* ur = reinterpret_cast<bf16*>(a.u_out) + (((long)n * T + f0) * V + r) * a.u_ld + 32 * ct + 4 * lh;
 #pragma unroll
           for (int q4 = 0; q4 < 4; ++q4) {
-            const bf16x4 zr = {};
-            rv_[i][q4] = ok ? *reinterpret_cast<const bf16x4*>(xres + (long)r * a.x_ld + 32 * ct + 8 * q4 + 4 * lh) : zr;
+            bf16x4 uv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) uv[e] = (bf16)(acc[i][4 * q4 + e] + piv);
+            *reinterpret_cast<bf16x4*>(ur + 8 * q4) = uv;
           }
+          if (ct == 0 && lane == 0)
+            reinterpret_cast<float2*>(a.st2_out)[(long)n * T + f0 + fo] = make_float2(piv + dmean[i], rstd[i]);
         }
-        // z = acc + bias; per row tile ti and each of the <= 3 frames its 32 rows touch (V > 16): the
-        // (sum, sum of squares) of this wave's 32 channels over the tile's rows of that frame -> LDS,
-        // shifted by the pivot
+        // y = relu(((d - dmean) * rstd) * gamma + beta + x) as relu(fma(fma(d, A, B), gamma, beta) + x), A = rstd,
+        // B = -dmean * rstd, on pairs of channels (packed FMAs)
+        const f32x2 A2 = {rstd[i], rstd[i]}, B2 = {-dmean[i] * rstd[i], -dmean[i] * rstd[i]};
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+          const int co = 32 * ct + 8 * q4 + 4 * lh;
+          const float4 g4 = *reinterpret_cast<const float4*>(sGam + jw * CGP + co);
+          const float4 b4 = *reinterpret_cast<const float4*>(sBet + jw * CGP + co);
+          const f32x2 g01 = {g4.x, g4.y}, g23 = {g4.z, g4.w}, b01 = {b4.x, b4.y}, b23 = {b4.z, b4.w};
+          const f32x2 r01 = {(float)rv[i][q4][0], (float)rv[i][q4][1]}, r23 = {(float)rv[i][q4][2], (float)rv[i][q4][3]};
+          const f32x2 d01 = {acc[i][4 * q4], acc[i][4 * q4 + 1]}, d23 = {acc[i][4 * q4 + 2], acc[i][4 * q4 + 3]};
+          f32x2 t01 = __builtin_elementwise_fma(__builtin_elementwise_fma(d01, A2, B2), g01, b01) + r01;
+          f32x2 t23 = __builtin_elementwise_fma(__builtin_elementwise_fma(d23, A2, B2), g23, b23) + r23;
+          bf16x4 o;
+          o[0] = (bf16)fmaxf(t01.x, 0.f);
+          o[1] = (bf16)fmaxf(t01.y, 0.f);
+          o[2] = (bf16)fmaxf(t23.x, 0.f);
+          o[3] = (bf16)fmaxf(t23.y, 0.f);
+          *reinterpret_cast<bf16x4*>(zt + (long)r * a.z_ld + co) = o;
+        }
+      }
+      const long long pl2 = ptime();
+      pa[4] += pl2 - pl1;
+      lds_barrier();  // S_s: the GCN waves may overwrite the frames this step read
+      pa[2] += ptime() - pl2;
+    }
+    if constexpr (PROF) prof_out();
+    return;
+  } else {
+    const int ct = wave & 1, rh = wave >> 1;
+    // this lane's output rows (step-relative frame fo, joint w) per row tile; rows past CF*V clamp to row 0
+    int fo_[RT], hw_[RT], jw_[RT];
+    bool rok[RT];
+#pragma unroll
+    for (int i = 0; i < RT; ++i) {
+      const int r = (rh * RT + i) * 32 + lr;
+      rok[i] = r < CF * V;
+      const int rr = rok[i] ? r : 0;
+      fo_[i] = rr / V;
+      jw_[i] = rr - fo_[i] * V;
+      hw_[i] = jw_[i] * RSH + lh * 16;
+    }
+    const int wlane = ct * 4 * 512 + lane * 8;  // 1-KiB block [dt][ct][ks] of the [9][2][4] image
+    int wcur = wlane;  // element offset re-materialised per step (opaque): LICM would otherwise hoist all 36
+                       // weight fragments of the step out of the step loop and spill them.  An integer, not the
+                       // pointer: a pointer laundered through asm loses its address space, and the loads become
+                       // flat loads that also count on lgkmcnt (every LDS wait then drained the weight ring)
+    auto load_w = [&](int s) {
+      const int dt = s >> 2, ks = s & 3;
+      int o = wcur + dt * 8 * 512;  // per-load opaque tap base (ks offsets fit the instruction's immediate)
+      asm volatile("" : "+v"(o));
+      return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(wt + o + ks * 512));
+    };
+    // row tiles of this wave: CF*V rows = nrt tiles of 32, the first RT to row half 0
+    const int nrt = (CF * V + 31) / 32;
+    const int rtn = rh == 0 ? min(RT, nrt) : nrt - RT;
+    static_assert(KSTEPS % NB == 0, "the weight ring runs on across steps");
+    bf16x8 fw[NB];  // k-step k's fragment in slot k % NB, the same every step
+#pragma unroll
+    for (int k = 0; k < NB - 1; ++k) fw[k] = load_w(k);
+    if (DBG & 32) fw[NB - 1] = load_w(NB - 1);
+    // BN2 partials: per row half, the (count, mean, M2) of the run's rows of each channel (row block * 2 + rh of
+    // stats): per-lane sums over the whole run in registers, reduced across the lanes once at the run's end (a
+    // per-step reduction measured 28.6 K of the role's 147 K cycles)
+    float4* const st_out = a.stats ? reinterpret_cast<float4*>(a.stats) + ((long)blockIdx.x * 2 + rh) * C : nullptr;
+    const f32x16 zero = {};
+    char* const zs = smem + g.off_zs + wave * ZSB;  // BN: this wave's partials scratch
+    lds_barrier();  // S_0
+    // the step loop per row-tile count (compile-time: no per-k-step branches in the MFMA stream)
+    auto tcn_run = [&]<int RTN>() {
+      float s1[16], s2[16];  // BN: per-lane (sum, sum of squares) of z - bias over the run's rows
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s1[r] = s2[r] = 0.f;
+      int cnt_run = 0;
+      for (int s = 1; s <= nsteps; ++s) {
+        if (DBG & 2) {
+          lds_barrier();
+          continue;
+        }
+        wcur = wlane;
+        asm volatile("" : "+v"(wcur));
+        const int f0 = R0 + CF * (s - 1);           // first output frame of the step
+        const int base = (CF * (s - 1)) % RF;       // ring slot of run frame 8(s-1) (= output frame f0 - 4)
+        // byte offset of h row (frame f0 + fo + dt - 4, joint w) = slot(base + fo + dt) * vrs + w * RSH
+        int q_[RT];
+#pragma unroll
+        for (int i = 0; i < RT; ++i) q_[i] = base + fo_[i];
+        auto hoff = [&](int i, int dt) {
+          const int sl = q_[i] + dt;
+          return (sl >= RF ? sl - RF : sl) * vrs + hw_[i];
+        };
+        f32x16 acc[RT];
+#pragma unroll
+        for (int i = 0; i < RT; ++i) acc[i] = zero;
+        bf16x8 fb[3][RT];  // h fragments two k-steps ahead (LDS latency under eight waves' traffic)
+        int ad[RT];  // h byte offsets of the current tap (recomputed per tap, opaque to LICM: hoisting all 36
+                     // k-steps' addresses out of the unrolled loop would spill)
 #pragma unroll
         for (int i = 0; i < RT; ++i) {
-          if (i >= RTN) break;
-          const int r = (rh * RT + i) * 32 + lr;
-          const bool ok = rok[i] && r < vrows;
-          float su = 0.f, sq = 0.f;
-#pragma unroll
-          for (int q = 0; q < 16; ++q) {
-            acc[i][q] += tb[q];
-            const float d = acc[i][q] - piv;
-            su += d;
-            sq = fmaf(d, d, sq);
+          ad[i] = hoff(i, 0);
+          asm volatile("" : "+v"(ad[i]));
+          if (i < RTN) {
+            fb[0][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sH + ad[i]));
+            fb[1][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sH + ad[i] + 32));
+            if (DBG & 64) fb[2][i] = fb[0][i];
           }
-          const int ti = rh * RT + i, flo = ti * 32 / V;
+        }
+        const long long pk0 = ptime();
+        static_for<KSTEPS>([&]<int k>() {
+          if constexpr (!(DBG & 32)) fw[(k + NB - 1) % NB] = load_w((k + NB - 1) % KSTEPS);  // runs into the next step's first k-steps
+          if constexpr (k + 2 < KSTEPS && !(DBG & 64)) {
+            constexpr int dt2 = (k + 2) >> 2, ks2 = (k + 2) & 3;
+            if constexpr (ks2 == 0) {
 #pragma unroll
-          for (int k = 0; k < 3; ++k) {
-            const bool m = ok && fo_[i] == flo + k;
-            float ts = 0.f, tq = 0.f;
-            if (!(DBG & 8)) {
-              ts = wave_total(m ? su : 0.f);
-              tq = wave_total(m ? sq : 0.f);
+              for (int i = 0; i < RT; ++i) {
+                ad[i] = hoff(i, dt2);
+                asm volatile("" : "+v"(ad[i]));
+              }
             }
-            if (lane == 0) sRed[(ti * 3 + k) * 2 + ct] = make_float2(ts, tq);
+#pragma unroll
+            for (int i = 0; i < RT; ++i)
+              if (i < RTN)
+                fb[(k + 2) % 3][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sH + ad[i] + ks2 * 32));
           }
+#pragma unroll
+          for (int i = 0; i < RT; ++i)
+            if (i < RTN) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[k % NB], fb[k % 3][i], acc[i], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        });
+        const long long pk1 = ptime();
+        pa[0] += pk1 - pk0;
+        // epilogue: acc[i][r] = out^T[co = 32ct + 8(r>>2) + 4lh + (r&3)][row (rh*RT + i)*32 + lr]
+        const int vrows = min(CF, R1 - f0) * V;
+        bf16* zt = zg + ((long)n * T + f0) * V * a.z_ld;
+        // the temporal-conv bias from LDS: a global load here would sit behind the weight-fragment prefetch and,
+        // on gfx9's single in-order vmcnt, behind the z stores of the row tiles before it (each tile's stores
+        // were waited out by the next: measured 60 of the 84 us of the temporal-conv role)
+        float tb[16];
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+          const float4 b4 = *reinterpret_cast<const float4*>(sTb + 32 * ct + 8 * q4 + 4 * lh);
+          tb[4 * q4] = b4.x;
+          tb[4 * q4 + 1] = b4.y;
+          tb[4 * q4 + 2] = b4.z;
+          tb[4 * q4 + 3] = b4.w;
         }
-        // hand-off among the 4 TCN waves only (a block barrier would also wait for the GCN waves' next
-        // frames and serialise the two roles): an LDS arrival counter
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const long long pl0 = ptime();
-        pa[1] += pl0 - pk1;
-        if (lane == 0) __hip_atomic_fetch_add(sCnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        arrivals += NWT;
-        while (__hip_atomic_load(sCnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < arrivals)
-          __builtin_amdgcn_s_sleep(1);
-        const long long pl1 = ptime();
-        pa[5] += pl1 - pl0;
+        // z = acc + bias (8-B stores of 4 channels per lane and row: routing them through LDS into 64-B row runs
+        // measured slower, 90 vs 84.5 us)
 #pragma unroll
         for (int i = 0; i < RT; ++i) {
           const int r = (rh * RT + i) * 32 + lr;
-          if (i >= RTN || !rok[i] || r >= vrows) continue;
-          // the row's frame statistics from the partials of the (<= 2) tiles holding the frame, fixed order
-          const int fo = fo_[i];
-          float su = 0.f, sq = 0.f;
-          for (int tj = fo * V / 32; tj <= (fo * V + V - 1) / 32; ++tj) {
-            const int k = fo - tj * 32 / V;
-            const float2 u0 = sRed[(tj * 3 + k) * 2], u1 = sRed[(tj * 3 + k) * 2 + 1];
-            su += u0.x + u1.x;
-            sq += u0.y + u1.y;
-          }
-          const float cnt = (float)(V * C), dmean = su / cnt;  // mean of z - piv
-          const float2 st = make_float2(piv + dmean, 1.f / sqrtf(fmaxf(sq - su * dmean, 0.f) / (cnt - 1.f) + 1e-5f));
-          const int w = jw_[i];
-          if (a.u_out) {  // training forward: u = z (pre-LN2, bias included) rows and the frame's LN2 statistics
-            bf16* ur = reinterpret_cast<bf16*>(a.u_out) + (((long)n * T + f0) * V + r) * a.u_ld + 32 * ct + 4 * lh;
+          if (rok[i] && r < vrows) {
 #pragma unroll
             for (int q4 = 0; q4 < 4; ++q4) {
-              bf16x4 uv;
+              bf16x4 o;
 #pragma unroll
-              for (int e = 0; e < 4; ++e) uv[e] = (bf16)acc[i][4 * q4 + e];
-              *reinterpret_cast<bf16x4*>(ur + 8 * q4) = uv;
-            }
-            if (ct == 0 && w == 0 && lh == 0) reinterpret_cast<float2*>(a.st2_out)[(long)n * T + f0 + fo] = st;
-          }
-#pragma unroll
-          for (int q4 = 0; q4 < 4; ++q4) {
-            const int co = 32 * ct + 8 * q4 + 4 * lh;
-            const float4 gb0 = *reinterpret_cast<const float4*>(sG2 + w * CG2 + co);
-            const float4 gb1 = *reinterpret_cast<const float4*>(sG2 + w * CG2 + co + 2);
-            const float4 g4 = make_float4(gb0.x, gb0.z, gb1.x, gb1.z), b4 = make_float4(gb0.y, gb0.w, gb1.y, gb1.w);
-            float rv[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) rv[e] = (float)rv_[i][q4][e];
-            bf16x4 o;
-            o[0] = (bf16)fmaxf(fmaf((acc[i][4 * q4 + 0] - st.x) * st.y, g4.x, b4.x) + rv[0], 0.f);
-            o[1] = (bf16)fmaxf(fmaf((acc[i][4 * q4 + 1] - st.x) * st.y, g4.y, b4.y) + rv[1], 0.f);
-            o[2] = (bf16)fmaxf(fmaf((acc[i][4 * q4 + 2] - st.x) * st.y, g4.z, b4.z) + rv[2], 0.f);
-            o[3] = (bf16)fmaxf(fmaf((acc[i][4 * q4 + 3] - st.x) * st.y, g4.w, b4.w) + rv[3], 0.f);
-            *reinterpret_cast<bf16x4*>(zt + (long)r * a.z_ld + co) = o;
-          }
-        }
-        const long long pl2 = ptime();
-        pa[4] += pl2 - pl1;
-        lds_barrier();  // S_s
-        pa[2] += ptime() - pl2;
-        continue;
-      }
-      // z = acc + bias (8-B stores of 4 channels per lane and row: routing them through LDS into 64-B row runs
-      // measured slower, 90 vs 84.5 us)
-#pragma unroll
-      for (int i = 0; i < RT; ++i) {
-        const int r = (rh * RT + i) * 32 + lr;
-        if (rok[i] && r < vrows) {
-#pragma unroll
-          for (int q4 = 0; q4 < 4; ++q4) {
-            bf16x4 o;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float v = acc[i][4 * q4 + e];
-              s1[4 * q4 + e] += v;
-              s2[4 * q4 + e] = fmaf(v, v, s2[4 * q4 + e]);
-              o[e] = (bf16)(v + tb[4 * q4 + e]);
-            }
-            bf16* const zp = zt + (long)r * a.z_ld + 32 * ct + 8 * q4 + 4 * lh;
-            if (DBG & 16) {
-            } else if (DBG & 512) {
-              __builtin_nontemporal_store(__builtin_bit_cast(u32x2n, o), reinterpret_cast<u32x2n*>(zp));
-            } else {
-              *reinterpret_cast<bf16x4*>(zp) = o;
+              for (int e = 0; e < 4; ++e) {
+                const float v = acc[i][4 * q4 + e];
+                s1[4 * q4 + e] += v;
+                s2[4 * q4 + e] = fmaf(v, v, s2[4 * q4 + e]);
+                o[e] = (bf16)(v + tb[4 * q4 + e]);
+              }
+              bf16* const zp = zt + (long)r * a.z_ld + 32 * ct + 8 * q4 + 4 * lh;
+              if (DBG & 16) {
+              } else if (DBG & 512) {
+                __builtin_nontemporal_store(__builtin_bit_cast(u32x2n, o), reinterpret_cast<u32x2n*>(zp));
+              } else {
+                *reinterpret_cast<bf16x4*>(zp) = o;
+              }
             }
           }
         }
+        const long long pk15 = ptime();
+        pa[4] += pk15 - pk1;
+        cnt_run += max(0, min(vrows - rh * RT * 32, RTN * 32));
+        const long long pk2 = ptime();
+        pa[1] += pk2 - pk15;
+        lds_barrier();  // S_s: the GCN waves may overwrite the frames this step read
+        pa[2] += ptime() - pk2;
       }
-      const long long pk15 = ptime();
-      pa[4] += pk15 - pk1;
-      cnt_run += max(0, min(vrows - rh * RT * 32, RTN * 32));
-      const long long pk2 = ptime();
-      pa[1] += pk2 - pk15;
-      lds_barrier();  // S_s: the GCN waves may overwrite the frames this step read
-      pa[2] += ptime() - pk2;
-    }
-    if (st_out && !(DBG & (16 | 256))) {  // the run's sums over this wave's rows (lanes) -> (count, mean, M2)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        s1[r] = half_sum(s1[r]);
-        s2[r] = half_sum(s2[r]);
-      }
-      // the 32 channels' partials gathered in LDS by the two lanes holding them, then one 512-B store
-      float4* const ss = reinterpret_cast<float4*>(zs);
-      if (lr == 31) {
-        const float inv = cnt_run ? 1.f / (float)cnt_run : 0.f;
+      if (st_out && !(DBG & (16 | 256))) {  // the run's sums over this wave's rows (lanes) -> (count, mean, M2)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float mu = s1[r] * inv;  // mean of z - bias over the run's rows (bias added back below)
-          ss[8 * (r >> 2) + 4 * lh + (r & 3)] =
-              cnt_run ? make_float4((float)cnt_run, sTb[32 * ct + 8 * (r >> 2) + 4 * lh + (r & 3)] + mu,
-                                    fmaxf(s2[r] - s1[r] * mu, 0.f), 0.f)
-                      : make_float4(0.f, 0.f, 0.f, 0.f);
+          s1[r] = half_sum(s1[r]);
+          s2[r] = half_sum(s2[r]);
         }
+        // the 32 channels' partials gathered in LDS by the two lanes holding them, then one 512-B store
+        float4* const ss = reinterpret_cast<float4*>(zs);
+        if (lr == 31) {
+          const float inv = cnt_run ? 1.f / (float)cnt_run : 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float mu = s1[r] * inv;  // mean of z - bias over the run's rows (bias added back below)
+            ss[8 * (r >> 2) + 4 * lh + (r & 3)] =
+                cnt_run ? make_float4((float)cnt_run, sTb[32 * ct + 8 * (r >> 2) + 4 * lh + (r & 3)] + mu,
+                                      fmaxf(s2[r] - s1[r] * mu, 0.f), 0.f)
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
+        if (lane < 32) st_out[32 * ct + lane] = ss[lane];
       }
-      if (lane < 32) st_out[32 * ct + lane] = ss[lane];
-    }
-  };
-  if (rtn >= 4)
-    tcn_run.template operator()<4>();
-  else if (rtn == 3)
-    tcn_run.template operator()<3>();
-  else if (rtn == 2)
-    tcn_run.template operator()<2>();
-  else
-    tcn_run.template operator()<1>();
-  if constexpr (PROF) prof_out();
+    };
+    if (rtn >= 4)
+      tcn_run.template operator()<4>();
+    else if (rtn == 3)
+      tcn_run.template operator()<3>();
+    else if (rtn == 2)
+      tcn_run.template operator()<2>();
+    else
+      tcn_run.template operator()<1>();
+    if constexpr (PROF) prof_out();
+  }
 }
 
 FGeom plan(int N, int T) {
@@ -814,11 +921,11 @@ int layer_fused_launch(const stgcn_layer_fused_desc& a, hipStream_t s) {
   if (nblk > 0x7fffffffL) return STGCN_EBADSHAPE;
   const int K16 = a.P * G * 2;
   g.off_tab = 2 * K16 * 1024;
-  g.off_ring = g.off_tab + ((a.ln ? a.V * CG2 * 8 : (C + a.V * CBP) * 4) + C * 4 + 255) / 256 * 256;
+  g.off_ring = g.off_tab + ((a.ln ? 2 * a.V * CGP * 4 : (C + a.V * CBP) * 4) + C * 4 + 255) / 256 * 256;
   g.off_h = g.off_ring + NWG * SLOTS * PANEL;
   g.off_red = g.off_h + (RF * a.V * RSH + 255) / 256 * 256;
   g.off_zs = g.off_red + 2 * C * 8;
-  const size_t lds = (size_t)g.off_red + (a.ln ? 2 * RT * 3 * 2 * 8 + 16 : 2 * C * 8 + NWT * ZSB);
+  const size_t lds = (size_t)g.off_red + (a.ln ? NWT * 4 * 8 + NWT * 4 : 2 * C * 8 + NWT * ZSB);
   if (lds > (size_t)LDS_MAX) return STGCN_EBADSHAPE;
   typedef void (*KFn)(const stgcn_layer_fused_desc, const FGeom);
   static const KFn tab[2][3] = {{layer_fused_kernel<1, false>, layer_fused_kernel<2, false>, layer_fused_kernel<3, false>},
