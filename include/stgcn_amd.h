@@ -393,6 +393,10 @@ typedef struct {
   float* st1_out;
   float* st2_out;
   int g_ld, u_ld;
+  /* optional with the training outputs (NULL otherwise): h = relu(LN1(g)) rows, h_ld — the temporal conv's input,
+   * which the layer's weight gradient reads (saves recomputing it in the backward) */
+  void* h_out;
+  int h_ld;
 } stgcn_layer_fused_desc;
 
 int stgcn_layer_fused_fwd(const stgcn_layer_fused_desc* d, void* stream);

@@ -71,7 +71,8 @@ class LayerFusedDesc(ctypes.Structure):
     _fields_ = [(n, c_void_p) for n in ("x", "z", "wg_frag", "A", "gbias", "n1_scale", "n1_shift", "wt_frag", "tbias",
                                         "stats")] + [(n, c_int) for n in ("N", "T", "V", "P", "x_ld", "z_ld")] + \
                [(n, c_void_p) for n in ("ln1_g", "ln1_b", "ln2_g", "ln2_b")] + [("ln", c_int), ("residual", c_int)] + \
-               [(n, c_void_p) for n in ("g_out", "u_out", "st1_out", "st2_out")] + [("g_ld", c_int), ("u_ld", c_int)]
+               [(n, c_void_p) for n in ("g_out", "u_out", "st1_out", "st2_out")] + [("g_ld", c_int), ("u_ld", c_int)] + \
+               [("h_out", c_void_p), ("h_ld", c_int)]
 
 
 class BnBwdDesc(ctypes.Structure):

@@ -413,6 +413,10 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
                 }
             }
           }
+          // training forward with h_out: this run's own frames of h also go to HBM (the backward's weight gradient)
+          bf16* const hg = (a.h_out && fa >= HALO && fa < HALO + (R1 - R0))
+                               ? reinterpret_cast<bf16*>(a.h_out) + (((long)n * T + (R0 - HALO + fa)) * V + lr) * a.h_ld + 4 * lh
+                               : nullptr;
           if (jv) {
             // h = relu(fma(fma(g, A, B), gamma, beta)), A = rstd, B = -mean * rstd, on channel pairs
             char* hr = hrow + lr * RSH;
@@ -434,6 +438,7 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
                 hv[2] = (bf16)fmaxf(h23.x, 0.f);
                 hv[3] = (bf16)fmaxf(h23.y, 0.f);
                 *reinterpret_cast<bf16x4*>(hr + (32 * t + 8 * q4 + 4 * lh) * 2) = hv;
+                if (hg) *reinterpret_cast<bf16x4*>(hg + 32 * t + 8 * q4) = hv;
               }
           }
         }
@@ -914,6 +919,7 @@ int layer_fused_launch(const stgcn_layer_fused_desc& a, hipStream_t s) {
   const int ntrain = !!a.g_out + !!a.u_out + !!a.st1_out + !!a.st2_out;
   if (ntrain != 0 && (ntrain != 4 || !a.ln || a.g_ld < C || a.g_ld % 4 || a.u_ld < C || a.u_ld % 4))
     return STGCN_EBADSHAPE;
+  if (a.h_out && (ntrain != 4 || a.h_ld < C || a.h_ld % 4)) return STGCN_EBADSHAPE;
   if (a.N < 1 || a.T < 1 || a.V <= 16 || a.V > VMAX || a.P < 1 || a.P > 3) return STGCN_EBADSHAPE;
   if (a.x_ld < C || a.x_ld % 8 || a.z_ld < C || a.z_ld % 4) return STGCN_EBADSHAPE;
   FGeom g = plan(a.N, a.T);

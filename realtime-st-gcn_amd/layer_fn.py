@@ -133,32 +133,35 @@ def plan_layer_packs(plan, layer, A, M, dtype):
     return pk
 
 
-def _ln_vc(p, V, C):
-    """LayerNorm([C,1,V]) parameter -> [V][C] fp32 (the fused kernel's per-joint rows)."""
-    return p.detach().float().reshape(C, V).t().contiguous()
-
-
 def fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, sup, dtype, tag=None, cache=None,
-                        norm=BN, train=False):
+                        norm=BN, train=False, packs=None):
     """StgcnLayer.forward (stgcn.py:181-193) through layer_fused.hip.  BatchNorm: the two-pass fused form
     (SURVEY §7): pass 1 = graph conv statistics only (gcn_tile, no g stores) -> BN1 scale/shift; pass 2 =
     graph conv recomputed per tile + BN1 + ReLU + temporal conv in one kernel (z + BN2 partials); then
     y = relu(BN2(z) + x).  LayerNorm (per-frame norms): the whole layer is the one kernel; ``train``: it also
     writes what the unfused backward reads and this returns (y, g, u, ls1, ls2).
-    x: channels-last bf16 (N, 64, T, V)."""
+    x: channels-last bf16 (N, 64, T, V).  ``packs``: the step's LayerPacks (training): the temporal-conv fragment
+    image and the bias through A come from the model's one prep launch instead of per-layer launches."""
     N, Cin, T, V = x.shape
     P = A32.shape[0]
     Cout = wt.shape[0]
     dev = x.device
-    bias2d = K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
-    wimg, cpg, kwg, wtp = _packs(cache, wg, wt, P, Cin, Cout, dtype)
+    if packs is not None and packs.wt is not None and packs.gw is not None:
+        bias2d = packs.gw[1]
+        wgf = wg.detach().float().view(P, Cout, Cin).permute(1, 0, 2).reshape(Cout, P * Cin)
+        wimg, cpg, kwg = K.pack_gcn_weight(wgf, dtype)
+        wtp = packs.wt[0]
+    else:
+        bias2d = K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
+        wimg, cpg, kwg, wtp = _packs(cache, wg, wt, P, Cin, Cout, dtype)
     if norm == LN:
-        # the [V][64] parameter rows, re-laid-out only when a LayerNorm parameter changed (4 copy launches)
+        # the LayerNorm([64,1,V]) parameters as per-joint [V][64] rows, re-laid-out when one changed (every
+        # training step): one stacking launch for the four (the kernel reads 16-B channel runs per joint)
         lkey = tuple((t.data_ptr(), t._version) for t in (n1w, n1b, n2w, n2b))
         if cache is not None and cache.get("ln_key") == lkey:
             ln = cache["ln_val"]
         else:
-            ln = (_ln_vc(n1w, V, Cout), _ln_vc(n1b, V, Cout), _ln_vc(n2w, V, Cout), _ln_vc(n2b, V, Cout))
+            ln = tuple(torch.stack([p.detach().float().reshape(Cout, V).t() for p in (n1w, n1b, n2w, n2b)]).unbind(0))
             if cache is not None:
                 cache["ln_key"], cache["ln_val"] = lkey, ln
         return K.layer_fused(x, A32, wimg, bias2d, None, None, wtp, bt.detach().float().contiguous(), tag=tag,
@@ -233,13 +236,13 @@ class StgcnLayerFunction(torch.autograd.Function):
             # training forward of a LayerNorm 64 -> 64 stride-1 layer: the one-kernel layer (g and h on chip for
             # the temporal conv) also writes g, u and both LN statistics — exactly what the unfused forward
             # saves — so the backward below is unchanged (ln/ configs)
-            y, g, u, ls1, ls2 = fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, sup, dtype,
-                                                    cache=cache, norm=LN, train=True)
+            y, g, u, ls1, ls2, h = fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, sup,
+                                                       dtype, cache=cache, norm=LN, train=True, packs=packs)
             ctx.cfg = cfg
             ctx.sup = sup
             ctx.dims = (N, Cin, Cout, T, T_out, V, P, pad, False)
             ctx.packs = None
-            ctx.save_for_backward(x, A32, None, g, u, y, wg, bg, wt, n1w, n1b, n2w, n2b, ls1, ls2, None)
+            ctx.save_for_backward(x, A32, None, g, u, y, wg, bg, wt, n1w, n1b, n2w, n2b, ls1, ls2, h)
             ctx.in_dtype = A.dtype
             return y
         # gathered path: bias2d comes from the weight preparation below

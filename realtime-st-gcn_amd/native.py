@@ -607,8 +607,8 @@ def layer_fused(x, A, wimg, gbias, n1_scale, n1_shift, wt_packed, tbias, stats=N
     """stgcn_layer_fused_fwd.  BatchNorm layer: z rows (N, 64, T, V) = tcn(relu(BN1(gcn(x)))) + tbias, g kept
     on chip (+ BN2 partials).  ln = (g1, b1, g2, b2) LayerNorm parameters as [V][64] fp32: the whole layer
     y = relu(LN2(tcn(relu(LN1(gcn(x))))) + residual * x) in this one kernel.  ``train`` (LayerNorm only): also
-    the backward's inputs — returns (y, g, u, ls1, ls2): g / u the graph-conv / temporal-conv outputs (bias
-    included) as rows, ls1 / ls2 their per-frame (mean, rstd) [N*T][2] (ln_stats's layout)."""
+    the backward's inputs — returns (y, g, u, ls1, ls2, h): g / u the graph-conv / temporal-conv outputs (bias
+    included) as rows, ls1 / ls2 their per-frame (mean, rstd) [N*T][2] (ln_stats's layout), h = relu(LN1(g))."""
     N, C, T, V = x.shape
     if getattr(wt_packed, "frag_stride", None) != 1:
         raise RuntimeError("stgcn_amd: layer_fused needs the stride-1 fragment image of the temporal weight")
@@ -634,6 +634,8 @@ def layer_fused(x, A, wimg, gbias, n1_scale, n1_shift, wt_packed, tbias, stats=N
         st = torch.empty((2, N * T, 2), dtype=torch.float32, device=x.device)
         d.g_out, d.u_out, d.st1_out, d.st2_out = g.data_ptr(), u.data_ptr(), st[0].data_ptr(), st[1].data_ptr()
         d.g_ld, d.u_ld = rows_ld(g), rows_ld(u)
+        hh = cl_empty(N, C, T, V, x.dtype, x.device)
+        d.h_out, d.h_ld = hh.data_ptr(), rows_ld(hh)
     hook = EVENT_HOOK if tag is not None else None
     if hook:
         hook(tag, "start", None)
@@ -641,7 +643,7 @@ def layer_fused(x, A, wimg, gbias, n1_scale, n1_shift, wt_packed, tbias, stats=N
     if hook:
         hook(tag, "end", None)
     if train:
-        return z, g, u, st[0], st[1]
+        return z, g, u, st[0], st[1], hh
     return z
 
 

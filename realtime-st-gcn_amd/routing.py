@@ -6,14 +6,16 @@ routes on MI355X.  The environment variables are read once at import
 also assign the attributes directly.
 
     fused_inference     STGCN_FUSED=0         no_grad forward of LayerNorm 64->64 stride-1 layers through the one-kernel
-                                              layer layer_fused.hip (default on: 0.14 vs 0.20 ms unfused)
+                                              layer layer_fused.hip (default on: 0.126 vs 0.208 ms unfused)
     fused_bn_inference  STGCN_FUSED_BN=1      BatchNorm layers too (default OFF: the two-pass fused forward loses on the
                                               driver's boxes, BENCH_r04 0.1757 vs 0.1657 ms eager / 0.1725 vs 0.1709
                                               graph-replayed, r05a 0.1758 vs 0.1664 / 0.1741 vs 0.1714)
-    fused_ln_train      STGCN_FUSED_LN_TRAIN=1  training forward of LayerNorm 64->64 stride-1 layers through the same
-                                              one-kernel layer (it also writes g, u and both LN statistics for the
-                                              unfused backward).  Default off since the LayerNorm kernels of ln.hip:
-                                              the LN training step measured 8.77 ms unfused vs 8.86 fused (r04k)
+    fused_ln_train      STGCN_FUSED_LN_TRAIN=0  training forward of LayerNorm 64->64 stride-1 layers through the same
+                                              one-kernel layer (it also writes g, u, h and both LN statistics for the
+                                              unfused backward).  Default on since round 5 (frame-aligned LN2
+                                              epilogue, h written by the kernel, packs from the prep launch): LN
+                                              training step 8.397-8.430 fused vs 8.442-8.456 ms unfused (r05, 3
+                                              interleaved runs; round 4: 8.86 vs 8.77)
     prep_plan           STGCN_PREP_PLAN=0     stgcn.Model training forwards pack every weight per call instead of
                                               in the one-launch plan (native.PrepPlan; default on)
 
@@ -31,7 +33,7 @@ class _Routing:
         e = os.environ.get
         self.fused_inference = e("STGCN_FUSED", "1") != "0"
         self.fused_bn_inference = e("STGCN_FUSED_BN", "0") == "1"
-        self.fused_ln_train = e("STGCN_FUSED_LN_TRAIN", "0") == "1"
+        self.fused_ln_train = e("STGCN_FUSED_LN_TRAIN", "1") != "0"
         self.prep_plan = e("STGCN_PREP_PLAN", "1") != "0"
 
 
