@@ -229,7 +229,9 @@ int stgcn_bn_finalize(const void* part_f4, int nblocks, int ld_part, int C, cons
  *   reduce: dz = dy*mask; sums[c] = (sum dz, sum dz*xhat1, sum dz*xhat2, 0)
  *   apply : out1 = g1*rstd1*(dz - S0/M - xhat1*S1/M) (or dz when x1 == NULL);
  *           out2 (+)= g2*rstd2*(dz - S0/M - xhat2*S2/M) (or dz when x2 == NULL);  osum[c] = (sum out1,
- *           sum out2) — the conv-bias gradients.  mask: 0 none | 1 mref > 0 | 2 mref*msc + msh > 0.
+ *           sum out2) — the conv-bias gradients.  mask: 0 none | 1 mref > 0 | 2 mref*msc + msh > 0 |
+ *           3 (bf16, C % 8 == 0) mref = the bit mask stgcn_bn_apply_bits wrote: byte [m * ldm + c / 8], bit c % 8
+ *           set where the stored output was > 0 (ldm = bytes per row, >= C / 8) — 1/16 of the bytes of mask 1.
  * Replaces: autograd of stgcn.py:160,171,191-193 (BN2 / residual BN / ReLU / add) and :152-153. */
 typedef struct {
   const void* dy;
@@ -259,6 +261,12 @@ int stgcn_bn_bwd_fused_apply(const stgcn_bn_bwd_desc* d, int dtype, void* stream
 int stgcn_bn_apply(const void* u, int ldu, const float* sc, const float* sh, int res_mode, const void* r, int ldr,
                    const float* rsc, const float* rsh, int relu, void* y, int ldy, long M, int C, int dtype,
                    void* stream);
+/* stgcn_bn_apply (bf16, C % 8 == 0) that also writes the output's sign bits for the backward's ReLU mask:
+ * bits[m * (C / 8) + c / 8] bit c % 8 = (stored y[m][c] > 0) — what the fused backward reads as mask 3
+ * instead of re-reading y (1/16 of the bytes). */
+int stgcn_bn_apply_bits(const void* u, int ldu, const float* sc, const float* sh, int res_mode, const void* r, int ldr,
+                        const float* rsc, const float* rsh, int relu, void* y, int ldy, long M, int C, void* bits,
+                        void* stream);
 /* sums_f2[c] = (sum dz, sum dz*xhat) with dz = dy * mask (mask 0 none | 1 mref>0 | 2 mref*msc+msh>0);
  * x may be NULL (then only sum dz).  part_f2 scratch: [stgcn_bn_stat_blocks(M)][C] float2. */
 int stgcn_bn_bwd_reduce(const void* dy, int lddy, int mask, const void* mref, int ldm, const float* msc,

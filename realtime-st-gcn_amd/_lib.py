@@ -134,6 +134,8 @@ _SIGS = {
                                   c_void_p, c_void_p]),
     "stgcn_bn_apply": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
                                c_int, c_void_p, c_int, c_long, c_int, c_int, c_void_p]),
+    "stgcn_bn_apply_bits": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                                    c_int, c_void_p, c_int, c_long, c_int, c_void_p, c_void_p]),
     "stgcn_bn_bwd_reduce": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
                                     c_void_p, c_long, c_int, c_void_p, c_void_p, c_int, c_void_p]),
     "stgcn_bn_bwd_apply": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,

@@ -72,7 +72,10 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_fused_kernel(const stgcn_bn
         ok[u] = m < me;
         const long mm = ok[u] ? m : mb;
         Udz[u] = *reinterpret_cast<const uint4*>(dy + mm * a.lddy + c0);
-        Umr[u] = *reinterpret_cast<const uint4*>(mref + mm * a.ldm + c0);
+        if constexpr (MASK == 3)  // the forward's sign bits: one byte per 8 channels
+          Umr[u].x = reinterpret_cast<const unsigned char*>(a.mref)[mm * a.ldm + cu];
+        else
+          Umr[u] = *reinterpret_cast<const uint4*>(mref + mm * a.ldm + c0);
         if (!same_x) Uxa[u] = *reinterpret_cast<const uint4*>(x1 + mm * a.ldx1 + c0);
         if (X2) Uxb[u] = *reinterpret_cast<const uint4*>(x2 + mm * a.ldx2 + c0);
       }
@@ -81,7 +84,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_fused_kernel(const stgcn_bn
         if (!ok[u]) continue;
         float dz[1][VEC], mr[1][VEC], xa[1][VEC], xb[1][VEC];
         unpack16(Udz[u], dz[0], (T*)nullptr);
-        unpack16(Umr[u], mr[0], (T*)nullptr);
+        if constexpr (MASK != 3) unpack16(Umr[u], mr[0], (T*)nullptr);
         unpack16(same_x ? Umr[u] : Uxa[u], xa[0], (T*)nullptr);
         if (X2) unpack16(Uxb[u], xb[0], (T*)nullptr);
 #pragma unroll
@@ -89,6 +92,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_fused_kernel(const stgcn_bn
           float d = dz[0][j];
           if (MASK == 1 && !(mr[0][j] > 0.f)) d = 0.f;
           if (MASK == 2 && !(mr[0][j] * msc[j] + msh[j] > 0.f)) d = 0.f;
+          if (MASK == 3 && !((Umr[u].x >> j) & 1u)) d = 0.f;
           s0[j] += d;
           s1[j] += d * (xa[0][j] - mu1[j]) * rs1[j];
           if (X2) s2[j] += d * (xb[0][j] - mu2[j]) * rs2[j];
@@ -212,7 +216,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(const stgcn_bn_
         lok[u] = m < me;
         const long mm = lok[u] ? m : mb;
         Ldz[u] = *reinterpret_cast<const uint4*>(dy + mm * a.lddy + c0);
-        Lmr[u] = *reinterpret_cast<const uint4*>(mref + mm * a.ldm + c0);
+        if constexpr (MASK == 3)
+          Lmr[u].x = reinterpret_cast<const unsigned char*>(a.mref)[mm * a.ldm + cu];
+        else
+          Lmr[u] = *reinterpret_cast<const uint4*>(mref + mm * a.ldm + c0);
         if (!same_x) Lxa[u] = *reinterpret_cast<const uint4*>(x1 + mm * a.ldx1 + c0);
         if (O2 == 1) Lxb[u] = *reinterpret_cast<const uint4*>(x2 + mm * a.ldx2 + c0);
         if (O2 && a.acc2) Lpa[u] = *reinterpret_cast<const uint4*>(o2 + mm * a.ldo2 + c0);
@@ -228,7 +235,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(const stgcn_bn_
         const long m = m0 + (long)u * g.RPI;
         float dz[VEC], mr[VEC], xa[VEC], xb[VEC], pa[VEC];
         unpack16(Udz[u], dz, (T*)nullptr);
-        unpack16(Umr[u], mr, (T*)nullptr);
+        if constexpr (MASK != 3) unpack16(Umr[u], mr, (T*)nullptr);
         unpack16(same_x ? Umr[u] : Uxa[u], xa, (T*)nullptr);
         if (O2 == 1) unpack16(Uxb[u], xb, (T*)nullptr);
         if (O2 && a.acc2) unpack16(Upa[u], pa, (T*)nullptr);
@@ -238,6 +245,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_fused_kernel(const stgcn_bn_
           float d = dz[j];
           if (MASK == 1 && !(mr[j] > 0.f)) d = 0.f;
           if (MASK == 2 && !(mr[j] * msc[j] + msh[j] > 0.f)) d = 0.f;
+          if (MASK == 3 && !((Umr[u].x >> j) & 1u)) d = 0.f;
           r1[j] = k11[j] * d + k21[j] * xa[j] + k31[j];
           r2[j] = O2 == 1 ? k12[j] * d + k22[j] * xb[j] + k32[j] : d;
           if (O2 && a.acc2) r2[j] += pa[j];
@@ -310,7 +318,8 @@ bool fits(const stgcn_bn_bwd_desc& a, int dtype, int& vec) {
   vec = dtype == 1 ? 8 : 4;
   if (a.C % vec || a.C / vec > 256 || a.C > 2048) return false;
   auto al = [&](int ld) { return ld % vec == 0; };
-  return al(a.lddy) && (!a.mask || al(a.ldm)) && (!a.x1 || al(a.ldx1)) && (!a.x2 || al(a.ldx2)) &&
+  if (a.mask == 3 && dtype != 1) return false;
+  return al(a.lddy) && (!a.mask || a.mask == 3 || al(a.ldm)) && (!a.x1 || al(a.ldx1)) && (!a.x2 || al(a.ldx2)) &&
          (!a.out1 || al(a.ldo1)) && (!a.out2 || al(a.ldo2));
 }
 
@@ -322,7 +331,7 @@ long bn_bwd_fused_work_floats_impl(long M, int C, int dtype) {
 template <typename T, int VEC, int MASK, bool X2>
 void launch_reduce(const stgcn_bn_bwd_desc& a, const Geo& g, hipStream_t s) {
   // input streams: dy, the mask reference, x1 (shared with the mask reference for BN1), x2
-  constexpr int UR = ur_for(2 + (MASK == 2 ? 0 : 1) + (X2 ? 1 : 0));
+  constexpr int UR = ur_for(2 + (MASK == 1 ? 1 : 0) + (X2 ? 1 : 0));  // mask 2 reads x1, mask 3 one byte
   hipLaunchKernelGGL((bn_bwd_reduce_fused_kernel<T, VEC, MASK, X2, UR>), dim3(g.nb), dim3(256), 0, s, a, g);
 }
 template <typename T, int VEC>
@@ -330,6 +339,11 @@ void reduce_dispatch(const stgcn_bn_bwd_desc& a, const Geo& g, hipStream_t s) {
   if (a.mask == 1) {
     if (a.x2) launch_reduce<T, VEC, 1, true>(a, g, s);
     else launch_reduce<T, VEC, 1, false>(a, g, s);
+  } else if (a.mask == 3) {
+    if constexpr (VEC == 8) {
+      if (a.x2) launch_reduce<T, VEC, 3, true>(a, g, s);
+      else launch_reduce<T, VEC, 3, false>(a, g, s);
+    }
   } else {
     if (a.x2) launch_reduce<T, VEC, 2, true>(a, g, s);
     else launch_reduce<T, VEC, 2, false>(a, g, s);
@@ -338,7 +352,7 @@ void reduce_dispatch(const stgcn_bn_bwd_desc& a, const Geo& g, hipStream_t s) {
 
 template <typename T, int VEC, int MASK, int O2>
 void launch_apply(const stgcn_bn_bwd_desc& a, const Geo& g, hipStream_t s) {
-  constexpr int UR = ur_for(2 + (MASK == 2 ? 0 : 1) + (O2 == 1 ? 1 : 0));  // (+ out2 read-back when acc2)
+  constexpr int UR = ur_for(2 + (MASK == 1 ? 1 : 0) + (O2 == 1 ? 1 : 0));  // (+ out2 read-back when acc2)
   if (a.osum)
     hipLaunchKernelGGL((bn_bwd_apply_fused_kernel<T, VEC, MASK, O2, true, UR>), dim3(g.nb), dim3(256), 0, s, a, g);
   else
@@ -351,6 +365,12 @@ void apply_dispatch(const stgcn_bn_bwd_desc& a, const Geo& g, hipStream_t s) {
     if (o2 == 1) launch_apply<T, VEC, 1, 1>(a, g, s);
     else if (o2 == 2) launch_apply<T, VEC, 1, 2>(a, g, s);
     else launch_apply<T, VEC, 1, 0>(a, g, s);
+  } else if (a.mask == 3) {
+    if constexpr (VEC == 8) {
+      if (o2 == 1) launch_apply<T, VEC, 3, 1>(a, g, s);
+      else if (o2 == 2) launch_apply<T, VEC, 3, 2>(a, g, s);
+      else launch_apply<T, VEC, 3, 0>(a, g, s);
+    }
   } else {
     if (o2 == 1) launch_apply<T, VEC, 2, 1>(a, g, s);
     else if (o2 == 2) launch_apply<T, VEC, 2, 2>(a, g, s);
@@ -364,7 +384,7 @@ long bn_bwd_fused_work_floats(long M, int C, int dtype) { return bn_bwd_fused_wo
 
 int bn_bwd_fused_reduce_launch(const stgcn_bn_bwd_desc& a, int dtype, hipStream_t s) {
   int vec;
-  if (!fits(a, dtype, vec) || !a.work || !a.sums || !a.x1 || !a.mref || (a.mask != 1 && a.mask != 2))
+  if (!fits(a, dtype, vec) || !a.work || !a.sums || !a.x1 || !a.mref || a.mask < 1 || a.mask > 3)
     return STGCN_EBADSHAPE;
   const Geo g = geo(a.M, a.C, vec);
   if (dtype == 1) reduce_dispatch<bf16, 8>(a, g, s);
@@ -375,8 +395,8 @@ int bn_bwd_fused_reduce_launch(const stgcn_bn_bwd_desc& a, int dtype, hipStream_
 
 int bn_bwd_fused_apply_launch(const stgcn_bn_bwd_desc& a, int dtype, hipStream_t s) {
   int vec;
-  if (!fits(a, dtype, vec) || !a.out1 || !a.sums || !a.x1 || !a.mref || (a.osum && !a.work) ||
-      (a.mask != 1 && a.mask != 2))
+  if (!fits(a, dtype, vec) || !a.out1 || !a.sums || !a.x1 || !a.mref || (a.osum && !a.work) || a.mask < 1 ||
+      a.mask > 3)
     return STGCN_EBADSHAPE;
   const Geo g = geo(a.M, a.C, vec, STGCN_BN_APPLY_TB);
   if (dtype == 1) apply_dispatch<bf16, 8>(a, g, s);

@@ -63,7 +63,8 @@ int bn_finalize_launch(const float4* part, int nb, int ldp, int C, const float* 
                        float2* mean_rstd, float* scale, float* shift, hipStream_t s);
 int bn_apply_launch(const void* u, int ldu, const float* sc, const float* sh, int res_mode, const void* r, int ldr,
                     const float* rsc, const float* rsh, int relu, void* y, int ldy, long M, int C, int dtype,
-                    hipStream_t s);
+                    hipStream_t s,
+                    unsigned char* bits = nullptr);
 int bn_bwd_reduce_launch(const void* dy, int lddy, int mask, const void* mref, int ldm, const float* msc,
                          const float* msh, const void* x, int ldx, const float2* mean_rstd, long M, int C,
                          float2* part, float2* out, int dtype, hipStream_t s);
@@ -212,14 +213,14 @@ long stgcn_bn_bwd_fused_workspace(long M, int C, int dtype) {
 int stgcn_bn_bwd_fused_reduce(const stgcn_bn_bwd_desc* d, int dtype, void* stream) {
   CHECK_DTYPE(dtype);
   if (!d || !d->dy || d->M <= 0 || d->C <= 0 || (d->mask && !d->mref) || (d->mask == 2 && (!d->msc || !d->msh)) ||
-      (d->x1 && !d->mean_rstd1) || (d->x2 && !d->mean_rstd2))
+      (d->x1 && !d->mean_rstd1) || (d->x2 && !d->mean_rstd2) || (d->mask == 3 && (dtype != 1 || d->C % 8 || d->ldm < d->C / 8)))
     return STGCN_EBADSHAPE;
   return bn_bwd_fused_reduce_launch(*d, dtype, STREAM(stream));
 }
 int stgcn_bn_bwd_fused_apply(const stgcn_bn_bwd_desc* d, int dtype, void* stream) {
   CHECK_DTYPE(dtype);
   if (!d || !d->dy || d->M <= 0 || d->C <= 0 || (d->mask && !d->mref) || (d->mask == 2 && (!d->msc || !d->msh)) ||
-      (d->x1 && !d->mean_rstd1) || (d->x2 && !d->mean_rstd2))
+      (d->x1 && !d->mean_rstd1) || (d->x2 && !d->mean_rstd2) || (d->mask == 3 && (dtype != 1 || d->C % 8 || d->ldm < d->C / 8)))
     return STGCN_EBADSHAPE;
   return bn_bwd_fused_apply_launch(*d, dtype, STREAM(stream));
 }
@@ -330,6 +331,13 @@ int stgcn_bn_apply(const void* u, int ldu, const float* sc, const float* sh, int
   CHECK_DTYPE(dtype);
   if (res_mode && !r) return STGCN_EBADSHAPE;
   return bn_apply_launch(u, ldu, sc, sh, res_mode, r, ldr, rsc, rsh, relu, y, ldy, M, C, dtype, STREAM(stream));
+}
+int stgcn_bn_apply_bits(const void* u, int ldu, const float* sc, const float* sh, int res_mode, const void* r, int ldr,
+                        const float* rsc, const float* rsh, int relu, void* y, int ldy, long M, int C, void* bits,
+                        void* stream) {
+  if ((res_mode && !r) || !bits || C % 8) return STGCN_EBADSHAPE;
+  return bn_apply_launch(u, ldu, sc, sh, res_mode, r, ldr, rsc, rsh, relu, y, ldy, M, C, 1, STREAM(stream),
+                         static_cast<unsigned char*>(bits));
 }
 int stgcn_bn_bwd_reduce(const void* dy, int lddy, int mask, const void* mref, int ldm, const float* msc,
                         const float* msh, const void* x, int ldx, const void* mean_rstd, long M, int C, void* part,

@@ -157,7 +157,8 @@ template <typename T, int VEC>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ u, int ldu, const float* sc,
                                                        const float* sh, int res_mode, const T* __restrict__ r,
                                                        int ldr, const float* rsc, const float* rsh, int relu,
-                                                       T* __restrict__ y, int ldy, long M, int C, long rpb) {
+                                                       T* __restrict__ y, int ldy, long M, int C, long rpb,
+                                                       unsigned char* __restrict__ bits) {
   int CU, RPI;
   row_layout(C, VEC, CU, RPI);
   const int cu = threadIdx.x % CU, rs = threadIdx.x / CU;
@@ -218,6 +219,21 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ u, 
       if (relu & 1) {
 #pragma unroll
         for (int j = 0; j < VEC; ++j) f[j] = fmaxf(f[j], 0.f);
+      }
+      if constexpr (VEC == 8 && sizeof(T) == 2) {
+        if (bits) {  // the stored values' sign bits (> 0: nonzero, sign clear), one byte per 8 channels
+          const uint4 p = pack16(f, (T*)nullptr);
+          *reinterpret_cast<uint4*>(y + m * ldy + c0) = p;
+          const unsigned w[4] = {p.x, p.y, p.z, p.w};
+          unsigned b = 0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const unsigned h = (w[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+            b |= ((h & 0x8000u) == 0u && h != 0u) ? (1u << j) : 0u;
+          }
+          bits[m * (C / 8) + cu] = (unsigned char)b;
+          continue;
+        }
       }
       stv<T, VEC>(y + m * ldy + c0, f);
     }
@@ -613,13 +629,15 @@ int bn_finalize_launch(const float4* part, int nb, int ldp, int C, const float* 
 
 int bn_apply_launch(const void* u, int ldu, const float* sc, const float* sh, int res_mode, const void* r, int ldr,
                     const float* rsc, const float* rsh, int relu, void* y, int ldy, long M, int C, int dtype,
-                    hipStream_t s) {
+                    hipStream_t s, unsigned char* bits) {
   if (!rows_fit(C, dtype)) return STGCN_EBADSHAPE;
+  // bit-mask output: the 16-B (8 x bf16) path only
+  if (bits && (dtype != 1 || C % 8 || ldu % 8 || ldy % 8 || (res_mode && ldr % 8))) return STGCN_EBADSHAPE;
   const long rpb = elt_rows_per_block(M);
   const int nb = (int)((M + rpb - 1) / rpb);
   DISPATCH_VEC(dtype, C, hipLaunchKernelGGL((bn_apply_kernel<T, VEC>), dim3(nb), dim3(256), 0, s,
                                             (const T*)u, ldu, sc, sh, res_mode, (const T*)r, ldr, rsc, rsh, relu,
-                                            (T*)y, ldy, M, C, rpb));
+                                            (T*)y, ldy, M, C, rpb, bits));
   RET_HIP;
 }
 

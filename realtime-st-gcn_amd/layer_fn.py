@@ -309,10 +309,16 @@ class StgcnLayerFunction(torch.autograd.Function):
         # ---- y = relu(norm2(u) + res)
         if norm == BN:
             mr2, sc2, sh2 = K.bn_finalize(st2, st2.shape[0], cpt, Cout, n2w.detach().float(), n2b.detach().float())
+            # the output's sign bits for the backward's ReLU mask (the fused BN backward reads them instead of y:
+            # 1/16 of the bytes in both of its passes)
+            ybits = torch.empty((M2, Cout // 8), dtype=torch.uint8, device=dev) \
+                if (ROUTING.bn_mask_bits and dtype == torch.bfloat16 and K.bn_fused_ok(Cout, dtype) and Cout % 8 == 0) \
+                else None
             if res_conv:
-                y = K.bn_apply(u, sc2, sh2, M2, Cout, res_mode=2, r=r, rsc=scr, rsh=shr)
+                y = K.bn_apply(u, sc2, sh2, M2, Cout, res_mode=2, r=r, rsc=scr, rsh=shr, bits=ybits)
             else:
-                y = K.bn_apply(u, sc2, sh2, M2, Cout, res_mode=1 if residual else 0, r=x if residual else None)
+                y = K.bn_apply(u, sc2, sh2, M2, Cout, res_mode=1 if residual else 0, r=x if residual else None,
+                               bits=ybits)
         else:
             ls2 = K.ln_stats(u, N * T_out, V, Cout)
             g2, b2 = _flat_ln(n2w), _flat_ln(n2b)
@@ -329,7 +335,7 @@ class StgcnLayerFunction(torch.autograd.Function):
         ctx.packs = (cpg, kpg, cpt, kpt)
         saved = [x, A32, XA, g, u, y, wg, bg, wt, n1w, n1b, n2w, n2b]
         if norm == BN:
-            saved += [mr1, sc1, sh1, mr2]
+            saved += [mr1, sc1, sh1, mr2, ybits]
         else:
             saved += [ls1, ls2, h]
         if res_conv:
@@ -346,8 +352,8 @@ class StgcnLayerFunction(torch.autograd.Function):
         x, A32, XA, g, u, y, wg, bg, wt, n1w, n1b, n2w, n2b = sv[:13]
         rest = sv[13:]
         if norm == BN:
-            mr1, sc1, sh1, mr2 = rest[:4]
-            rest = rest[4:]
+            mr1, sc1, sh1, mr2, ybits = rest[:5]
+            rest = rest[5:]
         else:
             ls1, ls2, h = rest[:3]
             rest = rest[3:]
@@ -379,6 +385,8 @@ class StgcnLayerFunction(torch.autograd.Function):
             # one reduce + one apply pass: du, the residual branch's dr (or dx = dz), and the conv-bias
             # gradients (column sums of du / dr) together
             kw = dict(mask=1, mref=y, x1=u, mr1=mr2, g1=n2w.detach().float(), out1=du, bias_sums=True)
+            if ybits is not None:
+                kw.update(mask=3, mref=ybits)
             if res_conv:
                 dr = K.cl_empty(N, Cout, T_out, V, dtype, dev)
                 kw.update(x2=r, mr2=strr, g2=nrw.detach().float(), out2=dr)

@@ -763,16 +763,24 @@ def bn_finalize(part, nb, ld_part, C, gamma, beta, eps=1e-5):
     return mr, sc, sh
 
 
-def bn_apply(u, sc, sh, M, C, res_mode=0, r=None, rsc=None, rsh=None, relu=True, out=None, ldu=None, ldy=None):
+def bn_apply(u, sc, sh, M, C, res_mode=0, r=None, rsc=None, rsh=None, relu=True, out=None, ldu=None, ldy=None,
+             bits=None):
+    """y = act(u*sc + sh + res) (stgcn_bn_apply).  ``bits`` (uint8 [M][C/8], bf16 and C % 8 == 0 only): also the
+    output's sign bits (stgcn_bn_apply_bits), the backward's ReLU mask at 1/16 of y's bytes (bn_bwd_fused mask 3)."""
     if out is None:
         out = torch.empty_like(u)
     h = KTIME_HOOK
     if h:
         ktag = _k_start(h, "bn_apply", f"C{C}", None, u.element_size() * M * C * (3 if r is not None else 2))
-    L.check(L.lib().stgcn_bn_apply(u.data_ptr(), ldu or rows_ld(u), sc.data_ptr(), sh.data_ptr(), res_mode, L.ptr(r),
-                                   rows_ld(r) if r is not None else 0, L.ptr(rsc), L.ptr(rsh), int(relu),
-                                   out.data_ptr(), ldy or rows_ld(out), M, C, L.dtype_code(u.dtype), L.stream()),
-            "bn_apply")
+    args = (u.data_ptr(), ldu or rows_ld(u), sc.data_ptr(), sh.data_ptr(), res_mode, L.ptr(r),
+            rows_ld(r) if r is not None else 0, L.ptr(rsc), L.ptr(rsh), int(relu), out.data_ptr(),
+            ldy or rows_ld(out), M, C)
+    if bits is not None:
+        if u.dtype != torch.bfloat16 or C % 8 or bits.dtype != torch.uint8 or bits.numel() < M * (C // 8):
+            raise RuntimeError("stgcn_amd: bn_apply bits need bf16 rows, C % 8 == 0 and a uint8 [M][C/8] buffer")
+        L.check(L.lib().stgcn_bn_apply_bits(*args, bits.data_ptr(), L.stream()), "bn_apply_bits")
+    else:
+        L.check(L.lib().stgcn_bn_apply(*args, L.dtype_code(u.dtype), L.stream()), "bn_apply")
     if h:
         h(ktag, "end", None)
     return out
@@ -806,6 +814,7 @@ def bn_fused_ok(C: int, dtype) -> bool:
 
 def bn_bwd_fused(dy, M, C, mask=0, mref=None, msc=None, msh=None, x1=None, mr1=None, g1=None, out1=None,
                  x2=None, mr2=None, g2=None, out2=None, acc2=False, bias_sums=False):
+    # mask 3: mref = the uint8 [M][C/8] sign bits of the forward's output (bn_apply(bits=...))
     """Fused BN backward (stgcn_bn_bwd_fused_*).  Returns (sums [3, C] = (sum dz, sum dz*xhat1, sum dz*xhat2),
     osum [3, C] = (sum out1, sum out2, -) or None), contiguous rows.  out1 / out2 are written in place."""
     code = L.dtype_code(dy.dtype)
@@ -820,7 +829,7 @@ def bn_bwd_fused(dy, M, C, mask=0, mref=None, msc=None, msh=None, x1=None, mr1=N
     d.out1, d.out2, d.osum, d.work = L.ptr(out1), L.ptr(out2), L.ptr(osum), work.data_ptr()
     d.M, d.C, d.mask = M, C, mask
     d.lddy = rows_ld(dy)
-    d.ldm = rows_ld(mref) if mref is not None else 0
+    d.ldm = (C // 8 if mask == 3 else rows_ld(mref)) if mref is not None else 0
     d.ldx1 = rows_ld(x1) if x1 is not None else 0
     d.ldx2 = rows_ld(x2) if x2 is not None else 0
     d.ldo1 = rows_ld(out1) if out1 is not None else 0

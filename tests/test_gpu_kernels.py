@@ -434,3 +434,38 @@ def test_wgrad_1x1(K, Cin, Cout, N, T):
     dw = torch.zeros((1, Cout, Cin), device=DEV)
     got = K.conv_wgrad(cl(x.float(), torch.bfloat16), cl(dy.float(), torch.bfloat16), Cin, Cout, T, T, dw=dw)
     assert_close(got.reshape(Cout, Cin).cpu(), ref, 1e-4, "wgrad 1x1")
+
+
+@pytest.mark.parametrize("mode", ["identity", "conv_res"])
+def test_bn_apply_bits_and_mask3(K, mode):
+    """bn_apply's sign-bit output (bit c % 8 of byte [m][c / 8] = stored y > 0) and the fused BN backward reading it
+    as mask 3: bit-identical to mask 1 on the stored y (same dz, same sums, same outputs)."""
+    torch.manual_seed(77)
+    N, C, T, V = 3, 64, 23, 25
+    M = N * T * V
+    bf = torch.bfloat16
+    u, x, r = (cl(torch.randn(N, C, T, V) * s + o, bf) for s, o in ((2, 0.3), (1, -0.2), (1, 0.1)))
+    sc, sh = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV)
+    rsc, rsh = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV)
+    kw = dict(res_mode=2, r=r, rsc=rsc, rsh=rsh) if mode == "conv_res" else dict(res_mode=1, r=x)
+    y_ref = K.bn_apply(u, sc, sh, M, C, **kw)
+    bits = torch.empty((M, C // 8), dtype=torch.uint8, device=DEV)
+    y = K.bn_apply(u, sc, sh, M, C, bits=bits, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_ref)
+    rows = y.permute(0, 2, 3, 1).reshape(M, C)
+    expect = (rows > 0).to(torch.uint8).view(M, C // 8, 8)
+    weights = (2 ** torch.arange(8, device=DEV)).to(torch.uint8)
+    assert torch.equal(bits, (expect * weights).sum(-1).to(torch.uint8))
+    dy = cl(torch.randn(N, C, T, V), bf)
+    mr = torch.stack([torch.randn(C, device=DEV), torch.rand(C, device=DEV) + 0.5], 1).contiguous()
+    gam = torch.rand(C, device=DEV) + 0.5
+    outs = []
+    for mk in (dict(mask=1, mref=y), dict(mask=3, mref=bits)):
+        du, dx = torch.empty_like(u), torch.empty_like(u)
+        extra = dict(x2=r, mr2=mr, g2=gam) if mode == "conv_res" else {}
+        s, o = K.bn_bwd_fused(dy, M, C, x1=u, mr1=mr, g1=gam, out1=du, out2=dx, bias_sums=True, **extra, **mk)
+        torch.cuda.synchronize()
+        outs.append((du, dx, s.clone(), o.clone()))
+    for a_, b_ in zip(outs[0], outs[1]):
+        assert torch.equal(a_, b_)
