@@ -145,6 +145,13 @@ typedef struct {
   const float* bias; /* [V][Cout] or NULL */
   float* stats;
   int NT, V, J, Cin, Cout, Cin_pad, Cout_pad, in_ld, out_ld, accumulate;
+  /* optional masked residual (bf16, accumulate = 0, 16-B aligned rows): out = result + res * mask with mask bit
+   * c % 8 of byte res_bits[row * (Cout / 8) + c / 8] (stgcn_bn_apply_bits' layout) — the identity residual's
+   * gradient dz = dy * [y > 0] of stgcn.py:191-193 added in the data gradient's epilogue instead of being
+   * written by the BatchNorm backward and read back here.  res rows: ld res_ld, rows as out. */
+  const void* res;
+  const void* res_bits;
+  int res_ld;
 } stgcn_gconv_desc;
 
 int stgcn_gconv(const stgcn_gconv_desc* d, int dtype, void* stream);

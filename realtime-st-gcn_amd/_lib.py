@@ -58,7 +58,7 @@ class GconvDesc(ctypes.Structure):
     _fields_ = [("in_", c_void_p), ("out", c_void_p), ("w", c_void_p), ("nbr", c_void_p), ("deg", c_void_p),
                 ("bias", c_void_p), ("stats", c_void_p)] + \
                [(n, c_int) for n in ("NT", "V", "J", "Cin", "Cout", "Cin_pad", "Cout_pad", "in_ld", "out_ld",
-                                     "accumulate")]
+                                     "accumulate")] + [("res", c_void_p), ("res_bits", c_void_p), ("res_ld", c_int)]
 
 
 class GconvWgradDesc(ctypes.Structure):

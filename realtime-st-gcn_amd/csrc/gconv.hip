@@ -393,6 +393,16 @@ __global__ __launch_bounds__(WM * WN * 64, (NSTG && (WM * TM + WN * TN) * 32 * 1
 #pragma unroll
               for (int e = 0; e < VEC; ++e) f[e] += o[e];
               *reinterpret_cast<uint4*>(p) = pack16(f, (T*)nullptr);
+            } else if (sizeof(T) == 2 && a.res) {  // masked residual (launcher: bf16, VEC = 8 = one mask byte)
+              const long grow = (long)(i0 + rb + row) * V + jt;
+              const int cc = c0 + u * VEC;
+              unpack16(*reinterpret_cast<const uint4*>(scratch + row * SROW + u * 16), f, (T*)nullptr);
+              unpack16(*reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.res) + grow * a.res_ld + cc), o,
+                       (T*)nullptr);
+              const unsigned mb = reinterpret_cast<const unsigned char*>(a.res_bits)[grow * (a.Cout / 8) + cc / 8];
+#pragma unroll
+              for (int e = 0; e < VEC; ++e) f[e] += ((mb >> e) & 1u) ? o[e] : 0.f;
+              *reinterpret_cast<uint4*>(p) = pack16(f, (T*)nullptr);
             } else {
               *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(scratch + row * SROW + u * 16);
             }
@@ -467,6 +477,8 @@ int launch_gconv(const stgcn_gconv_desc& a, hipStream_t s) {
     return STGCN_EHIP;
   // 16-B row stores through the LDS scratch whenever rows are 16-B aligned (per-element stores otherwise)
   const bool accv = (a.out_ld % VEC) == 0 && (a.Cout % VEC) == 0;
+  if (a.res && (!accv || sizeof(T) != 2 || a.accumulate || !a.res_bits || a.Cout % 8 || a.res_ld % 8))
+    return STGCN_EBADSHAPE;  // the masked residual rides on the 16-B bf16 epilogue only
   if (accv)
     hipLaunchKernelGGL((gconv_kernel<T, WM, WN, TM, TN, KC, true, NSTG>), dim3((unsigned)nblk), dim3(WM * WN * 64),
                        lds, s, a, g);

@@ -351,6 +351,7 @@ class StgcnLayerFunction(torch.autograd.Function):
         sv = list(ctx.saved_tensors)
         x, A32, XA, g, u, y, wg, bg, wt, n1w, n1b, n2w, n2b = sv[:13]
         rest = sv[13:]
+        ybits = None
         if norm == BN:
             mr1, sc1, sh1, mr2, ybits = rest[:5]
             rest = rest[5:]
@@ -380,6 +381,9 @@ class StgcnLayerFunction(torch.autograd.Function):
         dx = K.cl_empty(N, Cin, T, V, dtype, dev)
         dx_written = False
         fused = norm == BN and K.bn_fused_ok(Cout, dtype)
+        # identity residual with the forward's sign bits and the gathered graph conv: its masked gradient
+        # dy * [y > 0] is added in the graph conv's data-gradient epilogue (not written to dx by the BN backward)
+        res_in_gconv = fused and residual and not res_conv and ybits is not None and ctx.sup is not None
         bt_done = False
         if fused:
             # one reduce + one apply pass: du, the residual branch's dr (or dx = dz), and the conv-bias
@@ -390,7 +394,7 @@ class StgcnLayerFunction(torch.autograd.Function):
             if res_conv:
                 dr = K.cl_empty(N, Cout, T_out, V, dtype, dev)
                 kw.update(x2=r, mr2=strr, g2=nrw.detach().float(), out2=dr)
-            elif residual:
+            elif residual and not res_in_gconv:
                 kw.update(out2=dx)
                 dx_written = True
             sums2, osum2 = K.bn_bwd_fused(dy, M2, Cout, **kw)
@@ -479,7 +483,8 @@ class StgcnLayerFunction(torch.autograd.Function):
             dA = grads.pop("dA")
             wgT = packs.gwT if packs is not None and packs.gwT is not None else \
                 K.gconv_weights(A32, wg2, sup, Cout, Cin, True, dtype)
-            K.gconv(dg, wgT, sup, Cout, Cin, trans=True, out=dx, accumulate=dx_written)
+            K.gconv(dg, wgT, sup, Cout, Cin, trans=True, out=dx, accumulate=dx_written,
+                    res=(dy, ybits) if res_in_gconv else None)
         else:
             # DW[(n,t,w)][p*Cin+ci] = sum_c dg[(n,t,w)][c] Wg[p*Cout+c][ci]
             wgT = wg.detach().float().view(P, Cout, Cin).permute(0, 2, 1).reshape(1, P * Cin, Cout)

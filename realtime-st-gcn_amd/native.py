@@ -647,8 +647,10 @@ def layer_fused(x, A, wimg, gbias, n1_scale, n1_shift, wt_packed, tbias, stats=N
     return z
 
 
-def gconv(x, wpk, sup, Cin, Cout, trans=False, bias=None, stats=None, out=None, accumulate=False, tag=None):
-    """out rows (N, Cout, T, V) (+)= joint-gathered GEMM of x rows with packed effective weights."""
+def gconv(x, wpk, sup, Cin, Cout, trans=False, bias=None, stats=None, out=None, accumulate=False, tag=None,
+          res=None):
+    """out rows (N, Cout, T, V) (+)= joint-gathered GEMM of x rows with packed effective weights.
+    ``res`` = (rows, sign bits): out = GEMM + rows * mask (bf16; the identity residual's masked gradient)."""
     N, _, T, V = x.shape
     if out is None:
         out = cl_empty(N, Cout, T, V, x.dtype, x.device)
@@ -659,6 +661,11 @@ def gconv(x, wpk, sup, Cin, Cout, trans=False, bias=None, stats=None, out=None, 
     d.NT, d.V, d.J, d.Cin, d.Cout = N * T, V, sup.J, Cin, Cout
     d.Cin_pad, d.Cout_pad = wpk.shape[3], wpk.shape[2]
     d.in_ld, d.out_ld, d.accumulate = rows_ld(x), rows_ld(out), int(accumulate)
+    if res is not None:
+        rr, rbits = res
+        if accumulate or rbits.dtype != torch.uint8:
+            raise RuntimeError("stgcn_amd: gconv's masked residual needs accumulate=False and uint8 sign bits")
+        d.res, d.res_bits, d.res_ld = rr.data_ptr(), rbits.data_ptr(), rows_ld(rr)
     h = KTIME_HOOK
     if h:
         ktag = _k_start(h, "gconv_dgrad" if trans else "gconv_fwd", f"{Cin}->{Cout}" if not trans else f"{Cout}->{Cin}",

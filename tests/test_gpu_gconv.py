@@ -117,3 +117,29 @@ def test_gconv_finish_bias_merged(K, pkg, Cin, Cout):
     dW, dA, db = K.gconv_finish_bias(dweff, A, W, sup, Cout, Cin, b, S)
     torch.cuda.synchronize()
     assert torch.equal(dW, dW_ref) and torch.equal(dA, dA_ref) and torch.equal(db, db_ref)
+
+
+@pytest.mark.parametrize("Cin,Cout", [(64, 64), (256, 256), (128, 64)])
+def test_gconv_dgrad_masked_residual(K, pkg, Cin, Cout):
+    """The data gradient with the identity residual's masked gradient added in its epilogue (res = (dy, sign
+    bits)) is bit-identical to writing dz = dy * mask first and accumulating (the route it replaces)."""
+    torch.manual_seed(11)
+    A = torch.tensor(pkg.Graph(**pkg.PKU_MMD).A, dtype=torch.float32, device=DEV)
+    P, V = A.shape[0], A.shape[-1]
+    N, T = 2, 23
+    bf = torch.bfloat16
+    sup = K.GraphSupport(A)
+    W = torch.randn(P * Cout, Cin, device=DEV) / Cin ** 0.5
+    wT = K.gconv_weights(A, W, sup, Cout, Cin, True, bf)
+    dg = cl(torch.randn(N, Cout, T, V), bf)
+    dy = cl(torch.randn(N, Cin, T, V), bf)
+    y = cl(torch.randn(N, Cin, T, V), bf)
+    M = N * T * V
+    rows = y.permute(0, 2, 3, 1).reshape(M, Cin)
+    w8 = (2 ** torch.arange(8, device=DEV)).to(torch.uint8)
+    bits = ((rows > 0).to(torch.uint8).view(M, Cin // 8, 8) * w8).sum(-1).to(torch.uint8)
+    dz = (dy.float() * (y.float() > 0)).to(bf).contiguous(memory_format=torch.channels_last)
+    ref = K.gconv(dg, wT, sup, Cout, Cin, trans=True, out=dz.clone(memory_format=torch.channels_last), accumulate=True)
+    out = K.gconv(dg, wT, sup, Cout, Cin, trans=True, res=(dy, bits))
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
