@@ -412,6 +412,12 @@ typedef struct {
    * which the layer's weight gradient reads (saves recomputing it in the backward) */
   void* h_out;
   int h_ld;
+  /* BatchNorm layers, optional: the graph-conv output g (bias included) as INPUT rows (ld g_in_ld) instead of
+   * recomputing it — the kernel is then the temporal conv of the training forward: h = relu(g * n1_scale +
+   * n1_shift) staged into its LDS ring once per frame, z = tcn(h) + tbias and BN2 partials out (wg_frag, A,
+   * gbias unused, may be NULL).  Replaces conv_wide's 64-channel forward (stgcn.py:151-159). */
+  const void* g_in;
+  int g_in_ld;
 } stgcn_layer_fused_desc;
 
 int stgcn_layer_fused_fwd(const stgcn_layer_fused_desc* d, void* stream);

@@ -72,7 +72,7 @@ class LayerFusedDesc(ctypes.Structure):
                                         "stats")] + [(n, c_int) for n in ("N", "T", "V", "P", "x_ld", "z_ld")] + \
                [(n, c_void_p) for n in ("ln1_g", "ln1_b", "ln2_g", "ln2_b")] + [("ln", c_int), ("residual", c_int)] + \
                [(n, c_void_p) for n in ("g_out", "u_out", "st1_out", "st2_out")] + [("g_ld", c_int), ("u_ld", c_int)] + \
-               [("h_out", c_void_p), ("h_ld", c_int)]
+               [("h_out", c_void_p), ("h_ld", c_int), ("g_in", c_void_p), ("g_in_ld", c_int)]
 
 
 class BnBwdDesc(ctypes.Structure):

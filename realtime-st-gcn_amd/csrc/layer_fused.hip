@@ -154,7 +154,7 @@ struct FGeom {
   int off_tab, off_ring, off_h, off_red, off_zs;  // LDS offsets
 };
 
-template <int P, bool LN>
+template <int P, bool LN, bool GIN = false>
 __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_layer_fused_desc a, const FGeom g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int K16 = P * G * 2;  // 16-wide K steps of W' (P*64 / 16)
@@ -182,9 +182,11 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
 
   // ---- per block: W' slice, BN1 tables, zeroed panel rings (rows V..31 stay zero)
   {
-    const uint4* wsrc = reinterpret_cast<const uint4*>(a.wg_frag);
-    uint4* wdst = reinterpret_cast<uint4*>(sW);
-    for (int e = tid; e < 2 * K16 * 64; e += NW * 64) wdst[e] = wsrc[e];
+    if (!GIN) {
+      const uint4* wsrc = reinterpret_cast<const uint4*>(a.wg_frag);
+      uint4* wdst = reinterpret_cast<uint4*>(sW);
+      for (int e = tid; e < 2 * K16 * 64; e += NW * 64) wdst[e] = wsrc[e];
+    }
     if (LN) {
       for (int e = tid; e < V * C; e += NW * 64) {
         sGam[(e / C) * CGP + e % C] = a.ln2_g[e];
@@ -212,7 +214,64 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
     if (lane == 0 && blockIdx.x < PROF_BLOCKS)
       for (int j = 0; j < 6; ++j) g_fused_prof[((long)blockIdx.x * 8 + wave) * 6 + j] = pa[j];
   };
-  if (wave >= NWT) {
+  if constexpr (GIN) {
+    if (wave >= NWT) {
+      // ============ staging waves (g_in): h = relu(g * s1 + shift) of the step's frames into the ring ============
+      // (the BN1 table sBp holds the shift per joint: no graph-conv bias here, g already carries it)
+      const int gw = wave - NWT;
+      const bf16* __restrict__ gsrc = reinterpret_cast<const bf16*>(a.g_in) + (long)n * T * V * a.g_in_ld;
+      constexpr int UPL = (VMAX * 8 + 63) / 64;  // 16-B units of a frame per lane
+      auto stage = [&](int fa0) {
+        const long long pt0 = ptime();
+        uint4 u[FPW][UPL];
+#pragma unroll
+        for (int i = 0; i < FPW; ++i) {  // all loads of both frames first
+          const int fa = fa0 + NWG * i, f = R0 - HALO + fa;
+          const int fc = min(max(f, 0), T - 1);
+#pragma unroll
+          for (int k = 0; k < UPL; ++k) {
+            const int e = min(lane + 64 * k, V * 8 - 1);
+            u[i][k] = *reinterpret_cast<const uint4*>(gsrc + ((long)fc * V + (e >> 3)) * a.g_in_ld + (e & 7) * 8);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < FPW; ++i) {
+          const int fa = fa0 + NWG * i, f = R0 - HALO + fa;
+          if (fa >= nfr) continue;
+          const bool okf = f >= 0 && f < T;  // padding frame: h = 0 (the conv's zero padding applies to h)
+          char* hrow = sH + (fa % RF) * vrs;
+#pragma unroll
+          for (int k = 0; k < UPL; ++k) {
+            const int e = lane + 64 * k;
+            if (e >= V * 8) break;
+            const int row = e >> 3, c0 = (e & 7) * 8;
+            uint4 o = make_uint4(0, 0, 0, 0);
+            if (okf) {
+              float v[8];
+              unpack16(u[i][k], v, (bf16*)nullptr);
+              const float* bp = sBp + row * CBP + c0;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) v[j] = fmaxf(fmaf(v[j], sSc[c0 + j], bp[j]), 0.f);
+              o = pack16(v, (bf16*)nullptr);
+            }
+            *reinterpret_cast<uint4*>(hrow + row * RSH + c0 * 2) = o;
+          }
+        }
+        pa[1] += ptime() - pt0;
+      };
+      stage(gw);
+      stage(CF + gw);
+      lds_barrier();  // S_0: frames 0..15 ready
+      for (int s = 1; s <= nsteps; ++s) {
+        if (s < nsteps) stage(CF * (s + 1) + gw);
+        const long long pb = ptime();
+        lds_barrier();  // S_s
+        pa[2] += ptime() - pb;
+      }
+      if constexpr (PROF) prof_out();
+      return;
+    }
+  } else if (wave >= NWT) {
     // =============================== GCN waves: h frames ===============================
     const int gw = wave - NWT;
     bf16x8 ac[P][2];  // stage-1 B operands: B[k = input joint u][n = output joint o] = A[p][u][o]
@@ -913,7 +972,9 @@ long layer_fused_row_blocks(int N, int T) {
 }
 
 int layer_fused_launch(const stgcn_layer_fused_desc& a, hipStream_t s) {
-  if (!a.x || !a.z || !a.wg_frag || !a.A || !a.wt_frag) return STGCN_EBADSHAPE;
+  const bool gin = a.g_in != nullptr;
+  if (!a.z || !a.wt_frag || (!gin && (!a.x || !a.wg_frag || !a.A))) return STGCN_EBADSHAPE;
+  if (gin && (a.ln || a.g_out || a.u_out || a.h_out || a.gbias || a.g_in_ld < C || a.g_in_ld % 8)) return STGCN_EBADSHAPE;
   if (a.ln ? (!a.ln1_g || !a.ln1_b || !a.ln2_g || !a.ln2_b || a.stats) : (!a.n1_scale || !a.n1_shift))
     return STGCN_EBADSHAPE;
   const int ntrain = !!a.g_out + !!a.u_out + !!a.st1_out + !!a.st2_out;
@@ -936,7 +997,7 @@ int layer_fused_launch(const stgcn_layer_fused_desc& a, hipStream_t s) {
   typedef void (*KFn)(const stgcn_layer_fused_desc, const FGeom);
   static const KFn tab[2][3] = {{layer_fused_kernel<1, false>, layer_fused_kernel<2, false>, layer_fused_kernel<3, false>},
                                 {layer_fused_kernel<1, true>, layer_fused_kernel<2, true>, layer_fused_kernel<3, true>}};
-  const KFn k = tab[a.ln ? 1 : 0][a.P - 1];
+  const KFn k = gin ? layer_fused_kernel<1, false, true> : tab[a.ln ? 1 : 0][a.P - 1];
   if (stgcn_lds_attr((const void*)k, LDS_MAX, s)) return STGCN_EHIP;
   hipLaunchKernelGGL(k, dim3((unsigned)nblk), dim3(NW * 64), lds, s, a, g);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;

@@ -192,7 +192,7 @@ def _stats_arena(cache, dev, dtype, shapes, route):
     st = cache.get(key)
     if st is None:
         old = [k for k in list(cache) if isinstance(k, tuple) and k[:1] == ("bn_stats",)]
-        for k in old[:-3]:  # keep a few shapes (config 4 alternates 64- and 65-window units)
+        for k in old[:-6]:  # keep a few shapes and routes (config 4 alternates 64- and 65-window units)
             del cache[k]
         st = cache[key] = K.zeros_arena(dev, *shapes)
     return st
@@ -302,9 +302,16 @@ class StgcnLayerFunction(torch.autograd.Function):
         wtp, cpt, kpt = packs.wt if packs is not None else \
             K.pack_weight(wt.detach().float().squeeze(-1).permute(2, 0, 1), dtype, stride=stride)  # [Kt][Cout][Cin]
 
-        u = K.conv_rows(g if norm == BN else h, wtp, Cout, Cout, cpt, kpt, T, T_out, Kt=kt, stride=stride, pad=pad,
-                        bias=bt.detach().float().contiguous(), stats=st2 if norm == BN else None,
-                        tag=f"tcn_fwd_c{Cout}" if stride == 1 else None, **pro1)
+        if (norm == BN and gather and ROUTING.bn_tcn_fused and getattr(wtp, "frag_stride", None) == 1
+                and K.layer_fused_ok(sup, P, Cin, Cout, V, kt, stride, dtype)):
+            # 64 -> 64 stride-1: layer_fused.hip's g-input mode (BN1 + ReLU staged once per frame into its LDS
+            # ring, the 9-tap conv from there) instead of conv_wide's per-tile prologue
+            st2 = _stats_arena(cache, dev, x.dtype, [(K.layer_fused_row_blocks(N, T), Cout, 4)], "tcn")[0]
+            u = K.layer_tcn(g, sc1, sh1, wtp, bt.detach().float().contiguous(), st2, tag=f"tcn_fwd_c{Cout}")
+        else:
+            u = K.conv_rows(g if norm == BN else h, wtp, Cout, Cout, cpt, kpt, T, T_out, Kt=kt, stride=stride,
+                            pad=pad, bias=bt.detach().float().contiguous(), stats=st2 if norm == BN else None,
+                            tag=f"tcn_fwd_c{Cout}" if stride == 1 else None, **pro1)
 
         # ---- y = relu(norm2(u) + res)
         if norm == BN:

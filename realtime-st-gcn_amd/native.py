@@ -647,6 +647,28 @@ def layer_fused(x, A, wimg, gbias, n1_scale, n1_shift, wt_packed, tbias, stats=N
     return z
 
 
+def layer_tcn(g, n1_scale, n1_shift, wt_packed, tbias, stats, tag=None):
+    """stgcn_layer_fused_fwd in its g-input mode: z rows (N, 64, T, V) = tcn(relu(g * n1_scale + n1_shift)) +
+    tbias with BN2 partials into ``stats`` ([layer_fused_row_blocks(N, T)][64][4], every block written) — the
+    BatchNorm training forward's temporal conv on the graph-conv output g (bias included)."""
+    N, C, T, V = g.shape
+    if getattr(wt_packed, "frag_stride", None) != 1:
+        raise RuntimeError("stgcn_amd: layer_tcn needs the stride-1 fragment image of the temporal weight")
+    z = cl_empty(N, C, T, V, g.dtype, g.device)
+    d = L.LayerFusedDesc()
+    d.g_in, d.g_in_ld, d.z = g.data_ptr(), rows_ld(g), z.data_ptr()
+    d.n1_scale, d.n1_shift = L.ptr(n1_scale), L.ptr(n1_shift)
+    d.wt_frag, d.tbias, d.stats = wt_packed.frag_ptr, L.ptr(tbias), L.ptr(stats)
+    d.N, d.T, d.V, d.P, d.x_ld, d.z_ld = N, T, V, 1, rows_ld(g), rows_ld(z)
+    hook = EVENT_HOOK if tag is not None else None
+    if hook:
+        hook(tag, "start", None)
+    L.check(L.lib().stgcn_layer_fused_fwd(d, L.stream()), "layer_fused (g input)")
+    if hook:
+        hook(tag, "end", None)
+    return z
+
+
 def gconv(x, wpk, sup, Cin, Cout, trans=False, bias=None, stats=None, out=None, accumulate=False, tag=None,
           res=None):
     """out rows (N, Cout, T, V) (+)= joint-gathered GEMM of x rows with packed effective weights.

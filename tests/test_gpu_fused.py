@@ -393,3 +393,78 @@ def test_ln_model_fused_training(P, monkeypatch):
     assert_close(out[True][0], out[False][0], 2e-2, "fused vs unfused logits")
     for k, gu in out[False][1].items():
         assert_grad_close(out[True][1][k], gu, 4e-2, f"fused vs unfused {k}", reduction=True)
+
+
+@pytest.mark.parametrize("N,T", [(2, 37), (3, 9), (64, 300)])
+def test_layer_tcn_kernel(P, N, T):
+    """layer_fused's g-input mode (native.layer_tcn, the BatchNorm training forward's temporal conv at 64 -> 64
+    stride 1): z = conv(relu(g * s1 + shift1)) + bias (stgcn.py:151-159) and its BN2 partials against torch fp32
+    on the same bf16 g, at a partial last step, a run shorter than the halo and the bench shape."""
+    K = P.native
+    torch.manual_seed(5 * N + T)
+    V, C = 25, 64
+    g = rb(torch.randn(N, C, T, V) * 2 + 0.3)
+    wt = rb(torch.randn(C, C, 9, 1) / (9 * C) ** 0.5)
+    bt = torch.randn(C) * 0.1
+    sc, sh = torch.rand(C) + 0.5, torch.randn(C) * 0.5
+    h = torch.relu(g * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1))
+    ref = F.conv2d(rb(h), wt, bt, padding=(4, 0))
+    wtp, _, _ = K.pack_weight(wt.squeeze(-1).permute(2, 0, 1).to(DEV), BF, stride=1)
+    st = torch.full((K.layer_fused_row_blocks(N, T), C, 4), float("nan"), device=DEV)  # every row is written
+    z = K.layer_tcn(cl(g, BF), sc.to(DEV), sh.to(DEV), wtp, bt.to(DEV), st)
+    assert_close(z.float(), ref, 2e-2, "tcn z")
+    mr, _, _ = K.bn_finalize(st, st.shape[0], C, C, None, None)
+    assert_close(mr[:, 0].cpu(), ref.mean(dim=(0, 2, 3)), 2e-2, "bn2 mean")
+    assert_close(mr[:, 1].cpu(), 1 / torch.sqrt(ref.var(dim=(0, 2, 3), unbiased=False) + 1e-5), 1e-2, "bn2 rstd")
+
+
+@pytest.mark.parametrize("N,T,residual", [(3, 37, True), (2, 20, False)])
+def test_bn_layer_tcn_training(P, monkeypatch, N, T, residual):
+    """Training forward of a BatchNorm 64 -> 64 stride-1 layer with its temporal conv through layer_fused's
+    g-input mode (routing bn_tcn_fused) against conv_wide's route and the fp32 oracle (stgcn.py:181-193): y and
+    every gradient at the bf16 layer tolerance; the g-input kernel ran once."""
+    from conftest import assert_grad_close, grad_floor
+    calls = []
+    orig = P.native.layer_tcn
+
+    def spy(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+
+    monkeypatch.setattr(P.native, "layer_tcn", spy)
+    g = torch.Generator().manual_seed(41 + T)
+    A = _graph(P)
+    torch.manual_seed(41 + T)
+    layer = P.StgcnLayer(64, 64, (9, 25), 3, 25, stride=1, residual=residual, normalization="BatchNorm")
+    sd = {k: v.clone().requires_grad_(True) for k, v in layer.state_dict().items() if v.is_floating_point()}
+    x = torch.randn(N, 64, T, 25, generator=g)
+    dy = torch.randn(N, 64, T, 25, generator=g)
+    xr = x.clone().requires_grad_(True)
+    Ar = A.clone().requires_grad_(True)
+    ref = O.stgcn_layer(xr, Ar, sd, "", 9, 1, residual, "BatchNorm")
+    ref.backward(dy)
+    layer = P.set_compute_dtype(layer.to(DEV), "bf16")
+    out = {}
+    for route in (True, False):
+        monkeypatch.setattr(P.routing.ROUTING, "bn_tcn_fused", route)
+        layer.zero_grad(set_to_none=True)
+        xg = x.to(DEV).requires_grad_(True)
+        Ag = A.to(DEV).requires_grad_(True)
+        y = layer(xg, Ag)
+        y.backward(dy.to(DEV))
+        torch.cuda.synchronize()
+        out[route] = (y.detach().float().cpu(), xg.grad.float().cpu(), Ag.grad.float().cpu(),
+                      {k: p.grad.float().cpu() for k, p in layer.named_parameters()})
+    assert calls == [1], calls
+    (yf, dxf, dAf, gf), (yu, dxu, dAu, gu) = out[True], out[False]
+    assert_close(yf, yu, 2e-2, "g-input vs conv_wide y")
+    assert_grad_close(dxf, dxu, 4e-2, "g-input vs conv_wide dx")
+    for k in gu:
+        assert_grad_close(gf[k], gu[k], 4e-2, f"g-input vs conv_wide {k}", reduction=True)
+    tol = 4e-2
+    assert_close(yf, ref, tol, "y")
+    assert_grad_close(dxf, xr.grad, tol, "dx")
+    assert_grad_close(dAf, Ar.grad, tol, "dA", reduction=True)
+    grads = {k: v.grad for k, v in sd.items() if v.grad is not None}
+    for k, gr in grads.items():
+        assert_grad_close(gf[k], gr, tol, k, grad_floor(grads, k), reduction=True)
