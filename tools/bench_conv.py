@@ -63,6 +63,31 @@ for name, N, T, V, Cin, Cout, Kt, s, trans, pro in cases:
     byts = (N * Ti * V * Cin + N * To * V * Cout) * 2
     print(f"{name:16s} {ms*1e3:9.1f} us  {flops/ms/1e9:8.1f} TFLOP/s  {byts/ms/1e6:8.1f} GB/s", flush=True)
 
+# the 64-channel temporal conv kernels outside conv_rows: tconv_frame (forward with the BN1 prologue, bias and
+# BN partials; data grad) and layer_fused's g-input mode
+for name in ("tf_fwd_c64", "tf_dgrad_c64", "tcn_gin_c64"):
+    if only and name != only:
+        continue
+    N, T, V, C = 64, 300, 25, 64
+    x = torch.randn(N, C, T, V, device=dev).to(dt).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(9, C, C, device=dev) * 0.05
+    trans = name == "tf_dgrad_c64"
+    wp, cp, kp = K.pack_weight(w, dt, stride=1, trans=trans)
+    sc = torch.rand(C, device=dev) + 0.5
+    sh = torch.randn(C, device=dev)
+    b = torch.randn(C, device=dev)
+    if name == "tf_fwd_c64":
+        st = torch.zeros((K.tconv_frame_row_blocks(N, T), cp, 4), device=dev)
+        f = lambda: K.tconv_frame(x, wp, cp, kp, bias=b, pro_a=sc, pro_b=sh, stats=st)
+    elif trans:
+        f = lambda: K.tconv_frame(x, wp, cp, kp, trans=True)
+    else:
+        st = torch.zeros((K.layer_fused_row_blocks(N, T), C, 4), device=dev)
+        f = lambda: K.layer_tcn(x, sc, sh, wp, b, st)
+    ms = timeit(f)
+    flops = 2.0 * N * T * V * C * C * 9
+    print(f"{name:16s} {ms*1e3:9.1f} us  {flops/ms/1e9:8.1f} TFLOP/s  {4*N*T*V*C/ms/1e6:8.1f} GB/s", flush=True)
+
 wcases = [  # name, N, T, V, Cin, Cout, Kt, stride, pro
     ("tcn_wgrad_c64", 64, 300, 25, 64, 64, 9, 1, 1),
     ("tcn_wgrad_c128", 64, 150, 25, 128, 128, 9, 1, 1),
