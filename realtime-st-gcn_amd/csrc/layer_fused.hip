@@ -713,26 +713,49 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
         dmean[i] = su / cnt;
         rstd[i] = 1.f / sqrtf(fmaxf(sq - su * dmean[i], 0.f) / (cnt - 1.f) + 1e-5f);
       }
+      // 16-B stores: a lane holds 4 channels of each 8-channel group; one v_permlane32_swap per dword gives lanes
+      // 0-31 group 2p and lanes 32-63 group 2p + 1 whole (jv is the same for lanes lr and lr + 32)
+      auto store_swapped = [&](bf16* row, unsigned (&pk)[4][2]) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            const auto sw = __builtin_amdgcn_permlane32_swap(pk[2 * p][d], pk[2 * p + 1][d], false, false);
+            pk[2 * p][d] = sw[0];
+            pk[2 * p + 1][d] = sw[1];
+          }
+        if (jv) {
+#pragma unroll
+          for (int p = 0; p < 2; ++p)
+            *reinterpret_cast<uint4*>(row + 32 * ct + 16 * p + 8 * lh) =
+                make_uint4(pk[2 * p][0], pk[2 * p][1], pk[2 * p + 1][0], pk[2 * p + 1][1]);
+        }
+      };
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int fo = 4 * fg + i;
-        if (fo >= nfv || !jv) continue;
-        const int r = fo * V + lr;
+        if (fo >= nfv) continue;
+        const int r = fo * V + min(lr, V - 1);
         if (a.u_out) {  // training forward: u = z (pre-LN2, bias included) rows and the frame's LN2 statistics
-          bf16* ur = reinterpret_cast<bf16*>(a.u_out) + (((long)n * T + f0) * V + r) * a.u_ld + 32 * ct + 4 * lh;
+          bf16* ur = reinterpret_cast<bf16*>(a.u_out) + (((long)n * T + f0) * V + r) * a.u_ld;
+          unsigned pk[4][2];
 #pragma unroll
           for (int q4 = 0; q4 < 4; ++q4) {
             bf16x4 uv;
 #pragma unroll
             for (int e = 0; e < 4; ++e) uv[e] = (bf16)(acc[i][4 * q4 + e] + piv);
-            *reinterpret_cast<bf16x4*>(ur + 8 * q4) = uv;
+            const u32x2n w2 = __builtin_bit_cast(u32x2n, uv);
+            pk[q4][0] = w2.x;
+            pk[q4][1] = w2.y;
           }
+          store_swapped(ur, pk);
           if (ct == 0 && lane == 0)
             reinterpret_cast<float2*>(a.st2_out)[(long)n * T + f0 + fo] = make_float2(piv + dmean[i], rstd[i]);
         }
         // y = relu(((d - dmean) * rstd) * gamma + beta + x) as relu(fma(fma(d, A, B), gamma, beta) + x), A = rstd,
         // B = -dmean * rstd, on pairs of channels (packed FMAs)
         const f32x2 A2 = {rstd[i], rstd[i]}, B2 = {-dmean[i] * rstd[i], -dmean[i] * rstd[i]};
+        unsigned pk[4][2];
 #pragma unroll
         for (int q4 = 0; q4 < 4; ++q4) {
           const int co = 32 * ct + 8 * q4 + 4 * lh;
@@ -748,8 +771,11 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
           o[1] = (bf16)fmaxf(t01.y, 0.f);
           o[2] = (bf16)fmaxf(t23.x, 0.f);
           o[3] = (bf16)fmaxf(t23.y, 0.f);
-          *reinterpret_cast<bf16x4*>(zt + (long)r * a.z_ld + co) = o;
+          const u32x2n w2 = __builtin_bit_cast(u32x2n, o);
+          pk[q4][0] = w2.x;
+          pk[q4][1] = w2.y;
         }
+        store_swapped(zt + (long)r * a.z_ld, pk);
       }
       const long long pl2 = ptime();
       pa[4] += pl2 - pl1;
@@ -876,30 +902,43 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
           tb[4 * q4 + 2] = b4.z;
           tb[4 * q4 + 3] = b4.w;
         }
-        // z = acc + bias (8-B stores of 4 channels per lane and row: routing them through LDS into 64-B row runs
-        // measured slower, 90 vs 84.5 us)
+        // z = acc + bias: a lane holds 4 channels of each 8-channel group; one v_permlane32_swap per dword gives
+        // lanes 0-31 group 2p and lanes 32-63 group 2p + 1 whole, so each lane stores 16 B per group pair (the 8-B
+        // stores of 4 channels were store-issue bound; routing them through LDS into 64-B row runs measured slower)
 #pragma unroll
         for (int i = 0; i < RT; ++i) {
           const int r = (rh * RT + i) * 32 + lr;
-          if (rok[i] && r < vrows) {
+          const bool ok = rok[i] && r < vrows;  // the same for lanes lr and lr + 32 (one row)
+          unsigned pk[4][2];
 #pragma unroll
-            for (int q4 = 0; q4 < 4; ++q4) {
-              bf16x4 o;
+          for (int q4 = 0; q4 < 4; ++q4) {
+            bf16x4 o;
 #pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const float v = acc[i][4 * q4 + e];
+            for (int e = 0; e < 4; ++e) {
+              const float v = acc[i][4 * q4 + e];
+              if (ok) {
                 s1[4 * q4 + e] += v;
                 s2[4 * q4 + e] = fmaf(v, v, s2[4 * q4 + e]);
-                o[e] = (bf16)(v + tb[4 * q4 + e]);
               }
-              bf16* const zp = zt + (long)r * a.z_ld + 32 * ct + 8 * q4 + 4 * lh;
-              if (DBG & 16) {
-              } else if (DBG & 512) {
-                __builtin_nontemporal_store(__builtin_bit_cast(u32x2n, o), reinterpret_cast<u32x2n*>(zp));
-              } else {
-                *reinterpret_cast<bf16x4*>(zp) = o;
-              }
+              o[e] = (bf16)(v + tb[4 * q4 + e]);
             }
+            const u32x2n w2 = __builtin_bit_cast(u32x2n, o);
+            pk[q4][0] = w2.x;
+            pk[q4][1] = w2.y;
+          }
+#pragma unroll
+          for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int d = 0; d < 2; ++d) {
+              const auto sw = __builtin_amdgcn_permlane32_swap(pk[2 * p][d], pk[2 * p + 1][d], false, false);
+              pk[2 * p][d] = sw[0];
+              pk[2 * p + 1][d] = sw[1];
+            }
+          if (ok && !(DBG & 16)) {
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+              *reinterpret_cast<uint4*>(zt + (long)r * a.z_ld + 32 * ct + 16 * p + 8 * lh) =
+                  make_uint4(pk[2 * p][0], pk[2 * p][1], pk[2 * p + 1][0], pk[2 * p + 1][1]);
           }
         }
         const long long pk15 = ptime();
@@ -978,11 +1017,11 @@ int layer_fused_launch(const stgcn_layer_fused_desc& a, hipStream_t s) {
   if (a.ln ? (!a.ln1_g || !a.ln1_b || !a.ln2_g || !a.ln2_b || a.stats) : (!a.n1_scale || !a.n1_shift))
     return STGCN_EBADSHAPE;
   const int ntrain = !!a.g_out + !!a.u_out + !!a.st1_out + !!a.st2_out;
-  if (ntrain != 0 && (ntrain != 4 || !a.ln || a.g_ld < C || a.g_ld % 4 || a.u_ld < C || a.u_ld % 4))
+  if (ntrain != 0 && (ntrain != 4 || !a.ln || a.g_ld < C || a.g_ld % 4 || a.u_ld < C || a.u_ld % 8))
     return STGCN_EBADSHAPE;
   if (a.h_out && (ntrain != 4 || a.h_ld < C || a.h_ld % 4)) return STGCN_EBADSHAPE;
   if (a.N < 1 || a.T < 1 || a.V <= 16 || a.V > VMAX || a.P < 1 || a.P > 3) return STGCN_EBADSHAPE;
-  if (a.x_ld < C || a.x_ld % 8 || a.z_ld < C || a.z_ld % 4) return STGCN_EBADSHAPE;
+  if (a.x_ld < C || a.x_ld % 8 || a.z_ld < C || a.z_ld % 8) return STGCN_EBADSHAPE;
   FGeom g = plan(a.N, a.T);
   const long nblk = (long)a.N * g.runs_n;
   if (nblk > 0x7fffffffL) return STGCN_EBADSHAPE;

@@ -353,25 +353,43 @@ __global__ __launch_bounds__(RW * 64, 1) void tcr_kernel(const stgcn_conv_desc a
   const f32x16 zero = {};
   int bs = 0;  // physical slot of q = 256 s
   f32x16 ap[2] = {zero, zero};  // the previous step's accumulators
-  // one epilogue unit: tile i, channels 32 ct + 8 q4 + 4 lh .. + 3 of output row r0 + 256 sp + 32 (rq + 4 i) + lr
-  auto ep_unit = [&](int i, int q4, int sp) {
+  // one epilogue unit: tile i, channel groups q4 = 2 pr, 2 pr + 1 of output row r0 + 256 sp + 32 (rq + 4 i) + lr.
+  // A lane holds 4 channels of each group (32 ct + 8 q4 + 4 lh ..); one v_permlane32_swap per dword gives lanes
+  // 0-31 the 8 channels of group 2 pr and lanes 32-63 those of group 2 pr + 1: ONE 16-B store per lane instead of
+  // two 8-B stores (the epilogue is store-issue bound)
+  auto ep_unit = [&](int i, int pr, int sp) {
     const int o = r0 + RSTEP * sp + 32 * (rq + 4 * i) + lr;
     const bool ok = o < r1;
-    if (q4 == 0) cnt += ok ? 1 : 0;
-    const float4 b4 = *reinterpret_cast<const float4*>(sbias + 32 * ct + 8 * q4 + 4 * lh);
-    const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
-    bf16x4 st;
+    if (pr == 0) cnt += ok ? 1 : 0;
+    unsigned pk[2][2];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float v = ap[i][4 * q4 + e];
-      if (STATS && ok) {
-        s1[4 * q4 + e] += v;
-        s2[4 * q4 + e] = fmaf(v, v, s2[4 * q4 + e]);
+    for (int h = 0; h < 2; ++h) {
+      const int q4 = 2 * pr + h;
+      const float4 b4 = *reinterpret_cast<const float4*>(sbias + 32 * ct + 8 * q4 + 4 * lh);
+      const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
+      bf16x4 st;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float v = ap[i][4 * q4 + e];
+        if (STATS && ok) {
+          s1[4 * q4 + e] += v;
+          s2[4 * q4 + e] = fmaf(v, v, s2[4 * q4 + e]);
+        }
+        st[e] = (bf16)(v + bb[e]);
       }
-      st[e] = (bf16)(v + bb[e]);
+      const u32x2 w2 = __builtin_bit_cast(u32x2, st);
+      pk[h][0] = w2.x;
+      pk[h][1] = w2.y;
+    }
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      const auto r = __builtin_amdgcn_permlane32_swap(pk[0][d], pk[1][d], false, false);
+      pk[0][d] = r[0];
+      pk[1][d] = r[1];
     }
     if (ok && !(TDBG & 4))
-      *reinterpret_cast<u32x2*>(out + (long)o * a.out_ld + 32 * ct + 8 * q4 + 4 * lh) = __builtin_bit_cast(u32x2, st);
+      *reinterpret_cast<uint4*>(out + (long)o * a.out_ld + 32 * ct + 16 * pr + 8 * lh) =
+          make_uint4(pk[0][0], pk[0][1], pk[1][0], pk[1][1]);
   };
   long long pa[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const long long pstart = tstamp();
@@ -425,8 +443,8 @@ __global__ __launch_bounds__(RW * 64, 1) void tcr_kernel(const stgcn_conv_desc a
       else w = fw[k % 3];
       acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w, fb[k % 3][0], acc[0], 0, 0, 0);
       acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w, fb[k % 3][1], acc[1], 0, 0, 0);
-      if constexpr (k < 8) {
-        if (prev) ep_unit(k >> 2, k & 3, s - 1);
+      if constexpr (k < 4) {
+        if (prev) ep_unit(k >> 1, k & 1, s - 1);
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the reads two k-steps ahead (the scheduler sinks them to their use)
     });
@@ -452,7 +470,7 @@ __global__ __launch_bounds__(RW * 64, 1) void tcr_kernel(const stgcn_conv_desc a
   {
     const long long p3 = tstamp();
 #pragma unroll
-    for (int u = 0; u < 8; ++u) ep_unit(u >> 2, u & 3, nsteps - 1);
+    for (int u = 0; u < 4; ++u) ep_unit(u >> 1, u & 1, nsteps - 1);
     pa[2] += tstamp() - p3;
   }
   if constexpr (TPROF) {

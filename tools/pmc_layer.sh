@@ -15,5 +15,5 @@ for norm in BatchNorm LayerNorm; do
     timeout -s KILL 90 rocprofv3 --pmc $set -d $D/p$i -o p --output-format csv -- python3 tools/bench_layer.py 3 $norm > $D/p$i.log 2>&1 || { echo "pass $i failed rc=$?"; tail -3 $D/p$i.log; exit 1; }
   done
 done
-python3 tools/pmc_json.py gpurun_out/pmc_layer_BatchNorm "layer_fused_kernel<3, false>" profiles/pmc_layer_fused.json
-python3 tools/pmc_json.py gpurun_out/pmc_layer_LayerNorm "layer_fused_kernel<3, true>" profiles/pmc_layer_fused_ln.json
+python3 tools/pmc_json.py gpurun_out/pmc_layer_BatchNorm "layer_fused_kernel<3, false, false>" profiles/pmc_layer_fused.json
+python3 tools/pmc_json.py gpurun_out/pmc_layer_LayerNorm "layer_fused_kernel<3, true, false>" profiles/pmc_layer_fused_ln.json
