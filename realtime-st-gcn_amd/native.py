@@ -663,7 +663,12 @@ def layer_tcn(g, n1_scale, n1_shift, wt_packed, tbias, stats, tag=None):
     hook = EVENT_HOOK if tag is not None else None
     if hook:
         hook(tag, "start", None)
+    kh = KTIME_HOOK
+    if kh:
+        ktag = _k_start(kh, "tcn_fwd", f"{C}->{C} s1", 2.0 * N * T * V * C * C * 9, g.element_size() * N * T * V * 2 * C)
     L.check(L.lib().stgcn_layer_fused_fwd(d, L.stream()), "layer_fused (g input)")
+    if kh:
+        kh(ktag, "end", None)
     if hook:
         hook(tag, "end", None)
     return z
