@@ -24,7 +24,10 @@
 extern "C" {
 #endif
 
-#define STGCN_ABI_VERSION 1
+/* Bumped on every change of a descriptor's layout or of an entry point's signature; realtime-st-gcn_amd/_lib.py
+ * refuses a library whose stgcn_abi_version() differs from the version it was written against.
+ *   1: rounds 1-4;  2: round 5 (stgcn_gconv_desc gained res / res_bits / res_ld). */
+#define STGCN_ABI_VERSION 2
 
 /* Implicit-GEMM (Kt x 1) row convolution; see conv_rows.hip for the exact contract.
  * Replaces: nn.Conv2d tcn.2 (models/stgcn/stgcn.py:154-159), residual.0 (stgcn.py:165-170),
@@ -50,9 +53,10 @@ typedef struct {
 int stgcn_conv_rows(const stgcn_conv_desc* d, int dtype, void* stream);
 /* The 64-channel Kt = 9 stride-1 temporal conv (stgcn.py:151-159) forward (trans 0, pro 0 or 1: BN1 scale /
  * shift + ReLU on the input, bias_mode 0/1, optional BN partial statistics [stgcn_tconv_frame_row_blocks(N, T)]
- * [Cout_pad]) and data gradient (trans 1, pro 0), bf16, on the frame-streaming kernel (tconv_frame.hip): the same
+ * [Cout_pad]) and data gradient (trans 1, pro 0), bf16, on the row-streaming kernel (tconv_frame.hip): the same
  * arithmetic as stgcn_conv_rows for these shapes; w_frag = the MFMA-fragment image of the packed weight
- * (stgcn_pack_weight_frag, Kt = 9), Cin = Cout = 64, pad = 4, 16 < V <= 32, no accumulate. */
+ * (stgcn_pack_weight_frag, Kt = 9), Cin = Cout = 64, pad = 4, 16 < V <= 25, in_ld % 8 == 0, out_ld % 8 == 0 (16-B
+ * row stores), no accumulate; other shapes return STGCN_EBADSHAPE (use stgcn_conv_rows). */
 int stgcn_tconv_frame(const stgcn_conv_desc* d, void* stream);
 long stgcn_tconv_frame_row_blocks(int N, int T);
 /* Pack an fp32 weight given as any strided [Kt][Cout][Cin] view (element (k,co,ci) at src[k*s0+co*s1+ci*s2])

@@ -13,6 +13,9 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("STGCN_LIB") or os.path.join(_HERE, "lib", "libstgcn_amd.so")  # STGCN_LIB: A/B builds
 
+# the STGCN_ABI_VERSION of include/stgcn_amd.h these bindings mirror (test_cpu_host checks the two agree)
+ABI_VERSION = 2
+
 _ERR = {1: "bad shape/arguments", 2: "unsupported dtype", 3: "HIP launch error"}
 
 c_void_p = ctypes.c_void_p
@@ -209,6 +212,10 @@ def load_library(path: str = LIB_PATH):
         fn = getattr(lib, name)  # AttributeError if the symbol is missing
         fn.restype = res
         fn.argtypes = args
+    got = lib.stgcn_abi_version()
+    if got != ABI_VERSION:
+        raise RuntimeError(f"stgcn_amd: {path} implements C-ABI version {got}, these bindings need {ABI_VERSION} "
+                           "(stale build: run __graft_entry__.build())")
     _lib = lib
     return lib
 

@@ -224,7 +224,7 @@ class StgcnLayerFunction(torch.autograd.Function):
         # ---- graph convolution: g = sum_p A_p-mix(x) W_p + bias2d
         sup = cfg[5] if len(cfg) > 5 else None
         gather = sup is not None and A32.dim() == 3 and not sup.dense(P)
-        if (gather and len(cfg) > 7 and cfg[7] and (norm == LN or ROUTING.fused_bn_inference)
+        if (gather and len(cfg) > 7 and cfg[7] and ROUTING.fused_inference and (norm == LN or ROUTING.fused_bn_inference)
                 and K.layer_fused_ok(sup, P, Cin, Cout, V, kt, stride, dtype)):
             # inference: the fused layer kernel (g never leaves the chip; nothing saved for backward).
             # LayerNorm layers: one kernel, 0.14 vs 0.20 ms unfused; BatchNorm layers (routing.fused_bn_inference,
@@ -247,14 +247,22 @@ class StgcnLayerFunction(torch.autograd.Function):
             return y
         # gathered path: bias2d comes from the weight preparation below
         bias2d = None if gather else K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
+        # BatchNorm 64 -> 64 stride-1 training forward: the temporal conv through layer_fused.hip's g-input mode
+        # (routing.bn_tcn_fused, off by default: step-neutral); it writes its own BN2 partials
+        wtp, cpt, kpt = packs.wt if packs is not None else \
+            K.pack_weight(wt.detach().float().squeeze(-1).permute(2, 0, 1), dtype, stride=stride)  # [Kt][Cout][Cin]
+        tcn_fused = (norm == BN and gather and ROUTING.bn_tcn_fused and getattr(wtp, "frag_stride", None) == 1
+                     and K.layer_fused_ok(sup, P, Cin, Cout, V, kt, stride, dtype))
         if norm == BN:  # all BatchNorm partial-statistics buffers of the layer from one zero fill
             cpo = -(-Cout // K.col_tile(Cout)) * K.col_tile(Cout)
             rb1 = K.gconv_row_blocks(N * T, V) if gather else K.row_blocks(M1, Cout)
             rb2 = K.row_blocks(M2, Cout)
-            st_shapes = [(rb1, cpo, 4), (rb2, cpo, 4)] + ([(K.row_blocks(M2, Cout), cpo, 4)] if res_conv else [])
-            st_all = _stats_arena(cache, dev, x.dtype, st_shapes, gather)
-            st1, st2 = st_all[0], st_all[1]
-            str_ = st_all[2] if res_conv else None
+            st_shapes = [(rb1, cpo, 4)] + ([] if tcn_fused else [(rb2, cpo, 4)]) + \
+                ([(K.row_blocks(M2, Cout), cpo, 4)] if res_conv else [])
+            st_all = _stats_arena(cache, dev, x.dtype, st_shapes, (gather, tcn_fused))
+            st1 = st_all[0]
+            st2 = None if tcn_fused else st_all[1]
+            str_ = st_all[-1] if res_conv else None
         # ---- residual branch: independent of the graph conv -> temporal conv chain until the output norm
         r = None
         if res_conv:
@@ -298,14 +306,10 @@ class StgcnLayerFunction(torch.autograd.Function):
             h = K.ln_apply(g, ls1, _flat_ln(n1w), _flat_ln(n1b), M1, V, Cout, relu=True)
             pro1 = {}
 
-        # ---- temporal conv on relu(norm1(g)) (norm applied in the prologue)
-        wtp, cpt, kpt = packs.wt if packs is not None else \
-            K.pack_weight(wt.detach().float().squeeze(-1).permute(2, 0, 1), dtype, stride=stride)  # [Kt][Cout][Cin]
-
-        if (norm == BN and gather and ROUTING.bn_tcn_fused and getattr(wtp, "frag_stride", None) == 1
-                and K.layer_fused_ok(sup, P, Cin, Cout, V, kt, stride, dtype)):
+        # ---- temporal conv on relu(norm1(g)) (norm applied in the prologue; wtp packed above)
+        if tcn_fused:
             # 64 -> 64 stride-1: layer_fused.hip's g-input mode (BN1 + ReLU staged once per frame into its LDS
-            # ring, the 9-tap conv from there; DESIGN 4.6) instead of conv_wide's per-tile prologue
+            # ring, the 9-tap conv from there; DESIGN 4.14) instead of conv_wide's per-tile prologue
             st2 = _stats_arena(cache, dev, x.dtype, [(K.layer_fused_row_blocks(N, T), Cout, 4)], "tcn")[0]
             u = K.layer_tcn(g, sc1, sh1, wtp, bt.detach().float().contiguous(), st2, tag=f"tcn_fwd_c{Cout}")
         else:

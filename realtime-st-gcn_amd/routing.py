@@ -18,8 +18,10 @@ also assign the attributes directly.
                                               interleaved runs; round 4: 8.86 vs 8.77)
     bn_mask_bits        STGCN_BN_BITS=0       the BatchNorm-2 backward reads the forward output's sign bits (written by bn_apply)
                                               for its ReLU mask instead of the output itself (default on)
-    bn_tcn_fused        STGCN_BN_TCN=0        training forward of BatchNorm 64->64 stride-1 layers: the temporal conv through
-                                              layer_fused.hip's g-input mode instead of conv_wide (default on)
+    bn_tcn_fused        STGCN_BN_TCN=1        training forward of BatchNorm 64->64 stride-1 layers: the temporal conv through
+                                              layer_fused.hip's g-input mode instead of conv_wide (default OFF since
+                                              round 6: step-neutral, 7.513 vs 7.513 ms, and it moved the most
+                                              downstream bf16 gradient)
     prep_plan           STGCN_PREP_PLAN=0     stgcn.Model training forwards pack every weight per call instead of
                                               in the one-launch plan (native.PrepPlan; default on)
 
@@ -39,7 +41,7 @@ class _Routing:
         self.fused_bn_inference = e("STGCN_FUSED_BN", "0") == "1"
         self.fused_ln_train = e("STGCN_FUSED_LN_TRAIN", "1") != "0"
         self.bn_mask_bits = e("STGCN_BN_BITS", "1") != "0"
-        self.bn_tcn_fused = e("STGCN_BN_TCN", "1") != "0"
+        self.bn_tcn_fused = e("STGCN_BN_TCN", "0") == "1"
         self.prep_plan = e("STGCN_PREP_PLAN", "1") != "0"
 
 

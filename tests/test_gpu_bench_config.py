@@ -299,11 +299,9 @@ def test_model_bf16_bench_config(K, pkg, model_ref):
 def test_model_bf16_vs_fp32_per_tensor(K, pkg, model_ref):
     """Per tensor, the bf16 perf path against the HIP fp32 path on the same inputs (the same kernels' schedule in
     the two precisions): every gradient points the same way — cosine >= 0.95 — except the conv biases that feed a
-    batch-statistics BatchNorm, whose exact gradient is 0 (both values are rounding noise).  A tensor below 0.95
-    passes only if bf16 arithmetic itself is that noisy there: our bf16 gradient no further from the fp64 oracle
-    than the REFERENCE's own bf16 (autocast) gradient of the same tensor (round 5: norm_in.norm.weight, the
-    gradient at the end of all 9 layers' backward, cos 0.93 to our fp32 at L2 0.37 from fp64, where the
-    reference's bf16 sits at L2 0.42; edge_importance.1 0.37 vs 0.47)."""
+    batch-statistics BatchNorm, whose exact gradient is 0 (both values are rounding noise).  (Round 5 relaxed this
+    bar for the g-input temporal-conv route, which was step-neutral; round 6 turned that route off and restored
+    the bar for every tensor.)"""
     sd_model, x, dy, refs = model_ref
     r64, r16 = refs["f64"], refs["ac16"]
     g16 = _run_model(pkg, sd_model, x, dy, "bf16")
@@ -313,15 +311,81 @@ def test_model_bf16_vs_fp32_per_tensor(K, pkg, model_ref):
         if bn_fed_bias(k):
             continue
         cos = torch.nn.functional.cosine_similarity(g16[k].reshape(1, -1), ref.reshape(1, -1)).item()
-        print(f"[err] bf16 vs fp32 {k}: cos {cos:.5f} L2 {_errs(g16[k], ref)[0]:.2e}", flush=True)
+        print(f"[err] bf16 vs fp32 {k}: cos {cos:.5f} L2 {_errs(g16[k], ref)[0]:.2e} (fp64 L2 ours "
+              f"{_errs(g16[k], r64[k])[0]:.3e}, reference bf16 {_errs(r16[k], r64[k])[0]:.3e})", flush=True)
         worst = min(worst, (cos, k))
         if not cos >= 0.95:
-            ours, theirs = _errs(g16[k], r64[k])[0], _errs(r16[k], r64[k])[0]
-            print(f"[err]   {k}: bf16 L2 from fp64 ours {ours:.3e} vs reference bf16 {theirs:.3e}", flush=True)
-            if not (cos >= 0.9 and ours <= theirs):
-                bad.append((k, round(cos, 4)))
+            bad.append((k, round(cos, 4)))
     print(f"[err] bf16 vs fp32 worst cosine {worst[0]:.5f} ({worst[1]})", flush=True)
     assert not bad, f"bf16 gradients with cosine < 0.95 to the HIP fp32 path: {bad}"
+
+
+@pytest.fixture(scope="module")
+def ln_model_ref(pkg):
+    """The LayerNorm twin of model_ref: the bench's widths with LayerNorm everywhere (ln/ configs, layernorm.py:22-28;
+    the 64 -> 64 layers take the one-kernel fused LN training forward, routing.fused_ln_train, by default) on one
+    seeded N=64 T=300 batch, oracle fwd + bwd in fp64 and under the reference's bf16 autocast."""
+    torch.manual_seed(1538574472)
+    arch = dict(ARCH, graph=pkg.PKU_MMD, normalization="LayerNorm")
+    model = pkg.MODELS["st-gcn"](rank=None, **arch)
+    with torch.no_grad():
+        for p in model.edge_importance:
+            p.add_(0.1 * torch.randn(p.shape))
+        for name, p in model.named_parameters():  # LayerNorm affines off their (1, 0) init: dgamma / dbeta carry signal
+            if ("norm" in name or "tcn.0" in name or "tcn.3" in name) and p.dim() == 3:
+                p.add_(0.1 * torch.randn(p.shape))
+    sd_model = {k: v.clone() for k, v in model.state_dict().items()}
+    gen = torch.Generator().manual_seed(1)
+    x = torch.randn(N, 3, T, V, generator=gen)
+    dy = torch.randn(N, 52, 1, generator=gen)
+    fn = lambda xx, sd: O.stgcn_model(xx, sd, arch)  # noqa: E731
+    refs = {"f64": oracle_fwd_bwd(fn, x, dy, sd_model, torch.float64),
+            "ac16": oracle_fwd_bwd(fn, x, dy, sd_model, torch.float32, autocast_bf16=True)}
+    return sd_model, x, dy, refs, arch
+
+
+def test_ln_model_bf16_bench_config(K, pkg, ln_model_ref):
+    """The LayerNorm model at the bench's size (N=64 T=300, 9 layers, bf16) fwd + bwd vs the fp64 oracle beside the
+    reference's own bf16 (autocast), exactly as test_model_bf16_bench_config does for BatchNorm: the default LN
+    training route (the one-kernel fused layer writing g, u, h and both LN statistics, then the unfused backward)
+    pinned to the oracle at a realistic size — logits, dx and every parameter gradient."""
+    sd_model, x, dy, refs, arch = ln_model_ref
+    r64, r16 = refs["f64"], refs["ac16"]
+    assert pkg.routing.ROUTING.fused_ln_train, "the default LN training route is the fused one"
+    calls = []
+    orig = K.layer_fused
+
+    def counted(*a, **k):
+        calls.append(bool(k.get("train")))
+        return orig(*a, **k)
+
+    K.layer_fused = counted
+    try:
+        m = pkg.MODELS["st-gcn"](rank=None, **arch)
+        m.load_state_dict(sd_model, strict=True)
+        m = m.to(DEV).set_compute_dtype("bf16")
+        xg = x.to(DEV).requires_grad_(True)
+        y = m(xg)
+        y.backward(dy.to(DEV))
+        torch.cuda.synchronize()
+    finally:
+        K.layer_fused = orig
+    assert calls and all(calls), f"the 64 -> 64 LN layers did not take the fused training route: {calls}"
+    got = {"logits": y.detach(), "dx": xg.grad}
+    got.update({k: p.grad for k, p in m.named_parameters()})
+    got = {k: v.detach().double().cpu() for k, v in got.items()}
+    assert_close(got["logits"], r64["logits"], BF16_MODEL_TOL, "logits")
+    rows, bad = {}, []
+    for k, ref in r64.items():
+        eo, e16 = _errs(got[k], ref), _errs(r16[k], ref)
+        cos = torch.nn.functional.cosine_similarity(got[k].reshape(1, -1), ref.reshape(1, -1)).item()
+        rows[k] = {"ours": eo, "ref_bf16": e16, "cos": (cos, cos)}
+        if k == "logits":
+            continue
+        if eo[0] > 3 * e16[0] + 0.02 or cos < 0.9:
+            bad.append(k)
+    _report("ln bf16", rows)
+    assert not bad, f"LN bf16 gradients further from fp64 than 3x the reference's bf16 (or cosine < 0.9): {bad}"
 
 
 @pytest.mark.parametrize("cin,cout,stride", [(64, 64, 1), (128, 256, 2)])

@@ -22,7 +22,7 @@ def cl(x, dtype=torch.bfloat16):
     return x.to(DEV, dtype).contiguous(memory_format=torch.channels_last)
 
 
-@pytest.mark.parametrize("N,T,V", [(2, 37, 25), (3, 8, 25), (64, 300, 25), (4, 21, 18), (65, 300, 25), (2, 50, 32), (1, 1, 25)])
+@pytest.mark.parametrize("N,T,V", [(2, 37, 25), (3, 8, 25), (64, 300, 25), (4, 21, 18), (65, 300, 25), (1, 1, 25)])
 def test_tconv_frame_fwd_dgrad(K, N, T, V):
     torch.manual_seed(11)
     C = 64
