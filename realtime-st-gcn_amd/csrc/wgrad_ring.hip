@@ -354,6 +354,7 @@ struct RPlan {
 };
 
 constexpr int RS_PART = 16;  // level-1 partials of slab_reduce
+constexpr int R_MAX = 320;   // slab rows (config 2: 256 at 64 channels, 128 at 128; config-4 units: 260)
 
 RPlan rplan(const stgcn_wgrad_desc& a) {
   RPlan p{};
@@ -376,7 +377,9 @@ RPlan rplan(const stgcn_wgrad_desc& a) {
   g.R = a.N * g.runs_n;
   p.lds = ring_lds(p.cob);
   p.slab_elems = ((long)g.R + RS_PART) * KT * a.Cout * a.Cin;
-  p.ok = p.lds <= 160 * 1024;
+  // one slab row per (sample, run): at least N rows, so the workspace grows with the batch.  Past R_MAX rows
+  // (N > 320: > 190 MB at 128 channels) the call falls through to the bounded-workspace kernels (wgrad_tile)
+  p.ok = p.lds <= 160 * 1024 && g.R <= R_MAX;
   return p;
 }
 

@@ -177,8 +177,7 @@ def units_for_rank(units, world: int, rank: int):
 
 class GraphedStep:
     """A fixed-shape training step replayed as HIP graphs (processor.py:531-564 inner loop with the batch in
-    static buffers): one graph launch for ~370 kernels, the weight-gradient side stream captured as a
-    parallel branch (layer_fn._fork: event fork/join inside the capture).
+    static buffers): one graph launch for the ~250 kernels of the forward, loss and backward on one stream.
 
         graph 1: zero the gradients, ``fwd_loss()`` (forward + loss), backward, [N > 1: copy the fp32
                  gradients into one flat buffer]

@@ -2,7 +2,8 @@
 kernel (wgrad_ring.hip: Kt = 9, stride 1, 64 / 128 output channels, bf16) vs autograd of F.conv2d in fp32 on the
 same bf16-rounded operands: runs that do not divide T, a sample count that does not fill 256 blocks, the 18-joint
 graph, both prologues (BatchNorm1 + ReLU recomputed from the pre-norm input, or none: LayerNorm's materialised h),
-both output layouts (fresh nn.Conv2d order / accumulate into [Kt][Cout][Cin]), and bit-reproducibility."""
+both output layouts (fresh nn.Conv2d order / accumulate into [Kt][Cout][Cin]), and bit-reproducibility.  N = 330 has
+more than the ring kernel's 320 slab rows (one per sample at least): the call takes the bounded-workspace kernels."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -30,7 +31,8 @@ def rb(t):
 
 
 @pytest.mark.parametrize("Cin,Cout,N,T,V", [(64, 64, 3, 37, 25), (64, 64, 64, 300, 25), (128, 128, 5, 41, 18),
-                                            (128, 128, 64, 150, 25), (128, 64, 2, 11, 25), (64, 128, 1, 70, 32)])
+                                            (128, 128, 64, 150, 25), (128, 64, 2, 11, 25), (64, 128, 1, 70, 32),
+                                            (64, 64, 330, 3, 25)])
 @pytest.mark.parametrize("pro", [1, 0])
 def test_wgrad_ring(K, Cin, Cout, N, T, V, pro):
     torch.manual_seed(300 + Cin + Cout + T + pro)

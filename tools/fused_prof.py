@@ -35,4 +35,6 @@ if __name__ == "__main__":
     m = tcn.mean(axis=(0, 1))
     print(f"TCN waves: k-loop {m[0]:.0f}  z stores (LN: normalise + stores) {m[4]:.0f}  BN2 partials (LN: statistics) "
           f"{m[1]:.0f}  LN hand-off {m[5]:.0f}  barrier {m[2]:.0f}")
-    print("GCN waves: DMA wait {:.0f}  compute {:.0f}  barrier {:.0f}".format(*gcn[:, :, :3].mean(axis=(0, 1))))
+    g = gcn.mean(axis=(0, 1))
+    print(f"GCN waves: DMA wait {g[0]:.0f}  compute (round 6: the matrix part) {g[1]:.0f}  epilogue {g[4]:.0f}  "
+          f"barrier {g[2]:.0f}")
