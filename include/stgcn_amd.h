@@ -26,8 +26,10 @@ extern "C" {
 
 /* Bumped on every change of a descriptor's layout or of an entry point's signature; realtime-st-gcn_amd/_lib.py
  * refuses a library whose stgcn_abi_version() differs from the version it was written against.
- *   1: rounds 1-4;  2: round 5 (stgcn_gconv_desc gained res / res_bits / res_ld). */
-#define STGCN_ABI_VERSION 2
+ *   1: rounds 1-4;  2: round 5 (stgcn_gconv_desc gained res / res_bits / res_ld);
+ *   3: round 6 (stgcn_gcn_tile removed; stgcn_layer_fused_desc is the LayerNorm layer only: the BatchNorm
+ *      fields n1_scale / n1_shift / stats / ln / g_in / g_in_ld and stgcn_layer_fused_row_blocks removed). */
+#define STGCN_ABI_VERSION 3
 
 /* Implicit-GEMM (Kt x 1) row convolution; see conv_rows.hip for the exact contract.
  * Replaces: nn.Conv2d tcn.2 (models/stgcn/stgcn.py:154-159), residual.0 (stgcn.py:165-170),
@@ -160,32 +162,6 @@ typedef struct {
 
 int stgcn_gconv(const stgcn_gconv_desc* d, int dtype, void* stream);
 
-/* Fused graph convolution (bf16; gcn_tile.hip): per frame, the joint mix and the 1x1 conv as two chained
- * MFMA products (the mix's accumulators feed the conv directly):
- *   trans_a 0 (forward, tgcn.py:71-79):  out[(i,w)][co] (+)= sum_{p,ci} W'[co][p*Cin+ci] sum_v A[p][v][w] in[(i,v)][ci]
- *                                          (+ bias[w][co])
- *   trans_a 1 (data grad):               out[(i,v)][c]  (+)= sum_{p,k} W'[c][p*Cin+k]  sum_w A[p][v][w] in[(i,w)][k]
- * w_frag = the Kt = 1 MFMA-fragment image (stgcn_pack_weight_frag, [Cout_pad][Kw_pad], Kw_pad >= P*Cin)
- * of W'' with the columns of every 16-wide group permuted: W''[c][16m + 8h + j] = W'[c][16m + 8(j/4) + 4h + j%4]
- * (h < 2, j < 8); forward W'[co][p*Cin+ci] = W[p*Cout+co][ci]; data grad (in = dg, Cin = conv Cout,
- * Cout = conv Cin) W'[ci][p*Cout+co] = W[p*Cout+co][ci].  A: [P][V][V] fp32 (A * edge importance),
- * P <= 3, 16 < V <= 32; Cin % 32 == 0, Cout % 64 == 0.  dmax is unused (kept for ABI stability).
- * Optional BN partial statistics [stgcn_gcn_tile_row_blocks(NT, V, Cout)][Cout_pad] as stgcn_conv_rows.
- * out = NULL: statistics only (pass 1 of stgcn_layer_fused_fwd; no output stores).
- * Replaces: conv1x1 + einsum of ConvTemporalGraphical.forward (tgcn.py:71-79) and its input grad. */
-typedef struct {
-  const void* in;
-  void* out;
-  const void* w_frag;
-  const float* A;
-  const float* bias; /* [V][Cout] or NULL */
-  float* stats;
-  int NT, V, P, Cin, Cout, Cout_pad, Kw_pad, in_ld, out_ld, trans_a, accumulate;
-  int dmax[4];
-} stgcn_gcn_tile_desc;
-
-int stgcn_gcn_tile(const stgcn_gcn_tile_desc* d, int dtype, void* stream);
-long stgcn_gcn_tile_row_blocks(int NT, int V, int Cout);
 long stgcn_gconv_row_blocks(int NT, int V);
 int stgcn_gconv_weights(const float* A, const float* W, const int* nbr, const int* deg, int P, int V, int J, int Cout,
                         int Cin, int trans, void* out, int rows_pad, int cols_pad, int dtype, void* stream);
@@ -369,44 +345,36 @@ int stgcn_seg_loss(const float* p, int ldp, const long* labels, const float* wt,
 int stgcn_seg_loss_bwd(const float* dce, const float* dmse, const float* gce, const float* gmse, long n, float* dp,
                        void* stream);
 
-/* The fused ST-GCN layer forward (layer_fused.hip; BASELINE north_star): per tile of 16 frames, the
- * graph conv (as stgcn_gcn_tile forward) of the tile and its 4-frame temporal halo is recomputed on the
- * matrix cores into LDS, normalised h = relu(g * n1_scale + n1_shift) (BN1 folded; the conv bias pushed
- * through A, gbias [V][64], is added first), and the Kt = 9 temporal conv (+ tbias) runs on h from LDS:
- *   z[(n,t,w)][co] = tbias[co] + sum_{dt<9, ci} W[dt][co][ci] h[(n, t+dt-4, w)][ci]   (h = 0 outside [0,T))
- * g never reaches HBM.  BatchNorm statistics of g come from pass 1 (stgcn_gcn_tile with out = NULL +
- * stgcn_bn_finalize); z's partials (count, mean, M2), one row per (block, 8-frame step, row half), go to
- * stats [stgcn_layer_fused_row_blocks][64]
- * (or NULL) for bn_finalize.  bf16; Cin = Cout = 64; stride 1; P <= 3; 16 < V <= 25.
- * wg_frag: the stgcn_gcn_tile weight image of W'[co][p*64+ci] = W[p*64+co][ci] (Kw_pad = P*64);
- * wt_frag: the stgcn_pack_weight_frag image of the temporal weight [9][64][64].
- * Replaces: StgcnLayer.forward's gcn + tcn[0:3] (models/stgcn/stgcn.py:151-159,181-193) with
- * ConvTemporalGraphical.forward (models/utils/tgcn.py:58-79). */
+/* The fused ST-GCN layer (layer_fused.hip; BASELINE north_star) of a LayerNorm StgcnLayer, 64 -> 64 channels,
+ * stride 1, Kt = 9, identity or no residual, as ONE kernel:
+ *   g = ConvTemporalGraphical(x) (tgcn.py:58-79; graph conv recomputed per frame on the matrix cores, never stored),
+ *   h = relu(LN1(g)), u = tcn(h) + tbias (stgcn.py:151-159), y = relu(LN2(u) + residual * x) (stgcn.py:181-193),
+ * with LayerNorm([64,1,V]) per frame over C x V, unbiased variance (layernorm.py:22-28); y is written to z.
+ * bf16; P <= 3; 16 < V <= 25.  wg_frag: the Kt = 1 MFMA-fragment image of W'[co][p*64+ci] = W[p*64+co][ci] with
+ * the columns of every 16-wide group permuted (realtime-st-gcn_amd/native.py pack_gcn_weight):
+ * W''[c][16m + 8h + j] = W'[c][16m + 8(j/4) + 4h + j%4] (h < 2, j < 8); wt_frag: the stgcn_pack_weight_frag image
+ * of the temporal weight [9][64][64]; gbias: the conv bias through A [V][64] (or NULL); ln*_g / ln*_b: the
+ * LayerNorm([64,1,V]) parameters TRANSPOSED to [V][64] fp32.
+ * Replaces: StgcnLayer.forward (models/stgcn/stgcn.py:181-193) of a LayerNorm layer. */
 typedef struct {
   const void* x;         /* bf16 rows [N][T][V][x_ld], 64 channels */
-  void* z;               /* bf16 rows [N][T][V][z_ld] */
+  void* z;               /* bf16 rows [N][T][V][z_ld]: the layer output y */
   const void* wg_frag;
   const float* A;        /* [P][V][V] fp32 (A * edge importance) */
   const float* gbias;    /* [V][64] or NULL */
-  const float* n1_scale; /* [64] */
-  const float* n1_shift; /* [64] */
   const void* wt_frag;
   const float* tbias;    /* [64] or NULL */
-  float* stats;          /* float4 [stgcn_layer_fused_row_blocks(N, T)][64] or NULL */
   int N, T, V, P, x_ld, z_ld;
-  /* LayerNorm layer (ln = 1): the whole layer y = relu(LN2(z) + residual * x) (layernorm.py:22-28 twice,
-   * stgcn.py:181-193) is written to z; n1_scale / n1_shift / stats unused (NULL); ln*_g / ln*_b are the
-   * LayerNorm([64,1,V]) parameters TRANSPOSED to [V][64] fp32. */
   const float* ln1_g;
   const float* ln1_b;
   const float* ln2_g;
   const float* ln2_b;
-  int ln, residual;
-  /* LayerNorm training forward (ln = 1; all four set, or all NULL for inference): what the layer's backward
-   * (StgcnLayerFunction's unfused LN backward) reads besides y — g_out: the graph-conv output incl. its bias
-   * (pre-LN1) rows [N][T][V][g_ld]; u_out: the temporal-conv output incl. its bias (pre-LN2) rows, u_ld;
-   * st1_out / st2_out: per-frame LayerNorm statistics (mean, 1/sqrt(unbiased var + 1e-5)) of g and u, float2
-   * [N*T] — stgcn_ln_stats's layout, computed here from the fp32 values before their bf16 rounding. */
+  int residual, pad_;
+  /* training forward (all four set, or all NULL for inference): what the layer's backward (StgcnLayerFunction's
+   * unfused LN backward) reads besides y — g_out: the graph-conv output incl. its bias (pre-LN1) rows
+   * [N][T][V][g_ld]; u_out: the temporal-conv output incl. its bias (pre-LN2) rows, u_ld; st1_out / st2_out:
+   * per-frame LayerNorm statistics (mean, 1/sqrt(unbiased var + 1e-5)) of g and u, float2 [N*T] —
+   * stgcn_ln_stats's layout, computed here from the fp32 values before their bf16 rounding. */
   void* g_out;
   void* u_out;
   float* st1_out;
@@ -415,17 +383,10 @@ typedef struct {
   /* optional with the training outputs (NULL otherwise): h = relu(LN1(g)) rows, h_ld — the temporal conv's input,
    * which the layer's weight gradient reads (saves recomputing it in the backward) */
   void* h_out;
-  int h_ld;
-  /* BatchNorm layers, optional: the graph-conv output g (bias included) as INPUT rows (ld g_in_ld) instead of
-   * recomputing it — the kernel is then the temporal conv of the training forward: h = relu(g * n1_scale +
-   * n1_shift) staged into its LDS ring once per frame, z = tcn(h) + tbias and BN2 partials out (wg_frag, A,
-   * gbias unused, may be NULL).  Replaces conv_wide's 64-channel forward (stgcn.py:151-159). */
-  const void* g_in;
-  int g_in_ld;
+  int h_ld, pad2_;
 } stgcn_layer_fused_desc;
 
 int stgcn_layer_fused_fwd(const stgcn_layer_fused_desc* d, void* stream);
-long stgcn_layer_fused_row_blocks(int N, int T);
 
 /* Segment metrics of one trial (evaluation): labels / pred int64 [L] framewise classes (device).
  * out fp32 [K + 1]: F1@overlap[k] (utils/metrics/f1.py:14-52; NaN when the trial has no hit, as the

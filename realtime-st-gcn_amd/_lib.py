@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("STGCN_LIB") or os.path.join(_HERE, "lib", "libstgcn_amd.so")  # STGCN_LIB: A/B builds
 
 # the STGCN_ABI_VERSION of include/stgcn_amd.h these bindings mirror (test_cpu_host checks the two agree)
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _ERR = {1: "bad shape/arguments", 2: "unsupported dtype", 3: "HIP launch error"}
 
@@ -35,13 +35,6 @@ class ConvDesc(ctypes.Structure):
                [(n, c_int) for n in ("N", "T_in", "T_out", "V", "Cin", "Cout", "Cin_pad", "Cout_pad", "Kt", "stride",
                                      "pad", "trans", "pro", "bias_mode", "accumulate", "in_ld", "out_ld")] + \
                [("w_frag", c_void_p)]
-
-
-class GcnTileDesc(ctypes.Structure):
-    _fields_ = [("in_", c_void_p), ("out", c_void_p), ("w_frag", c_void_p), ("A", c_void_p), ("bias", c_void_p),
-                ("stats", c_void_p)] + \
-               [(n, c_int) for n in ("NT", "V", "P", "Cin", "Cout", "Cout_pad", "Kw_pad", "in_ld", "out_ld",
-                                     "trans_a", "accumulate")] + [("dmax", c_int * 4)]
 
 
 class WgradDesc(ctypes.Structure):
@@ -71,11 +64,11 @@ class GconvWgradDesc(ctypes.Structure):
 
 
 class LayerFusedDesc(ctypes.Structure):
-    _fields_ = [(n, c_void_p) for n in ("x", "z", "wg_frag", "A", "gbias", "n1_scale", "n1_shift", "wt_frag", "tbias",
-                                        "stats")] + [(n, c_int) for n in ("N", "T", "V", "P", "x_ld", "z_ld")] + \
-               [(n, c_void_p) for n in ("ln1_g", "ln1_b", "ln2_g", "ln2_b")] + [("ln", c_int), ("residual", c_int)] + \
+    _fields_ = [(n, c_void_p) for n in ("x", "z", "wg_frag", "A", "gbias", "wt_frag", "tbias")] + \
+               [(n, c_int) for n in ("N", "T", "V", "P", "x_ld", "z_ld")] + \
+               [(n, c_void_p) for n in ("ln1_g", "ln1_b", "ln2_g", "ln2_b")] + [("residual", c_int), ("pad_", c_int)] + \
                [(n, c_void_p) for n in ("g_out", "u_out", "st1_out", "st2_out")] + [("g_ld", c_int), ("u_ld", c_int)] + \
-               [("h_out", c_void_p), ("h_ld", c_int), ("g_in", c_void_p), ("g_in_ld", c_int)]
+               [("h_out", c_void_p), ("h_ld", c_int), ("pad2_", c_int)]
 
 
 class BnBwdDesc(ctypes.Structure):
@@ -120,8 +113,6 @@ _SIGS = {
     "stgcn_gcn_bias_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "stgcn_pack_weight": (c_int, [c_void_p, ctypes.c_long, ctypes.c_long, ctypes.c_long, c_int, c_int, c_int,
                                   c_void_p, c_int, c_int, c_int, c_void_p]),
-    "stgcn_gcn_tile": (c_int, [ctypes.POINTER(GcnTileDesc), c_int, c_void_p]),
-    "stgcn_gcn_tile_row_blocks": (ctypes.c_long, [c_int, c_int, c_int]),
     "stgcn_tconv_frame": (c_int, [ctypes.POINTER(ConvDesc), c_void_p]),
     "stgcn_tconv_frame_row_blocks": (ctypes.c_long, [c_int, c_int]),
     "stgcn_pack_weight_s2frag": (c_int, [c_void_p, ctypes.c_long, ctypes.c_long, ctypes.c_long, c_int, c_int,
@@ -168,7 +159,6 @@ _SIGS = {
     "stgcn_attn_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "stgcn_layer_fused_fwd": (c_int, [ctypes.POINTER(LayerFusedDesc), c_void_p]),
-    "stgcn_layer_fused_row_blocks": (ctypes.c_long, [c_int, c_int]),
     "stgcn_rt_frame_in": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "stgcn_rt_frame_gcn": (c_int, [c_void_p, c_int, c_int, c_int, c_int] + [c_void_p] * 10),
     "stgcn_rt_frame_norm": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int,

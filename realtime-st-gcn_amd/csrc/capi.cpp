@@ -21,8 +21,6 @@ long conv_rows_num_row_blocks(long M, int cout);
 int conv_wgrad_launch(WgradArgs a, int dtype, hipStream_t s);
 int pack_s2frag_launch(const float* src, long s0, long s1, long s2, int Co, int Ci, void* dst, int trans,
                        hipStream_t s);
-int gcn_tile_launch(const stgcn_gcn_tile_desc& a, hipStream_t s);
-long gcn_tile_row_blocks(int NT, int V, int Cout);
 long wgrad_tile_workspace(const WgradArgs& a, int dtype);
 long wgrad_wide_workspace(const WgradArgs& a, int dtype);
 long wgrad_ring_workspace(const WgradArgs& a, int dtype);
@@ -101,7 +99,6 @@ int attn_proj_launch(const void* x, int ldx, long M, int Cin, const float* W, co
 int attn_bwd_launch(const void* th, const void* ph, int ld, int N, int T_, int V, int P, int ce, const float* C,
                     const float* dC, float* dS, void* dth, void* dph, int dtype, hipStream_t s);
 int layer_fused_launch(const stgcn_layer_fused_desc& a, hipStream_t s);
-long layer_fused_row_blocks(int N, int T);
 int rt_in_launch(const float* x, int V, const float* g, const float* b, const float* W, const float* bias, int C0,
                  float* out, hipStream_t s);
 int rt_gcn_launch(const float* x, int V, int Cin, int Cout, int P, const float* A, const float* W, const float* bias2d,
@@ -151,14 +148,6 @@ int stgcn_conv_rows(const stgcn_conv_desc* d, int dtype, void* stream) {
 }
 
 int stgcn_conv_rows_col_tile(int cout) { return conv_rows_bn_tile(cout); }
-int stgcn_gcn_tile(const stgcn_gcn_tile_desc* d, int dtype, void* stream) {
-  if (dtype != 1) return STGCN_EDTYPE;
-  if (!d || !d->in || !d->w_frag || !d->A) return STGCN_EBADSHAPE;
-  if (!d->out && (!d->stats || d->accumulate)) return STGCN_EBADSHAPE;  /* out = NULL: statistics only */
-  if (d->in_ld < d->Cin || d->out_ld < d->Cout) return STGCN_EBADSHAPE;
-  return gcn_tile_launch(*d, STREAM(stream));
-}
-long stgcn_gcn_tile_row_blocks(int NT, int V, int Cout) { return gcn_tile_row_blocks(NT, V, Cout); }
 int stgcn_pack_weight(const float* src, long s0, long s1, long s2, int Kt, int Co, int Ci, void* dst, int Cout_pad,
                       int Cin_pad, int dtype, void* stream) {
   CHECK_DTYPE(dtype);
@@ -429,7 +418,6 @@ int stgcn_layer_fused_fwd(const stgcn_layer_fused_desc* d, void* stream) {
   if (!d) return STGCN_EBADSHAPE;
   return layer_fused_launch(*d, STREAM(stream));
 }
-long stgcn_layer_fused_row_blocks(int N, int T) { return layer_fused_row_blocks(N, T); }
 
 int stgcn_rt_frame_in(const float* x, int V, const float* ln_w, const float* ln_b, const float* w, const float* b, int C0,
                       float* out, void* stream) {

@@ -1,15 +1,13 @@
-// The fused ST-GCN layer forward (BASELINE north_star): ConvTemporalGraphical (tgcn.py:58-79) -> BN1 ->
-// ReLU -> temporal Conv2d (Kt = 9) + bias (stgcn.py:151-159) in ONE kernel, with the graph-conv output
-// g and its normalised form h = relu(BN1(g)) living only in LDS.  The second BatchNorm's batch
-// statistics are emitted as per-block partials (the consumer folds BN2 + residual + ReLU, stgcn.py:160,193).
+// The fused ST-GCN layer (BASELINE north_star) for LayerNorm layers: ConvTemporalGraphical (tgcn.py:58-79) ->
+// LN1 -> ReLU -> temporal Conv2d (Kt = 9) + bias (stgcn.py:151-159) -> LN2 -> + residual -> ReLU (stgcn.py:181-193)
+// as ONE kernel: the graph-conv output g and h = relu(LN1(g)) live only in LDS, and no statistics leave the chip,
+// because both LayerNorm([64,1,V]) norms are per frame over C x V (layernorm.py:22-28, unbiased variance).
+// (BatchNorm layers cannot be one kernel: BN1's batch statistics need all of g before any h is consumed.  The
+// two-pass BatchNorm form of this kernel lost to the unfused forward on every box and was removed in round 6;
+// DESIGN 4.6 keeps its numbers.)
 //
-// BatchNorm needs global statistics of g before the temporal conv can consume h, so the layer is the
-// two-pass form of SURVEY §7: pass 1 = the fused graph conv with statistics only (gcn_tile.hip, no output
-// stores), bn_finalize -> BN1 scale/shift; pass 2 = this kernel, which RECOMPUTES the graph conv of its
-// frames on the matrix cores instead of reading g back from HBM.
-//
-// Shapes: bf16, Cin = Cout = 64, stride 1, Kt = 9 (pad 4), P <= 3 partitions, 16 < V <= 25 — the
-// north_star layer (N = 64, C = 64, T = 300, V = 25) and config 2's layers 0-2.
+// Shapes: bf16, Cin = Cout = 64, stride 1, Kt = 9 (pad 4), P <= 3 partitions, 16 < V <= 25 — the north_star
+// layer (N = 64, C = 64, T = 300, V = 25) and the 64 -> 64 layers of the ln/ configs.
 //
 // Block = 8 waves, one contiguous run of output frames of one sample (a quarter of a sample at N = 64:
 // 256 blocks), walked in steps of CF = 8 frames.  Two roles run concurrently, one wave of each per SIMD,
@@ -17,26 +15,20 @@
 //   GCN waves 4-7 (producers): per step, the 8 h frames the NEXT step needs.  A frame's x rows arrive as
 //     two 32-channel panels [32 joint rows][32 ch] by global->LDS DMA (issued one step ahead); stage 1
 //     mixes the joints (X^T A_p on MFMA, X^T by transposing LDS reads, A_p in registers), stage 2 runs the
-//     1x1 conv from the stage-1 accumulators (W' in LDS) — gcn_tile.hip's two chained products.  Epilogue:
-//     h = relu(g * s1 + (bias2d * s1 + b1)) (BN1 folded) -> bf16 -> the h ring.  Frames outside [0, T) are
-//     written as zeros (the temporal conv's zero padding applies to h).
-//   TCN waves 0-3 (consumers): out^T[co][row] = sum_{dt,ci} W[dt][co][ci] h[frame + dt - 4][row's joint][ci]
-//     over the step's 8*V rows, 32x32x16 MFMAs with the weight fragments streamed from L2 (conv_wide.hip's
-//     fragment image) through a register ring and the h fragments read from LDS.  Wave = (32 output
-//     channels, 4 row tiles of 32).  Epilogue: + bias, 8-B stores of 4 consecutive channels per lane; BN2
-//     (sum, sum of squares) kept in registers over the run and written once as (count, mean, M2) partials.
+//     1x1 conv from the stage-1 accumulators (W' in LDS).  A frame's 64 x V graph-conv values are one wave's
+//     accumulators (initialised with the bias through A) -> the frame's mean and variance by two DPP wave
+//     reductions -> h = relu(LN1(g)) -> bf16 -> the h ring.  Frames outside [0, T) are written as zeros (the
+//     temporal conv's zero padding applies to h).
+//   TCN waves 0-3 (consumers): out^T[co][row] = sum_{dt,ci} W[dt][co][ci] h[frame + dt - 4][row's joint][ci],
+//     32x32x16 MFMAs with the weight fragments streamed from L2 (conv_wide.hip's fragment image) through a
+//     register ring and the h fragments read from LDS.  Wave = (32 output channels, 4 frame-aligned row
+//     tiles); each frame's LN2 (sum, sum of squares) is one DPP wave reduction plus ONE exchange with the
+//     partner wave (the other 32 channels) through LDS, combined in a fixed order (deterministic); then
+//     y = relu(LN2(z) + x) (identity residual of the 64 -> 64 stride-1 layer, x rows re-read from L2,
+//     gamma2/beta2 staged in LDS) with 16-B stores.
 // The h ring holds RF = 24 frames (a frame at slot a % RF): 16 being read for step s (frames 8s-4 ..
 // 8s+11 of the run) and 8 being written for step s+1; one block barrier per step hands them over.
-//
-// LayerNorm variant (LN = true; the ln/ configs): both norms are per frame over C x V (layernorm.py:22-28,
-// unbiased), so the WHOLE layer is this one kernel, no second pass and no statistics leave the chip:
-//   GCN waves: a frame's 64 x V graph-conv values are one wave's accumulators -> the frame's mean and
-//     variance by two DPP wave reductions -> h = relu(LN1(g)) into the ring;
-//   TCN waves: per step, per row tile and frame, the (sum, sum of squares) of the wave's 32 channels by DPP
-//     wave reductions -> LDS; after a TCN-wave-only hand-off (an LDS arrival counter: a block barrier
-//     would wait for the GCN waves too) each lane combines the (<= 4) partials of its
-//     row's frame in a fixed order (deterministic) and stores y = relu(LN2(z) + x) (identity residual of the
-//     64 -> 64 stride-1 layer, x rows re-read from L2; gamma2/beta2 staged in LDS) instead of z.
+// Training forward: the kernel also writes g, u = z (pre-LN2), h and both LN statistics for the backward.
 #include "common.h"
 #include "../../include/stgcn_amd.h"
 #include <stdlib.h>
@@ -71,16 +63,14 @@ constexpr int PRO = 2 * HALO + CF;     // h frames before the first step (16)
 constexpr int RSH = 2 * C + 16;        // h row bytes (144: conflict-free ds_read_b128 for any row offset)
 // per-joint LDS tables read by 32 lanes of 32 different joints at once: row strides padded off the 256-B
 // bank period (16 B further per joint), or every lane of a ds_read_b128 group hits the same four banks
-constexpr int CBP = C + 4;             // BN: bias2d * scale + shift row, floats
-constexpr int CGP = C + 4;             // LN: gamma2 / beta2 row, floats (two planes)
-constexpr int ZSB = 32 * 16;  // BN: per temporal-conv wave, 32 float4 BN2 partials
+constexpr int CGP = C + 4;             // gamma2 / beta2 row, floats (two planes)
 constexpr int PANEL = 32 * 64;         // [32 joint rows][32 ch] bf16
 constexpr int SLOTS = FPW * G;         // panel slots per GCN wave (one step's panels)
 constexpr int RT = 4;                  // 32-row output tiles per TCN wave (8 frames x 25 joints = 7 tiles)
 constexpr int NB = 9;                  // temporal-conv weight fragment ring depth (divides KSTEPS)
 constexpr int KSTEPS = KT * C / 16;    // 36 k-steps of the temporal conv
 constexpr int VMAX = 25;
-constexpr int TARGET_BLOCKS = 256;     // MI355X CUs: runs per sample = 256 / N (fixed: the host sizes stats by it)
+constexpr int TARGET_BLOCKS = 256;     // MI355X CUs: runs per sample = 256 / N
 constexpr int LDS_MAX = 160 * 1024;
 static_assert(CF * VMAX <= 2 * RT * 32, "row tiles");
 
@@ -151,10 +141,10 @@ struct FGeom {
   int runs_n;  // runs per sample
   int run;     // frames per run (multiple of CF)
   int nsm;     // steps per run (run / CF)
-  int off_tab, off_ring, off_h, off_red, off_zs;  // LDS offsets
+  int off_tab, off_ring, off_h, off_red;  // LDS offsets
 };
 
-template <int P, bool LN, bool GIN = false>
+template <int P>
 __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_layer_fused_desc a, const FGeom g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int K16 = P * G * 2;  // 16-wide K steps of W' (P*64 / 16)
@@ -170,37 +160,24 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
   const int nfr = (R1 - R0) + 2 * HALO;  // h frames the run needs: a in [0, nfr) <-> frame R0 - 4 + a
 
   char* const sW = smem;                                          // [2][K16] 1-KiB W' fragment blocks
-  float* const sSc = reinterpret_cast<float*>(smem + g.off_tab);  // [64] BN1 scale
-  float* const sBp = sSc + C;                                     // [V][CBP] bias2d * scale + shift
   char* const sH = smem + g.off_h;                                // [RF * V][RSH]
   float* const sGam = reinterpret_cast<float*>(smem + g.off_tab);  // LN: [V][CGP] gamma2, then [V][CGP] beta2
   float* const sBet = sGam + V * CGP;
   float2* const sPart = reinterpret_cast<float2*>(smem + g.off_red);  // LN: [TCN wave][4 frames] (sum, sum of squares)
   unsigned* const sCnt = reinterpret_cast<unsigned*>(smem + g.off_red + NWT * 4 * 8);  // LN: per TCN wave, last step posted
   const int vrs = V * RSH;  // bytes per h frame
-  float* const sTb = reinterpret_cast<float*>(smem + g.off_tab + (LN ? 2 * V * CGP * 4 : (C + V * CBP) * 4));  // [64] tcn bias
+  float* const sTb = reinterpret_cast<float*>(smem + g.off_tab + 2 * V * CGP * 4);  // [64] tcn bias
 
-  // ---- per block: W' slice, BN1 tables, zeroed panel rings (rows V..31 stay zero)
+  // ---- per block: W' slice, LN2 tables, zeroed panel rings (rows V..31 stay zero)
   {
-    if (!GIN) {
-      const uint4* wsrc = reinterpret_cast<const uint4*>(a.wg_frag);
-      uint4* wdst = reinterpret_cast<uint4*>(sW);
-      for (int e = tid; e < 2 * K16 * 64; e += NW * 64) wdst[e] = wsrc[e];
+    const uint4* wsrc = reinterpret_cast<const uint4*>(a.wg_frag);
+    uint4* wdst = reinterpret_cast<uint4*>(sW);
+    for (int e = tid; e < 2 * K16 * 64; e += NW * 64) wdst[e] = wsrc[e];
+    for (int e = tid; e < V * C; e += NW * 64) {
+      sGam[(e / C) * CGP + e % C] = a.ln2_g[e];
+      sBet[(e / C) * CGP + e % C] = a.ln2_b[e];
     }
-    if (LN) {
-      for (int e = tid; e < V * C; e += NW * 64) {
-        sGam[(e / C) * CGP + e % C] = a.ln2_g[e];
-        sBet[(e / C) * CGP + e % C] = a.ln2_b[e];
-      }
-      if (tid < NWT) sCnt[tid] = 0u;
-    } else {
-      for (int c = tid; c < C; c += NW * 64) sSc[c] = a.n1_scale[c];
-      for (int e = tid; e < V * C; e += NW * 64) {
-        const int c = e % C;
-        const float b = a.gbias ? a.gbias[e] : 0.f;
-        sBp[(e / C) * CBP + c] = fmaf(b, a.n1_scale[c], a.n1_shift[c]);
-      }
-    }
+    if (tid < NWT) sCnt[tid] = 0u;
     for (int c = tid; c < C; c += NW * 64) sTb[c] = a.tbias ? a.tbias[c] : 0.f;
     uint4* z = reinterpret_cast<uint4*>(smem + g.off_ring);
     for (int e = tid; e < NWG * SLOTS * PANEL / 16; e += NW * 64) z[e] = make_uint4(0, 0, 0, 0);
@@ -214,64 +191,7 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
     if (lane == 0 && blockIdx.x < PROF_BLOCKS)
       for (int j = 0; j < 6; ++j) g_fused_prof[((long)blockIdx.x * 8 + wave) * 6 + j] = pa[j];
   };
-  if constexpr (GIN) {
-    if (wave >= NWT) {
-      // ============ staging waves (g_in): h = relu(g * s1 + shift) of the step's frames into the ring ============
-      // (the BN1 table sBp holds the shift per joint: no graph-conv bias here, g already carries it)
-      const int gw = wave - NWT;
-      const bf16* __restrict__ gsrc = reinterpret_cast<const bf16*>(a.g_in) + (long)n * T * V * a.g_in_ld;
-      constexpr int UPL = (VMAX * 8 + 63) / 64;  // 16-B units of a frame per lane
-      auto stage = [&](int fa0) {
-        const long long pt0 = ptime();
-        uint4 u[FPW][UPL];
-#pragma unroll
-        for (int i = 0; i < FPW; ++i) {  // all loads of both frames first
-          const int fa = fa0 + NWG * i, f = R0 - HALO + fa;
-          const int fc = min(max(f, 0), T - 1);
-#pragma unroll
-          for (int k = 0; k < UPL; ++k) {
-            const int e = min(lane + 64 * k, V * 8 - 1);
-            u[i][k] = *reinterpret_cast<const uint4*>(gsrc + ((long)fc * V + (e >> 3)) * a.g_in_ld + (e & 7) * 8);
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < FPW; ++i) {
-          const int fa = fa0 + NWG * i, f = R0 - HALO + fa;
-          if (fa >= nfr) continue;
-          const bool okf = f >= 0 && f < T;  // padding frame: h = 0 (the conv's zero padding applies to h)
-          char* hrow = sH + (fa % RF) * vrs;
-#pragma unroll
-          for (int k = 0; k < UPL; ++k) {
-            const int e = lane + 64 * k;
-            if (e >= V * 8) break;
-            const int row = e >> 3, c0 = (e & 7) * 8;
-            uint4 o = make_uint4(0, 0, 0, 0);
-            if (okf) {
-              float v[8];
-              unpack16(u[i][k], v, (bf16*)nullptr);
-              const float* bp = sBp + row * CBP + c0;
-#pragma unroll
-              for (int j = 0; j < 8; ++j) v[j] = fmaxf(fmaf(v[j], sSc[c0 + j], bp[j]), 0.f);
-              o = pack16(v, (bf16*)nullptr);
-            }
-            *reinterpret_cast<uint4*>(hrow + row * RSH + c0 * 2) = o;
-          }
-        }
-        pa[1] += ptime() - pt0;
-      };
-      stage(gw);
-      stage(CF + gw);
-      lds_barrier();  // S_0: frames 0..15 ready
-      for (int s = 1; s <= nsteps; ++s) {
-        if (s < nsteps) stage(CF * (s + 1) + gw);
-        const long long pb = ptime();
-        lds_barrier();  // S_s
-        pa[2] += ptime() - pb;
-      }
-      if constexpr (PROF) prof_out();
-      return;
-    }
-  } else if (wave >= NWT) {
+  if (wave >= NWT) {
     // =============================== GCN waves: h frames ===============================
     const int gw = wave - NWT;
     bf16x8 ac[P][2];  // stage-1 B operands: B[k = input joint u][n = output joint o] = A[p][u][o]
@@ -338,16 +258,15 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
           fx[i][cb][1] = trfrag(pan, 16, lane);
         }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ring read: refill it with the next batch
-      // LN: the DMA goes out after the epilogue instead, whose parameter loads (global) would otherwise wait
-      // behind it on the in-order vmcnt
-      if (!LN && next >= 0) issue(next);
+      // the DMA goes out after the epilogue, whose parameter loads (global) would otherwise wait behind it on the
+      // in-order vmcnt
       // the FPW frames' chains interleaved per (channel block, partition): mix (stage 1) of every frame, then
       // bf16 + 1x1 conv (stage 2) of every frame, so one frame's MFMA latency hides under the other's MFMAs
       // (padding frames are computed too and replaced by zeros below)
       f32x16 accf[FPW][2];
 #pragma unroll
       for (int i = 0; i < FPW; ++i) accf[i][0] = accf[i][1] = zero;
-      if constexpr (LN) {
+{
         // LN: the graph-conv bias enters as the accumulators' initial value (acc layout: lane = joint lr,
         // register r of tile t = channel 32t + 8(r>>2) + 4lh + (r&3)), loaded before the MFMAs run
         if (a.gbias) {
@@ -398,7 +317,7 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
               }
           }
       }
-      if constexpr (LN) {
+{
         // the frames' LayerNorm statistics over their 64 x V values (lanes lr < V), both frames' wave reductions
         // interleaved; gamma1 / beta1 of this lane's joint and channels loaded once for both frames
         const int lc = min(lr, V - 1);
@@ -501,41 +420,8 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
               }
           }
         }
-      } else {
-#pragma unroll
-        for (int i = 0; i < FPW; ++i) {
-          const int fa = fa0 + NWG * i;
-          if (fa >= nfr) continue;
-          char* hrow = sH + (fa % RF) * vrs;
-          if (!frame_ok(fa)) {  // padding frame: h = 0
-            for (int e = lane; e < V * 8; e += 64)
-              *reinterpret_cast<uint4*>(hrow + (e >> 3) * RSH + (e & 7) * 16) = make_uint4(0, 0, 0, 0);
-            continue;
-          }
-          // epilogue: lane = joint lr, acc[t][r] = g^T[co = 32t + 8(r>>2) + 4lh + (r&3)][lr]; BN1 folded
-          if (lr < V) {
-            char* hr = hrow + lr * RSH;
-            const float* bp = sBp + lr * CBP;
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-              for (int q4 = 0; q4 < 4; ++q4) {
-                const int co = 32 * t + 8 * q4 + 4 * lh;
-                const float4 s4 = *reinterpret_cast<const float4*>(sSc + co);
-                const float4 b4 = *reinterpret_cast<const float4*>(bp + co);
-                const float v[4] = {accf[i][t][4 * q4], accf[i][t][4 * q4 + 1], accf[i][t][4 * q4 + 2],
-                                    accf[i][t][4 * q4 + 3]};
-                bf16x4 hv;
-                hv[0] = (bf16)fmaxf(fmaf(v[0], s4.x, b4.x), 0.f);
-                hv[1] = (bf16)fmaxf(fmaf(v[1], s4.y, b4.y), 0.f);
-                hv[2] = (bf16)fmaxf(fmaf(v[2], s4.z, b4.z), 0.f);
-                hv[3] = (bf16)fmaxf(fmaf(v[3], s4.w, b4.w), 0.f);
-                *reinterpret_cast<bf16x4*>(hr + co * 2) = hv;
-              }
-          }
-        }
       }
-      if (LN && next >= 0) issue(next);
+      if (next >= 0) issue(next);
       pa[1] += ptime() - pt1;
     };
     // prologue: frames 0..15 in two batches of 8 (base 0 and 8); then step s produces base 8s + 8
@@ -557,7 +443,7 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
   // =============================== TCN waves: temporal conv ===============================
   const bf16* __restrict__ wt = reinterpret_cast<const bf16*>(a.wt_frag);
   bf16* __restrict__ zg = reinterpret_cast<bf16*>(a.z);
-  if constexpr (LN) {
+{
     // LayerNorm: frame-aligned row tiles.  TCN wave w = (channel half ct = w & 1, frame group fg = w >> 1) owns
     // row tile i = frame 4fg + i of every step (lane = joint, lanes >= V pad) for its 32 output channels, so a
     // frame's LN2 statistics are one wave reduction per (frame, channel half) plus ONE exchange with the partner
@@ -784,202 +670,6 @@ __global__ __launch_bounds__(NW * 64, 1) void layer_fused_kernel(const stgcn_lay
     }
     if constexpr (PROF) prof_out();
     return;
-  } else {
-    const int ct = wave & 1, rh = wave >> 1;
-    // this lane's output rows (step-relative frame fo, joint w) per row tile; rows past CF*V clamp to row 0
-    int fo_[RT], hw_[RT], jw_[RT];
-    bool rok[RT];
-#pragma unroll
-    for (int i = 0; i < RT; ++i) {
-      const int r = (rh * RT + i) * 32 + lr;
-      rok[i] = r < CF * V;
-      const int rr = rok[i] ? r : 0;
-      fo_[i] = rr / V;
-      jw_[i] = rr - fo_[i] * V;
-      hw_[i] = jw_[i] * RSH + lh * 16;
-    }
-    const int wlane = ct * 4 * 512 + lane * 8;  // 1-KiB block [dt][ct][ks] of the [9][2][4] image
-    int wcur = wlane;  // element offset re-materialised per step (opaque): LICM would otherwise hoist all 36
-                       // weight fragments of the step out of the step loop and spill them.  An integer, not the
-                       // pointer: a pointer laundered through asm loses its address space, and the loads become
-                       // flat loads that also count on lgkmcnt (every LDS wait then drained the weight ring)
-    auto load_w = [&](int s) {
-      const int dt = s >> 2, ks = s & 3;
-      int o = wcur + dt * 8 * 512;  // per-load opaque tap base (ks offsets fit the instruction's immediate)
-      asm volatile("" : "+v"(o));
-      return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(wt + o + ks * 512));
-    };
-    // row tiles of this wave: CF*V rows = nrt tiles of 32, the first RT to row half 0
-    const int nrt = (CF * V + 31) / 32;
-    const int rtn = rh == 0 ? min(RT, nrt) : nrt - RT;
-    static_assert(KSTEPS % NB == 0, "the weight ring runs on across steps");
-    bf16x8 fw[NB];  // k-step k's fragment in slot k % NB, the same every step
-#pragma unroll
-    for (int k = 0; k < NB - 1; ++k) fw[k] = load_w(k);
-    if (DBG & 32) fw[NB - 1] = load_w(NB - 1);
-    // BN2 partials: per row half, the (count, mean, M2) of the run's rows of each channel (row block * 2 + rh of
-    // stats): per-lane sums over the whole run in registers, reduced across the lanes once at the run's end (a
-    // per-step reduction measured 28.6 K of the role's 147 K cycles)
-    float4* const st_out = a.stats ? reinterpret_cast<float4*>(a.stats) + ((long)blockIdx.x * 2 + rh) * C : nullptr;
-    const f32x16 zero = {};
-    char* const zs = smem + g.off_zs + wave * ZSB;  // BN: this wave's partials scratch
-    lds_barrier();  // S_0
-    // the step loop per row-tile count (compile-time: no per-k-step branches in the MFMA stream)
-    auto tcn_run = [&]<int RTN>() {
-      float s1[16], s2[16];  // BN: per-lane (sum, sum of squares) of z - bias over the run's rows
-#pragma unroll
-      for (int r = 0; r < 16; ++r) s1[r] = s2[r] = 0.f;
-      int cnt_run = 0;
-      for (int s = 1; s <= nsteps; ++s) {
-        if (DBG & 2) {
-          lds_barrier();
-          continue;
-        }
-        wcur = wlane;
-        asm volatile("" : "+v"(wcur));
-        const int f0 = R0 + CF * (s - 1);           // first output frame of the step
-        const int base = (CF * (s - 1)) % RF;       // ring slot of run frame 8(s-1) (= output frame f0 - 4)
-        // byte offset of h row (frame f0 + fo + dt - 4, joint w) = slot(base + fo + dt) * vrs + w * RSH
-        int q_[RT];
-#pragma unroll
-        for (int i = 0; i < RT; ++i) q_[i] = base + fo_[i];
-        auto hoff = [&](int i, int dt) {
-          const int sl = q_[i] + dt;
-          return (sl >= RF ? sl - RF : sl) * vrs + hw_[i];
-        };
-        f32x16 acc[RT];
-#pragma unroll
-        for (int i = 0; i < RT; ++i) acc[i] = zero;
-        bf16x8 fb[3][RT];  // h fragments two k-steps ahead (LDS latency under eight waves' traffic)
-        int ad[RT];  // h byte offsets of the current tap (recomputed per tap, opaque to LICM: hoisting all 36
-                     // k-steps' addresses out of the unrolled loop would spill)
-#pragma unroll
-        for (int i = 0; i < RT; ++i) {
-          ad[i] = hoff(i, 0);
-          asm volatile("" : "+v"(ad[i]));
-          if (i < RTN) {
-            fb[0][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sH + ad[i]));
-            fb[1][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sH + ad[i] + 32));
-            if (DBG & 64) fb[2][i] = fb[0][i];
-          }
-        }
-        const long long pk0 = ptime();
-        static_for<KSTEPS>([&]<int k>() {
-          if constexpr (!(DBG & 32)) fw[(k + NB - 1) % NB] = load_w((k + NB - 1) % KSTEPS);  // runs into the next step's first k-steps
-          if constexpr (k + 2 < KSTEPS && !(DBG & 64)) {
-            constexpr int dt2 = (k + 2) >> 2, ks2 = (k + 2) & 3;
-            if constexpr (ks2 == 0) {
-#pragma unroll
-              for (int i = 0; i < RT; ++i) {
-                ad[i] = hoff(i, dt2);
-                asm volatile("" : "+v"(ad[i]));
-              }
-            }
-#pragma unroll
-            for (int i = 0; i < RT; ++i)
-              if (i < RTN)
-                fb[(k + 2) % 3][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sH + ad[i] + ks2 * 32));
-          }
-#pragma unroll
-          for (int i = 0; i < RT; ++i)
-            if (i < RTN) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[k % NB], fb[k % 3][i], acc[i], 0, 0, 0);
-          __builtin_amdgcn_sched_barrier(0);
-        });
-        const long long pk1 = ptime();
-        pa[0] += pk1 - pk0;
-        // epilogue: acc[i][r] = out^T[co = 32ct + 8(r>>2) + 4lh + (r&3)][row (rh*RT + i)*32 + lr]
-        const int vrows = min(CF, R1 - f0) * V;
-        bf16* zt = zg + ((long)n * T + f0) * V * a.z_ld;
-        // the temporal-conv bias from LDS: a global load here would sit behind the weight-fragment prefetch and,
-        // on gfx9's single in-order vmcnt, behind the z stores of the row tiles before it (each tile's stores
-        // were waited out by the next: measured 60 of the 84 us of the temporal-conv role)
-        float tb[16];
-#pragma unroll
-        for (int q4 = 0; q4 < 4; ++q4) {
-          const float4 b4 = *reinterpret_cast<const float4*>(sTb + 32 * ct + 8 * q4 + 4 * lh);
-          tb[4 * q4] = b4.x;
-          tb[4 * q4 + 1] = b4.y;
-          tb[4 * q4 + 2] = b4.z;
-          tb[4 * q4 + 3] = b4.w;
-        }
-        // z = acc + bias: a lane holds 4 channels of each 8-channel group; one v_permlane32_swap per dword gives
-        // lanes 0-31 group 2p and lanes 32-63 group 2p + 1 whole, so each lane stores 16 B per group pair (the 8-B
-        // stores of 4 channels were store-issue bound; routing them through LDS into 64-B row runs measured slower)
-#pragma unroll
-        for (int i = 0; i < RT; ++i) {
-          const int r = (rh * RT + i) * 32 + lr;
-          const bool ok = rok[i] && r < vrows;  // the same for lanes lr and lr + 32 (one row)
-          unsigned pk[4][2];
-#pragma unroll
-          for (int q4 = 0; q4 < 4; ++q4) {
-            bf16x4 o;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float v = acc[i][4 * q4 + e];
-              if (ok) {
-                s1[4 * q4 + e] += v;
-                s2[4 * q4 + e] = fmaf(v, v, s2[4 * q4 + e]);
-              }
-              o[e] = (bf16)(v + tb[4 * q4 + e]);
-            }
-            const u32x2n w2 = __builtin_bit_cast(u32x2n, o);
-            pk[q4][0] = w2.x;
-            pk[q4][1] = w2.y;
-          }
-#pragma unroll
-          for (int p = 0; p < 2; ++p)
-#pragma unroll
-            for (int d = 0; d < 2; ++d) {
-              const auto sw = __builtin_amdgcn_permlane32_swap(pk[2 * p][d], pk[2 * p + 1][d], false, false);
-              pk[2 * p][d] = sw[0];
-              pk[2 * p + 1][d] = sw[1];
-            }
-          if (ok && !(DBG & 16)) {
-#pragma unroll
-            for (int p = 0; p < 2; ++p)
-              *reinterpret_cast<uint4*>(zt + (long)r * a.z_ld + 32 * ct + 16 * p + 8 * lh) =
-                  make_uint4(pk[2 * p][0], pk[2 * p][1], pk[2 * p + 1][0], pk[2 * p + 1][1]);
-          }
-        }
-        const long long pk15 = ptime();
-        pa[4] += pk15 - pk1;
-        cnt_run += max(0, min(vrows - rh * RT * 32, RTN * 32));
-        const long long pk2 = ptime();
-        pa[1] += pk2 - pk15;
-        lds_barrier();  // S_s: the GCN waves may overwrite the frames this step read
-        pa[2] += ptime() - pk2;
-      }
-      if (st_out && !(DBG & (16 | 256))) {  // the run's sums over this wave's rows (lanes) -> (count, mean, M2)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          s1[r] = half_sum(s1[r]);
-          s2[r] = half_sum(s2[r]);
-        }
-        // the 32 channels' partials gathered in LDS by the two lanes holding them, then one 512-B store
-        float4* const ss = reinterpret_cast<float4*>(zs);
-        if (lr == 31) {
-          const float inv = cnt_run ? 1.f / (float)cnt_run : 0.f;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float mu = s1[r] * inv;  // mean of z - bias over the run's rows (bias added back below)
-            ss[8 * (r >> 2) + 4 * lh + (r & 3)] =
-                cnt_run ? make_float4((float)cnt_run, sTb[32 * ct + 8 * (r >> 2) + 4 * lh + (r & 3)] + mu,
-                                      fmaxf(s2[r] - s1[r] * mu, 0.f), 0.f)
-                        : make_float4(0.f, 0.f, 0.f, 0.f);
-          }
-        }
-        if (lane < 32) st_out[32 * ct + lane] = ss[lane];
-      }
-    };
-    if (rtn >= 4)
-      tcn_run.template operator()<4>();
-    else if (rtn == 3)
-      tcn_run.template operator()<3>();
-    else if (rtn == 2)
-      tcn_run.template operator()<2>();
-    else
-      tcn_run.template operator()<1>();
-    if constexpr (PROF) prof_out();
   }
 }
 
@@ -997,28 +687,19 @@ FGeom plan(int N, int T) {
 }  // namespace
 
 // PROF builds: copy the per-wave cycle accounts [block][8 waves][6] (long long; GCN: DMA wait, compute, barrier,
-// total; TCN: k-loop, BN2 partials, barrier, total, z stores) to host memory; -1 in the shipped library
+// total; TCN: k-loop, LN2 statistics, barrier, total, normalise + stores, partner hand-off) to host memory; -1 in the
+// shipped library
 extern "C" int stgcn_fused_prof(void* dst, long n) {
   if (!PROF) return -1;
   if (n > (long)PROF_BLOCKS * 8 * 6) n = (long)PROF_BLOCKS * 8 * 6;
   return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_fused_prof), n * sizeof(long long), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 
-long layer_fused_row_blocks(int N, int T) {
-  if (N < 1 || T < 1) return 1;
-  const FGeom g = plan(N, T);
-  return (long)N * g.runs_n * 2;  // one BN2 partial row per block and row half
-}
-
 int layer_fused_launch(const stgcn_layer_fused_desc& a, hipStream_t s) {
-  const bool gin = a.g_in != nullptr;
-  if (!a.z || !a.wt_frag || (!gin && (!a.x || !a.wg_frag || !a.A))) return STGCN_EBADSHAPE;
-  if (gin && (a.ln || a.g_out || a.u_out || a.h_out || a.gbias || a.g_in_ld < C || a.g_in_ld % 8)) return STGCN_EBADSHAPE;
-  if (a.ln ? (!a.ln1_g || !a.ln1_b || !a.ln2_g || !a.ln2_b || a.stats) : (!a.n1_scale || !a.n1_shift))
+  if (!a.z || !a.wt_frag || !a.x || !a.wg_frag || !a.A || !a.ln1_g || !a.ln1_b || !a.ln2_g || !a.ln2_b)
     return STGCN_EBADSHAPE;
   const int ntrain = !!a.g_out + !!a.u_out + !!a.st1_out + !!a.st2_out;
-  if (ntrain != 0 && (ntrain != 4 || !a.ln || a.g_ld < C || a.g_ld % 4 || a.u_ld < C || a.u_ld % 8))
-    return STGCN_EBADSHAPE;
+  if (ntrain != 0 && (ntrain != 4 || a.g_ld < C || a.g_ld % 4 || a.u_ld < C || a.u_ld % 8)) return STGCN_EBADSHAPE;
   if (a.h_out && (ntrain != 4 || a.h_ld < C || a.h_ld % 4)) return STGCN_EBADSHAPE;
   if (a.N < 1 || a.T < 1 || a.V <= 16 || a.V > VMAX || a.P < 1 || a.P > 3) return STGCN_EBADSHAPE;
   if (a.x_ld < C || a.x_ld % 8 || a.z_ld < C || a.z_ld % 8) return STGCN_EBADSHAPE;
@@ -1027,16 +708,14 @@ int layer_fused_launch(const stgcn_layer_fused_desc& a, hipStream_t s) {
   if (nblk > 0x7fffffffL) return STGCN_EBADSHAPE;
   const int K16 = a.P * G * 2;
   g.off_tab = 2 * K16 * 1024;
-  g.off_ring = g.off_tab + ((a.ln ? 2 * a.V * CGP * 4 : (C + a.V * CBP) * 4) + C * 4 + 255) / 256 * 256;
+  g.off_ring = g.off_tab + (2 * a.V * CGP * 4 + C * 4 + 255) / 256 * 256;
   g.off_h = g.off_ring + NWG * SLOTS * PANEL;
   g.off_red = g.off_h + (RF * a.V * RSH + 255) / 256 * 256;
-  g.off_zs = g.off_red + 2 * C * 8;
-  const size_t lds = (size_t)g.off_red + (a.ln ? NWT * 4 * 8 + NWT * 4 : 2 * C * 8 + NWT * ZSB);
+  const size_t lds = (size_t)g.off_red + NWT * 4 * 8 + NWT * 4;
   if (lds > (size_t)LDS_MAX) return STGCN_EBADSHAPE;
   typedef void (*KFn)(const stgcn_layer_fused_desc, const FGeom);
-  static const KFn tab[2][3] = {{layer_fused_kernel<1, false>, layer_fused_kernel<2, false>, layer_fused_kernel<3, false>},
-                                {layer_fused_kernel<1, true>, layer_fused_kernel<2, true>, layer_fused_kernel<3, true>}};
-  const KFn k = gin ? layer_fused_kernel<1, false, true> : tab[a.ln ? 1 : 0][a.P - 1];
+  static const KFn tab[3] = {layer_fused_kernel<1>, layer_fused_kernel<2>, layer_fused_kernel<3>};
+  const KFn k = tab[a.P - 1];
   if (stgcn_lds_attr((const void*)k, LDS_MAX, s)) return STGCN_EHIP;
   hipLaunchKernelGGL(k, dim3((unsigned)nblk), dim3(NW * 64), lds, s, a, g);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;

@@ -82,7 +82,7 @@ def gcn_backward(x, A32, XA, wg, bg, dg, dx, accumulate, dtype):
 
 
 def _packs(cache, wg, wt, P, Cin, Cout, dtype):
-    """Packed graph-conv (gcn_tile image) and temporal-conv (fragment image) weights, reused while the
+    """Packed graph-conv (the fused layer's W' image) and temporal-conv (fragment image) weights, reused while the
     parameters are unchanged (keyed by storage and in-place version): inference packs once."""
     key = (wg.data_ptr(), wg._version, wt.data_ptr(), wt._version, dtype)
     if cache is not None and cache.get("key") == key:
@@ -133,19 +133,16 @@ def plan_layer_packs(plan, layer, A, M, dtype):
     return pk
 
 
-def fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, sup, dtype, tag=None, cache=None,
-                        norm=BN, train=False, packs=None):
-    """StgcnLayer.forward (stgcn.py:181-193) through layer_fused.hip.  BatchNorm: the two-pass fused form
-    (SURVEY §7): pass 1 = graph conv statistics only (gcn_tile, no g stores) -> BN1 scale/shift; pass 2 =
-    graph conv recomputed per tile + BN1 + ReLU + temporal conv in one kernel (z + BN2 partials); then
-    y = relu(BN2(z) + x).  LayerNorm (per-frame norms): the whole layer is the one kernel; ``train``: it also
-    writes what the unfused backward reads and this returns (y, g, u, ls1, ls2).
-    x: channels-last bf16 (N, 64, T, V).  ``packs``: the step's LayerPacks (training): the temporal-conv fragment
-    image and the bias through A come from the model's one prep launch instead of per-layer launches."""
+def fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, dtype, tag=None, cache=None,
+                        train=False, packs=None):
+    """StgcnLayer.forward (stgcn.py:181-193) of a LayerNorm layer through layer_fused.hip: both norms are per frame,
+    so the whole layer is one kernel (g and h stay on chip).  ``train``: the kernel also writes what the unfused
+    backward reads and this returns (y, g, u, ls1, ls2, h).  x: channels-last bf16 (N, 64, T, V).  ``packs``: the
+    step's LayerPacks (training): the temporal-conv fragment image and the bias through A come from the model's one
+    prep launch instead of per-layer launches."""
     N, Cin, T, V = x.shape
     P = A32.shape[0]
     Cout = wt.shape[0]
-    dev = x.device
     if packs is not None and packs.wt is not None and packs.gw is not None:
         bias2d = packs.gw[1]
         wgf = wg.detach().float().view(P, Cout, Cin).permute(1, 0, 2).reshape(Cout, P * Cin)
@@ -154,28 +151,17 @@ def fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, su
     else:
         bias2d = K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
         wimg, cpg, kwg, wtp = _packs(cache, wg, wt, P, Cin, Cout, dtype)
-    if norm == LN:
-        # the LayerNorm([64,1,V]) parameters as per-joint [V][64] rows, re-laid-out when one changed (every
-        # training step): one stacking launch for the four (the kernel reads 16-B channel runs per joint)
-        lkey = tuple((t.data_ptr(), t._version) for t in (n1w, n1b, n2w, n2b))
-        if cache is not None and cache.get("ln_key") == lkey:
-            ln = cache["ln_val"]
-        else:
-            ln = tuple(torch.stack([p.detach().float().reshape(Cout, V).t() for p in (n1w, n1b, n2w, n2b)]).unbind(0))
-            if cache is not None:
-                cache["ln_key"], cache["ln_val"] = lkey, ln
-        return K.layer_fused(x, A32, wimg, bias2d, None, None, wtp, bt.detach().float().contiguous(), tag=tag,
-                             ln=ln, residual=residual, train=train)
-    rb2 = K.layer_fused_row_blocks(N, T)
-    st2 = torch.empty((rb2, Cout, 4), dtype=torch.float32, device=dev)
-    # both kernels write every row block of their statistics: no zero fill
-    rb1 = K.gcn_tile_row_blocks(N * T, V, Cout)
-    st1 = torch.empty((rb1, cpg, 4), dtype=torch.float32, device=dev)
-    K.gcn_tile(x, A32, wimg, kwg, Cin, Cout, cpg, sup, bias=bias2d, stats=st1, stats_only=True)
-    _, sc1, sh1 = K.bn_finalize(st1, rb1, cpg, Cout, n1w.detach().float(), n1b.detach().float())
-    z = K.layer_fused(x, A32, wimg, bias2d, sc1, sh1, wtp, bt.detach().float().contiguous(), stats=st2, tag=tag)
-    _, sc2, sh2 = K.bn_finalize(st2, rb2, Cout, Cout, n2w.detach().float(), n2b.detach().float())
-    return K.bn_apply(z, sc2, sh2, N * T * V, Cout, res_mode=1 if residual else 0, r=x if residual else None)
+    # the LayerNorm([64,1,V]) parameters as per-joint [V][64] rows, re-laid-out when one changed (every training
+    # step): one stacking launch for the four (the kernel reads 16-B channel runs per joint)
+    lkey = tuple((t.data_ptr(), t._version) for t in (n1w, n1b, n2w, n2b))
+    if cache is not None and cache.get("ln_key") == lkey:
+        ln = cache["ln_val"]
+    else:
+        ln = tuple(torch.stack([p.detach().float().reshape(Cout, V).t() for p in (n1w, n1b, n2w, n2b)]).unbind(0))
+        if cache is not None:
+            cache["ln_key"], cache["ln_val"] = lkey, ln
+    return K.layer_fused(x, A32, wimg, bias2d, wtp, bt.detach().float().contiguous(), ln, tag=tag, residual=residual,
+                         train=train)
 
 
 def _stats_arena(cache, dev, dtype, shapes, route):
@@ -224,20 +210,18 @@ class StgcnLayerFunction(torch.autograd.Function):
         # ---- graph convolution: g = sum_p A_p-mix(x) W_p + bias2d
         sup = cfg[5] if len(cfg) > 5 else None
         gather = sup is not None and A32.dim() == 3 and not sup.dense(P)
-        if (gather and len(cfg) > 7 and cfg[7] and ROUTING.fused_inference and (norm == LN or ROUTING.fused_bn_inference)
+        if (gather and len(cfg) > 7 and cfg[7] and ROUTING.fused_inference and norm == LN
                 and K.layer_fused_ok(sup, P, Cin, Cout, V, kt, stride, dtype)):
-            # inference: the fused layer kernel (g never leaves the chip; nothing saved for backward).
-            # LayerNorm layers: one kernel, 0.14 vs 0.20 ms unfused; BatchNorm layers (routing.fused_bn_inference,
-            # opt-in): the two-pass form, 0.176 vs 0.166 ms unfused on the r05a box
-            return fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, sup, dtype,
-                                       cache=cache, norm=norm)
+            # inference of a LayerNorm 64 -> 64 stride-1 layer: the one-kernel layer (g never leaves the chip;
+            # nothing saved for backward): 0.12 vs 0.15-0.21 ms unfused
+            return fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, dtype, cache=cache)
         if (gather and norm == LN and ROUTING.fused_ln_train and not (len(cfg) > 7 and cfg[7])
                 and K.layer_fused_ok(sup, P, Cin, Cout, V, kt, stride, dtype)):
             # training forward of a LayerNorm 64 -> 64 stride-1 layer: the one-kernel layer (g and h on chip for
             # the temporal conv) also writes g, u and both LN statistics — exactly what the unfused forward
             # saves — so the backward below is unchanged (ln/ configs)
-            y, g, u, ls1, ls2, h = fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, sup,
-                                                       dtype, cache=cache, norm=LN, train=True, packs=packs)
+            y, g, u, ls1, ls2, h = fused_layer_forward(x, A32, wg, bg, n1w, n1b, wt, bt, n2w, n2b, residual, dtype,
+                                                       cache=cache, train=True, packs=packs)
             ctx.cfg = cfg
             ctx.sup = sup
             ctx.dims = (N, Cin, Cout, T, T_out, V, P, pad, False)
@@ -247,22 +231,14 @@ class StgcnLayerFunction(torch.autograd.Function):
             return y
         # gathered path: bias2d comes from the weight preparation below
         bias2d = None if gather else K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
-        # BatchNorm 64 -> 64 stride-1 training forward: the temporal conv through layer_fused.hip's g-input mode
-        # (routing.bn_tcn_fused, off by default: step-neutral); it writes its own BN2 partials
-        wtp, cpt, kpt = packs.wt if packs is not None else \
-            K.pack_weight(wt.detach().float().squeeze(-1).permute(2, 0, 1), dtype, stride=stride)  # [Kt][Cout][Cin]
-        tcn_fused = (norm == BN and gather and ROUTING.bn_tcn_fused and getattr(wtp, "frag_stride", None) == 1
-                     and K.layer_fused_ok(sup, P, Cin, Cout, V, kt, stride, dtype))
         if norm == BN:  # all BatchNorm partial-statistics buffers of the layer from one zero fill
             cpo = -(-Cout // K.col_tile(Cout)) * K.col_tile(Cout)
             rb1 = K.gconv_row_blocks(N * T, V) if gather else K.row_blocks(M1, Cout)
             rb2 = K.row_blocks(M2, Cout)
-            st_shapes = [(rb1, cpo, 4)] + ([] if tcn_fused else [(rb2, cpo, 4)]) + \
-                ([(K.row_blocks(M2, Cout), cpo, 4)] if res_conv else [])
-            st_all = _stats_arena(cache, dev, x.dtype, st_shapes, (gather, tcn_fused))
-            st1 = st_all[0]
-            st2 = None if tcn_fused else st_all[1]
-            str_ = st_all[-1] if res_conv else None
+            st_shapes = [(rb1, cpo, 4), (rb2, cpo, 4)] + ([(K.row_blocks(M2, Cout), cpo, 4)] if res_conv else [])
+            st_all = _stats_arena(cache, dev, x.dtype, st_shapes, gather)
+            st1, st2 = st_all[0], st_all[1]
+            str_ = st_all[2] if res_conv else None
         # ---- residual branch: independent of the graph conv -> temporal conv chain until the output norm
         r = None
         if res_conv:
@@ -306,16 +282,12 @@ class StgcnLayerFunction(torch.autograd.Function):
             h = K.ln_apply(g, ls1, _flat_ln(n1w), _flat_ln(n1b), M1, V, Cout, relu=True)
             pro1 = {}
 
-        # ---- temporal conv on relu(norm1(g)) (norm applied in the prologue; wtp packed above)
-        if tcn_fused:
-            # 64 -> 64 stride-1: layer_fused.hip's g-input mode (BN1 + ReLU staged once per frame into its LDS
-            # ring, the 9-tap conv from there) instead of conv_wide's per-tile prologue
-            st2 = _stats_arena(cache, dev, x.dtype, [(K.layer_fused_row_blocks(N, T), Cout, 4)], "tcn")[0]
-            u = K.layer_tcn(g, sc1, sh1, wtp, bt.detach().float().contiguous(), st2, tag=f"tcn_fwd_c{Cout}")
-        else:
-            u = K.conv_rows(g if norm == BN else h, wtp, Cout, Cout, cpt, kpt, T, T_out, Kt=kt, stride=stride,
-                            pad=pad, bias=bt.detach().float().contiguous(), stats=st2 if norm == BN else None,
-                            tag=f"tcn_fwd_c{Cout}" if stride == 1 else None, **pro1)
+        # ---- temporal conv on relu(norm1(g)) (norm applied in the prologue)
+        wtp, cpt, kpt = packs.wt if packs is not None else \
+            K.pack_weight(wt.detach().float().squeeze(-1).permute(2, 0, 1), dtype, stride=stride)  # [Kt][Cout][Cin]
+        u = K.conv_rows(g if norm == BN else h, wtp, Cout, Cout, cpt, kpt, T, T_out, Kt=kt, stride=stride,
+                        pad=pad, bias=bt.detach().float().contiguous(), stats=st2 if norm == BN else None,
+                        tag=f"tcn_fwd_c{Cout}" if stride == 1 else None, **pro1)
 
         # ---- y = relu(norm2(u) + res)
         if norm == BN:

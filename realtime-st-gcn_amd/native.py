@@ -471,10 +471,6 @@ class GraphSupport:
 
         self.nbr, self.deg = pack(S)
         self.rnbr, self.rdeg = pack(R)
-        # per-partition max degree of a column (forward mix) / row (data-grad mix) of A[p] (gcn_tile)
-        ap = (A.detach() != 0).cpu().numpy()  # [P][v][w]
-        self.dmax_fwd = [int(ap[p].sum(0).max()) for p in range(ap.shape[0])]
-        self.dmax_bwd = [int(ap[p].sum(1).max()) for p in range(ap.shape[0])]
 
     def dense(self, P):
         """A-first (amix) is cheaper when the support is denser than P entries per output joint."""
@@ -534,17 +530,13 @@ def pack_frag1(w2: torch.Tensor, dtype) -> tuple:
     return buf[cp * kp:], cp, kp
 
 
-def gcn_tile_row_blocks(NT: int, V: int, Cout: int) -> int:
-    return L.lib().stgcn_gcn_tile_row_blocks(NT, V, Cout)
-
-
 _PERM16 = {}
 
 
 def pack_gcn_weight(w2: torch.Tensor, dtype) -> tuple:
-    """[Cout][P*Cin] fp32 W' -> the stgcn_gcn_tile weight image: the Kt = 1 fragment image of W' with the
-    columns of every 16-wide group in the order of the mix accumulators' rows (include/stgcn_amd.h):
-    (image, Cout_pad, K_pad)."""
+    """[Cout][P*Cin] fp32 W' -> the graph-conv weight image of stgcn_layer_fused_fwd (wg_frag): the Kt = 1 fragment
+    image of W' with the columns of every 16-wide group in the order of the joint-mix accumulators' rows
+    (include/stgcn_amd.h): (image, Cout_pad, K_pad)."""
     K = w2.shape[1]
     key = (K, w2.device)
     perm = _PERM16.get(key)
@@ -555,29 +547,6 @@ def pack_gcn_weight(w2: torch.Tensor, dtype) -> tuple:
         perm = (torch.arange(K) // 16 * 16 + within.repeat(K // 16)).to(w2.device)
         _PERM16[key] = perm
     return pack_frag1(w2.float().index_select(1, perm), dtype)
-
-
-def gcn_tile(x, A, wimg, kw_pad, Cin, Cout, cp, sup, trans_a=False, bias=None, stats=None, out=None,
-             accumulate=False, stats_only=False):
-    """Fused graph conv (stgcn_gcn_tile): out rows (N, Cout, T, V) (+)= W' . A-mix(x) (+ bias[w][co]).
-    stats_only: no output, BN partial statistics only (pass 1 of the fused layer); returns None."""
-    N, _, T, V = x.shape
-    if out is None and not stats_only:
-        out = cl_empty(N, Cout, T, V, x.dtype, x.device)
-    A = _dense(A)
-    d = L.GcnTileDesc()
-    d.in_, d.out, d.w_frag, d.A = x.data_ptr(), L.ptr(out), wimg.data_ptr(), A.data_ptr()
-    d.bias, d.stats = L.ptr(bias), L.ptr(stats)
-    d.NT, d.V, d.P, d.Cin, d.Cout, d.Cout_pad, d.Kw_pad = N * T, V, A.shape[0], Cin, Cout, cp, kw_pad
-    d.in_ld, d.out_ld = rows_ld(x), (rows_ld(out) if out is not None else Cout)
-    d.trans_a, d.accumulate = int(trans_a), int(accumulate)
-    dm = sup.dmax_bwd if trans_a else sup.dmax_fwd
-    for i, v in enumerate(dm[:4]):
-        d.dmax[i] = v
-    if d.out is None and not (out is None and stats_only and stats is not None):
-        raise RuntimeError("stgcn_amd: gcn_tile needs an output or stats_only with a stats buffer")
-    L.check(L.lib().stgcn_gcn_tile(d, L.dtype_code(x.dtype), L.stream()), "gcn_tile")
-    return out
 
 
 def gcn_bias_plan(A, b, Cout, plan, M=None):
@@ -592,24 +561,18 @@ def gcn_bias_plan(A, b, Cout, plan, M=None):
 
 
 def layer_fused_ok(sup, P, Cin, Cout, V, kt, stride, dtype) -> bool:
-    """Whether a layer's forward can run as the fused graph conv + BN1 + ReLU + temporal conv kernel
-    (layer_fused.hip): bf16, 64 -> 64 channels, stride 1, Kt = 9, a batch-shared graph, 16 < V <= 25.  A shape
-    check only: each caller tests its own routing switch (fused_inference, fused_ln_train, bn_tcn_fused)."""
+    """Whether a LayerNorm layer's forward can run as the one-kernel layer (layer_fused.hip): bf16, 64 -> 64
+    channels, stride 1, Kt = 9, a batch-shared graph, 16 < V <= 25.  A shape check only: each caller tests its
+    own routing switch (fused_inference, fused_ln_train)."""
     return (dtype == torch.bfloat16 and sup is not None and P <= 3 and 16 < V <= 25
             and Cin == 64 and Cout == 64 and kt == 9 and stride == 1)
 
 
-def layer_fused_row_blocks(N: int, T: int) -> int:
-    return L.lib().stgcn_layer_fused_row_blocks(N, T)
-
-
-def layer_fused(x, A, wimg, gbias, n1_scale, n1_shift, wt_packed, tbias, stats=None, tag=None, ln=None,
-                residual=False, train=False):
-    """stgcn_layer_fused_fwd.  BatchNorm layer: z rows (N, 64, T, V) = tcn(relu(BN1(gcn(x)))) + tbias, g kept
-    on chip (+ BN2 partials).  ln = (g1, b1, g2, b2) LayerNorm parameters as [V][64] fp32: the whole layer
-    y = relu(LN2(tcn(relu(LN1(gcn(x))))) + residual * x) in this one kernel.  ``train`` (LayerNorm only): also
-    the backward's inputs — returns (y, g, u, ls1, ls2, h): g / u the graph-conv / temporal-conv outputs (bias
-    included) as rows, ls1 / ls2 their per-frame (mean, rstd) [N*T][2] (ln_stats's layout), h = relu(LN1(g))."""
+def layer_fused(x, A, wimg, gbias, wt_packed, tbias, ln, tag=None, residual=False, train=False):
+    """stgcn_layer_fused_fwd: the whole LayerNorm layer y = relu(LN2(tcn(relu(LN1(gcn(x))))) + residual * x) in one
+    kernel; ln = (g1, b1, g2, b2) LayerNorm parameters as [V][64] fp32.  ``train``: also the backward's inputs —
+    returns (y, g, u, ls1, ls2, h): g / u the graph-conv / temporal-conv outputs (bias included) as rows, ls1 / ls2
+    their per-frame (mean, rstd) [N*T][2] (ln_stats's layout), h = relu(LN1(g))."""
     N, C, T, V = x.shape
     if getattr(wt_packed, "frag_stride", None) != 1:
         raise RuntimeError("stgcn_amd: layer_fused needs the stride-1 fragment image of the temporal weight")
@@ -617,19 +580,15 @@ def layer_fused(x, A, wimg, gbias, n1_scale, n1_shift, wt_packed, tbias, stats=N
     A = _dense(A)
     d = L.LayerFusedDesc()
     d.x, d.z, d.wg_frag, d.A = x.data_ptr(), z.data_ptr(), wimg.data_ptr(), A.data_ptr()
-    d.gbias, d.n1_scale, d.n1_shift = L.ptr(gbias), L.ptr(n1_scale), L.ptr(n1_shift)
-    d.wt_frag, d.tbias, d.stats = wt_packed.frag_ptr, L.ptr(tbias), L.ptr(stats)
+    d.gbias, d.wt_frag, d.tbias = L.ptr(gbias), wt_packed.frag_ptr, L.ptr(tbias)
     d.N, d.T, d.V, d.P, d.x_ld, d.z_ld = N, T, V, A.shape[0], rows_ld(x), rows_ld(z)
-    if ln is not None:
-        ln = [_f32c(t) for t in ln]
-        if any(t.numel() != V * C for t in ln):
-            raise RuntimeError("stgcn_amd: layer_fused LayerNorm parameters must be [V][64]")
-        d.ln1_g, d.ln1_b, d.ln2_g, d.ln2_b = (t.data_ptr() for t in ln)
-        d.ln, d.residual = 1, int(bool(residual))
-        d._keep = ln
+    ln = [_f32c(t) for t in ln]
+    if any(t.numel() != V * C for t in ln):
+        raise RuntimeError("stgcn_amd: layer_fused LayerNorm parameters must be [V][64]")
+    d.ln1_g, d.ln1_b, d.ln2_g, d.ln2_b = (t.data_ptr() for t in ln)
+    d.residual = int(bool(residual))
+    d._keep = ln
     if train:
-        if ln is None:
-            raise RuntimeError("stgcn_amd: the fused training forward is the LayerNorm layer's")
         g = cl_empty(N, C, T, V, x.dtype, x.device)
         u = cl_empty(N, C, T, V, x.dtype, x.device)
         st = torch.empty((2, N * T, 2), dtype=torch.float32, device=x.device)
@@ -645,33 +604,6 @@ def layer_fused(x, A, wimg, gbias, n1_scale, n1_shift, wt_packed, tbias, stats=N
         hook(tag, "end", None)
     if train:
         return z, g, u, st[0], st[1], hh
-    return z
-
-
-def layer_tcn(g, n1_scale, n1_shift, wt_packed, tbias, stats, tag=None):
-    """stgcn_layer_fused_fwd in its g-input mode: z rows (N, 64, T, V) = tcn(relu(g * n1_scale + n1_shift)) +
-    tbias with BN2 partials into ``stats`` ([layer_fused_row_blocks(N, T)][64][4], every block written) — the
-    BatchNorm training forward's temporal conv on the graph-conv output g (bias included)."""
-    N, C, T, V = g.shape
-    if getattr(wt_packed, "frag_stride", None) != 1:
-        raise RuntimeError("stgcn_amd: layer_tcn needs the stride-1 fragment image of the temporal weight")
-    z = cl_empty(N, C, T, V, g.dtype, g.device)
-    d = L.LayerFusedDesc()
-    d.g_in, d.g_in_ld, d.z = g.data_ptr(), rows_ld(g), z.data_ptr()
-    d.n1_scale, d.n1_shift = L.ptr(n1_scale), L.ptr(n1_shift)
-    d.wt_frag, d.tbias, d.stats = wt_packed.frag_ptr, L.ptr(tbias), L.ptr(stats)
-    d.N, d.T, d.V, d.P, d.x_ld, d.z_ld = N, T, V, 1, rows_ld(g), rows_ld(z)
-    hook = EVENT_HOOK if tag is not None else None
-    if hook:
-        hook(tag, "start", None)
-    kh = KTIME_HOOK
-    if kh:
-        ktag = _k_start(kh, "tcn_fwd", f"{C}->{C} s1", 2.0 * N * T * V * C * C * 9, g.element_size() * N * T * V * 2 * C)
-    L.check(L.lib().stgcn_layer_fused_fwd(d, L.stream()), "layer_fused (g input)")
-    if kh:
-        kh(ktag, "end", None)
-    if hook:
-        hook(tag, "end", None)
     return z
 
 

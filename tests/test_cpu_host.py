@@ -246,7 +246,7 @@ def test_descriptor_layouts_match_header(pkg, tmp_path):
     the library read garbage).  Compiled with gcc on the host: no GPU, no HIP headers (the header is plain C)."""
     L = pkg._lib
     structs = {"stgcn_conv_desc": L.ConvDesc, "stgcn_wgrad_desc": L.WgradDesc, "stgcn_amix_desc": L.AmixDesc,
-               "stgcn_gconv_desc": L.GconvDesc, "stgcn_gcn_tile_desc": L.GcnTileDesc,
+               "stgcn_gconv_desc": L.GconvDesc,
                "stgcn_gconv_wgrad_desc": L.GconvWgradDesc, "stgcn_bn_bwd_desc": L.BnBwdDesc,
                "stgcn_layer_fused_desc": L.LayerFusedDesc, "stgcn_prep_job": L.PrepJob,
                "stgcn_adam_entry": L.AdamEntry}

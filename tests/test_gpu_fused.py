@@ -1,13 +1,13 @@
-"""The fused ST-GCN layer forward (layer_fused.hip, the BASELINE north_star kernel: graph conv + BN1 + ReLU
-+ temporal conv with g kept on chip, two-pass BatchNorm per SURVEY §7).
+"""The fused ST-GCN layer (layer_fused.hip, the BASELINE north_star kernel): a LayerNorm StgcnLayer as ONE kernel —
+graph conv + LN1 + ReLU + temporal conv + LN2 + residual + ReLU with g and h kept on chip.
 
-* kernel level: stgcn_layer_fused_fwd through the C-ABI against torch fp32 on the same bf16-rounded
-  operands (oracle.tgcn = tgcn.py:58-79, F.conv2d = stgcn.py:154-159): z and its BN2 partial statistics,
-  at a short trial (a partial last tile, padding frames at both ends) and at the bench shape
-  (N=64 T=300: 1200 tiles, several per persistent block);
-* pass 1 (gcn_tile statistics only) against the statistics of the materialised graph conv;
-* layer / model level: StgcnLayer and the config-2 Model in inference (no autograd) — the path that
-  routes through the fused kernel — against the fp32 oracle (stgcn.py:80-97,181-193), bf16 tolerance.
+* kernel level: stgcn_layer_fused_fwd through the C-ABI against the fp32 oracle on the same bf16-rounded operands
+  (oracle.tgcn = tgcn.py:58-79, layernorm_cv = layernorm.py:22-28, F.conv2d = stgcn.py:154-159) at a short trial
+  (a partial last step, padding frames at both ends) and at the bench shape (N=64 T=300);
+* layer / model level: StgcnLayer and the config-2 Model in inference (no autograd) and training (routing
+  fused_ln_train) — the paths that route through the fused kernel — against the fp32 oracle (stgcn.py:80-97,
+  181-193), bf16 tolerance; BatchNorm layers take the unfused route (no one-kernel BatchNorm form: BN1's batch
+  statistics need all of g first).
 """
 import pytest
 import torch
@@ -42,47 +42,6 @@ def _graph(P):
     return A * (1 + 0.1 * torch.randn(A.shape, generator=g))  # edge importance applied
 
 
-@pytest.mark.parametrize("N,T", [(2, 37), (64, 300)])
-def test_layer_fused_kernel(P, N, T):
-    K = P.native
-    torch.manual_seed(N + T)
-    V, C = 25, 64
-    A = _graph(P)
-    Pp = A.shape[0]
-    x = rb(torch.randn(N, C, T, V))
-    wg = rb(torch.randn(Pp * C, C, 1, 1) / C ** 0.5)
-    bg = torch.randn(Pp * C) * 0.1
-    wt = rb(torch.randn(C, C, 9, 1) / (9 * C) ** 0.5)
-    bt = torch.randn(C) * 0.1
-    sc, sh = torch.rand(C) + 0.5, torch.randn(C) * 0.5
-    g = O.tgcn(x, wg, bg, A)
-    h = torch.relu(g * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1))
-    ref = F.conv2d(rb(h), wt, bt, padding=(4, 0))
-
-    A_d = A.to(DEV)
-    sup = K.GraphSupport(A_d)
-    bias2d = K.gcn_bias(A_d, bg.to(DEV), N, C)
-    wgf = wg.view(Pp, C, C).permute(1, 0, 2).reshape(C, Pp * C).to(DEV)
-    wimg, cpg, kwg = K.pack_gcn_weight(wgf, BF)
-    wtp, _, _ = K.pack_weight(wt.squeeze(-1).permute(2, 0, 1).to(DEV), BF, stride=1)
-    st = torch.full((K.layer_fused_row_blocks(N, T), C, 4), float("nan"), device=DEV)  # every row is written
-    z = K.layer_fused(cl(x, BF), A_d, wimg, bias2d, sc.to(DEV), sh.to(DEV), wtp, bt.to(DEV), stats=st)
-    assert_close(z.float(), ref, 2e-2, "fused z")
-    mr, _, _ = K.bn_finalize(st, st.shape[0], C, C, None, None)
-    zf = z.float().cpu()  # statistics are of the fp32 values before the bf16 store
-    assert_close(mr[:, 0].cpu(), ref.mean(dim=(0, 2, 3)), 2e-2, "bn2 mean")
-    assert_close(mr[:, 1].cpu(), 1 / torch.sqrt(ref.var(dim=(0, 2, 3), unbiased=False) + 1e-5), 1e-2, "bn2 rstd")
-    del zf
-
-    # pass 1: statistics of g without storing it
-    rb1 = K.gcn_tile_row_blocks(N * T, V, C)
-    st1 = torch.zeros((rb1, cpg, 4), device=DEV)
-    assert K.gcn_tile(cl(x, BF), A_d, wimg, kwg, C, C, cpg, sup, bias=bias2d, stats=st1, stats_only=True) is None
-    m1, _, _ = K.bn_finalize(st1, rb1, cpg, C, None, None)
-    assert_close(m1[:, 0].cpu(), g.mean(dim=(0, 2, 3)), 2e-2, "bn1 mean")
-    assert_close(m1[:, 1].cpu(), 1 / torch.sqrt(g.var(dim=(0, 2, 3), unbiased=False) + 1e-5), 1e-2, "bn1 rstd")
-
-
 def _count_fused(P, monkeypatch):
     calls = []
     orig = P.native.layer_fused
@@ -92,15 +51,14 @@ def _count_fused(P, monkeypatch):
         return orig(*a, **k)
 
     monkeypatch.setattr(P.native, "layer_fused", spy)
-    monkeypatch.setattr(P.routing.ROUTING, "fused_bn_inference", True)  # whatever the environment chose
+    monkeypatch.setattr(P.routing.ROUTING, "fused_inference", True)  # whatever the environment chose
     return calls
 
 
 def test_bn_inference_unfused_route(P, monkeypatch):
-    """With routing.fused_bn_inference off a BatchNorm layer's inference forward takes the unfused route and
-    still matches the fp32 oracle."""
+    """A BatchNorm layer's inference forward takes the unfused route (there is no one-kernel BatchNorm form) and
+    matches the fp32 oracle."""
     calls = _count_fused(P, monkeypatch)
-    monkeypatch.setattr(P.routing.ROUTING, "fused_bn_inference", False)
     torch.manual_seed(4)
     N, T, V = 4, 64, 25
     A = _graph(P)
@@ -113,15 +71,15 @@ def test_bn_inference_unfused_route(P, monkeypatch):
     with torch.no_grad():
         y = layer(x.to(DEV), A.to(DEV))
     torch.cuda.synchronize()
-    assert not calls, "BatchNorm inference took the fused kernel without fused_bn_inference"
+    assert not calls, "BatchNorm inference took the (LayerNorm-only) fused kernel"
     assert_close(y.float().cpu(), ref, 3e-2, "unfused inference layer")
 
 
 @pytest.mark.parametrize("norm", ["BatchNorm", "LayerNorm"])
 @pytest.mark.parametrize("residual", [True, False])
 def test_stgcn_layer_inference_fused(P, monkeypatch, residual, norm):
-    """StgcnLayer (64 -> 64, stride 1) under no_grad takes the fused kernel (BatchNorm: two passes + BN2
-    apply; LayerNorm: the whole layer in the one kernel); vs the fp32 oracle."""
+    """StgcnLayer (64 -> 64, stride 1) under no_grad: LayerNorm takes the one-kernel layer, BatchNorm the unfused
+    route; vs the fp32 oracle."""
     calls = _count_fused(P, monkeypatch)
     torch.manual_seed(3)
     N, T, V = 8, 100, 25
@@ -142,8 +100,8 @@ def test_stgcn_layer_inference_fused(P, monkeypatch, residual, norm):
     with torch.no_grad():
         y = layer(x.to(DEV), A.to(DEV))
     torch.cuda.synchronize()
-    assert len(calls) == 1, "the inference forward did not take the fused kernel"
-    assert_close(y.float().cpu(), ref, 3e-2, "fused layer")
+    assert len(calls) == (1 if norm == "LayerNorm" else 0), f"fused kernel calls {calls}"
+    assert_close(y.float().cpu(), ref, 3e-2, "inference layer")
 
 
 @pytest.mark.parametrize("T", [300, 37])
@@ -170,15 +128,15 @@ def test_layer_fused_ln_kernel(P, T):
     wimg, _, _ = K.pack_gcn_weight(wgf, BF)
     wtp, _, _ = K.pack_weight(wt.squeeze(-1).permute(2, 0, 1).to(DEV), BF, stride=1)
     vc = lambda t: t.reshape(C, V).t().contiguous().to(DEV)  # noqa: E731
-    y = K.layer_fused(cl(x, BF), A_d, wimg, bias2d, None, None, wtp, bt.to(DEV),
-                      ln=(vc(g1), vc(b1), vc(g2), vc(b2)), residual=True)
+    y = K.layer_fused(cl(x, BF), A_d, wimg, bias2d, wtp, bt.to(DEV), (vc(g1), vc(b1), vc(g2), vc(b2)), residual=True)
     assert_close(y.float(), ref, 3e-2, "fused LN layer")
 
 
 @pytest.mark.parametrize("norm", ["BatchNorm", "LayerNorm"])
 def test_model_inference_fused_config2(P, monkeypatch, norm):
     """The config-2 model (9 layers, N=16 T=300; as_is BatchNorm and the ln/ LayerNorm variant) in
-    inference: layers 0-2 run fused; logits vs the oracle."""
+    inference: the LayerNorm model's layers 0-2 run as the one-kernel layer (the BatchNorm model's unfused);
+    logits vs the oracle."""
     calls = _count_fused(P, monkeypatch)
     arch = {"strategy": "spatial", "in_feat": 3, "normalization": norm, "num_classes": 52,
             "output_type": "logits",
@@ -196,8 +154,8 @@ def test_model_inference_fused_config2(P, monkeypatch, norm):
     with torch.no_grad():
         y = m(x.to(DEV))
     torch.cuda.synchronize()
-    assert len(calls) == 3
-    assert_close(y.float().cpu(), ref, 3e-2, "model logits (fused inference)")
+    assert len(calls) == (3 if norm == "LayerNorm" else 0)
+    assert_close(y.float().cpu(), ref, 3e-2, "model logits (inference)")
 
 
 def _ln_layer(P, seed, tcn_bias=None):
@@ -393,78 +351,3 @@ def test_ln_model_fused_training(P, monkeypatch):
     assert_close(out[True][0], out[False][0], 2e-2, "fused vs unfused logits")
     for k, gu in out[False][1].items():
         assert_grad_close(out[True][1][k], gu, 4e-2, f"fused vs unfused {k}", reduction=True)
-
-
-@pytest.mark.parametrize("N,T", [(2, 37), (3, 9), (64, 300)])
-def test_layer_tcn_kernel(P, N, T):
-    """layer_fused's g-input mode (native.layer_tcn, the BatchNorm training forward's temporal conv at 64 -> 64
-    stride 1): z = conv(relu(g * s1 + shift1)) + bias (stgcn.py:151-159) and its BN2 partials against torch fp32
-    on the same bf16 g, at a partial last step, a run shorter than the halo and the bench shape."""
-    K = P.native
-    torch.manual_seed(5 * N + T)
-    V, C = 25, 64
-    g = rb(torch.randn(N, C, T, V) * 2 + 0.3)
-    wt = rb(torch.randn(C, C, 9, 1) / (9 * C) ** 0.5)
-    bt = torch.randn(C) * 0.1
-    sc, sh = torch.rand(C) + 0.5, torch.randn(C) * 0.5
-    h = torch.relu(g * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1))
-    ref = F.conv2d(rb(h), wt, bt, padding=(4, 0))
-    wtp, _, _ = K.pack_weight(wt.squeeze(-1).permute(2, 0, 1).to(DEV), BF, stride=1)
-    st = torch.full((K.layer_fused_row_blocks(N, T), C, 4), float("nan"), device=DEV)  # every row is written
-    z = K.layer_tcn(cl(g, BF), sc.to(DEV), sh.to(DEV), wtp, bt.to(DEV), st)
-    assert_close(z.float(), ref, 2e-2, "tcn z")
-    mr, _, _ = K.bn_finalize(st, st.shape[0], C, C, None, None)
-    assert_close(mr[:, 0].cpu(), ref.mean(dim=(0, 2, 3)), 2e-2, "bn2 mean")
-    assert_close(mr[:, 1].cpu(), 1 / torch.sqrt(ref.var(dim=(0, 2, 3), unbiased=False) + 1e-5), 1e-2, "bn2 rstd")
-
-
-@pytest.mark.parametrize("N,T,residual", [(3, 37, True), (2, 20, False)])
-def test_bn_layer_tcn_training(P, monkeypatch, N, T, residual):
-    """Training forward of a BatchNorm 64 -> 64 stride-1 layer with its temporal conv through layer_fused's
-    g-input mode (routing bn_tcn_fused) against conv_wide's route and the fp32 oracle (stgcn.py:181-193): y and
-    every gradient at the bf16 layer tolerance; the g-input kernel ran once."""
-    from conftest import assert_grad_close, grad_floor
-    calls = []
-    orig = P.native.layer_tcn
-
-    def spy(*a, **k):
-        calls.append(1)
-        return orig(*a, **k)
-
-    monkeypatch.setattr(P.native, "layer_tcn", spy)
-    g = torch.Generator().manual_seed(41 + T)
-    A = _graph(P)
-    torch.manual_seed(41 + T)
-    layer = P.StgcnLayer(64, 64, (9, 25), 3, 25, stride=1, residual=residual, normalization="BatchNorm")
-    sd = {k: v.clone().requires_grad_(True) for k, v in layer.state_dict().items() if v.is_floating_point()}
-    x = torch.randn(N, 64, T, 25, generator=g)
-    dy = torch.randn(N, 64, T, 25, generator=g)
-    xr = x.clone().requires_grad_(True)
-    Ar = A.clone().requires_grad_(True)
-    ref = O.stgcn_layer(xr, Ar, sd, "", 9, 1, residual, "BatchNorm")
-    ref.backward(dy)
-    layer = P.set_compute_dtype(layer.to(DEV), "bf16")
-    out = {}
-    for route in (True, False):
-        monkeypatch.setattr(P.routing.ROUTING, "bn_tcn_fused", route)
-        layer.zero_grad(set_to_none=True)
-        xg = x.to(DEV).requires_grad_(True)
-        Ag = A.to(DEV).requires_grad_(True)
-        y = layer(xg, Ag)
-        y.backward(dy.to(DEV))
-        torch.cuda.synchronize()
-        out[route] = (y.detach().float().cpu(), xg.grad.float().cpu(), Ag.grad.float().cpu(),
-                      {k: p.grad.float().cpu() for k, p in layer.named_parameters()})
-    assert calls == [1], calls
-    (yf, dxf, dAf, gf), (yu, dxu, dAu, gu) = out[True], out[False]
-    assert_close(yf, yu, 2e-2, "g-input vs conv_wide y")
-    assert_grad_close(dxf, dxu, 4e-2, "g-input vs conv_wide dx")
-    for k in gu:
-        assert_grad_close(gf[k], gu[k], 4e-2, f"g-input vs conv_wide {k}", reduction=True)
-    tol = 4e-2
-    assert_close(yf, ref, tol, "y")
-    assert_grad_close(dxf, xr.grad, tol, "dx")
-    assert_grad_close(dAf, Ar.grad, tol, "dA", reduction=True)
-    grads = {k: v.grad for k, v in sd.items() if v.grad is not None}
-    for k, gr in grads.items():
-        assert_grad_close(gf[k], gr, tol, k, grad_floor(grads, k), reduction=True)

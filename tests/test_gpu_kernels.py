@@ -373,41 +373,6 @@ def test_conv_wide_stride2_prologue_stats(K, cin, cout, T, N):
     assert_close(dx.float(), xr.grad, 2e-2, "s2 conv trans")
 
 
-@pytest.mark.parametrize("cin,cout,T,N", [(64, 64, 37, 3), (64, 128, 20, 2), (128, 128, 11, 3), (256, 256, 9, 2)])
-def test_gcn_tile(K, pkg, cin, cout, T, N):
-    """Fused frame-tiled graph conv (gcn_tile.hip, bf16) on the PKU-MMD graph: forward with bias and BN
-    partial statistics, and the data gradient (A^T mix), against the reference's conv1x1 + einsum in fp32."""
-    torch.manual_seed(11)
-    V = 25
-    A = torch.tensor(pkg.Graph(**pkg.PKU_MMD).A, dtype=torch.float32)
-    A = A * (1 + 0.1 * torch.randn(A.shape)) * (A != 0)
-    P = A.shape[0]
-    W = torch.randn(P * cout, cin) / cin ** 0.5
-    b = torch.randn(P * cout)
-    x = torch.randn(N, cin, T, V)
-    y = F.conv2d(x, W.view(P * cout, cin, 1, 1), b).view(N, P, cout, T, V)
-    ref = torch.einsum("npctv,pvw->nctw", y, A)
-    sup = K.GraphSupport(A.to(DEV))
-    A32 = A.to(DEV).contiguous()
-    wimg, cp, kw = K.pack_gcn_weight(W.view(P, cout, cin).permute(1, 0, 2).reshape(cout, P * cin).to(DEV), torch.bfloat16)
-    bias2d = K.gcn_bias(A32, b.to(DEV), N, cout)
-    st = torch.zeros((K.gcn_tile_row_blocks(N * T, V, cout), cp, 4), device=DEV)
-    g = K.gcn_tile(cl(x, torch.bfloat16), A32, wimg, kw, cin, cout, cp, sup, bias=bias2d, stats=st)
-    assert_close(g.float(), ref, 2e-2, "gcn_tile fwd")
-    mr, _, _ = K.bn_finalize(st, st.shape[0], cp, cout, None, None)
-    gr = g.float().cpu()
-    assert_close(mr[:, 0].cpu(), gr.mean(dim=(0, 2, 3)), 2e-3, "bn mean")
-    assert_close(mr[:, 1].cpu(), 1 / torch.sqrt(gr.var(dim=(0, 2, 3), unbiased=False) + 1e-5), 2e-3, "bn rstd")
-    # data grad: dx = autograd of the reference forward
-    xr = x.clone().requires_grad_(True)
-    yr = torch.einsum("npctv,pvw->nctw", F.conv2d(xr, W.view(P * cout, cin, 1, 1), b).view(N, P, cout, T, V), A)
-    dg = torch.randn(yr.shape)
-    yr.backward(dg)
-    wT, cq, kwT = K.pack_gcn_weight(W.view(P, cout, cin).permute(2, 0, 1).reshape(cin, P * cout).to(DEV), torch.bfloat16)
-    dx = K.gcn_tile(cl(dg, torch.bfloat16), A32, wT, kwT, cout, cin, cq, sup, trans_a=True)
-    assert_close(dx.float(), xr.grad, 2e-2, "gcn_tile dgrad")
-
-
 @pytest.mark.parametrize("Cin,Nout", [(64, 96), (128, 192), (256, 384), (16, 8)])
 def test_attn_proj(K, Cin, Nout):
     """stgcn_attn_proj: fp32 theta/phi from a bf16 activation with the weight split into two bf16 parts:

@@ -65,7 +65,7 @@ for name, N, T, V, Cin, Cout, Kt, s, trans, pro in cases:
 
 # the 64-channel temporal conv kernels outside conv_rows: tconv_frame (forward with the BN1 prologue, bias and
 # BN partials; data grad) and layer_fused's g-input mode
-for name in ("tf_fwd_c64", "tf_dgrad_c64", "tcn_gin_c64"):
+for name in ("tf_fwd_c64", "tf_dgrad_c64"):
     if only and name != only:
         continue
     N, T, V, C = 64, 300, 25, 64
@@ -79,11 +79,8 @@ for name in ("tf_fwd_c64", "tf_dgrad_c64", "tcn_gin_c64"):
     if name == "tf_fwd_c64":
         st = torch.zeros((K.tconv_frame_row_blocks(N, T), cp, 4), device=dev)
         f = lambda: K.tconv_frame(x, wp, cp, kp, bias=b, pro_a=sc, pro_b=sh, stats=st)
-    elif trans:
-        f = lambda: K.tconv_frame(x, wp, cp, kp, trans=True)
     else:
-        st = torch.zeros((K.layer_fused_row_blocks(N, T), C, 4), device=dev)
-        f = lambda: K.layer_tcn(x, sc, sh, wp, b, st)
+        f = lambda: K.tconv_frame(x, wp, cp, kp, trans=True)
     ms = timeit(f)
     flops = 2.0 * N * T * V * C * C * 9
     print(f"{name:16s} {ms*1e3:9.1f} us  {flops/ms/1e9:8.1f} TFLOP/s  {4*N*T*V*C/ms/1e6:8.1f} GB/s", flush=True)
@@ -140,22 +137,3 @@ for name, N, T, Cin, Cout in gcases:
     ms = timeit(lambda: K.gconv_wgrad(x, dg, sup, Cin, Cout))
     print(f"{name.replace('fwd', 'wgrad'):22s} {ms*1e3:9.1f} us  {flops/ms/1e9:8.1f} TFLOP/s", flush=True)
 
-# fused frame-tiled graph conv (gcn_tile.hip): same shapes, forward (+bias, stats) and data grad
-for name, N, T, Cin, Cout in gcases:
-    if only and not name.startswith(only.replace("gconv", "gcn_tile")) and not name.startswith(only):
-        continue
-    Pp, V = A0.shape[0], A0.shape[-1]
-    W = torch.randn(Pp * Cout, Cin, device=dev) / Cin ** 0.5
-    x = torch.randn(N, Cin, T, V, device=dev).to(dt).contiguous(memory_format=torch.channels_last)
-    dg = torch.randn(N, Cout, T, V, device=dev).to(dt).contiguous(memory_format=torch.channels_last)
-    wimg, cp, kw = K.pack_gcn_weight(W.view(Pp, Cout, Cin).permute(1, 0, 2).reshape(Cout, Pp * Cin), dt)
-    wT, cq, kwT = K.pack_gcn_weight(W.view(Pp, Cout, Cin).permute(2, 0, 1).reshape(Cin, Pp * Cout), dt)
-    b2 = K.gcn_bias(A0, torch.randn(Pp * Cout, device=dev), N, Cout)
-    st = torch.zeros((K.gcn_tile_row_blocks(N * T, V, Cout), cp, 4), device=dev)
-    flops = 2.0 * N * T * V * Pp * Cin * Cout
-    byts = (N * T * V * (Cin + Cout)) * 2
-    for tag, f in (("", lambda: K.gcn_tile(x, A0, wimg, kw, Cin, Cout, cp, sup, bias=b2, stats=st)),
-                   ("_dgrad", lambda: K.gcn_tile(dg, A0, wT, kwT, Cout, Cin, cq, sup, trans_a=True))):
-        ms = timeit(f)
-        print(f"{name.replace('gconv', 'gcn_tile') + tag:22s} {ms*1e3:9.1f} us  {flops/ms/1e9:8.1f} TFLOP/s  "
-              f"{byts/ms/1e6:8.1f} GB/s", flush=True)

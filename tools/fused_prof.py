@@ -1,5 +1,5 @@
 """Per-wave cycle accounts of the fused layer kernel (a -DSTGCN_FUSED_DBG=1024 build, pointed at by STGCN_LIB):
-runs the north_star layer's BatchNorm fused forward a few times, reads g_fused_prof and prints, per role, the
+runs the north_star layer's LayerNorm fused forward a few times, reads g_fused_prof and prints, per role, the
 mean cycles per block spent in each phase (GCN: DMA wait, compute, barrier; TCN: k-loop, epilogue, barrier).
 
     STGCN_LIB=$PWD/realtime-st-gcn_amd/lib_p/libstgcn_amd.so python tools/fused_prof.py
@@ -18,7 +18,7 @@ import bench  # noqa: E402
 if __name__ == "__main__":
     pkg = ge.load_package()
     dev = torch.device("cuda", 0)
-    norm = sys.argv[1] if len(sys.argv) > 1 else "BatchNorm"
+    norm = "LayerNorm"
     bench.layer_roofline(pkg, dev, reps=3, norm=norm)
     torch.cuda.synchronize()
     lib = pkg._lib.lib()
