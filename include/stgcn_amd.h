@@ -28,8 +28,9 @@ extern "C" {
  * refuses a library whose stgcn_abi_version() differs from the version it was written against.
  *   1: rounds 1-4;  2: round 5 (stgcn_gconv_desc gained res / res_bits / res_ld);
  *   3: round 6 (stgcn_gcn_tile removed; stgcn_layer_fused_desc is the LayerNorm layer only: the BatchNorm
- *      fields n1_scale / n1_shift / stats / ln / g_in / g_in_ld and stgcn_layer_fused_row_blocks removed). */
-#define STGCN_ABI_VERSION 3
+ *      fields n1_scale / n1_shift / stats / ln / g_in / g_in_ld and stgcn_layer_fused_row_blocks removed);
+ *   4: round 6 (stgcn_rt_frame + stgcn_rt_layer / stgcn_rt_frame_desc: the RT per-frame step in one launch). */
+#define STGCN_ABI_VERSION 4
 
 /* Implicit-GEMM (Kt x 1) row convolution; see conv_rows.hip for the exact contract.
  * Replaces: nn.Conv2d tcn.2 (models/stgcn/stgcn.py:154-159), residual.0 (stgcn.py:165-170),
@@ -418,6 +419,50 @@ int stgcn_rt_frame_norm(const float* a, const float* ln_w, const float* ln_b, in
                         const float* lnr_w, const float* lnr_b, int V, int C, int* idx, int fifo_size, int S, float* y,
                         void* stream);
 int stgcn_rt_frame_out(const float* x, int V, int C, const float* w, const float* b, int K, float* out, void* stream);
+
+/* The whole per-frame step of a LayerNorm RT-ST-GCN (Model.forward after prepare_benchmark, rtstgcn.py:130-153
+ * with every OnlineLayer, rtstgcn.py:528-553 + 591-627) as ONE persistent launch (rt_fused.hip): stgcn_rt_frame_in,
+ * then per layer stgcn_rt_frame_gcn's arithmetic spread over `blocks` workgroups (channel pairs), an in-launch grid
+ * barrier (agent-scope release / acquire on a counter), stgcn_rt_frame_norm's arithmetic redundantly in every
+ * workgroup (the next layer's input stays in LDS), the FIFO indices advanced, and stgcn_rt_frame_out.  Same math as
+ * the four entry points above (LN sums in another fixed order).  Per layer: a_buf / r_buf [V][Cout] device scratch
+ * (r_buf only when res_mode == 2), wr NULL unless res_mode == 2; lnr_w / lnr_b only for res_mode 2.
+ * sync: 16 device bytes, zeroed by this call (a memset on the stream ahead of the launch) — the barrier counter;
+ * status: a device int the kernel sets to 1 if a barrier wait gave up (bounded spin; never reset here).
+ * Workgroups of 1024 threads; the hand-off of a / r between workgroups is write-through (sc1) stores and loads.
+ * V <= 32, 4 <= C <= 256 (C % 4 == 0), V * C <= 7680, P <= 3, L <= STGCN_RT_MAX_LAYERS, blocks in [1, 256] (0 = 64). */
+#define STGCN_RT_MAX_LAYERS 12
+typedef struct {
+  int Cin, Cout, P, fifo_size, S, res_mode;
+  const float* A;       /* [P][V][V] graph * importance */
+  const float* w;       /* [P*Cout][Cin] */
+  const float* bias2d;  /* [V][Cout] or NULL */
+  const float* wr;      /* [Cout][Cin] residual conv (res_mode 2) or NULL */
+  const float* ln_w;    /* [V][Cout]: the LayerNorm([Cout,1,V]) affine in the rows' layout (transposed) */
+  const float* ln_b;
+  const float* lnr_w;   /* residual LN (res_mode 2), [V][Cout] */
+  const float* lnr_b;
+  float* fifo;          /* [fifo_size][V][Cout] */
+  float* acc;           /* [S][V][Cout] */
+  int* idx;             /* int[2] (fifo, acc) */
+  float* a_buf;         /* [V][Cout] hand-off scratch */
+  float* r_buf;         /* [V][Cout] (res_mode 2) */
+} stgcn_rt_layer;
+typedef struct {
+  int V, L, C0, K, blocks;
+  const float* x;       /* (1,3,1,V) frame, element c*V+v */
+  const float* ln_w;    /* [3*V] */
+  const float* ln_b;
+  const float* w_in;    /* [C0][3] */
+  const float* b_in;    /* [C0] */
+  const float* w_out;   /* [K][C_last] */
+  const float* b_out;   /* [K] or NULL */
+  float* out;           /* [K] */
+  unsigned* sync;       /* 16 B, zeroed per call */
+  int* status;
+  stgcn_rt_layer layers[STGCN_RT_MAX_LAYERS];
+} stgcn_rt_frame_desc;
+int stgcn_rt_frame(const stgcn_rt_frame_desc* d, void* stream);
 
 /* Window staging (window.hip): the first activation of a batch of sliding windows
  * (WindowSegment, utils/segment_generator.py:132-145) computed from the padded capture without forming the

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("STGCN_LIB") or os.path.join(_HERE, "lib", "libstgcn_amd.so")  # STGCN_LIB: A/B builds
 
 # the STGCN_ABI_VERSION of include/stgcn_amd.h these bindings mirror (test_cpu_host checks the two agree)
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _ERR = {1: "bad shape/arguments", 2: "unsupported dtype", 3: "HIP launch error"}
 
@@ -84,6 +84,22 @@ class PrepJob(ctypes.Structure):
                [(n, c_void_p) for n in ("src", "dst", "dst_frag", "A", "M", "nbr", "deg")] + \
                [(n, c_int) for n in ("P", "V", "J", "R_pad", "C_pad", "pad_")] + \
                [(n, c_void_p) for n in ("bconv", "bias2d")]
+
+
+RT_MAX_LAYERS = 12  # STGCN_RT_MAX_LAYERS
+
+
+class RtLayer(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in ("Cin", "Cout", "P", "fifo_size", "S", "res_mode")] + \
+               [(n, c_void_p) for n in ("A", "w", "bias2d", "wr", "ln_w", "ln_b", "lnr_w", "lnr_b", "fifo", "acc",
+                                        "idx", "a_buf", "r_buf")]
+
+
+class RtFrameDesc(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in ("V", "L", "C0", "K", "blocks")] + \
+               [(n, c_void_p) for n in ("x", "ln_w", "ln_b", "w_in", "b_in", "w_out", "b_out", "out", "sync",
+                                        "status")] + \
+               [("layers", RtLayer * RT_MAX_LAYERS)]
 
 
 # name -> (restype, argtypes)
@@ -164,6 +180,7 @@ _SIGS = {
     "stgcn_rt_frame_norm": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int,
                                     c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "stgcn_rt_frame_out": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "stgcn_rt_frame": (c_int, [ctypes.POINTER(RtFrameDesc), c_void_p]),
     "stgcn_window_stat_blocks": (c_int, [c_int, c_int]),
     "stgcn_window_stats": (c_int, [c_void_p] + [c_int] * 7 + [c_float, c_void_p, c_void_p]),
     "stgcn_window_expand": (c_int, [c_void_p] + [c_int] * 7 + [c_void_p] * 5 + [c_int, c_void_p, c_int, c_int,

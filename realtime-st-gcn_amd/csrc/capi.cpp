@@ -107,6 +107,7 @@ int rt_gcn_launch(const float* x, int V, int Cin, int Cout, int P, const float* 
 int rt_norm_launch(const float* a, const float* g, const float* b, int res_mode, const float* res, const float* gr,
                    const float* br, int V, int C, int* idx, int fifo_size, int S, float* y, hipStream_t s);
 int rt_out_launch(const float* x, int V, int C, const float* W, const float* bias, int K, float* out, hipStream_t s);
+int rt_frame_launch(const stgcn_rt_frame_desc& d, hipStream_t s);
 int window_stat_blocks_launch(int nw, int W);
 int window_stats_launch(const float* x, int Cin, int Lp, int V, int W, int n0, int nw, int mode, float eps, float* out,
                         hipStream_t s);
@@ -435,6 +436,9 @@ int stgcn_rt_frame_norm(const float* a, const float* ln_w, const float* ln_b, in
 }
 int stgcn_rt_frame_out(const float* x, int V, int C, const float* w, const float* b, int K, float* out, void* stream) {
   return rt_out_launch(x, V, C, w, b, K, out, STREAM(stream));
+}
+int stgcn_rt_frame(const stgcn_rt_frame_desc* d, void* stream) {
+  return d ? rt_frame_launch(*d, STREAM(stream)) : STGCN_EBADSHAPE;
 }
 
 int stgcn_window_stat_blocks(int nw, int W) { return window_stat_blocks_launch(nw, W); }

@@ -8,6 +8,8 @@ HIP stream; all arithmetic happens in the HIP kernels.
 from __future__ import annotations
 
 
+import ctypes
+
 import torch
 
 from . import _lib as L
@@ -1001,6 +1003,16 @@ def rt_frame_out(x, w, b):
     out = torch.empty((1, K, 1), dtype=torch.float32, device=x.device)
     L.check(L.lib().stgcn_rt_frame_out(x.data_ptr(), V, C, _f32c(w).data_ptr(), L.ptr(None if b is None else _f32c(b)),
                                        K, out.data_ptr(), L.stream()), "rt_frame_out")
+    return out
+
+
+def rt_frame(desc, x, out):
+    """The whole RT per-frame step in one launch (stgcn_rt_frame): x (1, 3, 1, V) -> out (1, K, 1); ``desc`` is
+    the model's stgcn_rt_frame_desc (rtstgcn.Model._build_frame_desc) with x / out filled in here."""
+    L.require_device(x)
+    x = _f32c(x)
+    desc.x, desc.out = x.data_ptr(), out.data_ptr()
+    L.check(L.lib().stgcn_rt_frame(ctypes.byref(desc), L.stream()), "rt_frame")
     return out
 
 

@@ -15,6 +15,9 @@ also assign the attributes directly.
                                               interleaved runs; round 4: 8.86 vs 8.77)
     bn_mask_bits        STGCN_BN_BITS=0       the BatchNorm-2 backward reads the forward output's sign bits (written by bn_apply)
                                               for its ReLU mask instead of the output itself (default on)
+    rt_one_launch       STGCN_RT_ONE_LAUNCH=0 per-frame RT-ST-GCN inference (LayerNorm, config 3) as ONE persistent launch with
+                                              in-launch grid barriers (stgcn_rt_frame) instead of 2 launches per layer
+                                              (default on)
     prep_plan           STGCN_PREP_PLAN=0     stgcn.Model training forwards pack every weight per call instead of
                                               in the one-launch plan (native.PrepPlan; default on)
 
@@ -36,6 +39,7 @@ class _Routing:
         self.fused_ln_train = e("STGCN_FUSED_LN_TRAIN", "1") != "0"
         self.bn_mask_bits = e("STGCN_BN_BITS", "1") != "0"
         self.prep_plan = e("STGCN_PREP_PLAN", "1") != "0"
+        self.rt_one_launch = e("STGCN_RT_ONE_LAUNCH", "1") != "0"
 
 
 ROUTING = _Routing()

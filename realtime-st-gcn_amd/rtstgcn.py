@@ -21,6 +21,7 @@ import torch.nn.functional as F
 
 from . import layer_fn as LF
 from . import native as K
+from .routing import ROUTING
 from .graph import Graph
 from .modules import BatchNorm1d, LayerNorm, make_norm, resolve_dtype
 from .stgcn import IN_PAD
@@ -247,6 +248,9 @@ class Model(nn.Module):
     def forward(self, x):
         if (self.online and self.normalization == "LayerNorm" and x.dim() == 4 and x.shape[0] == 1
                 and x.shape[2] == 1 and x.shape[1] == 3 and not torch.is_grad_enabled()):
+            if ROUTING.rt_one_launch and self._frame_desc_ok():
+                # the whole frame as ONE persistent launch (rt_fused.hip rt_frame_kernel)
+                return self._rt_frame(x)
             # per-frame inference: fused input head, two launches per layer, fused output head (rt_fused.hip)
             y = K.rt_frame_in(x, LF._flat_ln(self.norm_in.weight), LF._flat_ln(self.norm_in.bias),
                               self.fcn_in.weight.detach().reshape(self.fcn_in.out_channels, -1),
@@ -269,6 +273,86 @@ class Model(nn.Module):
         x = LF.PoolFunction.apply(x, dt, True)
         x = LF.Conv1x1Function.apply(x, self.fcn_out.weight, self.fcn_out.bias, dt)
         return x.squeeze(-1).float()
+
+    def _frame_desc_ok(self):
+        """Shapes the one-launch frame kernel takes (stgcn_rt_frame): LayerNorm online layers, C % 4 == 0, C <= 256,
+        V <= 32, V * C <= 7680, P <= 3, at most 12 layers."""
+        V = self.A.shape[-1]
+        if not (2 <= V <= 32 and len(self.st_gcn) <= K.L.RT_MAX_LAYERS and self.fcn_in.out_channels % 4 == 0):
+            return False
+        for l in self.st_gcn:
+            if not isinstance(l, OnlineLayer) or l.normalization != "LayerNorm" or l.aggregate.A.shape[0] > 3:
+                return False
+            C = l.aggregate.out_channels
+            if l.conv.in_channels % 4 or C % 4 or C > 256 or V * C > 7680:
+                return False
+        return True
+
+    def _frame_key(self):
+        """Key of the frame descriptor: data pointers and in-place versions of every parameter it reads (copies of
+        them live in the descriptor), data pointers only of the FIFO state (the kernel updates it in place, and
+        reset_state's zeroing must not rebuild the descriptor)."""
+        ts = [self.norm_in.weight, self.norm_in.bias, self.fcn_in.weight, self.fcn_in.bias, self.fcn_out.weight,
+              self.fcn_out.bias]
+        st = []
+        for l in self.st_gcn:
+            ts += [l.aggregate.A, l.conv.weight, l.conv.bias, l.bn_relu[0].weight, l.bn_relu[0].bias]
+            st += [l.aggregate.fifo, l.aggregate.accumulator, l.aggregate.idx]
+            if l.is_residual_conv:
+                ts += [l.residual[0].weight, l.residual[1].weight, l.residual[1].bias]
+        return tuple((t.data_ptr(), t._version) for t in ts) + tuple(t.data_ptr() for t in st)
+
+    def _rt_frame(self, x):
+        key = self._frame_key()
+        pk = getattr(self, "_frame_pack", None)
+        if pk is None or pk[0] != key:
+            pk = (key, self._build_frame_desc())
+            self._frame_pack = pk
+        desc, _keep = pk[1]
+        out = torch.empty((1, self.fcn_out.out_channels, 1), dtype=torch.float32, device=x.device)
+        return K.rt_frame(desc, x, out)
+
+    def _build_frame_desc(self):
+        """stgcn_rt_frame_desc of this model (K.L.RtFrameDesc) + the tensors it points to (kept alive with it)."""
+        V = self.A.shape[-1]
+        dev = self.A.device
+        keep = []
+
+        def p(t):
+            keep.append(t)
+            return t.data_ptr()
+
+        d = K.L.RtFrameDesc()
+        d.V, d.L, d.C0, d.K, d.blocks = V, len(self.st_gcn), self.fcn_in.out_channels, self.fcn_out.out_channels, 0
+        d.ln_w, d.ln_b = p(LF._flat_ln(self.norm_in.weight)), p(LF._flat_ln(self.norm_in.bias))
+        d.w_in = p(self.fcn_in.weight.detach().float().reshape(self.fcn_in.out_channels, -1).contiguous())
+        d.b_in = p(self.fcn_in.bias.detach().float().contiguous())
+        d.w_out = p(self.fcn_out.weight.detach().float().reshape(self.fcn_out.out_channels, -1).contiguous())
+        d.b_out = p(self.fcn_out.bias.detach().float().contiguous())
+        d.sync = p(torch.zeros(4, dtype=torch.int32, device=dev))
+        self._frame_status = torch.zeros(1, dtype=torch.int32, device=dev)
+        d.status = p(self._frame_status)
+        for i, l in enumerate(self.st_gcn):
+            ag = l.aggregate
+            Cin, Cout = l.conv.in_channels, ag.out_channels
+            A32, _, _, _, bias2d, _ = l._weights(Cin)
+            y = d.layers[i]
+            y.Cin, y.Cout, y.P, y.fifo_size, y.S = Cin, Cout, ag.A.shape[0], ag.fifo_size, ag.stride
+            y.res_mode = 2 if l.is_residual_conv else (1 if l.is_residual else 0)
+            y.A, y.w, y.bias2d = p(A32), p(l.conv.weight.detach().float().contiguous()), p(bias2d)
+            n = l.bn_relu[0]
+
+            def rows(t):  # LayerNorm([C,1,V]) affine (C,1,V) -> the rows' [V][C] layout
+                return t.detach().float().reshape(Cout, V).t().contiguous()
+
+            y.ln_w, y.ln_b = p(rows(n.weight)), p(rows(n.bias))
+            y.fifo, y.acc, y.idx = p(ag.fifo), p(ag.accumulator), p(ag.idx)
+            y.a_buf = p(torch.empty(V * Cout, dtype=torch.float32, device=dev))
+            if l.is_residual_conv:
+                y.wr = p(l.residual[0].weight.detach().float().reshape(Cout, Cin).contiguous())
+                y.lnr_w, y.lnr_b = p(rows(l.residual[1].weight)), p(rows(l.residual[1].bias))
+                y.r_buf = p(torch.empty(V * Cout, dtype=torch.float32, device=dev))
+        return d, keep
 
     def _swap_layers_for_inference(self):
         """Replace OfflineLayers by OnlineLayers carrying the same parameters (rtstgcn.py:160-187)."""

@@ -249,6 +249,6 @@ def test_descriptor_layouts_match_header(pkg, tmp_path):
                "stgcn_gconv_desc": L.GconvDesc,
                "stgcn_gconv_wgrad_desc": L.GconvWgradDesc, "stgcn_bn_bwd_desc": L.BnBwdDesc,
                "stgcn_layer_fused_desc": L.LayerFusedDesc, "stgcn_prep_job": L.PrepJob,
-               "stgcn_adam_entry": L.AdamEntry}
+               "stgcn_adam_entry": L.AdamEntry, "stgcn_rt_layer": L.RtLayer, "stgcn_rt_frame_desc": L.RtFrameDesc}
     got, expect = _c_layout(tmp_path, structs)
     assert got == expect

@@ -19,6 +19,25 @@ def P(pkg):
     return pkg
 
 
+@pytest.fixture(params=["one_launch", "per_layer"])
+def rt_route(request, pkg):
+    """Both per-frame routes: the whole frame as one persistent launch (stgcn_rt_frame, default) and the
+    two-launches-per-layer form (routing.rt_one_launch off)."""
+    R = pkg.routing.ROUTING
+    prev = R.rt_one_launch
+    R.rt_one_launch = request.param == "one_launch"
+    yield request.param
+    R.rt_one_launch = prev
+
+
+def _frame_status_ok(m, route):
+    """The one-launch kernel's barrier never gave up (its bounded spin sets the status word)."""
+    if route == "one_launch":
+        st = getattr(m, "_frame_status", None)
+        assert st is not None, "the one-launch route did not run"
+        assert int(st.item()) == 0, "stgcn_rt_frame: a grid-barrier wait gave up"
+
+
 @pytest.mark.parametrize("case", ["stride1", "ref_strides"])
 def test_rt_offline_golden(P, case):
     d = load_golden("rt_" + case)
@@ -37,7 +56,7 @@ def test_rt_offline_golden(P, case):
 
 
 @pytest.mark.parametrize("case", ["stride1", "ref_strides"])
-def test_rt_online_golden(P, case):
+def test_rt_online_golden(P, case, rt_route):
     d = load_golden("rt_" + case)
     m = P.MODELS["rt-st-gcn"](rank=None, **d["arch"])
     m.load_state_dict(sub(d, "sd/"), strict=True)
@@ -53,6 +72,7 @@ def test_rt_online_golden(P, case):
     with torch.no_grad():
         y2 = torch.cat([m(x[:, :, i:i + 1]) for i in range(x.shape[2])], dim=2)
     assert_close(y2, y, 1e-6, "online after reset")
+    _frame_status_ok(m, rt_route)
 
 
 CONFIG3_LAYERS = {"layers": 9, "kernel": 9, "in_ch": [64, 64, 64, 64, 128, 128, 128, 256, 256],
@@ -61,7 +81,7 @@ CONFIG3_LAYERS = {"layers": 9, "kernel": 9, "in_ch": [64, 64, 64, 64, 128, 128, 
 
 
 @pytest.mark.parametrize("strides", [[1] * 9, [1, 1, 1, 2, 1, 1, 2, 1, 1]], ids=["stride1", "ref_strides"])
-def test_rt_online_config3_widths(P, strides):
+def test_rt_online_config3_widths(P, strides, rt_route):
     """Config 3 at its own widths (config/pku-mmd/ln/rtstgcn_local.json: LayerNorm, K = 9, 64 -> 256 channels,
     V*C up to 6 400): the per-frame kernels (rt_fused.hip; rt_norm's several values per thread, rt_gcn at
     Cin 64-256) over 48 frames (> every FIFO: 17 frames at stride 2), eager and replayed as a HIP graph, vs
@@ -92,7 +112,7 @@ def test_rt_online_config3_widths(P, strides):
     with torch.no_grad():
         y = torch.cat([m(xd[:, :, i:i + 1]) for i in range(F_)], dim=2)
     torch.cuda.synchronize()
-    assert_close(y, ref, TOL, f"config-3 online eager {strides}")
+    assert_close(y, ref, TOL, f"config-3 online eager {strides} {rt_route}")
     # the same stream replayed as a HIP graph of one per-frame step (FIFO state on the device)
     m.reset_state()
     x_static = torch.zeros_like(xd[:, :, :1])
@@ -115,4 +135,38 @@ def test_rt_online_config3_widths(P, strides):
             graph.replay()
             outs.append(y_static.clone())
     torch.cuda.synchronize()
-    assert_close(torch.cat(outs, dim=2), ref, TOL, f"config-3 online graph {strides}")
+    assert_close(torch.cat(outs, dim=2), ref, TOL, f"config-3 online graph {strides} {rt_route}")
+    _frame_status_ok(m, rt_route)
+
+
+@pytest.mark.parametrize("blocks", [1, 3, 64, 200])
+def test_rt_frame_block_counts(P, blocks):
+    """stgcn_rt_frame at several workgroup counts (1: no cross-workgroup hand-off at all; 3: several channel pairs
+    per workgroup; 200: idle workgroups that only take part in the barriers) gives the same frames as the
+    two-launches-per-layer route, over 12 frames of config 3's widths (the FIFOs wrap), at fp32 rounding."""
+    R = P.routing.ROUTING
+    arch = {"strategy": "spatial", "in_feat": 3, "stages": 1, "kernel": 9, "output_type": "logits",
+            "normalization": "LayerNorm", "segment": 500, "num_classes": 52,
+            "rt-st-gcn": dict(CONFIG3_LAYERS, stride=[1, 1, 1, 2, 1, 1, 2, 1, 1]), "graph": P.PKU_MMD}
+    torch.manual_seed(5)
+    m = P.MODELS["rt-st-gcn"](rank=None, **arch).to(DEV).eval()
+    m.prepare_benchmark(arch)
+    x = torch.randn(1, 3, 12, 25, device=DEV)
+    prev = R.rt_one_launch
+    try:
+        R.rt_one_launch = False
+        with torch.no_grad():
+            ref = torch.cat([m(x[:, :, i:i + 1]) for i in range(12)], dim=2)
+        m.reset_state()
+        R.rt_one_launch = True
+        m._frame_pack = None
+        with torch.no_grad():
+            m(x[:, :, :1])  # builds the descriptor
+            m.reset_state()
+            m._frame_pack[1][0].blocks = blocks
+            y = torch.cat([m(x[:, :, i:i + 1]) for i in range(12)], dim=2)
+    finally:
+        R.rt_one_launch = prev
+    torch.cuda.synchronize()
+    assert int(m._frame_status.item()) == 0
+    assert_close(y, ref, 1e-4, f"rt_frame blocks={blocks}")

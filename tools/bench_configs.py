@@ -50,6 +50,50 @@ def config3(P, dev, frames):
     m.prepare_benchmark(RT_ARCH)
     gen = torch.Generator(device=dev).manual_seed(3)
     stream = torch.randn(frames + 64, 1, 3, 1, 25, device=dev, generator=gen)
+    R = P.routing.ROUTING
+    prev = R.rt_one_launch
+    try:
+        R.rt_one_launch = False
+        per_layer = _config3_route(m, stream, frames)
+        R.rt_one_launch = True
+        out = _config3_route(m, stream, frames)
+    finally:
+        R.rt_one_launch = prev
+    out["per_layer_route"] = per_layer
+    # workgroup count of the one-launch kernel: device time of 200 graph replays per count
+    sweep = {}
+    with torch.no_grad():
+        for G in (16, 32, 64, 128, 256):
+            m.reset_state()
+            x_static = stream[0].clone()
+            m(x_static)
+            m._frame_pack[1][0].blocks = G
+            g = torch.cuda.CUDAGraph()
+            s_ = torch.cuda.Stream()
+            s_.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s_):
+                with torch.cuda.graph(g):
+                    m(x_static)
+            torch.cuda.current_stream().wait_stream(s_)
+            for _ in range(20):
+                g.replay()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(200):
+                g.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            sweep[G] = round(e0.elapsed_time(e1) / 200, 4)
+            assert int(m._frame_status.item()) == 0
+        m._frame_pack[1][0].blocks = 0
+    out["one_launch_blocks_device_ms"] = sweep
+    return {"config": "3: rt-st-gcn online (ln/rtstgcn_local.json, LN, K=9, 9 layers), 1 frame (1,3,1,25)",
+            "metric": "per-frame latency", "unit": "ms", "frames": frames, "dtype": "fp32",
+            "route": "one persistent launch per frame (stgcn_rt_frame); per_layer_route: 2 launches per layer",
+            "reference_cpu": "2.7 ms/frame (SURVEY §8(a12), 9 layers)", **out}
+
+
+def _config3_route(m, stream, frames):
     out = {}
     with torch.no_grad():
         # eager: every kernel launched from Python per frame
@@ -93,9 +137,15 @@ def config3(P, dev, frames):
         warm = lat[32:]
         out["graph"] = {"p50_ms": round(1e3 * pct(warm, 0.5), 4), "p99_ms": round(1e3 * pct(warm, 0.99), 4),
                         "max_rel_diff_vs_eager": err}
-    return {"config": "3: rt-st-gcn online (ln/rtstgcn_local.json, LN, K=9, 9 layers), 1 frame (1,3,1,25)",
-            "metric": "per-frame latency", "unit": "ms", "frames": frames, "dtype": "fp32",
-            "reference_cpu": "2.7 ms/frame (SURVEY §8(a12), 9 layers)", **out}
+        # device time of one frame: HIP events around 200 back-to-back replays
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for i in range(200):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        out["graph"]["device_ms_per_frame"] = round(e0.elapsed_time(e1) / 200, 4)
+    return out
 
 
 def config5(P, dev, steps, warmup):
