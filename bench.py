@@ -84,9 +84,15 @@ def spawn_ranks(args):
     return subprocess.call(cmd)
 
 
-# The roofline kernel: conv_wide_kernel<128,9,8,1,0,64>, the Kt=9 stride-1 temporal-conv forward of the
-# C=128 (T=150) and C=256 (T=75) layers — the dominant kernel template of the step (with its data-grad
-# twin <128,9,8,0>), 4 launches per step.  Algorithmic work per launch = 2*N*T*V*C*C*Kt.
+# The roofline kernel (`roofline`): the step's largest kernel by time in the rocprofv3 summary,
+# gconv_wgrad3_kernel — the graph-conv weight gradient dWeff[w][j] = dy[:, w]^T x[:, S(w)_j] (gconv.hip), 8
+# launches per step (64->64 x3, 128->128 x2, 256->256 x2, 128->256 x1; the 64->128 layer runs gconv_wgrad2).  Its C-ABI
+# call is split (stgcn_gconv_wgrad_desc.phase) so HIP events bracket the kernel alone, not its slab reduction.
+# Algorithmic work per launch: 2*N*T*nnz(S)*Cin*Cout flops over (x + dy) = N*T*V*(Cin+Cout)*2 bytes; the bound is the
+# roof the launches' aggregate intensity falls under (HBM: ~228 flop/B < the ~312 ridge).
+ROOF_KERNEL = "gconv_wgrad3"
+# Secondary (`roofline_tcn_fwd`): conv_wide_kernel<128,9,8,1,0,64>, the Kt=9 stride-1 temporal-conv forward of the
+# C=128 (T=150) and C=256 (T=75) layers, 4 launches per step.  Algorithmic work per launch = 2*N*T*V*C*C*Kt.
 ROOF_TAGS = {"tcn_fwd_c128": 2.0 * N_BATCH * (T_LEN // 2) * V_J * 128 * 128 * 9,
              "tcn_fwd_c256": 2.0 * N_BATCH * (T_LEN // 4) * V_J * 256 * 256 * 9}
 
@@ -189,6 +195,51 @@ def layer_roofline(pkg, dev, reps=20, norm="LayerNorm"):
 
 
 RIDGE_FLOP_PER_BYTE = BF16_DENSE_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)  # ~312 flop/B
+
+
+def gwgrad_roofline(gw, world):
+    """`roofline` of the dominant kernel (ROOF_KERNEL) from its live HIP-event pairs: (tag, ms, work) per launch,
+    work = {"flop", "bytes", "shape"} (algorithmic).  Bound = the roof the aggregate intensity falls under; both
+    fractions are reported; traffic = PMC HBM bytes per launch (profiles/pmc_gconv_wgrad3_<shape>.json, the
+    rocprofv3 passes of tools/pmc_kernel.sh) averaged over the timed launches when every shape has one."""
+    ms = sum(t for _, t, _ in gw)
+    flop = sum(w["flop"] for _, _, w in gw)
+    nbytes = sum(w["bytes"] for _, _, w in gw)
+    mfma = flop / nbytes > RIDGE_FLOP_PER_BYTE
+    tf = flop / (ms * 1e-3) / 1e12
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    shapes = {}
+    for _, t, w in gw:
+        d = shapes.setdefault(w["shape"], [0.0, 0, w["flop"], w["bytes"]])
+        d[0] += t
+        d[1] += 1
+    per, traffic = {}, None
+    for sh in shapes:
+        f = os.path.join(ROOT, "profiles", f"pmc_gconv_wgrad3_{sh.replace('->', 'to')}.json")
+        if os.path.exists(f):
+            with open(f) as fh:
+                per[sh] = json.load(fh).get("hbm_bytes_per_launch")
+    if per and all(per.get(w["shape"]) for _, _, w in gw):
+        traffic = sum(per[w["shape"]] for _, _, w in gw) / len(gw)
+    n_steps = max(1, round(len(gw) / 8))
+    by = []
+    for sh, (t, n, fl, nb) in sorted(shapes.items(), key=lambda kv: -kv[1][0]):
+        a_us = 1e3 * t / n
+        m2 = fl / nb > RIDGE_FLOP_PER_BYTE
+        by.append({"shape": sh, "avg_us": round(a_us, 1), "launches_per_step": n / n_steps,
+                   "bound": "mfma" if m2 else "hbm", "flop": fl, "bytes": nb,
+                   "mfma_frac": round(fl / (a_us * 1e-6) / 1e12 / BF16_DENSE_PEAK_TFLOPS, 4),
+                   "hbm_frac": round(nb / (a_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                   "pmc_hbm_bytes": per.get(sh)})
+    return {"kernel": "gconv_wgrad3_kernel (graph-conv weight gradient dWeff = dy^T x per (joint, neighbour) pair, "
+                      "DMA-ring, the step's largest kernel in the rocprofv3 summary; 8 launches/step, bracketed "
+                      "alone by HIP events, its slab reduction outside)",
+            "bound": "mfma" if mfma else "hbm", "achieved": round(tf if mfma else gbs, 2),
+            "peak": BF16_DENSE_PEAK_TFLOPS if mfma else HBM_PEAK_GBS, "unit": "TFLOP/s" if mfma else "GB/s",
+            "frac": round((tf / BF16_DENSE_PEAK_TFLOPS) if mfma else (gbs / HBM_PEAK_GBS), 4),
+            "mfma_frac": round(tf / BF16_DENSE_PEAK_TFLOPS, 4), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
+            "algorithmic_flop_per_launch": round(flop / len(gw)), "algorithmic_bytes_per_launch": round(nbytes / len(gw)),
+            "traffic": traffic, "avg_launch_ms": round(ms / len(gw), 4), "launches_timed": len(gw), "by_shape": by}
 
 
 def kernel_table(K, step, nsteps, top=4):
@@ -374,7 +425,7 @@ def main():
     timing = {"on": False}
 
     def hook(tag, phase, work=None):
-        if tag not in ROOF_TAGS or not timing["on"]:
+        if (tag not in ROOF_TAGS and tag != ROOF_KERNEL) or not timing["on"]:
             return
         ev = torch.cuda.Event(enable_timing=True)
         ev.record(torch.cuda.current_stream())
@@ -475,9 +526,11 @@ def main():
         torch.distributed.all_reduce(t[1:], op=torch.distributed.ReduceOp.SUM)
         elapsed, frames = t[0].item(), t[1].item()
 
-    # (start, end) event pairs of the roofline launches: achieved = their algorithmic flops / their time
-    kt = [(events[i][0], events[i][1].elapsed_time(events[i + 1][1]), events[i][2])
-          for i in range(0, len(events) - 1, 2)]
+    # (start, end) event pairs of the roofline launches: achieved = their algorithmic work / their time
+    pairs = [(events[i][0], events[i][1].elapsed_time(events[i + 1][1]), events[i][2])
+             for i in range(0, len(events) - 1, 2)]
+    kt = [p for p in pairs if p[0] in ROOF_TAGS]
+    gw = [p for p in pairs if p[0] == ROOF_KERNEL]
     k_ms = sum(t for _, t, _ in kt) / len(kt) if kt else float("nan")
     achieved = sum(w for _, _, w in kt) / (sum(t for _, t, _ in kt) * 1e-3) / 1e12 if kt else None
 
@@ -494,6 +547,7 @@ def main():
                     per[g] = json.load(f).get("hbm_bytes_per_launch")
         if kt and all(per.get(g) for g, _, _ in kt) and args.config == 2:
             traffic = sum(per[g] for g, _, _ in kt) / len(kt)
+        roof = gwgrad_roofline(gw, world) if gw and args.config == 2 else None
         lay = world == 1 and not args.no_layer_roofline and args.config == 2
         lroof = layer_roofline(pkg, dev, norm="BatchNorm") if lay else None
         lroof_ln = layer_roofline(pkg, dev, norm="LayerNorm") if lay else None
@@ -518,8 +572,9 @@ def main():
             "config": {"workload": workload, "global_batch": N_BATCH * world, "seq_len": T_LEN, "joints": V_J,
                        "parallelism": f"dp{world}" if world > 1 else "single",
                        "launch": "eager" if not args.graph else "hip-graph replay (fwd+bwd | allreduce | Adam)"},
-            "roofline": {"kernel": "conv_wide_kernel<128,9,8,1,0,64> (persistent warp-specialised Kt=9 stride-1 "
-                                   "temporal conv fwd of the C=128 and C=256 layers, 4 launches/step)",
+            "roofline": roof,
+            "roofline_tcn_fwd": {"kernel": "conv_wide_kernel<128,9,8,1,0,64> (persistent warp-specialised Kt=9 "
+                                           "stride-1 temporal conv fwd of the C=128 and C=256 layers, 4 launches/step)",
                          "bound": "mfma", "achieved": round(achieved, 2) if achieved else None,
                          "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4) if achieved else None,

@@ -29,7 +29,8 @@ extern "C" {
  *   1: rounds 1-4;  2: round 5 (stgcn_gconv_desc gained res / res_bits / res_ld);
  *   3: round 6 (stgcn_gcn_tile removed; stgcn_layer_fused_desc is the LayerNorm layer only: the BatchNorm
  *      fields n1_scale / n1_shift / stats / ln / g_in / g_in_ld and stgcn_layer_fused_row_blocks removed);
- *   4: round 6 (stgcn_rt_frame + stgcn_rt_layer / stgcn_rt_frame_desc: the RT per-frame step in one launch). */
+ *   4: round 6 (stgcn_rt_frame + stgcn_rt_layer / stgcn_rt_frame_desc: the RT per-frame step in one launch;
+ *      stgcn_gconv_wgrad_desc gained phase). */
 #define STGCN_ABI_VERSION 4
 
 /* Implicit-GEMM (Kt x 1) row convolution; see conv_rows.hip for the exact contract.
@@ -184,6 +185,10 @@ typedef struct {
   void* work;
   long work_bytes;
   float* rowsum; /* optional [V][Cout]: rowsum[w][co] = sum_i dy[(i,w)][co] (bias through A), or NULL */
+  int phase;     /* 0: the whole gradient; 1: the accumulation kernel only (row-range partials left in work);
+                  * 2: the slab reduction only (work holds phase 1's partials of the same desc) — so a caller can
+                  * time the accumulation kernel alone; plans without a slab do everything in phase 1 */
+  int pad_;
 } stgcn_gconv_wgrad_desc;
 
 int stgcn_gconv_wgrad(const stgcn_gconv_wgrad_desc* d, int dtype, void* stream);

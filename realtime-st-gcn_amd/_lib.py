@@ -60,7 +60,7 @@ class GconvDesc(ctypes.Structure):
 class GconvWgradDesc(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("dy", c_void_p), ("nbr", c_void_p), ("deg", c_void_p), ("dweff", c_void_p)] + \
                [(n, c_int) for n in ("NT", "V", "J", "Cin", "Cout", "x_ld", "dy_ld")] + \
-               [("work", c_void_p), ("work_bytes", c_long), ("rowsum", c_void_p)]
+               [("work", c_void_p), ("work_bytes", c_long), ("rowsum", c_void_p), ("phase", c_int), ("pad_", c_int)]
 
 
 class LayerFusedDesc(ctypes.Structure):

@@ -926,14 +926,29 @@ DEV void wgrad3_body(const stgcn_gconv_wgrad_desc& a, const WGG& g, char* smem, 
     }
 }
 
+// STGCN_W3_XCD (A/B build flag): row-range-major block order remapped so that consecutive logical blocks share an
+// XCD (all joints of one row range on one XCD: the x rows a joint's neighbours also read stay in that XCD's L2)
+#ifndef STGCN_W3_XCD
+#define STGCN_W3_XCD 0
+#endif
 template <int LDSB>
 __global__ __launch_bounds__(256, LDSB > 80 * 1024 ? 1 : 2) void gconv_wgrad3_kernel(const stgcn_gconv_wgrad_desc a,
                                                                                     const WGG g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int ngrp = g.nco * g.nci;
+#if STGCN_W3_XCD
+  int wgi;
+  {
+    const int id = blockIdx.x, nblk = gridDim.x, x = id & 7, q = nblk >> 3, r = nblk & 7;
+    wgi = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (id >> 3);
+  }
+  const int rr = wgi / (a.V * ngrp), rem = wgi % (a.V * ngrp);
+  const int w = rem / ngrp, grp = rem % ngrp;
+#else
   const int w = blockIdx.x / (ngrp * g.R);
   const int rem = blockIdx.x % (ngrp * g.R);
   const int rr = rem / ngrp, grp = rem % ngrp;
+#endif
   // joints in decreasing-degree order (ties by index): the heaviest blocks are dispatched first and the
   // light ones fill the tail.  Scratch in the ring's first bytes, before any DMA is issued.
   int* sdeg = reinterpret_cast<int*>(smem);
@@ -1377,7 +1392,9 @@ long gconv_wgrad_workspace(const stgcn_gconv_wgrad_desc& a, int dtype) {
 
 int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s) {
   const long E = (long)a.V * a.J * a.Cout * a.Cin;
+  if (a.phase < 0 || a.phase > 2) return STGCN_EBADSHAPE;
   if (dtype != 1) {
+    if (a.phase == 2) return STGCN_OK;  // one kernel, run in phase 1
     hipLaunchKernelGGL(gconv_wgrad_f32_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, a);
     return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
   }
@@ -1402,8 +1419,8 @@ int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s
     auto* k = ring ? (deep ? gconv_wgrad3_kernel<160 * 1024> : gconv_wgrad3_kernel<80 * 1024>) : gconv_wgrad2_kernel<64>;
     if (stgcn_lds_attr((const void*)k, 160 * 1024, s)) return STGCN_EHIP;
     const long blocks = (long)a.V * g.nco * g.nci * g.R;
-    hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(ring ? 256 : cob / 16 * 64), lds, s, a, g);
-    if (direct) return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
+    if (a.phase != 2) hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(ring ? 256 : cob / 16 * 64), lds, s, a, g);
+    if (direct || a.phase == 1) return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
     if (a.rowsum) {  // slab reduction and row sums in one launch
       const long ER = (long)a.V * a.Cout;
       const int nb1 = (int)((E + 255) / 256);
@@ -1423,7 +1440,8 @@ int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s
   if (stgcn_lds_attr((const void*)gconv_wgrad_kernel, 160 * 1024, s)) return STGCN_EHIP;
   const long blocks = (long)a.V * a.J * g.nco * g.nci * g.R;
   const size_t lds = 2 * 4 * WKM * WPR;  // >= the 48 KB cross-wave reduction buffer
-  hipLaunchKernelGGL(gconv_wgrad_kernel, dim3((unsigned)blocks), dim3(256), lds, s, a, g);
+  if (a.phase != 2) hipLaunchKernelGGL(gconv_wgrad_kernel, dim3((unsigned)blocks), dim3(256), lds, s, a, g);
+  if (a.phase == 1) return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
   hipLaunchKernelGGL(gslab_reduce_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, (const float*)g.slab,
                      g.R, E, (long)a.Cout * a.Cin, a.deg, a.J, a.dweff);
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;

@@ -663,10 +663,25 @@ def gconv_wgrad(x, dy, sup, Cin, Cout, rowsum=None):
     if h:
         ktag = _k_start(h, "gconv_wgrad", f"{Cin}->{Cout}", 2.0 * N * T * sup.nnz * Cin * Cout,
                         x.element_size() * N * T * V * (Cin + Cout))
+    hook = EVENT_HOOK
+    if hook and gconv_wgrad3_shape(sup, Cin, Cout, x.dtype):
+        # bench.py's roofline: the accumulation kernel (gconv_wgrad3) bracketed alone, then its slab reduction
+        d.phase = 1
+        hook("gconv_wgrad3", "start", {"flop": 2.0 * N * T * sup.nnz * Cin * Cout,
+                                       "bytes": x.element_size() * N * T * V * (Cin + Cout), "shape": f"{Cin}->{Cout}"})
+        L.check(L.lib().stgcn_gconv_wgrad(d, code, L.stream()), "gconv_wgrad")
+        hook("gconv_wgrad3", "end", None)
+        d.phase = 2
     L.check(L.lib().stgcn_gconv_wgrad(d, code, L.stream()), "gconv_wgrad")
     if h:
         h(ktag, "end", None)
     return dweff
+
+
+def gconv_wgrad3_shape(sup, Cin, Cout, dtype) -> bool:
+    """Whether stgcn_gconv_wgrad runs the DMA-ring kernel gconv_wgrad3 for this shape (gconv.hip w2_cob / w3_ok:
+    bf16, channels % 64, <= 5 neighbours, not 64 -> 128)."""
+    return dtype == torch.bfloat16 and Cin % 64 == 0 and Cout % 64 == 0 and sup.J <= 5 and not (Cin == 64 and Cout == 128)
 
 
 def gconv_finish(dweff, A, W, sup, Cout, Cin, dW=None, dA=None):

@@ -116,7 +116,8 @@ for name, N, T, V, Cin, Cout, Kt, s, pro in wcases:
 A0 = torch.tensor(P.Graph(**P.PKU_MMD).A, dtype=torch.float32, device=dev)
 sup = K.GraphSupport(A0)
 gcases = [("gconv_fwd_c64", 64, 300, 64, 64), ("gconv_fwd_c128", 64, 150, 128, 128),
-          ("gconv_fwd_c256", 64, 75, 256, 256), ("gconv_fwd_64to128", 64, 300, 64, 128)]
+          ("gconv_fwd_c256", 64, 75, 256, 256), ("gconv_fwd_64to128", 64, 300, 64, 128),
+          ("gconv_fwd_128to256", 64, 150, 128, 256)]
 for name, N, T, Cin, Cout in gcases:
     if only and not name.startswith(only):
         continue
