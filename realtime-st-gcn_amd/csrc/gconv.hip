@@ -528,7 +528,13 @@ struct WGG {
   float* slab;     // [R][V*J][Cout][Cin]
   float* rowpart;  // joint-grouped kernel: [R][V][Cout] partial row sums of dy per joint, or NULL
   int zero_unused;  // direct plan (slab = dWeff): also write zeros into the slots j in [deg, J)
+  // direct plan, degree-balanced: the joints whose ring is shallow (deg >= W3_SPLIT_DEG) run as two half-row-range
+  // blocks that merge in-kernel; part = [V][ngrp][2][J*4096 + 64] half partials, cnt = [V*ngrp] arrival counters
+  // (zeroed ahead of every launch)
+  float* part;
+  unsigned* cnt;
 };
+constexpr int W3_SPLIT_DEG = 4;  // at 80 KB: ring depth 4 (deg 4) / 3 (deg 5) vs 5 at deg 3 (w3d)
 
 __global__ __launch_bounds__(256, 2) void gconv_wgrad_kernel(const stgcn_gconv_wgrad_desc a, const WGG g) {
   constexpr int PANEL = WKM * WPR;   // one 32-channel panel of a tile
@@ -826,15 +832,16 @@ DEV void glds16m(const void* src, unsigned lds_off) {
                : "=&s"(saved) : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_off)) : "memory");
 }
 
+// half: -1 = a whole (joint, group, row range) block; 0 / 1 = one half of a split direct-plan block (tiles t0..t1)
 template <int DEG, int LDSB>
-DEV void wgrad3_body(const stgcn_gconv_wgrad_desc& a, const WGG& g, char* smem, int w, int rr, int grp) {
+DEV void wgrad3_body(const stgcn_gconv_wgrad_desc& a, const WGG& g, char* smem, int w, int rr, int grp, int t0,
+                     int t1, int half) {
   constexpr int D = w3d(DEG, LDSB), PANEL = 32 * WPR, STAGE = w3_stage(DEG), NU = 1 + DEG;
   static_assert(D >= 3 && (D - 2) * NU <= 63, "ring");
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int cq = wave & 1, ch = wave >> 1;  // co half (32), ci half (32)
   const int V = a.V;
   const int co0 = (grp % g.nco) * 64, ci0 = (grp / g.nco) * 64;
-  const int t0 = rr * g.tpb, t1 = min(g.ntile, t0 + g.tpb);
   const bf16* __restrict__ dy = reinterpret_cast<const bf16*>(a.dy);
   const bf16* __restrict__ x = reinterpret_cast<const bf16*>(a.x);
   // this wave's DMA share of a tile: dy panel (wave >> 1) rows 16 (wave & 1) .. +15, and the same
@@ -900,17 +907,49 @@ DEV void wgrad3_body(const stgcn_gconv_wgrad_desc& a, const WGG& g, char* smem, 
     }
   }
   asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  float rs = 0.f;  // this block's row sum of column co0 + tid (tid < 64)
   if (rsum) {  // [row][64] in LDS, fixed-order column sums
     float* red = reinterpret_cast<float*>(smem);
 #pragma unroll
     for (int k = 0; k < 8; ++k) red[srow * 64 + scu * 8 + k] = sacc[k];
     __syncthreads();
-    if (tid < 64) {
-      float s = 0.f;
-      for (int r = 0; r < 32; ++r) s += red[r * 64 + tid];
-      g.rowpart[((long)rr * V + w) * a.Cout + co0 + tid] = s;
-    }
+    if (tid < 64)
+      for (int r = 0; r < 32; ++r) rs += red[r * 64 + tid];
   }
+  if (half >= 0) {
+    // split block: publish this half's partial write-through (sc1), drain, one arrival; the second arriver reads the
+    // other half (sc1) and adds it (a + b == b + a: the result does not depend on which half came last) and writes
+    // the outputs (MI355X_MICROARCH "Valid forms" row 1: sc1 stores and loads on both sides, no fences)
+    constexpr int PSZ_J = 4096;
+    const int ngrp = g.nco * g.nci;
+    const long PSZ = (long)a.J * PSZ_J + 64;
+    float* mine = g.part + (((long)w * ngrp + grp) * 2 + half) * PSZ;
+    const float* other = g.part + (((long)w * ngrp + grp) * 2 + (1 - half)) * PSZ;
+    const int el = (cq * 32) * 64 + ch * 32 + (lane & 31);  // + acc_row(r, lane) * 64
+#pragma unroll
+    for (int j = 0; j < DEG; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        __hip_atomic_store(mine + j * PSZ_J + el + acc_row(r, lane) * 64, acc[j][r], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (rsum && tid < 64) __hip_atomic_store(mine + a.J * PSZ_J + tid, rs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem);
+    if (tid == 0)
+      *flag = (int)__hip_atomic_fetch_add(g.cnt + (long)w * ngrp + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (*flag == 0) return;  // first arriver: the partner merges
+#pragma unroll
+    for (int j = 0; j < DEG; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        acc[j][r] += __hip_atomic_load(const_cast<float*>(other) + j * PSZ_J + el + acc_row(r, lane) * 64,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (rsum && tid < 64)
+      rs += __hip_atomic_load(const_cast<float*>(other) + a.J * PSZ_J + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (rsum && tid < 64) g.rowpart[((long)rr * V + w) * a.Cout + co0 + tid] = rs;
   const int cc = ci0 + ch * 32 + (lane & 31);
 #pragma unroll
   for (int j = 0; j < DEG; ++j) {
@@ -931,6 +970,14 @@ DEV void wgrad3_body(const stgcn_gconv_wgrad_desc& a, const WGG& g, char* smem, 
 #ifndef STGCN_W3_XCD
 #define STGCN_W3_XCD 0
 #endif
+// STGCN_W3_SPLIT: degree-balanced direct plan (W3_SPLIT_DEG); the XCD-order A/B build keeps the plain direct plan
+#if STGCN_W3_XCD
+#undef STGCN_W3_SPLIT
+#define STGCN_W3_SPLIT 0
+#endif
+#ifndef STGCN_W3_SPLIT
+#define STGCN_W3_SPLIT 1
+#endif
 template <int LDSB>
 __global__ __launch_bounds__(256, LDSB > 80 * 1024 ? 1 : 2) void gconv_wgrad3_kernel(const stgcn_gconv_wgrad_desc a,
                                                                                     const WGG g) {
@@ -945,8 +992,9 @@ __global__ __launch_bounds__(256, LDSB > 80 * 1024 ? 1 : 2) void gconv_wgrad3_ke
   const int rr = wgi / (a.V * ngrp), rem = wgi % (a.V * ngrp);
   const int w = rem / ngrp, grp = rem % ngrp;
 #else
-  const int w = blockIdx.x / (ngrp * g.R);
-  const int rem = blockIdx.x % (ngrp * g.R);
+  const int bid = g.part ? (int)(blockIdx.x % (a.V * ngrp)) : (int)blockIdx.x;  // split plan: slot 1 repeats slot 0
+  const int w = bid / (ngrp * g.R);
+  const int rem = bid % (ngrp * g.R);
   const int rr = rem / ngrp, grp = rem % ngrp;
 #endif
   // joints in decreasing-degree order (ties by index): the heaviest blocks are dispatched first and the
@@ -968,12 +1016,24 @@ __global__ __launch_bounds__(256, LDSB > 80 * 1024 ? 1 : 2) void gconv_wgrad3_ke
     wj = order[w];
     __syncthreads();
   }
+  int t0 = rr * g.tpb, t1 = min(g.ntile, t0 + g.tpb), half = -1;
+  if (g.part) {  // degree-balanced direct plan: grid = 2 x V x ngrp, slot 1 only for the split joints
+    const int slot = blockIdx.x / (a.V * ngrp);
+    const bool split = a.deg[wj] >= W3_SPLIT_DEG;
+    if (slot == 1 && !split) return;  // block-uniform exit before any barrier
+    if (split) {
+      half = slot;
+      const int tm = g.ntile / 2;
+      t0 = half ? tm : 0;
+      t1 = half ? g.ntile : tm;
+    }
+  }
   switch (a.deg[wj]) {
-    case 1: wgrad3_body<1, LDSB>(a, g, smem, wj, rr, grp); break;
-    case 2: wgrad3_body<2, LDSB>(a, g, smem, wj, rr, grp); break;
-    case 3: wgrad3_body<3, LDSB>(a, g, smem, wj, rr, grp); break;
-    case 4: wgrad3_body<4, LDSB>(a, g, smem, wj, rr, grp); break;
-    case 5: wgrad3_body<5, LDSB>(a, g, smem, wj, rr, grp); break;
+    case 1: wgrad3_body<1, LDSB>(a, g, smem, wj, rr, grp, t0, t1, half); break;
+    case 2: wgrad3_body<2, LDSB>(a, g, smem, wj, rr, grp, t0, t1, half); break;
+    case 3: wgrad3_body<3, LDSB>(a, g, smem, wj, rr, grp, t0, t1, half); break;
+    case 4: wgrad3_body<4, LDSB>(a, g, smem, wj, rr, grp, t0, t1, half); break;
+    case 5: wgrad3_body<5, LDSB>(a, g, smem, wj, rr, grp, t0, t1, half); break;
     default:  // deg 0: no pairs (the reduction skips j >= deg); the row sums still come from here
       if (g.rowpart != nullptr && grp / g.nco == 0 && threadIdx.x < 64) {
         const int co = (grp % g.nco) * 64 + threadIdx.x;
@@ -1380,11 +1440,21 @@ int gconv_weights_launch(const float* A, const float* W, const int* nbr, const i
   return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
 }
 
+// the degree-balanced direct plan's workspace: half partials [V][ngrp][2][J*4096 + 64] floats, then the arrival
+// counters [V*ngrp] (16-B padded)
+long w3_split_part_floats(const stgcn_gconv_wgrad_desc& a, const WGG& g) {
+  return (long)a.V * g.nco * g.nci * 2 * ((long)a.J * 4096 + 64);
+}
+long w3_split_cnt_bytes(const stgcn_gconv_wgrad_desc& a, const WGG& g) {
+  return (((long)a.V * g.nco * g.nci * 4) + 15) / 16 * 16;
+}
+
 long gconv_wgrad_workspace(const stgcn_gconv_wgrad_desc& a, int dtype) {
   if (dtype != 1) return 0;
   const int cob = w2_cob(a);
   const WGG g = cob ? wplan2(a, cob) : wplan(a);
-  if (cob && w3_ok(a) && g.R == 1) return 0;  // direct
+  if (cob && w3_ok(a) && g.R == 1)  // direct
+    return STGCN_W3_SPLIT ? w3_split_part_floats(a, g) * (long)sizeof(float) + w3_split_cnt_bytes(a, g) : 0;
   if (cob && a.rowsum)
     return ((long)g.R * a.V * a.J * a.Cout * a.Cin + (long)g.R * a.V * a.Cout) * (long)sizeof(float);
   return (long)g.R * a.V * a.J * a.Cout * a.Cin * (long)sizeof(float);
@@ -1409,6 +1479,13 @@ int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s
       g.slab = a.dweff;
       g.rowpart = a.rowsum;
       g.zero_unused = 1;
+      if (STGCN_W3_SPLIT) {  // degree-balanced: half partials + counters in the workspace, counters zeroed per launch
+        const long pf = w3_split_part_floats(a, g), cb = w3_split_cnt_bytes(a, g);
+        if (!a.work || a.work_bytes < pf * (long)sizeof(float) + cb) return STGCN_EBADSHAPE;
+        g.part = reinterpret_cast<float*>(a.work);
+        g.cnt = reinterpret_cast<unsigned*>(g.part + pf);
+        if (a.phase != 2 && hipMemsetAsync(g.cnt, 0, (size_t)cb, s) != hipSuccess) return STGCN_EHIP;
+      }
     } else {
       if (!a.work || a.work_bytes < need * (long)sizeof(float)) return STGCN_EBADSHAPE;
       g.slab = reinterpret_cast<float*>(a.work);
@@ -1418,7 +1495,7 @@ int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s
     const size_t lds = ring ? (size_t)(deep ? 160 : 80) * 1024 : 2 * (size_t)(cob / 32 + 2 * J2) * w2m(cob) * WPR;
     auto* k = ring ? (deep ? gconv_wgrad3_kernel<160 * 1024> : gconv_wgrad3_kernel<80 * 1024>) : gconv_wgrad2_kernel<64>;
     if (stgcn_lds_attr((const void*)k, 160 * 1024, s)) return STGCN_EHIP;
-    const long blocks = (long)a.V * g.nco * g.nci * g.R;
+    const long blocks = (long)a.V * g.nco * g.nci * g.R * (g.part ? 2 : 1);
     if (a.phase != 2) hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(ring ? 256 : cob / 16 * 64), lds, s, a, g);
     if (direct || a.phase == 1) return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
     if (a.rowsum) {  // slab reduction and row sums in one launch
