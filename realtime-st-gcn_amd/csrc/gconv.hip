@@ -37,6 +37,14 @@
 #ifndef GCONV_NSTG_W
 #define GCONV_NSTG_W 2
 #endif
+// row tiles of the wide DMA forms (A/B build flags): BM = 4 * TM * 32 rows; a taller tile re-reads each joint's
+// effective weights (deg x 64-channel chunks x 128 columns) fewer times per launch
+#ifndef GCONV_TM_W
+#define GCONV_TM_W 2
+#endif
+#ifndef GCONV_TM_M
+#define GCONV_TM_M 1
+#endif
 
 namespace {
 
@@ -1415,8 +1423,8 @@ int gconv_launch(const stgcn_gconv_desc& a, int dtype, hipStream_t s) {
     const bool dma = a.Cin % 64 == 0 && a.Cin == a.Cin_pad && a.in_ld % 8 == 0;
     if (dma) {
       if (!wide) return launch_gconv<bf16, 4, 1, 1, 2, 64, GCONV_NSTG_N>(a, s);
-      return a.Cin >= 256 ? launch_gconv<bf16, 4, 2, 2, 2, 64, GCONV_NSTG_W>(a, s)
-                          : launch_gconv<bf16, 4, 2, 1, 2, 64, GCONV_NSTG_M>(a, s);
+      return a.Cin >= 256 ? launch_gconv<bf16, 4, 2, GCONV_TM_W, 2, 64, GCONV_NSTG_W>(a, s)
+                          : launch_gconv<bf16, 4, 2, GCONV_TM_M, 2, 64, GCONV_NSTG_M>(a, s);
     }
     const bool k64 = a.Cin >= 128 && a.Cin_pad % 64 == 0;
     if (wide) return k64 ? launch_gconv<bf16, 4, 2, 1, 2, 64>(a, s) : launch_gconv<bf16, 4, 2, 2, 2, 32>(a, s);
