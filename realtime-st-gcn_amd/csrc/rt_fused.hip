@@ -316,12 +316,18 @@ DEV float2 rf_block_sum2(float2 v, float* red) {  // two sums at once; red holds
   return t;
 }
 
-// W rows of one channel-pair task, staged in LDS: rows [0, P*CB) = conv rows (p, cl) -> w[(p*Cout + co0 + cl)],
-// then CB residual rows (res_mode 2); each thread moves at most RF_WU float4 units
-constexpr int RF_WROWS = PMAX * CB + CB;
+// output channels per task of the one-launch kernel (build flag for A/B: 4 channels, one task per workgroup at
+// G = 64 up to C = 256, measured 0.127 vs 0.109 ms/frame: the 12-row conv spills)
+#ifndef STGCN_RT_CB
+#define STGCN_RT_CB 2
+#endif
+constexpr int RF_CB = STGCN_RT_CB;
+// W rows of one channel-group task, staged in LDS: rows [0, P*RF_CB) = conv rows (p, cl) -> w[(p*Cout + co0 + cl)],
+// then RF_CB residual rows (res_mode 2); each thread moves at most RF_WU float4 units
+constexpr int RF_WROWS = PMAX * RF_CB + RF_CB;
 constexpr int RF_WU = (RF_WROWS * CMAX / 4 + RF_PT - 1) / RF_PT;
 constexpr int RF_AU = (PMAX * VMAX * VMAX + RF_PT - 1) / RF_PT;  // A floats per worker
-constexpr int RF_FU = (VMAX * CB + RF_PT / 8 - 1) / (RF_PT / 8);  // FIFO outputs per 8-lane group
+constexpr int RF_FU = (VMAX * RF_CB + RF_PT / 8 - 1) / (RF_PT / 8);  // FIFO outputs per 8-lane group
 
 // everything a task needs from memory before its arithmetic: weight rows, A (first task of a layer only), and the
 // FIFO / accumulator values of its outputs
@@ -331,7 +337,7 @@ struct RfPre {
   float acc[RF_FU], fifo[RF_FU], bias[RF_FU];
 };
 
-DEV int rf_nrows(const stgcn_rt_layer& ly) { return ly.P * CB + (ly.res_mode == 2 ? CB : 0); }
+DEV int rf_nrows(const stgcn_rt_layer& ly) { return ly.P * RF_CB + (ly.res_mode == 2 ? RF_CB : 0); }
 
 DEV void rf_prefetch(const stgcn_rt_layer& ly, int co0, int V, int fi, int ai, bool withA, RfPre& r) {
   const int K4 = ly.Cin / 4, n = rf_nrows(ly) * K4;
@@ -342,8 +348,8 @@ DEV void rf_prefetch(const stgcn_rt_layer& ly, int co0, int V, int fi, int ai, b
     r.w[u] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (i < n) {
       const int row = i / K4, k4 = i - row * K4;
-      const bool res = row >= ly.P * CB;
-      const int cl = res ? row - ly.P * CB : row % CB, p = res ? 0 : row / CB, co = co0 + cl;
+      const bool res = row >= ly.P * RF_CB;
+      const int cl = res ? row - ly.P * RF_CB : row % RF_CB, p = res ? 0 : row / RF_CB, co = co0 + cl;
       if (co < ly.Cout) {
         const float* src = res ? ly.wr + (long)co * ly.Cin : ly.w + ((long)p * ly.Cout + co) * ly.Cin;
         r.w[u] = reinterpret_cast<const float4*>(src)[k4];
@@ -361,7 +367,7 @@ DEV void rf_prefetch(const stgcn_rt_layer& ly, int co0, int V, int fi, int ai, b
 #pragma unroll
   for (int u = 0; u < RF_FU; ++u) {
     const int tr = (pt >> 3) + (RF_PT / 8) * u;
-    const int cl = tr % CB, v = tr / CB, co = co0 + cl;
+    const int cl = tr % RF_CB, v = tr / RF_CB, co = co0 + cl;
     const bool ok = pt >= 0 && (pt & 7) == 0 && v < V && co < ly.Cout;
     const long e = (long)v * ly.Cout + co;
     r.acc[u] = ok ? ly.acc[ai * E + e] : 0.f;
@@ -450,15 +456,15 @@ DEV float sq4(float4 v, float m) {
 }
 
 // dynamic LDS carve (floats): xs [VMAX*CMAX] (the current layer's input), wsm, ys, As, red, idx
-constexpr int RF_LDS_FLOATS = VMAX * CMAX + RF_WROWS * CMAX + PMAX * VMAX * CB + PMAX * VMAX * VMAX + 64 +
+constexpr int RF_LDS_FLOATS = VMAX * CMAX + RF_WROWS * CMAX + PMAX * VMAX * RF_CB + PMAX * VMAX * VMAX + 64 +
                               2 * STGCN_RT_MAX_LAYERS;
 
 __global__ __launch_bounds__(RF_NT) void rt_frame_kernel(const stgcn_rt_frame_desc d) {
   extern __shared__ __attribute__((aligned(16))) float rf_sm[];
   float* xs = rf_sm;                     // [V][C] the current layer's input
   float* wsm = xs + VMAX * CMAX;         // [RF_WROWS][Cin] weight rows of the current task
-  float* ys = wsm + RF_WROWS * CMAX;     // [P][V][CB]
-  float* As = ys + PMAX * VMAX * CB;     // [P][V][V]
+  float* ys = wsm + RF_WROWS * CMAX;     // [P][V][RF_CB]
+  float* As = ys + PMAX * VMAX * RF_CB;     // [P][V][V]
   float* red = As + PMAX * VMAX * VMAX;  // [RF_NT / 64]
   int* sidx = reinterpret_cast<int*>(red + 64);  // (fifo, acc) index of every layer, read once at the start
   const int tid = threadIdx.x, kk = tid & 7, G = gridDim.x, V = d.V;
@@ -466,12 +472,12 @@ __global__ __launch_bounds__(RF_NT) void rt_frame_kernel(const stgcn_rt_frame_de
   __syncthreads();
   RfPre pre;
   // layer 0's first task: in flight during the input head
-  if ((int)blockIdx.x * CB < d.layers[0].Cout) rf_prefetch(d.layers[0], blockIdx.x * CB, V, sidx[0], sidx[1], true, pre);
+  if ((int)blockIdx.x * RF_CB < d.layers[0].Cout) rf_prefetch(d.layers[0], blockIdx.x * RF_CB, V, sidx[0], sidx[1], true, pre);
   else rf_prefetch(d.layers[0], 0, V, sidx[0], sidx[1], true, pre);  // A only is used
 
   // input head: LayerNorm([3,1,V]) + fcn_in (rt_in_kernel's arithmetic), every workgroup
   {
-    float* xi = ys;  // 3 * V <= 96 < PMAX * VMAX * CB
+    float* xi = ys;  // 3 * V <= 96 < PMAX * VMAX * RF_CB
     const int n = 3 * V;
     for (int i = tid; i < n; i += RF_NT) xi[i] = d.x[i];
     __syncthreads();
@@ -499,8 +505,8 @@ __global__ __launch_bounds__(RF_NT) void rt_frame_kernel(const stgcn_rt_frame_de
     RF_STAMP(l, 0);
     // (1) conv1x1 + A-mix + FIFO (+ residual conv) of this workgroup's channel pairs
     bool first = true;
-    for (int task = blockIdx.x; task * CB < Cout || first; task += G) {
-      const int co0 = task * CB;
+    for (int task = blockIdx.x; task * RF_CB < Cout || first; task += G) {
+      const int co0 = task * RF_CB;
       if (!first) {  // the first task's operands were prefetched (and staged during the previous norm phase)
         __syncthreads();  // every read of wsm by the previous task
         rf_prefetch(ly, co0, V, fi, ai, false, pre);
@@ -511,30 +517,30 @@ __global__ __launch_bounds__(RF_NT) void rt_frame_kernel(const stgcn_rt_frame_de
       first = false;
       if (co0 >= Cout) break;  // no pair here: A staged only (kept for uniformity)
       __syncthreads();
-      // conv rows: ys[(p*V + u)*CB + cl] = w_(p, co0+cl) . x[u]; half-wave h = joint u, its 32 lanes split Cin
-      // (k = lane, lane + 32, ...) and keep all P*CB rows' sums (one x read per k for the pair's rows), DPP-summed
+      // conv rows: ys[(p*V + u)*RF_CB + cl] = w_(p, co0+cl) . x[u]; half-wave h = joint u, its 32 lanes split Cin
+      // (k = lane, lane + 32, ...) and keep all P*RF_CB rows' sums (one x read per k for the pair's rows), DPP-summed
       {
         const int h = tid >> 5, l32 = tid & 31, u = h < V ? h : 0;
         const float4* x4 = reinterpret_cast<const float4*>(xs) + u * K4;
         const float4* w4 = reinterpret_cast<const float4*>(wsm);
-        float acc[PMAX * CB];
+        float acc[PMAX * RF_CB];
 #pragma unroll
-        for (int r = 0; r < PMAX * CB; ++r) acc[r] = 0.f;
+        for (int r = 0; r < PMAX * RF_CB; ++r) acc[r] = 0.f;
         for (int k = l32; k < K4; k += 32) {
           const float4 xv = x4[k];
 #pragma unroll
-          for (int r = 0; r < PMAX * CB; ++r) {
-            if (r < P * CB) {
+          for (int r = 0; r < PMAX * RF_CB; ++r) {
+            if (r < P * RF_CB) {
               const float4 wv = w4[r * K4 + k];
               acc[r] = fmaf(wv.x, xv.x, fmaf(wv.y, xv.y, fmaf(wv.z, xv.z, fmaf(wv.w, xv.w, acc[r]))));
             }
           }
         }
 #pragma unroll
-        for (int r = 0; r < PMAX * CB; ++r) {
-          if (r < P * CB) {
+        for (int r = 0; r < PMAX * RF_CB; ++r) {
+          if (r < P * RF_CB) {
             const float t = rf_half_sum(acc[r]);
-            if (l32 == 31 && h < V) ys[((r / CB) * V + u) * CB + r % CB] = t;
+            if (l32 == 31 && h < V) ys[((r / RF_CB) * V + u) * RF_CB + r % RF_CB] = t;
           }
         }
       }
@@ -546,14 +552,14 @@ __global__ __launch_bounds__(RF_NT) void rt_frame_kernel(const stgcn_rt_frame_de
       for (int q = 0; q < RF_FU; ++q) {
         if (tid < 64) break;  // wave-uniform
         const int tr = ((tid - 64) >> 3) + (RF_PT / 8) * q;
-        const int cl = tr % CB, v = tr / CB, co = co0 + cl;
+        const int cl = tr % RF_CB, v = tr / RF_CB, co = co0 + cl;
         const bool ok = v < V && co < Cout;
         float r = 0.f;
-        if (ly.res_mode == 2) r = rf_dot8(wsm + (P * CB + cl) * Cin, xs + (ok ? v : 0) * Cin, K4, kk);
+        if (ly.res_mode == 2) r = rf_dot8(wsm + (P * RF_CB + cl) * Cin, xs + (ok ? v : 0) * Cin, K4, kk);
         float s = 0.f;
         if (ok)
           for (int p = 0; p < P; ++p)
-            for (int u = kk; u < V; u += 8) s = fmaf(As[(p * V + u) * V + v], ys[(p * V + u) * CB + cl], s);
+            for (int u = kk; u < V; u += 8) s = fmaf(As[(p * V + u) * V + v], ys[(p * V + u) * RF_CB + cl], s);
 #pragma unroll
         for (int m = 1; m < 8; m <<= 1) s += __shfl_xor(s, m);
         if (ok && kk == 0) {
@@ -571,7 +577,7 @@ __global__ __launch_bounds__(RF_NT) void rt_frame_kernel(const stgcn_rt_frame_de
     RF_STAMP(l, 2);
     // the next layer's first task (weight rows, A, FIFO values): in flight across the barrier
     if (l + 1 < d.L) {
-      rf_prefetch(nx, (int)blockIdx.x * CB < nx.Cout ? blockIdx.x * CB : 0, V, sidx[2 * l + 2], sidx[2 * l + 3], true,
+      rf_prefetch(nx, (int)blockIdx.x * RF_CB < nx.Cout ? blockIdx.x * RF_CB : 0, V, sidx[2 * l + 2], sidx[2 * l + 3], true,
                   pre);
     }
     RfLn lnp;
