@@ -38,6 +38,10 @@ def test_abi_rejects_bad_args_without_gpu(pkg):
     assert lib.stgcn_tconv_frame(d, None) == 1          # out_ld % 8 == 4
     d.out_ld, d.V = 64, 32
     assert lib.stgcn_tconv_frame(d, None) == 1          # V > 25: no reference skeleton, no kernel form
+    g = L.GconvWgradDesc(phase=3)                       # phase outside {0, 1, 2}
+    assert lib.stgcn_gconv_wgrad(g, 1, None) == 1
+    r = L.RtFrameDesc()                                 # null pointers: refused before the barrier-counter memset
+    assert lib.stgcn_rt_frame(r, None) == 1
 
 
 @pytest.mark.parametrize("key,name", [("pku_mmd", "pku-mmd"), ("ntu_rgbpd", "ntu"), ("openpose", "op"),

@@ -143,3 +143,40 @@ def test_gconv_dgrad_masked_residual(K, pkg, Cin, Cout):
     out = K.gconv(dg, wT, sup, Cout, Cin, trans=True, res=(dy, bits))
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("Cin,Cout,N,T", [(64, 64, 8, 40), (256, 256, 8, 75), (128, 256, 4, 60)])
+def test_gconv_wgrad_phases(K, pkg, Cin, Cout, N, T):
+    """stgcn_gconv_wgrad split into its accumulation kernel (phase 1) and its slab reduction (phase 2) — what
+    bench.py's roofline brackets — writes exactly what the one-call form (phase 0) writes, for a slab plan (64 -> 64,
+    128 -> 256) and the degree-balanced direct plan (256 -> 256: joints of degree >= 4 as two half-row-range blocks
+    merged in-kernel; a + b == b + a, so the merge order does not change a bit)."""
+    import ctypes
+    torch.manual_seed(9)
+    A0 = torch.tensor(pkg.Graph(**pkg.PKU_MMD).A, dtype=torch.float32)
+    sup = K.GraphSupport(A0.to(DEV))
+    V = A0.shape[-1]
+    x = cl(torch.randn(N, Cin, T, V), torch.bfloat16)
+    dy = cl(torch.randn(N, Cout, T, V), torch.bfloat16)
+    S0 = torch.empty((V, Cout), device=DEV)
+    d0 = K.gconv_wgrad(x, dy, sup, Cin, Cout, rowsum=S0)
+    L = pkg._lib
+    outs = []
+    for rep in range(2):  # twice: the split plan's arrival counters are zeroed per launch
+        S = torch.empty((V, Cout), device=DEV)
+        dweff = torch.empty_like(d0)
+        d = L.GconvWgradDesc()
+        d.rowsum = S.data_ptr()
+        d.x, d.dy, d.nbr, d.deg, d.dweff = x.data_ptr(), dy.data_ptr(), sup.nbr.data_ptr(), sup.deg.data_ptr(), \
+            dweff.data_ptr()
+        d.NT, d.V, d.J, d.Cin, d.Cout, d.x_ld, d.dy_ld = N * T, V, sup.J, Cin, Cout, Cin, Cout
+        nbytes = L.lib().stgcn_gconv_wgrad_workspace(d, 1)
+        work = torch.empty(max(nbytes, 4) // 4, dtype=torch.float32, device=DEV)
+        d.work, d.work_bytes = work.data_ptr(), nbytes
+        for ph in (1, 2):
+            d.phase = ph
+            L.check(L.lib().stgcn_gconv_wgrad(ctypes.byref(d), 1, L.stream()), "gconv_wgrad")
+        outs.append((dweff, S))
+    torch.cuda.synchronize()
+    for dweff, S in outs:
+        assert torch.equal(dweff, d0) and torch.equal(S, S0)
