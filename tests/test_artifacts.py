@@ -39,11 +39,16 @@ def test_roofline_kernel_matches_rocprof():
     stats = os.path.join(PROF, f"{tag}_bench_kernel_stats.csv")
     assert os.path.exists(stats), stats
     b = json.load(open(bench))
-    m = re.match(r"(\w+)<([^>]*)>", b["roofline"]["kernel"])
-    name, targs = m.group(1), [t.strip() for t in m.group(2).split(",")]
-    # the bench names the leading template arguments; the trailing (defaulted) ones may be omitted
-    want = f"{name}<{', '.join(targs)}"
-    rows = [r for r in csv.DictReader(open(stats)) if re.search(re.escape(want) + r"[,>]", r["Name"])]
+    m = re.match(r"(\w+)(?:<([^>]*)>)?", b["roofline"]["kernel"])
+    name = m.group(1)
+    if m.group(2) is not None:
+        # the bench names the leading template arguments; the trailing (defaulted) ones may be omitted
+        targs = [t.strip() for t in m.group(2).split(",")]
+        want = f"{name}<{', '.join(targs)}"
+        rows = [r for r in csv.DictReader(open(stats)) if re.search(re.escape(want) + r"[,>]", r["Name"])]
+    else:  # every instantiation of the named kernel (the bench brackets all of its launches)
+        rows = [r for r in csv.DictReader(open(stats)) if re.search(r"\b" + re.escape(name) + r"[<(]", r["Name"])]
+        want = name
     assert rows, want
     prof_ms = float(rows[0]["AverageNs"]) / 1e6
     assert abs(prof_ms - b["roofline"]["avg_launch_ms"]) / prof_ms < 0.10
