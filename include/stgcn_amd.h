@@ -165,34 +165,6 @@ typedef struct {
 int stgcn_gconv(const stgcn_gconv_desc* d, int dtype, void* stream);
 
 long stgcn_gconv_row_blocks(int NT, int V);
-
-/* The same graph convolution in its A-first form for 64 -> 64 channels (bf16, P <= 3, V <= 25, J <= 8), one
- * persistent kernel: XA = the joint mix of x (fp32, rounded to bf16 once), then one GEMM with W' shared by every
- * joint (replaces stgcn_gconv's per-joint effective weights for this shape):
- *   trans 0: out[(i,w)][co] = bias[w][co] + sum_{p,ci} W[p*64+co][ci] sum_{j<deg[w]} c_p(nbr_j, w) x[(i,nbr_j)][ci]
- *   trans 1: out[(i,v)][ci] = sum_{p,co} W[p*64+co][ci] sum_{j<deg[v]} c_p(v, nbr_j) x[(i,nbr_j)][co]
- * c_p(v, w) = A[p][v][w] (* M[p][v][w] when M is given), W fp32 [P*64][64] (the 1x1 conv weight), nbr / deg the
- * support (trans 0) or reverse (trans 1) lists of stgcn_gconv.  stats: BN partials, one float4 (count, mean, M2, 0)
- * row of 64 per block (row stride stats_ld float4s), stgcn_gcn_af_blocks(NT, V) rows.  res / res_bits / res_ld /
- * accumulate as stgcn_gconv. */
-typedef struct {
-  const void* x;
-  void* out;
-  const float* A;
-  const float* M;
-  const float* w;
-  const int* nbr;
-  const int* deg;
-  const float* bias;
-  float* stats;
-  const void* res;
-  const void* res_bits;
-  long NT;
-  int V, P, J, trans, x_ld, out_ld, res_ld, stats_ld, accumulate, pad_;
-} stgcn_gcn_af_desc;
-
-long stgcn_gcn_af_blocks(long NT, int V);
-int stgcn_gcn_af(const stgcn_gcn_af_desc* d, void* stream);
 int stgcn_gconv_weights(const float* A, const float* W, const int* nbr, const int* deg, int P, int V, int J, int Cout,
                         int Cin, int trans, void* out, int rows_pad, int cols_pad, int dtype, void* stream);
 /* stgcn_gconv_weights (forward form, trans = 0) and stgcn_gcn_bias for a shared A in ONE launch:

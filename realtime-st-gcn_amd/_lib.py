@@ -57,12 +57,6 @@ class GconvDesc(ctypes.Structure):
                                      "accumulate")] + [("res", c_void_p), ("res_bits", c_void_p), ("res_ld", c_int)]
 
 
-class GcnAfDesc(ctypes.Structure):
-    _fields_ = [(n, c_void_p) for n in ("x", "out", "A", "M", "w", "nbr", "deg", "bias", "stats", "res", "res_bits")] + \
-               [("NT", c_long)] + [(n, c_int) for n in ("V", "P", "J", "trans", "x_ld", "out_ld", "res_ld", "stats_ld",
-                                                      "accumulate", "pad_")]
-
-
 class GconvWgradDesc(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("dy", c_void_p), ("nbr", c_void_p), ("deg", c_void_p), ("dweff", c_void_p)] + \
                [(n, c_int) for n in ("NT", "V", "J", "Cin", "Cout", "x_ld", "dy_ld")] + \
@@ -121,8 +115,6 @@ _SIGS = {
     "stgcn_bn_bwd_fused_reduce": (c_int, [ctypes.POINTER(BnBwdDesc), c_int, c_void_p]),
     "stgcn_bn_bwd_fused_apply": (c_int, [ctypes.POINTER(BnBwdDesc), c_int, c_void_p]),
     "stgcn_gconv_row_blocks": (c_long, [c_int, c_int]),
-    "stgcn_gcn_af": (c_int, [ctypes.POINTER(GcnAfDesc), c_void_p]),
-    "stgcn_gcn_af_blocks": (c_long, [c_long, c_int]),
     "stgcn_gconv_weights_bias": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_void_p, c_int, c_int, c_void_p, c_int,
                                                                        c_void_p]),
     "stgcn_gconv_weights": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p] + [c_int] * 6 + [c_void_p, c_int, c_int,

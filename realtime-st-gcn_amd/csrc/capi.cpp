@@ -31,8 +31,6 @@ long wgrad1x1_workspace(const WgradArgs& a, int dtype);
 int wgrad1x1_launch(const WgradArgs& a, int dtype, hipStream_t s);
 int amix_fwd_launch(const AmixArgs& a, int dtype, hipStream_t s);
 long gconv_row_blocks(int NT, int V);
-long gcn_af_blocks(long NT, int V);
-int gcn_af_launch(const stgcn_gcn_af_desc& a, hipStream_t s);
 long bn_bwd_fused_work_floats(long M, int C, int dtype);
 int bn_bwd_fused_reduce_launch(const stgcn_bn_bwd_desc& a, int dtype, hipStream_t s);
 int bn_bwd_fused_apply_launch(const stgcn_bn_bwd_desc& a, int dtype, hipStream_t s);
@@ -226,11 +224,6 @@ int stgcn_gconv(const stgcn_gconv_desc* d, int dtype, void* stream) {
   return gconv_launch(*d, dtype, STREAM(stream));
 }
 long stgcn_gconv_row_blocks(int NT, int V) { return gconv_row_blocks(NT, V); }
-long stgcn_gcn_af_blocks(long NT, int V) { return NT > 0 && V > 0 ? gcn_af_blocks(NT, V) : 0; }
-int stgcn_gcn_af(const stgcn_gcn_af_desc* d, void* stream) {
-  if (!d) return STGCN_EBADSHAPE;
-  return gcn_af_launch(*d, STREAM(stream));
-}
 int stgcn_gconv_weights(const float* A, const float* W, const int* nbr, const int* deg, int P, int V, int J, int Cout,
                         int Cin, int trans, void* out, int rows_pad, int cols_pad, int dtype, void* stream) {
   CHECK_DTYPE(dtype);

@@ -210,8 +210,6 @@ class StgcnLayerFunction(torch.autograd.Function):
         # ---- graph convolution: g = sum_p A_p-mix(x) W_p + bias2d
         sup = cfg[5] if len(cfg) > 5 else None
         gather = sup is not None and A32.dim() == 3 and not sup.dense(P)
-        # the A-first persistent graph conv for 64 -> 64 (gcn_af.hip): forward and data gradient
-        afirst = gather and ROUTING.gcn_af and K.gcn_af_ok(sup, P, Cin, Cout, V, dtype)
         if (gather and len(cfg) > 7 and cfg[7] and ROUTING.fused_inference and norm == LN
                 and K.layer_fused_ok(sup, P, Cin, Cout, V, kt, stride, dtype)):
             # inference of a LayerNorm 64 -> 64 stride-1 layer: the one-kernel layer (g never leaves the chip;
@@ -235,11 +233,10 @@ class StgcnLayerFunction(torch.autograd.Function):
         bias2d = None if gather else K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
         if norm == BN:  # all BatchNorm partial-statistics buffers of the layer from one zero fill
             cpo = -(-Cout // K.col_tile(Cout)) * K.col_tile(Cout)
-            rb1 = (K.gcn_af_blocks(N * T, V) if afirst else K.gconv_row_blocks(N * T, V)) if gather \
-                else K.row_blocks(M1, Cout)
+            rb1 = K.gconv_row_blocks(N * T, V) if gather else K.row_blocks(M1, Cout)
             rb2 = K.row_blocks(M2, Cout)
             st_shapes = [(rb1, cpo, 4), (rb2, cpo, 4)] + ([(K.row_blocks(M2, Cout), cpo, 4)] if res_conv else [])
-            st_all = _stats_arena(cache, dev, x.dtype, st_shapes, (gather, afirst))
+            st_all = _stats_arena(cache, dev, x.dtype, st_shapes, gather)
             st1, st2 = st_all[0], st_all[1]
             str_ = st_all[2] if res_conv else None
         # ---- residual branch: independent of the graph conv -> temporal conv chain until the output norm
@@ -254,14 +251,7 @@ class StgcnLayerFunction(torch.autograd.Function):
             else:
                 lsr = K.ln_stats(r, N * T_out, V, Cout)
 
-        if afirst:  # A-first: the joint mix and ONE GEMM with W shared by every joint, one persistent launch
-            bias2d = packs.gw[1] if packs is not None and packs.gw is not None else \
-                K.gcn_bias(A32, bg.detach().float().contiguous(), N, Cout)
-            cpg = Cout
-            g = K.gcn_af(x, A32, wg.detach().float().reshape(P * Cout, Cin), sup, bias=bias2d,
-                         stats=st1 if norm == BN else None)
-            XA = None
-        elif gather:  # joint-gathered GEMM over per-joint effective weights (gconv.hip), no XA in HBM
+        if gather:  # joint-gathered GEMM over per-joint effective weights (gconv.hip), no XA in HBM
             if packs is not None and packs.gw is not None:
                 wgp, bias2d = packs.gw
             else:
@@ -474,14 +464,10 @@ class StgcnLayerFunction(torch.autograd.Function):
             _gconv_wgrad_dweff(ctx, x, dg, A32, wg, wg2, bg, bgp, sup, grads, zero_targets, P, Cin, Cout, T, V, M1,
                                dtype, dev)
             dA = grads.pop("dA")
-            if ROUTING.gcn_af and K.gcn_af_ok(sup, P, Cin, Cout, V, dtype):
-                K.gcn_af(dg, A32, wg2, sup, trans=True, out=dx, accumulate=dx_written,
-                         res=(dy, ybits) if res_in_gconv else None)
-            else:
-                wgT = packs.gwT if packs is not None and packs.gwT is not None else \
-                    K.gconv_weights(A32, wg2, sup, Cout, Cin, True, dtype)
-                K.gconv(dg, wgT, sup, Cout, Cin, trans=True, out=dx, accumulate=dx_written,
-                        res=(dy, ybits) if res_in_gconv else None)
+            wgT = packs.gwT if packs is not None and packs.gwT is not None else \
+                K.gconv_weights(A32, wg2, sup, Cout, Cin, True, dtype)
+            K.gconv(dg, wgT, sup, Cout, Cin, trans=True, out=dx, accumulate=dx_written,
+                    res=(dy, ybits) if res_in_gconv else None)
         else:
             # DW[(n,t,w)][p*Cin+ci] = sum_c dg[(n,t,w)][c] Wg[p*Cout+c][ci]
             wgT = wg.detach().float().view(P, Cout, Cin).permute(0, 2, 1).reshape(1, P * Cin, Cout)

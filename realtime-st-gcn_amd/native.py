@@ -639,47 +639,6 @@ def gconv(x, wpk, sup, Cin, Cout, trans=False, bias=None, stats=None, out=None, 
     return out
 
 
-def gcn_af_ok(sup, P, Cin, Cout, V, dtype) -> bool:
-    """Shapes the A-first graph-conv kernel (gcn_af.hip) takes: bf16, 64 -> 64, P <= 3, V <= 25, J <= 8."""
-    return (dtype == torch.bfloat16 and sup is not None and Cin == 64 and Cout == 64 and P <= 3 and V <= 25
-            and sup.J <= 8)
-
-
-def gcn_af_blocks(NT: int, V: int) -> int:
-    return L.lib().stgcn_gcn_af_blocks(NT, V)
-
-
-def gcn_af(x, A, W, sup, trans=False, bias=None, stats=None, M=None, out=None, accumulate=False, res=None,
-           stats_ld=64, tag=None):
-    """stgcn_gcn_af: the 64 -> 64 graph conv in its A-first form (joint mix, then one GEMM with W [P*64][64]
-    fp32).  trans 0: out = bias2d + conv(mix_A(x)); trans 1: the data gradient of that map w.r.t. x.
-    ``stats``: fp32 [>= gcn_af_blocks(N*T, V)][stats_ld][4] BN partials; ``res`` / ``accumulate`` as gconv."""
-    N, C, T, V = x.shape
-    A = _dense(A)
-    if C != 64 or x.dtype != torch.bfloat16 or W.numel() != A.shape[0] * 64 * 64 or A.shape[-1] != V:
-        raise RuntimeError("stgcn_amd: gcn_af takes bf16 64-channel rows, W [P*64][64] and A [P][V][V]")
-    if out is None:
-        out = cl_empty(N, 64, T, V, x.dtype, x.device)
-    nbr, deg = (sup.rnbr, sup.rdeg) if trans else (sup.nbr, sup.deg)
-    W = _f32c(W.reshape(W.shape[0], -1))
-    d = L.GcnAfDesc()
-    d.x, d.out, d.A, d.M, d.w = x.data_ptr(), out.data_ptr(), A.data_ptr(), L.ptr(None if M is None else _dense(M)), \
-        W.data_ptr()
-    d.nbr, d.deg, d.bias, d.stats = nbr.data_ptr(), deg.data_ptr(), L.ptr(bias), L.ptr(stats)
-    d.NT, d.V, d.P, d.J, d.trans = N * T, V, A.shape[0], sup.J, int(trans)
-    d.x_ld, d.out_ld, d.stats_ld, d.accumulate = rows_ld(x), rows_ld(out), stats_ld, int(accumulate)
-    if res is not None:
-        rr, rbits = res
-        d.res, d.res_bits, d.res_ld = rr.data_ptr(), rbits.data_ptr(), rows_ld(rr)
-    hook = EVENT_HOOK if tag is not None else None
-    if hook:
-        hook(tag, "start", None)
-    L.check(L.lib().stgcn_gcn_af(d, L.stream()), "gcn_af")
-    if hook:
-        hook(tag, "end", None)
-    return out
-
-
 def gconv_wgrad_rowsum_ok(sup, Cin, Cout, dtype) -> bool:
     """Whether gconv_wgrad can also return the per-joint row sums of dy (joint-grouped kernel only)."""
     return dtype == torch.bfloat16 and Cin % 64 == 0 and Cout % 64 == 0 and sup.J <= 5

@@ -18,10 +18,6 @@ also assign the attributes directly.
     rt_one_launch       STGCN_RT_ONE_LAUNCH=0 per-frame RT-ST-GCN inference (LayerNorm, config 3) as ONE persistent launch with
                                               in-launch grid barriers (stgcn_rt_frame) instead of 2 launches per layer
                                               (default on)
-    gcn_af              STGCN_GCN_AF=1        the 64->64 graph conv of the training layer (forward with BN partials, data gradient
-                                              with the masked residual) through the A-first persistent kernel gcn_af.hip
-                                              (joint mix, then one GEMM with W shared by all joints) instead of the
-                                              joint-gathered GEMM gconv.hip (default off until it wins)
     prep_plan           STGCN_PREP_PLAN=0     stgcn.Model training forwards pack every weight per call instead of
                                               in the one-launch plan (native.PrepPlan; default on)
 
@@ -44,7 +40,6 @@ class _Routing:
         self.bn_mask_bits = e("STGCN_BN_BITS", "1") != "0"
         self.prep_plan = e("STGCN_PREP_PLAN", "1") != "0"
         self.rt_one_launch = e("STGCN_RT_ONE_LAUNCH", "1") != "0"
-        self.gcn_af = e("STGCN_GCN_AF", "0") != "0"
 
 
 ROUTING = _Routing()

@@ -42,11 +42,6 @@ def test_abi_rejects_bad_args_without_gpu(pkg):
     assert lib.stgcn_gconv_wgrad(g, 1, None) == 1
     r = L.RtFrameDesc()                                 # null pointers: refused before the barrier-counter memset
     assert lib.stgcn_rt_frame(r, None) == 1
-    f = L.GcnAfDesc(x=16, out=16, A=16, w=16, nbr=16, deg=16, NT=8, V=26, P=3, J=4, x_ld=64, out_ld=64)
-    assert lib.stgcn_gcn_af(f, None) == 1               # V > 25: no A-first kernel form
-    f.V, f.res = 25, 16                                 # a masked residual without its sign bits
-    assert lib.stgcn_gcn_af(f, None) == 1
-    assert lib.stgcn_gcn_af_blocks(64 * 300, 25) == 512 and lib.stgcn_gcn_af_blocks(6, 25) == 2
 
 
 @pytest.mark.parametrize("key,name", [("pku_mmd", "pku-mmd"), ("ntu_rgbpd", "ntu"), ("openpose", "op"),
@@ -255,7 +250,7 @@ def test_descriptor_layouts_match_header(pkg, tmp_path):
     the library read garbage).  Compiled with gcc on the host: no GPU, no HIP headers (the header is plain C)."""
     L = pkg._lib
     structs = {"stgcn_conv_desc": L.ConvDesc, "stgcn_wgrad_desc": L.WgradDesc, "stgcn_amix_desc": L.AmixDesc,
-               "stgcn_gconv_desc": L.GconvDesc, "stgcn_gcn_af_desc": L.GcnAfDesc,
+               "stgcn_gconv_desc": L.GconvDesc,
                "stgcn_gconv_wgrad_desc": L.GconvWgradDesc, "stgcn_bn_bwd_desc": L.BnBwdDesc,
                "stgcn_layer_fused_desc": L.LayerFusedDesc, "stgcn_prep_job": L.PrepJob,
                "stgcn_adam_entry": L.AdamEntry, "stgcn_rt_layer": L.RtLayer, "stgcn_rt_frame_desc": L.RtFrameDesc}

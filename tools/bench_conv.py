@@ -138,10 +138,3 @@ for name, N, T, Cin, Cout in gcases:
     ms = timeit(lambda: K.gconv_wgrad(x, dg, sup, Cin, Cout))
     print(f"{name.replace('fwd', 'wgrad'):22s} {ms*1e3:9.1f} us  {flops/ms/1e9:8.1f} TFLOP/s", flush=True)
 
-    if Cin == 64 and Cout == 64 and (not only or only.startswith("gcn_af") or only.startswith("gconv")):
-        # the A-first form of the same 64 -> 64 graph conv (gcn_af.hip), same inputs
-        sta = torch.zeros((K.gcn_af_blocks(N * T, V), 64, 4), device=dev)
-        for tag, f in (("gcn_af_fwd_c64", lambda: K.gcn_af(x, A0, W, sup, bias=b2, stats=sta)),
-                       ("gcn_af_dgrad_c64", lambda: K.gcn_af(dg, A0, W, sup, trans=True))):
-            ms = timeit(f)
-            print(f"{tag:22s} {ms*1e3:9.1f} us  {flops/ms/1e9:8.1f} TFLOP/s  {byts/ms/1e6:8.1f} GB/s", flush=True)
