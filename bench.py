@@ -86,7 +86,8 @@ def spawn_ranks(args):
 
 # The roofline kernel (`roofline`): the step's largest kernel by time in the rocprofv3 summary,
 # gconv_wgrad3_kernel — the graph-conv weight gradient dWeff[w][j] = dy[:, w]^T x[:, S(w)_j] (gconv.hip), 8
-# launches per step (64->64 x3, 128->128 x2, 256->256 x2, 128->256 x1; the 64->128 layer runs gconv_wgrad2).  Its C-ABI
+# launches per step (64->64 x3, 128->128 x2, 256->256 x2 as gconv_wgrad3w_kernel (128 x 128 groups), 128->256 x1; the
+# 64->128 layer runs gconv_wgrad2).  Its C-ABI
 # call is split (stgcn_gconv_wgrad_desc.phase) so HIP events bracket the kernel alone, not its slab reduction.
 # Algorithmic work per launch: 2*N*T*nnz(S)*Cin*Cout flops over (x + dy) = N*T*V*(Cin+Cout)*2 bytes; the bound is the
 # roof the launches' aggregate intensity falls under (HBM: ~228 flop/B < the ~312 ridge).
@@ -232,9 +233,11 @@ def gwgrad_roofline(gw, world):
                    "mfma_frac": round(fl / (a_us * 1e-6) / 1e12 / BF16_DENSE_PEAK_TFLOPS, 4),
                    "hbm_frac": round(nb / (a_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                    "pmc_hbm_bytes": per.get(sh)})
-    return {"kernel": "gconv_wgrad3_kernel (graph-conv weight gradient dWeff = dy^T x per (joint, neighbour) pair, "
-                      "DMA-ring, the step's largest kernel in the rocprofv3 summary; 8 launches/step, bracketed "
-                      "alone by HIP events, its slab reduction outside)",
+    return {"kernel": "gconv_wgrad3_kernel + gconv_wgrad3w_kernel (graph-conv weight gradient dWeff = dy^T x per "
+                      "(joint, neighbour) pair, DMA-ring; the C = 256 launches run the 128 x 128 wide plan; the step's "
+                      "largest kernel family in the rocprofv3 summary; 8 launches/step, bracketed alone by HIP events, "
+                      "the slab reduction outside)",
+            "rocprof_kernels": ["gconv_wgrad3_kernel", "gconv_wgrad3w_kernel"],
             "bound": "mfma" if mfma else "hbm", "achieved": round(tf if mfma else gbs, 2),
             "peak": BF16_DENSE_PEAK_TFLOPS if mfma else HBM_PEAK_GBS, "unit": "TFLOP/s" if mfma else "GB/s",
             "frac": round((tf / BF16_DENSE_PEAK_TFLOPS) if mfma else (gbs / HBM_PEAK_GBS), 4),

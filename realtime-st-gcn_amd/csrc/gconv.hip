@@ -1062,6 +1062,277 @@ __global__ __launch_bounds__(256, LDSB > 80 * 1024 ? 1 : 2) void gconv_wgrad3_ke
   }
 }
 
+// ---- wide plan (Cin, Cout % 128 == 0): block = (joint, 128 co x 128 ci group, row part), 4 waves (one per SIMD, 2 x 2
+// output tiles per neighbour each: 64*DEG accumulators, up to 512 registers per lane) and a 160 KB ring.  Against the 64 x 64 blocks above it halves the panels every block stages per MFMA (dy read by
+// Cin/128 instead of Cin/64 blocks, x by Cout/128) and gives each barrier twice the matrix work per SIMD.  Row
+// parts of one group merge in-kernel: every part publishes its partial write-through (sc1), takes a ticket, and
+// the last arriver sums the R partials in part-index order (a fixed order: the result does not depend on
+// arrival), then writes dWeff, the zero slots and the row sums.
+#ifndef STGCN_W3W
+#define STGCN_W3W 1
+#endif
+#ifndef STGCN_W3W_TARGET
+#define STGCN_W3W_TARGET 256
+#endif
+constexpr int W3W_LDS = 160 * 1024;
+constexpr int W3W_PSZ_J = 128 * 128;
+constexpr int W3W_JE = 3;  // neighbours per entry at most: joints of degree >= 4 run as two entries
+constexpr int w3w_stage(int deg) { return (4 + 4 * deg) * 32 * WPR; }
+constexpr int w3w_d(int deg) { return W3W_LDS / w3w_stage(deg) > 8 ? 8 : W3W_LDS / w3w_stage(deg); }
+
+template <int DEG>
+DEV void wgrad3w_body(const stgcn_gconv_wgrad_desc& a, const WGG& g, char* smem, int w, int e, int j0, int dtot, int rr,
+                      int grp, int t0, int t1) {
+  constexpr int D = w3w_d(DEG), PANEL = 32 * WPR, STAGE = w3w_stage(DEG), NU = 2 * (1 + DEG);
+  static_assert(D >= 3 && (D - 2) * NU <= 63, "ring");
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cp = wave & 1, ip = wave >> 1;  // co tiles 2cp, 2cp+1 and ci tiles 2ip, 2ip+1 (32 each) of the group
+  const int V = a.V;
+  const int co0 = (grp % g.nco) * 128, ci0 = (grp / g.nco) * 128;
+  const bf16* __restrict__ dy = reinterpret_cast<const bf16*>(a.dy);
+  const bf16* __restrict__ x = reinterpret_cast<const bf16*>(a.x);
+  // DMA share of a tile: panel `wave` of dy and of every neighbour's x, both 16-row halves;
+  // lane -> (row lane / 4 (+16), 16-B unit lane % 4)
+  const int prow = lane >> 2, pu = lane & 3;
+  const bf16* ysrc = dy + (long)w * a.dy_ld + co0 + wave * 32 + pu * 8;
+  const bf16* xsrc[DEG];
+#pragma unroll
+  for (int j = 0; j < DEG; ++j) xsrc[j] = x + (long)a.nbr[w * a.J + j0 + j] * a.x_ld + ci0 + wave * 32 + pu * 8;
+  const long ystep = (long)V * a.dy_ld, xstep = (long)V * a.x_ld;
+  const unsigned ring = lds_u32(smem);
+  const unsigned woff = (unsigned)(wave * PANEL);
+  auto issue = [&](int t) {
+    const unsigned slot = ring + (unsigned)(((t - t0) % D) * STAGE) + woff;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int i = min(t * 32 + 16 * h + prow, a.NT - 1);  // rows past NT: clamped here, dy zeroed in LDS below
+      glds16m(ysrc + i * ystep, slot + (unsigned)(h * 1024));
+#pragma unroll
+      for (int j = 0; j < DEG; ++j) glds16m(xsrc[j] + i * xstep, slot + (unsigned)((4 + 4 * j) * PANEL + h * 1024));
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < D - 1; ++k)
+    if (t0 + k < t1) issue(t0 + k);
+
+  f32x16 acc[DEG][2][2];
+#pragma unroll
+  for (int j = 0; j < DEG; ++j)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][u][c][r] = 0.f;
+  const bool rsum = g.rowpart != nullptr && grp / g.nco == 0 && j0 == 0;  // an entry's first neighbour slot: row sums
+  float sacc[2][8];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sacc[h][e] = 0.f;
+  // dy units of this thread (row sums, zeroing past NT): unit tid + 256 h -> row (unit / 16), channels (unit % 16) * 8
+  auto soff = [&](int h) {
+    const int u = tid + 256 * h, sr = u >> 4, sc = u & 15;
+    return (sc >> 2) * PANEL + sr * WPR + (sc & 3) * 16;
+  };
+
+  for (int t = t0; t < t1; ++t) {
+    const int after = min(D - 2, t1 - 1 - t);  // tiles issued after t
+    sfor<D - 1>([&]<int m>() {
+      if (after == m) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(m * NU) : "memory");
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (t + D - 1 < t1) issue(t + D - 1);  // into the slot of tile t - 1, free after the barrier
+    char* base = smem + ((t - t0) % D) * STAGE;
+    if (t * 32 + 32 > a.NT) {  // last, partial tile: zero dy rows >= NT (block-uniform branch)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (t * 32 + ((tid + 256 * h) >> 4) >= a.NT) *reinterpret_cast<uint4*>(base + soff(h)) = make_uint4(0, 0, 0, 0);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    if (rsum) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float f[8];
+        unpack16(*reinterpret_cast<const uint4*>(base + soff(h)), f, (bf16*)nullptr);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sacc[h][e] += f[e];
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 fa[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) fa[u] = trfrag(base + (2 * cp + u) * PANEL, ks * 16, lane);
+#pragma unroll
+      for (int j = 0; j < DEG; ++j) {
+        bf16x8 fb[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) fb[c] = trfrag(base + (4 + 4 * j + 2 * ip + c) * PANEL, ks * 16, lane);
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+            acc[j][u][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[u], fb[c], acc[j][u][c], 0, 0, 0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  float rs = 0.f;  // this block's row sum of column co0 + tid (tid < 128)
+  if (rsum) {      // [row][128] in LDS (first 16 KB), fixed-order column sums
+    float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int u = tid + 256 * h;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[(u >> 4) * 128 + (u & 15) * 8 + k] = sacc[h][k];
+    }
+    __syncthreads();
+    if (tid < 128)
+      for (int r = 0; r < 32; ++r) rs += red[r * 128 + tid];
+  }
+  // Epilogue through LDS, one neighbour at a time: the 128 x 128 tile staged as fp32 rows [co][132], then whole
+  // 512-B rows leave as 16-B stores (every address an LDS immediate or one running pointer: no per-element
+  // address registers next to the 64*DEG accumulators)
+  constexpr int SRS = 132;
+  float* stg = reinterpret_cast<float*>(smem + 20 * 1024);  // after the row sums and the ticket word
+  int* flag = reinterpret_cast<int*>(smem + 16 * 1024);
+  const bool merged = g.R > 1;
+  const int ngrp = g.nco * g.nci;
+  const long PSZ = (long)W3W_JE * W3W_PSZ_J + 128;
+  float* gp = merged ? g.part + ((long)e * ngrp + grp) * g.R * PSZ : nullptr;
+  const __amdgpu_buffer_rsrc_t prs =
+      __builtin_amdgcn_make_buffer_rsrc(merged ? gp : g.slab, 0, merged ? (int)(g.R * PSZ * 4) : 0, 0x00020000);
+  float* o0 = g.slab + (long)w * a.J * a.Cout * a.Cin + (long)co0 * a.Cin + ci0;  // dWeff[w][0][co0][ci0]
+  const long ojs = (long)a.Cout * a.Cin;
+#pragma unroll
+  for (int j = 0; j < DEG; ++j) {
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          stg[(cp * 64 + u * 32 + acc_row(r, lane)) * SRS + ip * 64 + c * 32 + (lane & 31)] = acc[j][u][c][r];
+    __syncthreads();
+    for (int e = tid; e < 128 * 32; e += 256) {
+      const int row = e >> 5, q4 = e & 31;
+      const float4 v = *reinterpret_cast<const float4*>(stg + row * SRS + q4 * 4);
+      if (!merged)
+        *reinterpret_cast<float4*>(o0 + (j0 + j) * ojs + (long)row * a.Cin + q4 * 4) = v;
+      else  // this part's partial, write-through (sc1): the last arriver reads it from another CU / XCD
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), prs,
+                                               (int)(((long)rr * PSZ + j * W3W_PSZ_J + row * 128 + q4 * 4) * 4), 0, 16);
+    }
+  }
+  if (merged) {
+    if (rsum && tid < 128)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, rs), prs,
+                                            (int)(((long)rr * PSZ + W3W_JE * W3W_PSZ_J + tid) * 4), 0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+      *flag = (int)__hip_atomic_fetch_add(g.cnt + (long)e * ngrp + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (*flag != g.R - 1) return;  // not the last part: the last arriver merges
+    // the R partials summed in part-index order (a fixed order: the result does not depend on arrival)
+    for (int j = 0; j < DEG; ++j)
+      for (int e = tid; e < 128 * 32; e += 256) {
+        const int row = e >> 5, q4 = e & 31;
+        const int off = (j * W3W_PSZ_J + row * 128 + q4 * 4) * 4;
+        float4 sum = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(prs, off, 0, 16));
+        for (int k = 1; k < g.R; ++k) {
+          const float4 v =
+              __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(prs, (int)(off + k * PSZ * 4), 0, 16));
+          sum.x += v.x;
+          sum.y += v.y;
+          sum.z += v.z;
+          sum.w += v.w;
+        }
+        *reinterpret_cast<float4*>(o0 + (j0 + j) * ojs + (long)row * a.Cin + q4 * 4) = sum;
+      }
+    if (rsum && tid < 128) {
+      rs = 0.f;
+      for (int k = 0; k < g.R; ++k) {
+        const float v = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(prs, (int)((k * PSZ + W3W_JE * W3W_PSZ_J + tid) * 4), 0, 16));
+        rs = k == 0 ? v : rs + v;
+      }
+    }
+  }
+  if (rsum && tid < 128) g.rowpart[(long)w * a.Cout + co0 + tid] = rs;
+  if (j0 == 0)
+  for (int j = dtot; j < a.J; ++j)  // the unused slots of this joint and group: zero (by the joint's first entry)
+    for (int e = tid; e < 128 * 32; e += 256)
+      *reinterpret_cast<float4*>(o0 + j * ojs + (long)(e >> 5) * a.Cin + (e & 31) * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+__global__ __launch_bounds__(256, 1) void gconv_wgrad3w_kernel(const stgcn_gconv_wgrad_desc a, const WGG g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int ngrp = g.nco * g.nci;
+  const int bid = blockIdx.x;
+  const int e = bid / (ngrp * g.R), rem = bid % (ngrp * g.R);
+  const int rr = rem / ngrp, grp = rem % ngrp;
+  // entries (joint, first neighbour slot, neighbour count) in decreasing-degree joint order (the heaviest blocks
+  // are dispatched first); a joint of degree >= 4 runs as two entries of <= 3 neighbours (its dy panels are staged
+  // twice, but 64*deg accumulators would exceed the register file and its ring would be shallow).  Scratch in the
+  // ring's first bytes, read before any DMA is issued.  Grid: 2V entries (the ones past the count exit at once).
+  int* sdeg = reinterpret_cast<int*>(smem);
+  int* order = sdeg + 64;
+  int* ent = order + 64;  // [0] = count, then (joint, j0, n) triples
+  const int tid = threadIdx.x;
+  if (tid < a.V) sdeg[tid] = a.deg[tid];
+  __syncthreads();
+  if (tid < a.V) {
+    const int d = sdeg[tid];
+    int r = 0;
+    for (int u = 0; u < a.V; ++u) r += (sdeg[u] > d) | ((sdeg[u] == d) & (u < tid));
+    order[r] = tid;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int E = 0;
+    for (int r = 0; r < a.V; ++r) {
+      const int w = order[r], d = sdeg[w];
+      if (d > W3W_JE) {
+        const int h = (d + 1) / 2;
+        ent[1 + 3 * E] = w, ent[2 + 3 * E] = 0, ent[3 + 3 * E] = h, ++E;
+        ent[1 + 3 * E] = w, ent[2 + 3 * E] = h, ent[3 + 3 * E] = d - h, ++E;
+      } else {
+        ent[1 + 3 * E] = w, ent[2 + 3 * E] = 0, ent[3 + 3 * E] = d, ++E;
+      }
+    }
+    ent[0] = E;
+  }
+  __syncthreads();
+  const int E = ent[0];
+  const int wj = e < E ? ent[1 + 3 * e] : 0, j0 = e < E ? ent[2 + 3 * e] : 0, n = e < E ? ent[3 + 3 * e] : 0;
+  const int dtot = e < E ? sdeg[wj] : 0;
+  __syncthreads();  // every thread has its entry: the ring may overwrite the scratch
+  if (e >= E) return;
+  const int t0 = rr * g.tpb, t1 = min(g.ntile, t0 + g.tpb);
+  switch (n) {
+    case 1: wgrad3w_body<1>(a, g, smem, wj, e, j0, dtot, rr, grp, t0, t1); break;
+    case 2: wgrad3w_body<2>(a, g, smem, wj, e, j0, dtot, rr, grp, t0, t1); break;
+    case 3: wgrad3w_body<3>(a, g, smem, wj, e, j0, dtot, rr, grp, t0, t1); break;
+    default:  // deg 0: no pairs; part 0 writes the zero slots and the row sums
+      if (rr != 0) break;
+      const int co0 = (grp % g.nco) * 128, ci0 = (grp / g.nco) * 128;
+      if (g.rowpart != nullptr && grp / g.nco == 0 && tid < 128) {
+        const bf16* dy = reinterpret_cast<const bf16*>(a.dy);
+        float s = 0.f;
+        for (int i = 0; i < a.NT; ++i) s += (float)dy[((long)i * a.V + wj) * a.dy_ld + co0 + tid];
+        g.rowpart[(long)wj * a.Cout + co0 + tid] = s;
+      }
+      for (int i = tid; i < a.J * 128 * 128; i += blockDim.x) {
+        const int j = i >> 14, co = (i >> 7) & 127, ci = i & 127;
+        g.slab[(((long)wj * a.J + j) * a.Cout + co0 + co) * a.Cin + ci0 + ci] = 0.f;
+      }
+      break;
+  }
+}
+
 // fp32 parity path of the gather wgrad: one thread per (pair, co, ci), loop over rows (small sizes)
 __global__ void gconv_wgrad_f32_kernel(const stgcn_gconv_wgrad_desc a) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1386,6 +1657,35 @@ WGG wplan2(const stgcn_gconv_wgrad_desc& a, int cob) {
   return g;
 }
 
+// taken where the machine fills with at most 2 row parts (C = 256: 100 groups; tools/bench_conv.py, us, wide vs the
+// 64 x 64 plans: C = 256 98.7 vs 101.5; with more parts the last arriver's serial merge of R partials dominates:
+// C = 128 (R = 8) 162 vs 73.5, 128 -> 256 (R = 4) 156 vs 126)
+bool w3w_ok(const stgcn_gconv_wgrad_desc& a) {
+  if (!STGCN_W3W || a.Cin % 128 || a.Cout % 128 || a.V > 64 || a.J > 2 * W3W_JE) return false;
+  const long groups = (long)a.V * (a.Cout / 128) * (a.Cin / 128);
+  return STGCN_W3W_TARGET / groups <= 2;
+}
+WGG wplan3w(const stgcn_gconv_wgrad_desc& a) {
+  WGG g{};
+  g.ntile = (a.NT + 31) / 32;
+  g.nco = a.Cout / 128;
+  g.nci = a.Cin / 128;
+  const long groups = (long)a.V * g.nco * g.nci;
+  long R = STGCN_W3W_TARGET / groups;
+  if (R > g.ntile) R = g.ntile;
+  if (R < 1) R = 1;
+  g.tpb = (int)((g.ntile + R - 1) / R);
+  g.R = (g.ntile + g.tpb - 1) / g.tpb;
+  return g;
+}
+// wide plan workspace: part partials [2V entries][ngrp][R][3*16384 + 128] floats, then the arrival counters [2V*ngrp]
+long w3w_part_floats(const stgcn_gconv_wgrad_desc& a, const WGG& g) {
+  return g.R > 1 ? 2L * a.V * g.nco * g.nci * g.R * ((long)W3W_JE * W3W_PSZ_J + 128) : 0;
+}
+long w3w_cnt_bytes(const stgcn_gconv_wgrad_desc& a, const WGG& g) {
+  return g.R > 1 ? ((2L * a.V * g.nco * g.nci * 4) + 15) / 16 * 16 : 0;
+}
+
 WGG wplan(const stgcn_gconv_wgrad_desc& a) {
   WGG g{};
   g.ntile = (a.NT + WKM - 1) / WKM;
@@ -1460,6 +1760,10 @@ long w3_split_cnt_bytes(const stgcn_gconv_wgrad_desc& a, const WGG& g) {
 long gconv_wgrad_workspace(const stgcn_gconv_wgrad_desc& a, int dtype) {
   if (dtype != 1) return 0;
   const int cob = w2_cob(a);
+  if (cob && w3w_ok(a)) {
+    const WGG g = wplan3w(a);
+    return w3w_part_floats(a, g) * (long)sizeof(float) + w3w_cnt_bytes(a, g);
+  }
   const WGG g = cob ? wplan2(a, cob) : wplan(a);
   if (cob && w3_ok(a) && g.R == 1)  // direct
     return STGCN_W3_SPLIT ? w3_split_part_floats(a, g) * (long)sizeof(float) + w3_split_cnt_bytes(a, g) : 0;
@@ -1478,6 +1782,24 @@ int gconv_wgrad_launch(const stgcn_gconv_wgrad_desc& a, int dtype, hipStream_t s
   }
   if (a.Cin % 8 || a.Cout % 8 || a.x_ld % 8 || a.dy_ld % 8) return STGCN_EBADSHAPE;
   const int cob = w2_cob(a);
+  if (cob && w3w_ok(a)) {  // wide plan: direct, row parts merged in-kernel
+    if (a.phase == 2) return STGCN_OK;
+    WGG g = wplan3w(a);
+    g.slab = a.dweff;
+    g.rowpart = a.rowsum;
+    g.zero_unused = 1;
+    if (g.R > 1) {
+      const long pf = w3w_part_floats(a, g), cb = w3w_cnt_bytes(a, g);
+      if (!a.work || a.work_bytes < pf * (long)sizeof(float) + cb) return STGCN_EBADSHAPE;
+      g.part = reinterpret_cast<float*>(a.work);
+      g.cnt = reinterpret_cast<unsigned*>(g.part + pf);
+      if (hipMemsetAsync(g.cnt, 0, (size_t)cb, s) != hipSuccess) return STGCN_EHIP;
+    }
+    if (stgcn_lds_attr((const void*)gconv_wgrad3w_kernel, W3W_LDS, s)) return STGCN_EHIP;
+    const long blocks = 2L * a.V * g.nco * g.nci * g.R;
+    hipLaunchKernelGGL(gconv_wgrad3w_kernel, dim3((unsigned)blocks), dim3(256), W3W_LDS, s, a, g);
+    return hipGetLastError() == hipSuccess ? STGCN_OK : STGCN_EHIP;
+  }
   if (cob) {
     WGG g = wplan2(a, cob);
     const bool ring = cob == 64 && w3_ok(a);

@@ -41,6 +41,14 @@ def test_roofline_kernel_matches_rocprof():
     b = json.load(open(bench))
     m = re.match(r"(\w+)(?:<([^>]*)>)?", b["roofline"]["kernel"])
     name = m.group(1)
+    if b["roofline"].get("rocprof_kernels"):  # a kernel family: the call-weighted mean over its kernels' rows
+        names = b["roofline"]["rocprof_kernels"]
+        rows = [r for r in csv.DictReader(open(stats))
+                if any(re.search(r"\b" + re.escape(n) + r"[<(]", r["Name"]) for n in names)]
+        assert rows, names
+        prof_ms = sum(float(r["TotalDurationNs"]) for r in rows) / sum(int(r["Calls"]) for r in rows) / 1e6
+        assert abs(prof_ms - b["roofline"]["avg_launch_ms"]) / prof_ms < 0.10
+        return
     if m.group(2) is not None:
         # the bench names the leading template arguments; the trailing (defaulted) ones may be omitted
         targs = [t.strip() for t in m.group(2).split(",")]

@@ -30,7 +30,7 @@ def ref_gcn(x, A, W, b):
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 2e-2)])
 @pytest.mark.parametrize("Cin,Cout,N,T", [(64, 64, 3, 37), (128, 256, 2, 19), (8, 64, 2, 11), (256, 128, 2, 7),
-                                          (24, 40, 3, 5)])
+                                          (24, 40, 3, 5), (256, 256, 2, 9)])
 def test_gconv_fwd_bwd(K, pkg, dtype, tol, Cin, Cout, N, T):
     torch.manual_seed(3)
     A0 = torch.tensor(pkg.Graph(**pkg.PKU_MMD).A, dtype=torch.float32)
@@ -149,8 +149,8 @@ def test_gconv_dgrad_masked_residual(K, pkg, Cin, Cout):
 def test_gconv_wgrad_phases(K, pkg, Cin, Cout, N, T):
     """stgcn_gconv_wgrad split into its accumulation kernel (phase 1) and its slab reduction (phase 2) — what
     bench.py's roofline brackets — writes exactly what the one-call form (phase 0) writes, for a slab plan (64 -> 64,
-    128 -> 256) and the degree-balanced direct plan (256 -> 256: joints of degree >= 4 as two half-row-range blocks
-    merged in-kernel; a + b == b + a, so the merge order does not change a bit)."""
+    128 -> 256) and the wide plan (256 -> 256: 128 x 128 groups, two row parts merged in-kernel by the last arriver
+    in part-index order, so the arrival order does not change a bit)."""
     import ctypes
     torch.manual_seed(9)
     A0 = torch.tensor(pkg.Graph(**pkg.PKU_MMD).A, dtype=torch.float32)
