@@ -374,6 +374,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-layer-roofline", action="store_true", help="skip the north_star layer timing (profiling)")
     ap.add_argument("--graph", action="store_true", help="config 2: replay the step as HIP graphs")
+    ap.add_argument("--sync-bn", action="store_true",
+                    help="N > 1: SyncBatchNorm statistics over the ranks (syncbn.py) instead of the reference's "
+                         "per-replica DataParallel statistics (the default)")
     ap.add_argument("--kernel-steps", type=int, default=3,
                     help="eager steps after the timed region whose kernel-wrapper launches are timed one by one "
                          "(the `kernels` table); 0 = off")
@@ -408,6 +411,10 @@ def main():
     model = model.to(dev).set_compute_dtype(args.dtype)
     params = [p for p in model.parameters() if p.requires_grad]
     train_model = model
+    if args.sync_bn:
+        if args.graph:
+            sys.exit("bench.py: --sync-bn exchanges statistics inside the forward (eager DDP step only)")
+        pkg.convert_sync_batchnorm(model)
     if world > 1 and not args.graph:
         train_model = par.ddp(model, dev)  # RCCL all-reduce in 4 MB buckets, overlapped with bwd
     elif world > 1:  # identical replicas (DistributedDataParallel's broadcast from rank 0)
@@ -580,6 +587,7 @@ def main():
             "data": "synthetic (randn skeletons, random labels/class weights), random-init weights",
             "config": {"workload": workload, "global_batch": N_BATCH * world, "seq_len": T_LEN, "joints": V_J,
                        "parallelism": f"dp{world}" if world > 1 else "single",
+                       "bn_stats": "sync (all ranks)" if args.sync_bn and world > 1 else "per-replica",
                        "launch": "eager" if not args.graph else "hip-graph replay (fwd+bwd | allreduce | Adam)"},
             "roofline": roof,
             "roofline_tcn_fwd": {"kernel": "conv_wide_kernel<128,9,8,1,0,64> (persistent warp-specialised Kt=9 "

@@ -30,8 +30,9 @@ extern "C" {
  *   3: round 6 (stgcn_gcn_tile removed; stgcn_layer_fused_desc is the LayerNorm layer only: the BatchNorm
  *      fields n1_scale / n1_shift / stats / ln / g_in / g_in_ld and stgcn_layer_fused_row_blocks removed);
  *   4: round 6 (stgcn_rt_frame + stgcn_rt_layer / stgcn_rt_frame_desc: the RT per-frame step in one launch;
- *      stgcn_gconv_wgrad_desc gained phase). */
-#define STGCN_ABI_VERSION 4
+ *      stgcn_gconv_wgrad_desc gained phase);
+ *   5: round 6 (stgcn_bn_merge: one (count, mean, M2) entry per channel, the SyncBatchNorm exchange unit). */
+#define STGCN_ABI_VERSION 5
 
 /* Implicit-GEMM (Kt x 1) row convolution; see conv_rows.hip for the exact contract.
  * Replaces: nn.Conv2d tcn.2 (models/stgcn/stgcn.py:154-159), residual.0 (stgcn.py:165-170),
@@ -218,6 +219,12 @@ long stgcn_bn_stat_blocks(long M);
 int stgcn_bn_stats_partial(const void* x, int ld, long M, int C, void* part_f4, int dtype, void* stream);
 int stgcn_bn_finalize(const void* part_f4, int nblocks, int ld_part, int C, const float* gamma, const float* beta,
                       float eps, void* mean_rstd_f2, float* scale, float* shift, void* stream);
+/* merged_f4[c] = the nblocks partials of channel c merged (fp64) into ONE (count, mean, M2, 0) entry: a rank's
+ * contribution to SyncBatchNorm (torch.nn.SyncBatchNorm's batch_norm_gather_stats_with_counts role, the
+ * north_star's optional SyncBN); the gathered [ranks][C] entries go back through stgcn_bn_finalize
+ * (nblocks = ranks, ld_part = C).  No reference counterpart: the reference's DataParallel keeps per-replica
+ * statistics (processor.py:32-33). */
+int stgcn_bn_merge(const void* part_f4, int nblocks, int ld_part, int C, void* merged_f4, void* stream);
 /* Fused BatchNorm backward (two row passes), see bn_fused.hip:
  *   reduce: dz = dy*mask; sums[c] = (sum dz, sum dz*xhat1, sum dz*xhat2, 0)
  *   apply : out1 = g1*rstd1*(dz - S0/M - xhat1*S1/M) (or dz when x1 == NULL);

@@ -4,7 +4,8 @@ Loaded by path (the directory name has dashes): see ``__graft_entry__.load_packa
 Public surface mirrors maximyudayev/Realtime-ST-GCN: ``MODELS`` (models/__init__.py:11-20),
 ``Graph``, ``StgcnLayer``, ``ConvTemporalGraphical``, ``LayerNorm``, ``BatchNorm1d``.
 """
-from . import _lib, data, loss, metrics, native, optim, parallel, routing, segment  # noqa: F401
+from . import _lib, data, loss, metrics, native, optim, parallel, routing, segment, syncbn  # noqa: F401
+from .syncbn import convert_sync_batchnorm, revert_sync_batchnorm  # noqa: F401
 from .graph import Graph, PKU_MMD  # noqa: F401
 from .modules import BatchNorm1d, ConvTemporalGraphical, LayerNorm, StgcnLayer, set_compute_dtype  # noqa: F401
 from .stgcn import Model as Stgcn  # noqa: F401

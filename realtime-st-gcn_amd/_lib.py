@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("STGCN_LIB") or os.path.join(_HERE, "lib", "libstgcn_amd.so")  # STGCN_LIB: A/B builds
 
 # the STGCN_ABI_VERSION of include/stgcn_amd.h these bindings mirror (test_cpu_host checks the two agree)
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _ERR = {1: "bad shape/arguments", 2: "unsupported dtype", 3: "HIP launch error"}
 
@@ -142,6 +142,7 @@ _SIGS = {
     "stgcn_bn_stats_partial": (c_int, [c_void_p, c_int, c_long, c_int, c_void_p, c_int, c_void_p]),
     "stgcn_bn_finalize": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p, c_void_p,
                                   c_void_p, c_void_p]),
+    "stgcn_bn_merge": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "stgcn_bn_apply": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,
                                c_int, c_void_p, c_int, c_long, c_int, c_int, c_void_p]),
     "stgcn_bn_apply_bits": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p,

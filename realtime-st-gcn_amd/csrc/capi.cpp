@@ -59,6 +59,7 @@ long norm_stats_num_blocks(long M);
 int bn_stats_partial_launch(const void* x, int ld, long M, int C, float4* part, int dtype, hipStream_t s);
 int bn_finalize_launch(const float4* part, int nb, int ldp, int C, const float* gamma, const float* beta, float eps,
                        float2* mean_rstd, float* scale, float* shift, hipStream_t s);
+int bn_merge_launch(const float4* part, int nb, int ldp, int C, float4* merged, hipStream_t s);
 int bn_apply_launch(const void* u, int ldu, const float* sc, const float* sh, int res_mode, const void* r, int ldr,
                     const float* rsc, const float* rsh, int relu, void* y, int ldy, long M, int C, int dtype,
                     hipStream_t s,
@@ -314,6 +315,9 @@ int stgcn_bn_finalize(const void* part, int nb, int ldp, int C, const float* gam
                       void* mean_rstd, float* scale, float* shift, void* stream) {
   return bn_finalize_launch((const float4*)part, nb, ldp, C, gamma, beta, eps, (float2*)mean_rstd, scale, shift,
                             STREAM(stream));
+}
+int stgcn_bn_merge(const void* part, int nb, int ldp, int C, void* merged, void* stream) {
+  return bn_merge_launch((const float4*)part, nb, ldp, C, (float4*)merged, STREAM(stream));
 }
 int stgcn_bn_apply(const void* u, int ldu, const float* sc, const float* sh, int res_mode, const void* r, int ldr,
                    const float* rsc, const float* rsh, int relu, void* y, int ldy, long M, int C, int dtype,

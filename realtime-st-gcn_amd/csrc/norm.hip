@@ -94,7 +94,8 @@ __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const T* __restri
 // one block per channel: merge nb (count, mean, M2) partials in fp64
 __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float4* part, int nb, int ldp, int C,
                                                           const float* gamma, const float* beta, float eps,
-                                                          float2* mean_rstd, float* scale, float* shift) {
+                                                          float2* mean_rstd, float* scale, float* shift,
+                                                          float4* merged) {
   // fp64 power sums (n, sum n*mean, sum M2 + n*mean^2) instead of pairwise Chan merges: adds only (no
   // division chain), a wave reduction and one LDS step; at fp64 the final var = S2/n - mean^2 loses
   // ~1e-16 * mean^2/var, far below the fp32 result
@@ -139,6 +140,10 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float4* part, i
     const double m = tn > 0 ? t1 / tn : 0.0;
     double var = tn > 0 ? t2 / tn - m * m : 0.0;  // biased (BatchNorm)
     if (var < 0) var = 0;
+    if (merged) {  // merge-only mode (SyncBN): this rank's channel statistics as ONE (count, mean, M2) partial
+      merged[c] = make_float4((float)tn, (float)m, (float)(var * tn), 0.f);
+      return;
+    }
     const float rstd = (float)(1.0 / sqrt(var + (double)eps));
     const float mu = (float)m;
     mean_rstd[c] = make_float2(mu, rstd);
@@ -623,7 +628,17 @@ int bn_finalize_launch(const float4* part, int nb, int ldp, int C, const float* 
                        float2* mean_rstd, float* scale, float* shift, hipStream_t s) {
   const int nt = nb > 2048 ? 1024 : 256;  // one 8-load batch per thread where the list allows
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(nt), 0, s, part, nb, ldp, C, gamma, beta, eps, mean_rstd,
-                     scale, shift);
+                     scale, shift, (float4*)nullptr);
+  RET_HIP;
+}
+
+// the nb partials of each channel merged into one (count, mean, M2, 0) entry [C] — what a SyncBatchNorm rank
+// contributes; the gathered [ranks][C] entries are finalized by bn_finalize_launch(nb = ranks, ldp = C)
+int bn_merge_launch(const float4* part, int nb, int ldp, int C, float4* merged, hipStream_t s) {
+  if (!part || !merged || nb < 1 || C < 1 || ldp < C) return STGCN_EBADSHAPE;
+  const int nt = nb > 2048 ? 1024 : 256;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(nt), 0, s, part, nb, ldp, C, (const float*)nullptr,
+                     (const float*)nullptr, 0.f, (float2*)nullptr, (float*)nullptr, (float*)nullptr, merged);
   RET_HIP;
 }
 

@@ -28,6 +28,7 @@ import torch
 
 from . import native as K
 from .routing import ROUTING
+from .syncbn import active_sync
 
 BN, LN = "BatchNorm", "LayerNorm"
 
@@ -206,6 +207,9 @@ class StgcnLayerFunction(torch.autograd.Function):
         # __dict__ copy) and run in one thread per device, so each thread only ever touches its own sub-dict
         # (dict.setdefault is atomic under the GIL)
         cache = cfg[8].setdefault(("dev", str(dev)), {}) if len(cfg) > 8 and cfg[8] is not None else None
+        # SyncBatchNorm (syncbn.py): the statistics of every rank, else this rank's (the reference's DataParallel)
+        sync = cfg[10] if len(cfg) > 10 else None
+        bn_finalize = sync.finalize if sync is not None else K.bn_finalize
 
         # ---- graph convolution: g = sum_p A_p-mix(x) W_p + bias2d
         sup = cfg[5] if len(cfg) > 5 else None
@@ -247,7 +251,7 @@ class StgcnLayerFunction(torch.autograd.Function):
             r = K.conv_rows(x, wrp, Cin, Cout, cpr, kpr, T, T_out, Kt=1, stride=stride, pad=0,
                             bias=br.detach().float().contiguous(), stats=str_ if norm == BN else None)
             if norm == BN:
-                mrr, scr, shr = K.bn_finalize(str_, str_.shape[0], cpr, Cout, nrw.detach().float(), nrb.detach().float())
+                mrr, scr, shr = bn_finalize(str_, str_.shape[0], cpr, Cout, nrw.detach().float(), nrb.detach().float())
             else:
                 lsr = K.ln_stats(r, N * T_out, V, Cout)
 
@@ -271,7 +275,7 @@ class StgcnLayerFunction(torch.autograd.Function):
             g = K.conv_rows(XA, wgp, P * Cin, Cout, cpg, kpg, T, T, bias=bias2d, bias_mode=bmode,
                             stats=st1 if norm == BN else None)
         if norm == BN:
-            mr1, sc1, sh1 = K.bn_finalize(st1, st1.shape[0], cpg, Cout, n1w.detach().float(), n1b.detach().float())
+            mr1, sc1, sh1 = bn_finalize(st1, st1.shape[0], cpg, Cout, n1w.detach().float(), n1b.detach().float())
             pro1 = dict(pro=1, pro_a=sc1, pro_b=sh1)
         else:
             # LayerNorm: h = relu(LN1(g)) is materialised (one HBM-bound pass, ln.hip) and the temporal conv runs
@@ -291,7 +295,7 @@ class StgcnLayerFunction(torch.autograd.Function):
 
         # ---- y = relu(norm2(u) + res)
         if norm == BN:
-            mr2, sc2, sh2 = K.bn_finalize(st2, st2.shape[0], cpt, Cout, n2w.detach().float(), n2b.detach().float())
+            mr2, sc2, sh2 = bn_finalize(st2, st2.shape[0], cpt, Cout, n2w.detach().float(), n2b.detach().float())
             # the output's sign bits for the backward's ReLU mask (the fused BN backward reads them instead of y:
             # 1/16 of the bytes in both of its passes)
             ybits = torch.empty((M2, Cout // 8), dtype=torch.uint8, device=dev) \
@@ -347,6 +351,7 @@ class StgcnLayerFunction(torch.autograd.Function):
         dy = K.to_rows(dy, dtype)
         M1, M2 = N * T * V, N * T_out * V
         packs = ctx.cfg[9] if len(ctx.cfg) > 9 else None
+        sync = ctx.cfg[10] if len(ctx.cfg) > 10 else None
         grads = {}
         # the temporal / residual weight gradients come back in nn.Conv2d order, overwritten (conv_wgrad_w); the
         # graph-conv accumulation targets (dW, dA, per-joint row sums) are zero-filled only on the routes that
@@ -380,7 +385,7 @@ class StgcnLayerFunction(torch.autograd.Function):
             elif residual and not res_in_gconv:
                 kw.update(out2=dx)
                 dx_written = True
-            sums2, osum2 = K.bn_bwd_fused(dy, M2, Cout, **kw)
+            sums2, osum2 = K.bn_bwd_fused(dy, M2, Cout, sync=sync, **kw)
             grads["n2w"], grads["n2b"] = sums2[1], sums2[0]
             grads["bt"] = osum2[0]
             bt_done = True
@@ -389,8 +394,10 @@ class StgcnLayerFunction(torch.autograd.Function):
                 grads["br"] = osum2[1]
         elif norm == BN:
             s2 = K.bn_bwd_reduce(dy, M2, Cout, mask=1, mref=y, x=u, mean_rstd=mr2)
-            K.bn_bwd_apply(dy, M2, Cout, du, mask=1, mref=y, x=u, mean_rstd=mr2, gamma=n2w.detach().float(), sums=s2)
             grads["n2w"], grads["n2b"] = s2[:, 1].clone(), s2[:, 0].clone()
+            if sync is not None:
+                sync.all_reduce_sums(s2, M2)
+            K.bn_bwd_apply(dy, M2, Cout, du, mask=1, mref=y, x=u, mean_rstd=mr2, gamma=n2w.detach().float(), sums=s2)
         else:
             dgb2 = torch.zeros((2, Cout * V), dtype=torch.float32, device=dev)
             K.ln_bwd(dy, u, ls2, _flat_ln(n2w), _flat_ln(n2b), N * T_out, V, Cout, du, mask=1, mref=y, dgb=dgb2)
@@ -401,9 +408,11 @@ class StgcnLayerFunction(torch.autograd.Function):
                 dr = K.cl_empty(N, Cout, T_out, V, dtype, dev)
                 if norm == BN:
                     sr = K.bn_bwd_reduce(dy, M2, Cout, mask=1, mref=y, x=r, mean_rstd=strr)
+                    grads["nrw"], grads["nrb"] = sr[:, 1].clone(), sr[:, 0].clone()
+                    if sync is not None:
+                        sync.all_reduce_sums(sr, M2)
                     K.bn_bwd_apply(dy, M2, Cout, dr, mask=1, mref=y, x=r, mean_rstd=strr,
                                    gamma=nrw.detach().float(), sums=sr)
-                    grads["nrw"], grads["nrb"] = sr[:, 1].clone(), sr[:, 0].clone()
                 else:
                     dgbr = torch.zeros((2, Cout * V), dtype=torch.float32, device=dev)
                     K.ln_bwd(dy, r, strr, _flat_ln(nrw), _flat_ln(nrb), N * T_out, V, Cout, dr, mask=1, mref=y,
@@ -442,13 +451,15 @@ class StgcnLayerFunction(torch.autograd.Function):
         dg = K.cl_empty(N, Cout, T, V, dtype, dev)
         if fused:
             s1, _ = K.bn_bwd_fused(dh, M1, Cout, mask=2, mref=g, msc=sc1, msh=sh1, x1=g, mr1=mr1,
-                                   g1=n1w.detach().float(), out1=dg)
+                                   g1=n1w.detach().float(), out1=dg, sync=sync)
             grads["n1w"], grads["n1b"] = s1[1], s1[0]
         elif norm == BN:
             s1 = K.bn_bwd_reduce(dh, M1, Cout, mask=2, mref=g, msc=sc1, msh=sh1, x=g, mean_rstd=mr1)
+            grads["n1w"], grads["n1b"] = s1[:, 1].clone(), s1[:, 0].clone()
+            if sync is not None:
+                sync.all_reduce_sums(s1, M1)
             K.bn_bwd_apply(dh, M1, Cout, dg, mask=2, mref=g, msc=sc1, msh=sh1, x=g, mean_rstd=mr1,
                            gamma=n1w.detach().float(), sums=s1)
-            grads["n1w"], grads["n1b"] = s1[:, 1].clone(), s1[:, 0].clone()
         else:
             dgb1 = torch.zeros((2, Cout * V), dtype=torch.float32, device=dev)
             K.ln_bwd(dh, g, ls1, _flat_ln(n1w), _flat_ln(n1b), N * T, V, Cout, dg, mask=2, dgb=dgb1)
@@ -638,7 +649,7 @@ class InputBatchNormFunction(torch.autograd.Function):
     (N,T).  Channels-last NTVC rows are exactly [N*T][V*C], so it is a row BatchNorm with V*C channels."""
 
     @staticmethod
-    def forward(ctx, x, w, b, dtype):
+    def forward(ctx, x, w, b, dtype, sync=None):
         x = K.to_rows(x, dtype)
         N, C, T, V = x.shape
         if K.rows_ld(x) != C:
@@ -646,11 +657,13 @@ class InputBatchNormFunction(torch.autograd.Function):
         F_, CV = N * T, V * C
         part, nb, _ = K.bn_stats_partial(x, F_, CV, ld=CV)
         # reference weight index = v*C + c == channels-last (v, c) order
-        mr, sc, sh = K.bn_finalize(part, nb, CV, CV, w.detach().float(), b.detach().float())
+        mr, sc, sh = (sync.finalize if sync is not None else K.bn_finalize)(part, nb, CV, CV, w.detach().float(),
+                                                                            b.detach().float())
         y = K.cl_empty(N, C, T, V, dtype, x.device)
         K.bn_apply(x, sc, sh, F_, CV, relu=False, out=y, ldu=CV, ldy=CV)
         ctx.save_for_backward(x, w, mr)
         ctx.dtype = dtype
+        ctx.sync = sync
         return y
 
     @staticmethod
@@ -662,9 +675,12 @@ class InputBatchNormFunction(torch.autograd.Function):
         if K.rows_ld(dy) != C:
             dy = dy.contiguous(memory_format=torch.channels_last)
         sums = _bn_reduce_flat(dy, x, mr, F_, CV)
+        dw, db = sums[:, 1].to(w.dtype, copy=True), sums[:, 0].to(w.dtype, copy=True)
+        if ctx.sync is not None:
+            ctx.sync.all_reduce_sums(sums, F_)
         dx = K.cl_empty(N, C, T, V, ctx.dtype, x.device)
         _bn_apply_flat(dy, x, mr, w.detach().float(), sums, F_, CV, dx)
-        return dx, sums[:, 1].to(w.dtype), sums[:, 0].to(w.dtype), None
+        return dx, dw, db, None, None
 
 
 @K.on_tensor_device
@@ -677,7 +693,7 @@ class WindowStageFunction(torch.autograd.Function):
     takes none, as in the reference where it is data)."""
 
     @staticmethod
-    def forward(ctx, capture, n0, nw, W, norm_w, norm_b, w, b, mode, dtype):
+    def forward(ctx, capture, n0, nw, W, norm_w, norm_b, w, b, mode, dtype, sync=None):
         Cout = w.shape[0]
         w2 = w.detach().float().reshape(Cout, -1)
         bias = b.detach().float() if b is not None else None
@@ -685,7 +701,9 @@ class WindowStageFunction(torch.autograd.Function):
         if mode == 0:
             part, nb = K.window_stats(capture, W, n0, nw, 0)
             VC = part.shape[1]
-            st, sc, sh = K.bn_finalize(part, nb, VC, VC, g, be)
+            # SyncBatchNorm: only the forward statistics are exchanged (the capture takes no gradient, and the
+            # parameter gradients are this rank's own sums)
+            st, sc, sh = (sync.finalize if sync is not None else K.bn_finalize)(part, nb, VC, VC, g, be)
             y = K.window_expand(capture, W, n0, nw, 0, sc, sh, None, w2, bias, dtype)
         else:
             st, _ = K.window_stats(capture, W, n0, nw, 1)
@@ -703,7 +721,7 @@ class WindowStageFunction(torch.autograd.Function):
         dg, dbe, dw, db = K.window_grad(dy, capture, W, n0, nw, mode, st, norm_w.detach().float().reshape(-1),
                                         norm_b.detach().float().reshape(-1), w.detach().float().reshape(Cout, -1))
         return (None, None, None, None, dg.view(norm_w.shape).to(norm_w.dtype), dbe.view(norm_b.shape).to(norm_b.dtype),
-                dw.view(w.shape).to(w.dtype), None if b is None else db.to(b.dtype), None, None)
+                dw.view(w.shape).to(w.dtype), None if b is None else db.to(b.dtype), None, None, None)
 
 
 def stage_window_batch(xb, norm_in, fcn_in, dtype):
@@ -711,7 +729,7 @@ def stage_window_batch(xb, norm_in, fcn_in, dtype):
     ln = not hasattr(norm_in, "norm")  # modules.BatchNorm1d wraps nn.BatchNorm1d as .norm
     g, b = (norm_in.weight, norm_in.bias) if ln else (norm_in.norm.weight, norm_in.norm.bias)
     return WindowStageFunction.apply(xb.capture, xb.n0, xb.nw, xb.W, g, b, fcn_in.weight, fcn_in.bias,
-                                     1 if ln else 0, dtype)
+                                     1 if ln else 0, dtype, None if ln else active_sync(norm_in))
 
 
 def _as_rows(t, F_, CV):
@@ -878,7 +896,9 @@ class RtOfflineLayerFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, A, wc, bc, nw, nb, wr, nrw, nrb, cfg):
-        Kt, S, residual, norm, dtype = cfg
+        Kt, S, residual, norm, dtype = cfg[:5]
+        sync = cfg[5] if len(cfg) > 5 else None
+        bn_finalize = sync.finalize if sync is not None else K.bn_finalize
         dev = x.device
         x = K.to_rows(x, dtype)
         N, Cin, L, V = x.shape
@@ -898,9 +918,9 @@ class RtOfflineLayerFunction(torch.autograd.Function):
             r = K.conv_rows(x, wrp, Cin, Cout, cq, kq, L, L, stats=str_ if norm == BN else None)
         if norm == BN:
             part, nbk, _ = K.bn_stats_partial(b, M, Cout)
-            mr, sc, sh = K.bn_finalize(part, nbk, Cout, Cout, nw.detach().float(), nb.detach().float())
+            mr, sc, sh = bn_finalize(part, nbk, Cout, Cout, nw.detach().float(), nb.detach().float())
             if res_conv:
-                mrr, scr, shr = K.bn_finalize(str_, str_.shape[0], str_.shape[1], Cout, nrw.detach().float(),
+                mrr, scr, shr = bn_finalize(str_, str_.shape[0], str_.shape[1], Cout, nrw.detach().float(),
                                               nrb.detach().float())
                 y = K.bn_apply(b, sc, sh, M, Cout, res_mode=2, r=r, rsc=scr, rsh=shr, relu=relu_mode)
             else:
@@ -930,7 +950,8 @@ class RtOfflineLayerFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        Kt, S, residual, norm, dtype = ctx.cfg
+        Kt, S, residual, norm, dtype = ctx.cfg[:5]
+        sync = ctx.cfg[5] if len(ctx.cfg) > 5 else None
         N, Cin, Cout, L, V, P, res_conv = ctx.dims
         sv = list(ctx.saved_tensors)
         x, A32, XA, b, y, st, wc, bc, nw, nb = sv[:10]
@@ -956,8 +977,10 @@ class RtOfflineLayerFunction(torch.autograd.Function):
             dr = K.cl_empty(N, Cout, L, V, dtype, dev)
             if norm == BN:
                 sr = K.bn_bwd_reduce(dq, M, Cout, x=r, mean_rstd=stn)
-                K.bn_bwd_apply(dq, M, Cout, dr, x=r, mean_rstd=stn, gamma=nrw.detach().float(), sums=sr)
                 g["nrw"], g["nrb"] = sr[:, 1].clone(), sr[:, 0].clone()
+                if sync is not None:
+                    sync.all_reduce_sums(sr, M)
+                K.bn_bwd_apply(dq, M, Cout, dr, x=r, mean_rstd=stn, gamma=nrw.detach().float(), sums=sr)
             else:
                 dgbr = torch.zeros((2, Cout * V), dtype=torch.float32, device=dev)
                 K.ln_bwd(dq, r, stn, _flat_ln(nrw), _flat_ln(nrb), N * L, V, Cout, dr, dgb=dgbr)
@@ -973,9 +996,11 @@ class RtOfflineLayerFunction(torch.autograd.Function):
         db = K.cl_empty(N, Cout, L, V, dtype, dev)
         if norm == BN:
             s1 = K.bn_bwd_reduce(dq, M, Cout, mask=2, mref=b, msc=sc, msh=sh, x=b, mean_rstd=st)
+            g["nw"], g["nb"] = s1[:, 1].clone(), s1[:, 0].clone()
+            if sync is not None:
+                sync.all_reduce_sums(s1, M)
             K.bn_bwd_apply(dq, M, Cout, db, mask=2, mref=b, msc=sc, msh=sh, x=b, mean_rstd=st,
                            gamma=nw.detach().float(), sums=s1)
-            g["nw"], g["nb"] = s1[:, 1].clone(), s1[:, 0].clone()
         else:
             dgb = torch.zeros((2, Cout * V), dtype=torch.float32, device=dev)
             K.ln_bwd(dq, b, st, _flat_ln(nw), _flat_ln(nb), N * L, V, Cout, db, mask=2, dgb=dgb)

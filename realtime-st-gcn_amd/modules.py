@@ -16,6 +16,7 @@ import torch.nn as nn
 
 from . import layer_fn as F_
 from . import native as K
+from .syncbn import active_sync
 
 _DTYPES = {"fp32": torch.float32, "bf16": torch.bfloat16, torch.float32: torch.float32,
            torch.bfloat16: torch.bfloat16}
@@ -48,7 +49,8 @@ class BatchNorm1d(nn.Module):
         self.compute_dtype = torch.float32
 
     def forward(self, x):
-        return F_.InputBatchNormFunction.apply(x, self.norm.weight, self.norm.bias, self.compute_dtype)
+        return F_.InputBatchNormFunction.apply(x, self.norm.weight, self.norm.bias, self.compute_dtype,
+                                               active_sync(self))
 
 
 def make_norm(normalization, channels, num_joints):
@@ -165,7 +167,8 @@ class StgcnLayer(nn.Module):
         infer = not torch.is_grad_enabled() or not (
             x.requires_grad or A.requires_grad or any(p.requires_grad for p in self.parameters()))
         cfg = (self.kernel_size[0], self.stride, self.is_residual, self.normalization, self.compute_dtype,
-               self.graph_support(A), not self._graph_bound, infer, self._fused_cache, None if infer else packs)
+               self.graph_support(A), not self._graph_bound, infer, self._fused_cache, None if infer else packs,
+               active_sync(self))
         return F_.StgcnLayerFunction.apply(x, A, self.gcn.conv.weight, self.gcn.conv.bias, n1.weight, n1.bias,
                                            conv.weight, conv.bias, n2.weight, n2.bias, wr, br, nrw, nrb, cfg)
 

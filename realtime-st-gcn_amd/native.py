@@ -747,6 +747,14 @@ def bn_finalize(part, nb, ld_part, C, gamma, beta, eps=1e-5):
     return mr, sc, sh
 
 
+def bn_merge(part, nb, ld_part, C):
+    """[C][4] float32: the nb (count, mean, M2) partials of each channel merged into one entry (stgcn_bn_merge) —
+    a rank's SyncBatchNorm contribution; the gathered [ranks][C][4] entries go through bn_finalize(nb = ranks)."""
+    out = torch.empty((C, 4), dtype=torch.float32, device=part.device)
+    L.check(L.lib().stgcn_bn_merge(part.data_ptr(), nb, ld_part, C, out.data_ptr(), L.stream()), "bn_merge")
+    return out
+
+
 def bn_apply(u, sc, sh, M, C, res_mode=0, r=None, rsc=None, rsh=None, relu=True, out=None, ldu=None, ldy=None,
              bits=None):
     """y = act(u*sc + sh + res) (stgcn_bn_apply).  ``bits`` (uint8 [M][C/8], bf16 and C % 8 == 0 only): also the
@@ -797,10 +805,12 @@ def bn_fused_ok(C: int, dtype) -> bool:
 
 
 def bn_bwd_fused(dy, M, C, mask=0, mref=None, msc=None, msh=None, x1=None, mr1=None, g1=None, out1=None,
-                 x2=None, mr2=None, g2=None, out2=None, acc2=False, bias_sums=False):
+                 x2=None, mr2=None, g2=None, out2=None, acc2=False, bias_sums=False, sync=None):
     # mask 3: mref = the uint8 [M][C/8] sign bits of the forward's output (bn_apply(bits=...))
     """Fused BN backward (stgcn_bn_bwd_fused_*).  Returns (sums [3, C] = (sum dz, sum dz*xhat1, sum dz*xhat2),
-    osum [3, C] = (sum out1, sum out2, -) or None), contiguous rows.  out1 / out2 are written in place."""
+    osum [3, C] = (sum out1, sum out2, -) or None), contiguous rows.  out1 / out2 are written in place.
+    ``sync`` (syncbn.BnSync): SyncBatchNorm — the apply pass uses the sums of every rank (exchanged between the
+    two passes); the returned sums stay this rank's own (the parameter gradients, which DDP then averages)."""
     code = L.dtype_code(dy.dtype)
     dev = dy.device
     work = torch.empty(L.lib().stgcn_bn_bwd_fused_workspace(M, C, code), dtype=torch.float32, device=dev)
@@ -827,6 +837,10 @@ def bn_bwd_fused(dy, M, C, mask=0, mref=None, msc=None, msh=None, x1=None, mr1=N
     L.check(L.lib().stgcn_bn_bwd_fused_reduce(d, code, L.stream()), "bn_bwd_fused_reduce")
     if h:
         h(ktag, "end", None)
+    if sync is not None and out1 is not None:
+        # the reduce pass wrote the per-channel sums twice: float4 rows [C] (what apply reads) and planar [3][C]
+        # (returned); only the rows are exchanged
+        sync.all_reduce_sums(sums[:4 * C].view(C, 4), M, count_lane=True)
     if out1 is not None:
         if h:
             n_out = 1 + (out2 is not None) * (2 if acc2 else 1)

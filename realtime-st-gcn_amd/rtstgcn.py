@@ -22,6 +22,7 @@ import torch.nn.functional as F
 from . import layer_fn as LF
 from . import native as K
 from .routing import ROUTING
+from .syncbn import active_sync
 from .graph import Graph
 from .modules import BatchNorm1d, LayerNorm, make_norm, resolve_dtype
 from .stgcn import IN_PAD
@@ -60,7 +61,8 @@ class OfflineLayer(nn.Module):
             wr, nrw, nrb = self.residual[0].weight, self.residual[1].weight, self.residual[1].bias
         else:
             wr = nrw = nrb = None
-        cfg = (self.kernel_size, self.stride, self.is_residual, self.normalization, self.compute_dtype)
+        cfg = (self.kernel_size, self.stride, self.is_residual, self.normalization, self.compute_dtype,
+               active_sync(self))
         return LF.RtOfflineLayerFunction.apply(x, A_eff, self.conv.weight, self.conv.bias, n.weight, n.bias, wr,
                                                nrw, nrb, cfg)
 
