@@ -12,8 +12,9 @@ N > 1: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) the ra
 (before anything touches the GPU) and exits with its status.  Each rank trains on its own trial's
 64-window subsegment (weak scaling; the subsegment's loss is self-contained, processor.py:377-392, so the
 data path has no collective); gradients are averaged over ranks by DistributedDataParallel (RCCL
-all-reduce in 4 MB buckets, ~4 for the 12.2 MB gradient, overlapped with backward) or, with --graph, by one all-reduce of the flat
-gradient between the two graphs — the reference's accumulation of ``loss / batch_size`` over trials.
+all-reduce in 4 MB buckets, ~4 for the 12.2 MB gradient, overlapped with backward) or, with --graph, by the same
+4 MB bucket all-reduces captured inside the step's one HIP graph (parallel.GraphedStep bucket mode) — the
+reference's accumulation of ``loss / batch_size`` over trials.
 
 Config 4 (--config 4): the long-trial DDP workload of SURVEY 8(d): synthetic trials of U[4000, 8000]
 frames (seed 2), cut into WindowSegment subsegments of 64 windows of T = 300 frames (the reference's
@@ -462,7 +463,9 @@ def main():
             frames_done[0] += N_BATCH * T_LEN
 
         if args.graph:  # its first (eager) step all-reduces too: the replicas stay identical
-            gstep = par.GraphedStep(fwd_loss, params, opt, world)
+            # N > 1: ONE graph per step with the per-bucket RCCL all-reduces captured inside it, each issued when its
+            # 4 MB bucket's gradients are accumulated (overlapped with the rest of the backward, as DDP eagerly)
+            gstep = par.GraphedStep(fwd_loss, params, opt, world, bucket_mb=4 if world > 1 else None)
 
             def step():
                 gstep()
@@ -588,7 +591,9 @@ def main():
             "config": {"workload": workload, "global_batch": N_BATCH * world, "seq_len": T_LEN, "joints": V_J,
                        "parallelism": f"dp{world}" if world > 1 else "single",
                        "bn_stats": "sync (all ranks)" if args.sync_bn and world > 1 else "per-replica",
-                       "launch": "eager" if not args.graph else "hip-graph replay (fwd+bwd | allreduce | Adam)"},
+                       "launch": "eager" if not args.graph else (
+                           "hip-graph replay (fwd+bwd | Adam)" if world == 1 else
+                           "hip-graph replay (fwd+bwd with captured 4 MB bucket all-reduces + Adam, one graph)")},
             "roofline": roof,
             "roofline_tcn_fwd": {"kernel": "conv_wide_kernel<128,9,8,1,0,64> (persistent warp-specialised Kt=9 "
                                            "stride-1 temporal conv fwd of the C=128 and C=256 layers, 4 launches/step)",

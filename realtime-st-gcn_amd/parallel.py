@@ -179,24 +179,37 @@ class GraphedStep:
     """A fixed-shape training step replayed as HIP graphs (processor.py:531-564 inner loop with the batch in
     static buffers): one graph launch for the ~250 kernels of the forward, loss and backward on one stream.
 
+    Flat mode (``bucket_mb=None``, any backend):
+
         graph 1: zero the gradients, ``fwd_loss()`` (forward + loss), backward, [N > 1: copy the fp32
                  gradients into one flat buffer]
-        N > 1:   all-reduce of the flat buffer over ``group`` (eager, one RCCL launch; not captured)
+        N > 1:   all-reduce of the flat buffer over ``group`` (eager, one collective; not captured)
         graph 2: [N > 1: the averaged flat gradient back into .grad] + ``opt.step()``
+
+    Bucket mode (``bucket_mb`` set; an initialised process group of a capturable backend — RCCL): ONE graph
+    holds the whole step
+    with the gradient exchange overlapped with the backward, as DistributedDataParallel does eagerly.  The
+    gradients of the trained parameters are views into per-bucket flat buffers (``bucket_mb`` MB of fp32
+    each, filled in reverse parameter order — the order the backward finishes them, as DDP assumes); a
+    post-accumulate-grad hook counts each bucket's parameters while the step is captured and, when the last
+    one is accumulated, issues that bucket's all-reduce asynchronously (RCCL's stream, captured as a fork of
+    the graph), so it runs under the rest of the backward; the graph joins every bucket's collective, divides
+    by N and runs ``opt.step()``.  Replays run the recorded collectives; the hooks fire only during capture.
 
     ``fwd_loss`` must only read tensors whose storage stays put between replays (copy new batches into the
     tensors it closes over).  The optimizer must be capturable: the package's ``optim.Adam`` (device-side step
     counters; what bench.py uses) or torch.optim.Adam(capturable=True).  One eager step runs first (on a side
     stream, as graph capture requires) so that every gradient and optimizer state tensor exists and keeps its
     address.  A parameter that got no gradient in it keeps ``grad = None`` and is left out of the captured zeroing,
-    the flat all-reduce and the update (the optimizers skip ``None`` gradients, as an eager step would: its Adam
+    the all-reduce and the update (the optimizers skip ``None`` gradients, as an eager step would: its Adam
     moments and, with weight decay, its value stay put).  Replays do not bump the parameters' version counters (host-side bookkeeping is not captured):
     call ``train()`` / ``eval()`` before an inference forward that should see replayed updates."""
 
-    def __init__(self, fwd_loss, params, opt, world: int = 1, group=None):
+    def __init__(self, fwd_loss, params, opt, world: int = 1, group=None, bucket_mb=None):
         self.fwd_loss, self.params, self.opt = fwd_loss, list(params), opt
         self.world, self.group = world, group
         self.flat = None
+        self.buckets = None
         dev = self.params[0].device
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream(dev))
@@ -206,19 +219,89 @@ class GraphedStep:
             # the parameters this step trains: the ones that received a gradient in the eager step
             self.used = [p for p in self.params if p.grad is not None]
             self.numels = [p.numel() for p in self.used]
-            if world > 1:
-                self.flat = torch.zeros(sum(self.numels), device=dev)
-                torch.cat([p.grad.reshape(-1) for p in self.used], out=self.flat)
-                self._allreduce()
-            self._apply()
-            self.g1, self.g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g1, stream=s):
-                for p in self.used:
-                    p.grad.zero_()
-                self.loss = self._fwd_bwd()
-            with torch.cuda.graph(self.g2, stream=s):
+            if bucket_mb is not None:  # (world 1 too: the collectives then are identities, still recorded)
+                self._make_buckets(bucket_mb)
+                for flat, _ in self.buckets:
+                    self._allreduce(flat)
                 self._apply()
+                self.g1, self.g2 = torch.cuda.CUDAGraph(), None
+                # thread-local capture: the process group's watchdog thread keeps querying its events meanwhile
+                with torch.cuda.graph(self.g1, stream=s, capture_error_mode="thread_local"):
+                    self.loss = self._bucketed_step()
+            else:
+                if world > 1:
+                    self.flat = torch.zeros(sum(self.numels), device=dev)
+                    torch.cat([p.grad.reshape(-1) for p in self.used], out=self.flat)
+                    self._allreduce(self.flat)
+                self._apply()
+                self.g1, self.g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.g1, stream=s):
+                    for p in self.used:
+                        p.grad.zero_()
+                    self.loss = self._fwd_bwd()
+                with torch.cuda.graph(self.g2, stream=s):
+                    self._apply()
         torch.cuda.current_stream(dev).wait_stream(s)
+
+    def _make_buckets(self, bucket_mb):
+        """Per-bucket flat fp32 buffers, the trained parameters' .grad re-pointed into them (current values kept),
+        and the readiness hooks."""
+        cap = max(1, int(bucket_mb * (1 << 20)) // 4)
+        groups, cur, n = [], [], 0
+        for p in reversed(self.used):
+            if p.grad.dtype != torch.float32:
+                raise ValueError("GraphedStep(bucket_mb=...): fp32 gradients only")
+            if cur and n + p.numel() > cap:
+                groups.append(cur)
+                cur, n = [], 0
+            cur.append(p)
+            n += p.numel()
+        if cur:
+            groups.append(cur)
+        self.buckets = []
+        for b, ps in enumerate(groups):
+            flat = torch.empty(sum(p.numel() for p in ps), dtype=torch.float32, device=ps[0].device)
+            o = 0
+            for p in ps:
+                v = flat[o:o + p.numel()].view(p.shape)
+                v.copy_(p.grad)
+                p.grad = v
+                o += p.numel()
+                p.register_post_accumulate_grad_hook(lambda _p, b=b: self._ready(b))
+            self.buckets.append((flat, len(ps)))
+        self._capturing = False
+
+    def _ready(self, b):
+        if not self._capturing:
+            return
+        self._count[b] += 1
+        if self._count[b] == self.buckets[b][1]:
+            import torch.distributed as dist
+            self._works.append(dist.all_reduce(self.buckets[b][0], group=self.group, async_op=True))
+            self._launched[b] = True
+
+    def _bucketed_step(self):
+        for flat, _ in self.buckets:
+            flat.zero_()
+        self._count = [0] * len(self.buckets)
+        self._launched = [False] * len(self.buckets)
+        self._works = []
+        self._capturing = True
+        try:
+            loss = self.fwd_loss()
+            loss.backward()
+        finally:
+            self._capturing = False
+        import torch.distributed as dist
+        for b, (flat, _) in enumerate(self.buckets):
+            if not self._launched[b]:  # a parameter of the bucket got no gradient in this step: exchange anyway
+                self._works.append(dist.all_reduce(flat, group=self.group, async_op=True))
+        for w in self._works:
+            w.wait()  # the capturing stream joins the collective's stream
+        for flat, _ in self.buckets:
+            flat.div_(self.world)
+        self.opt.step()
+        return loss.detach()
 
     def _fwd_bwd(self):
         loss = self.fwd_loss()
@@ -227,19 +310,23 @@ class GraphedStep:
             torch.cat([p.grad.reshape(-1) for p in self.used], out=self.flat)
         return loss.detach()
 
-    def _allreduce(self):
+    def _allreduce(self, t):
         import torch.distributed as dist
-        dist.all_reduce(self.flat, group=self.group)
+        dist.all_reduce(t, group=self.group)
 
     def _apply(self):
-        if self.flat is not None:
+        if self.buckets is not None:
+            for flat, _ in self.buckets:
+                flat.div_(self.world)
+        elif self.flat is not None:
             for p, g in zip(self.used, torch.split(self.flat, self.numels)):
                 p.grad.copy_(g.view_as(p.grad)).div_(self.world)
         self.opt.step()
 
     def __call__(self):
         self.g1.replay()
-        if self.flat is not None:
-            self._allreduce()
-        self.g2.replay()
+        if self.g2 is not None:
+            if self.flat is not None:
+                self._allreduce(self.flat)
+            self.g2.replay()
         return self.loss

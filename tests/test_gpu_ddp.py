@@ -226,3 +226,75 @@ def test_graphed_step_flat_allreduce(pkg):
                               f"eager rank {r} {k}", reduction=True)
             assert_grad_close(torch.from_numpy(got[r]["avg"][k]), torch.from_numpy(mean), 1e-3,
                               f"graph all-reduced {k}", reduction=True)
+
+
+def _bucket_graph_worker(rank, world, port, q):
+    """One rank, RCCL: GraphedStep's bucket mode (per-bucket all-reduces captured inside the one step graph, issued
+    from the backward's post-accumulate hooks) against eager steps of the same model and optimizer."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    try:
+        pkg = _pkg()
+        res = {}
+        x, labels = (t.to(dev) for t in _unit(0))
+        for mode in ("eager", "graph"):
+            m = _model(pkg, "BatchNorm", "bf16", dev)
+            params = [p for p in m.parameters() if p.requires_grad]
+            opt = pkg.optim.Adam(params, lr=1e-3)
+            crit = pkg.loss.Loss(dev, CLASS_DIST)
+
+            def fwd_loss():
+                ce, mse = crit(0, m(x).permute(2, 1, 0), labels)
+                return ce + mse
+
+            losses = []
+            if mode == "eager":
+                for _ in range(4):
+                    opt.zero_grad(set_to_none=False)
+                    loss = fwd_loss()
+                    loss.backward()
+                    opt.step()
+                    losses.append(float(loss))
+            else:
+                # 0.25 MB buckets: several buckets (and several captured collectives) for this small model
+                gstep = pkg.parallel.GraphedStep(fwd_loss, params, opt, world, bucket_mb=0.25)
+                res["n_buckets"] = len(gstep.buckets)
+                losses.append(None)  # the constructor's eager step
+                for _ in range(3):
+                    losses.append(float(gstep()))
+            torch.cuda.synchronize()
+            res[mode] = ({k: p.detach().float().cpu().numpy() for k, p in m.named_parameters()}, losses)
+        q.put((rank, res))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_graphed_step_bucketed_allreduce_rccl(pkg):
+    """GraphedStep(bucket_mb=...) on RCCL (one rank: the box has one GPU and RCCL refuses two ranks on it): the
+    captured per-bucket collectives and the gradients as bucket views give the eager step's parameters and losses
+    after 1 eager + 3 replayed steps."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_bucket_graph_worker, args=(0, 1, _free_port(), q))
+    p.start()
+    try:
+        got = dict(collect_ranks(q, [p], 1, timeout=240))
+    finally:
+        reap_ranks([p])
+    assert p.exitcode == 0
+    res = got[0]
+    assert res["n_buckets"] > 1
+    pe, le = res["eager"]
+    pg, lg = res["graph"]
+    for a, b in zip(le[1:], lg[1:]):
+        assert abs(a - b) <= 1e-5 * max(1.0, abs(a)), (le, lg)
+    for k in pe:
+        np.testing.assert_allclose(pg[k], pe[k], rtol=1e-5, atol=1e-6, err_msg=k)
