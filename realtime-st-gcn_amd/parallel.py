@@ -181,8 +181,9 @@ class GraphedStep:
 
     Flat mode (``bucket_mb=None``, any backend):
 
-        graph 1: zero the gradients, ``fwd_loss()`` (forward + loss), backward, [N > 1: copy the fp32
-                 gradients into one flat buffer]
+        graph 1: ``fwd_loss()`` (forward + loss), backward — the gradients are the backward's own outputs
+                 (captured with ``grad = None``, so static graph-pool tensors, written afresh by every replay) —
+                 [N > 1: copy the fp32 gradients into one flat buffer]
         N > 1:   all-reduce of the flat buffer over ``group`` (eager, one collective; not captured)
         graph 2: [N > 1: the averaged flat gradient back into .grad] + ``opt.step()``
 
@@ -235,10 +236,15 @@ class GraphedStep:
                     self._allreduce(self.flat)
                 self._apply()
                 self.g1, self.g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                # the gradients are created by the captured backward itself (AccumulateGrad takes the produced
+                # tensor, from the graph's private pool, static across replays): no per-parameter zero fill and
+                # accumulate-add kernels (~2 x 96 small launches per replay)
+                for p in self.used:
+                    p.grad = None
                 with torch.cuda.graph(self.g1, stream=s):
-                    for p in self.used:
-                        p.grad.zero_()
                     self.loss = self._fwd_bwd()
+                if any(p.grad is None for p in self.used):
+                    raise RuntimeError("GraphedStep: a parameter lost its gradient in the captured step")
                 with torch.cuda.graph(self.g2, stream=s):
                     self._apply()
         torch.cuda.current_stream(dev).wait_stream(s)
