@@ -675,8 +675,9 @@ class InputBatchNormFunction(torch.autograd.Function):
         if K.rows_ld(dy) != C:
             dy = dy.contiguous(memory_format=torch.channels_last)
         sums = _bn_reduce_flat(dy, x, mr, F_, CV)
-        dw, db = sums[:, 1].to(w.dtype, copy=True), sums[:, 0].to(w.dtype, copy=True)
-        if ctx.sync is not None:
+        dw, db = sums[:, 1].to(w.dtype), sums[:, 0].to(w.dtype)
+        if ctx.sync is not None:  # the parameter gradients keep this rank's own sums (copies: sums is exchanged)
+            dw, db = dw.clone(), db.clone()
             ctx.sync.all_reduce_sums(sums, F_)
         dx = K.cl_empty(N, C, T, V, ctx.dtype, x.device)
         _bn_apply_flat(dy, x, mr, w.detach().float(), sums, F_, CV, dx)
