@@ -206,9 +206,15 @@ class GraphedStep:
     moments and, with weight decay, its value stay put).  Replays do not bump the parameters' version counters (host-side bookkeeping is not captured):
     call ``train()`` / ``eval()`` before an inference forward that should see replayed updates."""
 
-    def __init__(self, fwd_loss, params, opt, world: int = 1, group=None, bucket_mb=None):
+    def __init__(self, fwd_loss, params, opt, world: int = 1, group=None, bucket_mb=None, capture: bool = True):
+        """``capture=False`` (bucket mode only): the same bucketed step run eagerly on every call — the hooks issue
+        the bucket all-reduces as the backward finishes them — for process groups that cannot be captured
+        (gloo) and for debugging the exchange outside a graph."""
         self.fwd_loss, self.params, self.opt = fwd_loss, list(params), opt
         self.world, self.group = world, group
+        self.capture = capture
+        if not capture and bucket_mb is None:
+            raise ValueError("GraphedStep(capture=False) needs bucket_mb (the flat mode is graph-only)")
         self.flat = None
         self.buckets = None
         dev = self.params[0].device
@@ -225,10 +231,12 @@ class GraphedStep:
                 for flat, _ in self.buckets:
                     self._allreduce(flat)
                 self._apply()
-                self.g1, self.g2 = torch.cuda.CUDAGraph(), None
-                # thread-local capture: the process group's watchdog thread keeps querying its events meanwhile
-                with torch.cuda.graph(self.g1, stream=s, capture_error_mode="thread_local"):
-                    self.loss = self._bucketed_step()
+                self.g1, self.g2 = None, None
+                if capture:
+                    self.g1 = torch.cuda.CUDAGraph()
+                    # thread-local capture: the process group's watchdog thread keeps querying its events meanwhile
+                    with torch.cuda.graph(self.g1, stream=s, capture_error_mode="thread_local"):
+                        self.loss = self._bucketed_step()
             else:
                 if world > 1:
                     self.flat = torch.zeros(sum(self.numels), device=dev)
@@ -278,7 +286,7 @@ class GraphedStep:
         self._capturing = False
 
     def _ready(self, b):
-        if not self._capturing:
+        if not self._capturing:  # set during the captured (or, capture=False, the eager) bucketed step
             return
         self._count[b] += 1
         if self._count[b] == self.buckets[b][1]:
@@ -330,6 +338,9 @@ class GraphedStep:
         self.opt.step()
 
     def __call__(self):
+        if self.g1 is None:  # capture=False: the bucketed step eagerly
+            self.loss = self._bucketed_step()
+            return self.loss
         self.g1.replay()
         if self.g2 is not None:
             if self.flat is not None:

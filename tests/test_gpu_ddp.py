@@ -170,7 +170,7 @@ def _unit(rank):
     return torch.randn(6, 3, W, 25, generator=g), torch.randint(0, 52, (1, 6), generator=g)
 
 
-def _graph_worker(rank, world, port, q):
+def _graph_worker(rank, world, port, q, bucketed=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -192,7 +192,11 @@ def _graph_worker(rank, world, port, q):
         opt.zero_grad(set_to_none=True)  # the rank's own (eager, local) gradient
         fwd_loss().backward()
         eager = _grads(m)
-        gstep = pkg.parallel.GraphedStep(fwd_loss, params, opt, world)
+        if bucketed:  # the bucket mode's hooks and exchange, uncaptured (gloo cannot be captured)
+            gstep = pkg.parallel.GraphedStep(fwd_loss, params, opt, world, bucket_mb=0.25, capture=False)
+            assert len(gstep.buckets) > 1
+        else:
+            gstep = pkg.parallel.GraphedStep(fwd_loss, params, opt, world)
         for _ in range(2):
             gstep()
         torch.cuda.synchronize()
@@ -202,12 +206,14 @@ def _graph_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_graphed_step_flat_allreduce(pkg):
-    """The bench's --graph step at N = 2: captured fwd + loss + bwd (side stream as a graph branch), one
-    flat all-reduce, captured optimizer; averaged gradient = mean of the per-rank gradients."""
+@pytest.mark.parametrize("bucketed", [False, True])
+def test_graphed_step_flat_allreduce(pkg, bucketed):
+    """GraphedStep at N = 2: captured fwd + loss + bwd, one flat all-reduce, captured optimizer — or (bucketed) the
+    bucket mode's post-accumulate hooks issuing per-bucket all-reduces during the backward (run uncaptured: gloo);
+    averaged gradient = mean of the per-rank gradients."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
-    got = _spawn(_graph_worker)
+    got = _spawn(_graph_worker, bucketed)
     dev = torch.device("cuda", 0)
     refs = []
     for r in range(WORLD):
