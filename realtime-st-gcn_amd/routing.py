@@ -28,6 +28,9 @@ Routes removed in round 5 after losing their A/Bs (last measurements in DESIGN 4
 graph conv (gcn_frame.hip: equal forward, slower data gradient) and graph-conv weight gradient
 (gconv_wgrad_frame.hip: 115 vs 72 us at C = 64), gcn_tile.hip as the training graph conv (equal inside the step), the tconv_frame.hip forward (67.1 vs 64.1 us; its data gradient
 ships), the weight-gradient side stream (8.68 vs 8.55 ms/step) and the forced A-first graph conv for shared graphs.
+Tried in round 6 and not kept: only the graph-conv weight gradient's latency-bound tail (slab reduction + dW / dA / db
+finish, ~33 us per layer) on a second stream beside the layer's graph-conv data gradient — 8.28 / 7.88 / 7.85 vs
+7.63 / (8.74) / 7.63 ms/step (interleaved, one box): co-running still slows the data gradient more than it hides.
 """
 import os
 
