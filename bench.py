@@ -385,8 +385,11 @@ def main():
     if args.config == 4 and args.graph:
         sys.exit("bench.py: --graph needs fixed shapes (config 2); config 4's units have 49-65 windows")
 
+    # STGCN_BENCH_REHEARSE=1: the N > 1 path (spawn, DDP, barriers, max-over-ranks timing, the JSON line) with every
+    # rank on GPU 0 over gloo — a one-GPU rehearsal of the multi-GPU bench; its numbers are not a measurement
+    rehearse = os.environ.get("STGCN_BENCH_REHEARSE") == "1"
     ndev = torch.cuda.device_count()  # does not initialise HIP (safe before spawning the ranks)
-    if ndev < args.gpus:
+    if ndev < args.gpus and not rehearse:
         sys.exit(f"bench.py: --gpus {args.gpus} needs {args.gpus} HIP devices, {ndev} visible")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args))
@@ -395,9 +398,13 @@ def main():
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if rehearse:
+        if args.graph:
+            sys.exit("bench.py: STGCN_BENCH_REHEARSE runs gloo, which HIP graphs cannot capture (no --graph)")
+        local = 0
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl")
+        dist.init_process_group("gloo" if rehearse else "nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -589,7 +596,8 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (randn skeletons, random labels/class weights), random-init weights",
             "config": {"workload": workload, "global_batch": N_BATCH * world, "seq_len": T_LEN, "joints": V_J,
-                       "parallelism": f"dp{world}" if world > 1 else "single",
+                       "parallelism": (f"dp{world}" if world > 1 else "single") + (
+                           " (REHEARSAL: all ranks on GPU 0 over gloo, not a measurement)" if rehearse else ""),
                        "bn_stats": "sync (all ranks)" if args.sync_bn and world > 1 else "per-replica",
                        "launch": "eager" if not args.graph else (
                            "hip-graph replay (fwd+bwd | Adam)" if world == 1 else
