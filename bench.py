@@ -398,9 +398,7 @@ def main():
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if rehearse:
-        if args.graph:
-            sys.exit("bench.py: STGCN_BENCH_REHEARSE runs gloo, which HIP graphs cannot capture (no --graph)")
+    if rehearse:  # (--graph: gloo cannot be captured, so the bucketed step then runs uncaptured)
         local = 0
     if world > 1:
         import torch.distributed as dist
@@ -472,7 +470,8 @@ def main():
         if args.graph:  # its first (eager) step all-reduces too: the replicas stay identical
             # N > 1: ONE graph per step with the per-bucket RCCL all-reduces captured inside it, each issued when its
             # 4 MB bucket's gradients are accumulated (overlapped with the rest of the backward, as DDP eagerly)
-            gstep = par.GraphedStep(fwd_loss, params, opt, world, bucket_mb=4 if world > 1 else None)
+            gstep = par.GraphedStep(fwd_loss, params, opt, world, bucket_mb=4 if world > 1 else None,
+                                    capture=not (rehearse and world > 1))
 
             def step():
                 gstep()
