@@ -273,6 +273,7 @@ class GraphedStep:
         if cur:
             groups.append(cur)
         self.buckets = []
+        self._hooks = []
         for b, ps in enumerate(groups):
             flat = torch.empty(sum(p.numel() for p in ps), dtype=torch.float32, device=ps[0].device)
             o = 0
@@ -281,9 +282,16 @@ class GraphedStep:
                 v.copy_(p.grad)
                 p.grad = v
                 o += p.numel()
-                p.register_post_accumulate_grad_hook(lambda _p, b=b: self._ready(b))
+                self._hooks.append(p.register_post_accumulate_grad_hook(lambda _p, b=b: self._ready(b)))
             self.buckets.append((flat, len(ps)))
         self._capturing = False
+
+    def remove_hooks(self):
+        """Detach the bucket mode's readiness hooks from the parameters (they hold this step object); the step
+        must not be called afterwards."""
+        for h in getattr(self, "_hooks", ()):
+            h.remove()
+        self._hooks = []
 
     def _ready(self, b):
         if not self._capturing:  # set during the captured (or, capture=False, the eager) bucketed step

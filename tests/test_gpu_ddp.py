@@ -272,6 +272,7 @@ def _bucket_graph_worker(rank, world, port, q):
                 losses.append(None)  # the constructor's eager step
                 for _ in range(3):
                     losses.append(float(gstep()))
+                gstep.remove_hooks()
             torch.cuda.synchronize()
             res[mode] = ({k: p.detach().float().cpu().numpy() for k, p in m.named_parameters()}, losses)
         q.put((rank, res))
