@@ -9,7 +9,8 @@
   the DDP-averaged gradient of the ranks' summed losses equal to that run's gradient / world size.  The same
   ranks without SyncBN (the reference's per-replica DataParallel semantics, the default) must NOT match
   (the test sees the statistics).  fp32 and bf16; plain batches, window-staged ones (WindowBatch, whose
-  input norm statistics come from window.hip), and the RT-ST-GCN training model (OfflineLayer's norms).
+  input norm statistics come from window.hip), the RT-ST-GCN training model (OfflineLayer's norms) and the
+  AAGCN model (per-sample graphs through the A-first graph conv; fp32).
 """
 import os
 
@@ -41,8 +42,22 @@ def _rt_model(pkg, dtype, dev):
     return m.to(dev).set_compute_dtype(dtype)
 
 
+def _aagcn_model(pkg, dtype, dev):
+    arch = {"strategy": "spatial", "in_feat": 3, "output_type": "logits", "normalization": "BatchNorm",
+            "num_classes": 52,
+            "aa-gcn": {"layers": 2, "kernel": 9, "importance": True, "in_feat": 3, "in_ch": [64, 64],
+                       "out_ch": [64, 128], "stride": [1, 2], "residual": [1, 1], "dropout": [0, 0]}}
+    torch.manual_seed(5)
+    m = pkg.MODELS["aa-gcn"](rank=None, **dict(arch, graph=pkg.PKU_MMD))
+    return m.to(dev).set_compute_dtype(dtype)
+
+
 def _make(pkg, route, dtype, dev):
-    return _rt_model(pkg, dtype, dev) if route == "rt" else _model(pkg, "BatchNorm", dtype, dev)
+    if route == "rt":
+        return _rt_model(pkg, dtype, dev)
+    if route == "aagcn":
+        return _aagcn_model(pkg, dtype, dev)
+    return _model(pkg, "BatchNorm", dtype, dev)
 
 
 def _input(pkg, route, x, cap, s, e, dev):
@@ -95,8 +110,10 @@ def _sync_worker(rank, world, port, q, dtype, route):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("route", ["tensor", "window", "rt"])
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+# AAGCN in fp32 only: its attention makes the model chaotic in its inputs (tests/test_aagcn_sensitivity.py), so two
+# bf16 runs with different rounding orders are not comparable per rank
+@pytest.mark.parametrize("dtype,route", [(d, r) for d in ("fp32", "bf16") for r in ("tensor", "window", "rt")]
+                         + [("fp32", "aagcn")])
 def test_syncbn_ddp_equals_single_process_batch(pkg, dtype, route):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
